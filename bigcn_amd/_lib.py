@@ -1,0 +1,154 @@
+"""ctypes binding of ``libbgcn.so`` (the C ABI declared in ``include/bgcn.h``).
+
+The library is built in-tree (``make -C bigcn_amd/csrc`` or ``__graft_entry__.build()``)
+and linked against ``libamdhip64.so.7`` by SONAME, so inside a PyTorch process it
+shares the HIP runtime torch already loaded (same streams, same device memory).
+
+There is deliberately no fallback: if the library is missing or no ROCm device is
+present, every op raises.  The oracle under ``oracle/`` is test infrastructure and
+is never imported from here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, Structure, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BGCN_LIB", os.path.join(_HERE, "libbgcn.so"))
+
+BGCN_DEGREE_ON_COL = 0
+BGCN_DEGREE_ON_ROW = 1
+BGCN_EPI_NONE = 0
+BGCN_EPI_RELU = 1
+
+# every symbol include/bgcn.h declares (checked by tests/test_capi.py)
+EXPORTED_SYMBOLS = (
+    "bgcn_abi_version", "bgcn_last_error",
+    "bgcn_graph_workspace_size", "bgcn_build_graph",
+    "bgcn_spmm_workspace_size", "bgcn_spmm",
+    "bgcn_gemm_xwt", "bgcn_gemm_xw", "bgcn_gemm_tn_workspace_size", "bgcn_gemm_tn",
+    "bgcn_colsum_workspace_size", "bgcn_colsum",
+    "bgcn_scatter_mean_workspace_size", "bgcn_scatter_mean_fwd", "bgcn_scatter_mean_bwd",
+    "bgcn_bigcn_workspace_size", "bgcn_bigcn_forward", "bgcn_bigcn_backward",
+    "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing",
+)
+
+
+class GraphView(Structure):
+    _fields_ = [
+        ("t_ptr", c_void_p), ("t_row", c_void_p), ("t_col", c_void_p), ("t_w", c_void_p),
+        ("s_ptr", c_void_p), ("s_row", c_void_p), ("s_col", c_void_p), ("s_w", c_void_p),
+        ("capacity", c_int64),
+    ]
+
+
+class BiGCNArgs(Structure):
+    _fields_ = [
+        ("x", c_void_p), ("ldx", c_int64), ("num_nodes", c_int64), ("num_graphs", c_int64),
+        ("in_feats", c_int64), ("hid", c_int64), ("batch", c_void_p), ("rootindex", c_void_p),
+        ("td", GraphView), ("bu", GraphView),
+        ("td_w1", c_void_p), ("td_b1", c_void_p), ("td_w2", c_void_p), ("td_b2", c_void_p),
+        ("bu_w1", c_void_p), ("bu_b1", c_void_p), ("bu_w2", c_void_p), ("bu_b2", c_void_p),
+        ("training", c_int), ("seed", c_uint64), ("keep_words", c_void_p),
+        ("tree_ptr", c_void_p), ("h1", c_void_p), ("h2", c_void_p), ("head_in", c_void_p),
+        ("dhead_in", c_void_p),
+        ("td_dw1", c_void_p), ("td_db1", c_void_p), ("td_dw2", c_void_p), ("td_db2", c_void_p),
+        ("bu_dw1", c_void_p), ("bu_db1", c_void_p), ("bu_dw2", c_void_p), ("bu_db2", c_void_p),
+    ]
+
+
+_SIGS = {
+    "bgcn_abi_version": (c_int, []),
+    "bgcn_last_error": (c_char_p, []),
+    "bgcn_graph_workspace_size": (c_size_t, [c_int64, c_int64]),
+    "bgcn_build_graph": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int,
+                                 c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_size_t, c_void_p]),
+    "bgcn_spmm_workspace_size": (c_size_t, [c_int64, c_int32]),
+    "bgcn_spmm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                          c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int, c_void_p,
+                          c_size_t, c_void_p]),
+    "bgcn_gemm_xwt": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                              c_int64, c_int64, c_int64, c_int64, c_void_p]),
+    "bgcn_gemm_xw": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64,
+                             c_int64, c_int64, c_void_p]),
+    "bgcn_gemm_tn_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
+    "bgcn_gemm_tn": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                             c_int64, c_int64, c_int64, c_int64, c_void_p, c_size_t, c_void_p]),
+    "bgcn_colsum_workspace_size": (c_size_t, [c_int64, c_int32]),
+    "bgcn_colsum": (c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_size_t,
+                            c_void_p]),
+    "bgcn_scatter_mean_workspace_size": (c_size_t, [c_int64]),
+    "bgcn_scatter_mean_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int32, c_int64,
+                                      c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t,
+                                      c_void_p]),
+    "bgcn_scatter_mean_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32,
+                                      c_int64, c_void_p, c_int64, c_void_p]),
+    "bgcn_bigcn_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64]),
+    "bgcn_bigcn_forward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
+    "bgcn_bigcn_backward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
+    "bgcn_keep_words": (c_int, [c_uint64, c_int64, c_int32, c_void_p, c_void_p]),
+    "bgcn_set_kernel_timing": (c_int, [c_int]),
+    "bgcn_kernel_timing": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class BGCNError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """Load and type the library (no GPU needed: used by the CPU symbol tests)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise ImportError(
+                f"libbgcn.so not found at {path}: build it with `make -C bigcn_amd/csrc` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.bgcn_abi_version() != 1:
+            raise ImportError("libbgcn.so ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def lib():
+    """The library, for device work: requires a ROCm device."""
+    if not torch.cuda.is_available():
+        raise BGCNError("the bigcn_amd HIP path needs a ROCm GPU (no CPU fallback exists)")
+    return load_library()
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load_library().bgcn_last_error().decode(errors="replace")
+        raise BGCNError(f"libbgcn error {rc}: {msg}")
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (or 0 for None)."""
+    if t is None:
+        return 0
+    return t.data_ptr()
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)

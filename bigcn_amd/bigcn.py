@@ -1,0 +1,142 @@
+"""BiGCN model classes with the reference's module structure and state_dict.
+
+Mirrors ``model/Twitter/BiGCN_Twitter.py:19-131`` (``TDrumorGCN``, ``BUrumorGCN``,
+``BiGCN``; 4 classes) and ``model/Weibo/BiGCN_Weibo.py:16-89`` (``Net``; 2 classes).
+Attribute names (``conv1``, ``conv2``, ``fc``, ``TDrumorGCN``, ``BUrumorGCN``) and the
+parameter layout are identical, so reference checkpoints load with ``load_state_dict``.
+
+``BiGCN.forward`` runs the fused bidirectional encoder (:func:`bigcn_amd.ops.bigcn_encoder`:
+both directions, conv1 for TD and BU in one pass over ``x``, the root extension /
+relu / dropout generated inside the conv2 GEMM).  ``TDrumorGCN.forward`` /
+``BUrumorGCN.forward`` called on their own follow the reference op sequence with the
+drop-in :class:`GCNConv` and :func:`scatter_mean`.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .conv import GCNConv
+from .ops import Graph, bigcn_encoder, build_graph, scatter_mean
+
+
+def _graphs(data, degree_on: str = "col"):
+    """Build (once per batch object) the TD and BU graphs: gcn_norm + CSR (K1)."""
+    cache = getattr(data, "_bgcn_graphs", None)
+    if cache is not None and cache[0] == degree_on:
+        return cache[1], cache[2]
+    n = data.x.size(0)
+    td = build_graph(data.edge_index, n, degree_on=degree_on)
+    bu = build_graph(data.BU_edge_index, n, degree_on=degree_on)
+    try:
+        data._bgcn_graphs = (degree_on, td, bu)
+    except AttributeError:
+        pass
+    return td, bu
+
+
+def _num_graphs(data) -> int:
+    ng = getattr(data, "num_graphs", None)
+    if ng is None:
+        ng = int(data.batch.max().item()) + 1  # the reference's max(data.batch)+1 (:47)
+    return int(ng)
+
+
+class _RumorGCN(torch.nn.Module):
+    """Shared body of TDrumorGCN (``BiGCN_Twitter.py:19-67``) / BUrumorGCN (``:70-114``)."""
+
+    edge_key = "edge_index"
+
+    def __init__(self, in_feats, hid_feats, out_feats, device=None):
+        super().__init__()
+        self.conv1 = GCNConv(in_feats, hid_feats)
+        self.conv2 = GCNConv(hid_feats + in_feats, out_feats)
+        self.device = device
+
+    def forward(self, data):
+        x = data.x.float()
+        td, bu = _graphs(data)
+        g = td if self.edge_key == "edge_index" else bu
+        batch, rootindex = data.batch, data.rootindex
+        root_of_node = rootindex[batch]                       # :46-50 as one gather
+        h1 = self.conv1(x, g)                                 # :42
+        x2 = h1.detach()                                      # :44 copy.copy -> new leaf
+        h = torch.cat((h1, x.index_select(0, root_of_node)), 1)  # :51
+        h = F.relu(h)                                         # :53
+        h = F.dropout(h, training=self.training)              # :54
+        h = self.conv2(h, g)                                  # :56
+        h = F.relu(h)                                         # :57
+        h = torch.cat((h, x2.index_select(0, root_of_node)), 1)  # :59-63
+        return scatter_mean(h, batch, dim=0, dim_size=_num_graphs(data))  # :65
+
+
+class TDrumorGCN(_RumorGCN):
+    edge_key = "edge_index"
+
+
+class BUrumorGCN(_RumorGCN):
+    edge_key = "BU_edge_index"
+
+
+def _draw_seed() -> int:
+    # host-side draw from torch's default generator: reproducible under torch.manual_seed,
+    # no device sync
+    return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+
+
+class BiGCN(torch.nn.Module):
+    """``BiGCN(in_feats, hid_feats, out_feats, device)`` (``BiGCN_Twitter.py:117-131``)."""
+
+    num_classes = 4
+
+    def __init__(self, in_feats, hid_feats, out_feats, device=None):
+        super().__init__()
+        if hid_feats != 64 or out_feats != 64:
+            raise ValueError("the fused MI355X encoder is specialised for hid = out = 64 "
+                             "(the reference configuration, BiGCN_Twitter.py:144)")
+        self.TDrumorGCN = TDrumorGCN(in_feats, hid_feats, out_feats, device)
+        self.BUrumorGCN = BUrumorGCN(in_feats, hid_feats, out_feats, device)
+        self.fc = torch.nn.Linear((out_feats + hid_feats) * 2, self.num_classes)
+        self.device = device
+        self.keep_words = None  # optional injected dropout draw (tests)
+
+    def encoder_params(self):
+        t, b = self.TDrumorGCN, self.BUrumorGCN
+        return (t.conv1.lin.weight, t.conv1.bias, t.conv2.lin.weight, t.conv2.bias,
+                b.conv1.lin.weight, b.conv1.bias, b.conv2.lin.weight, b.conv2.bias)
+
+    def encode(self, data, seed=None):
+        td, bu = _graphs(data)
+        if seed is None:
+            seed = _draw_seed() if self.training else 0
+        return bigcn_encoder(data.x, data.batch, data.rootindex, td, bu, _num_graphs(data),
+                             self.encoder_params(), training=self.training, seed=seed,
+                             keep_words=self.keep_words)
+
+    def forward(self, data, seed=None):
+        x = self.encode(data, seed)            # cat(BU_x, TD_x)  (:126-128)
+        x = self.fc(x)                         # :129
+        return F.log_softmax(x, dim=1)         # :130
+
+
+class Net(BiGCN):
+    """Weibo head: ``Net(in_feats, hid_feats, out_feats)`` with ``fc(256 -> 2)``
+    (``model/Weibo/BiGCN_Weibo.py:76-89``)."""
+
+    num_classes = 2
+
+    def __init__(self, in_feats, hid_feats, out_feats, device=None):
+        super().__init__(in_feats, hid_feats, out_feats, device)
+
+
+def make_optimizer(model: BiGCN, lr: float = 5e-4, weight_decay: float = 1e-4, fused: bool = False):
+    """Adam with the reference's three groups (``BiGCN_Twitter.py:146-153``)."""
+    bu_ids = {id(p) for p in model.BUrumorGCN.conv1.parameters()}
+    bu_ids |= {id(p) for p in model.BUrumorGCN.conv2.parameters()}
+    base = [p for p in model.parameters() if id(p) not in bu_ids]
+    kw = {"fused": True} if fused else {}
+    return torch.optim.Adam([
+        {"params": base},
+        {"params": list(model.BUrumorGCN.conv1.parameters()), "lr": lr / 5},
+        {"params": list(model.BUrumorGCN.conv2.parameters()), "lr": lr / 5},
+    ], lr=lr, weight_decay=weight_decay, **kw)

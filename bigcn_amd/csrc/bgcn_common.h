@@ -1,0 +1,116 @@
+// Shared device helpers and host-side error plumbing for libbgcn (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/bgcn.h"
+
+namespace bgcn {
+
+// ---------------------------------------------------------------- host errors
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define BGCN_CHECK_ARG(cond, msg)                   \
+  do {                                              \
+    if (!(cond)) return ::bgcn::fail(BGCN_EINVAL, msg); \
+  } while (0)
+
+#define BGCN_CHECK_HIP(expr)                                                           \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return ::bgcn::fail(BGCN_EHIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+#define BGCN_CHECK_LAUNCH() BGCN_CHECK_HIP(hipGetLastError())
+
+inline int propagate(int rc) { return rc; }
+#define BGCN_TRY(expr)           \
+  do {                           \
+    int _rc = (expr);            \
+    if (_rc != BGCN_OK) return _rc; \
+  } while (0)
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Simple bump allocator over a caller-provided workspace.
+struct Carve {
+  char* base;
+  size_t cap;
+  size_t off = 0;
+  Carve(void* b, size_t c) : base(static_cast<char*>(b)), cap(c) {}
+  template <class T>
+  T* take(size_t count) {
+    off = align_up(off, 256);
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += count * sizeof(T);
+    return p;
+  }
+  bool ok() const { return off <= cap; }
+};
+
+// kernel timing hook (bench.py): record HIP events around a launch of a class
+void timing_begin(int cls, hipStream_t s);
+void timing_end(int cls, hipStream_t s);
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- device
+// Dropout keep word for (seed, direction, node, word): 32 keep bits covering
+// columns [32*word, 32*word+32) of the [H + F] concat.  splitmix64 finalizer of a
+// unique 41-bit key; every bit is an independent fair coin (F.dropout p = 0.5).
+__device__ __forceinline__ uint32_t keep_word(uint64_t seed, uint32_t dir, uint32_t node,
+                                              uint32_t word) {
+  uint64_t key = (uint64_t(node) << 9) | (uint64_t(word & 255u) << 1) | uint64_t(dir & 1u);
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (key + 1ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return uint32_t(z >> 32);
+}
+
+// Keep word source used by the fused kernels.
+struct KeepSrc {
+  const uint32_t* words;  // injected [2][N][nw] or nullptr => generated
+  uint64_t seed;
+  int64_t num_nodes;
+  int32_t nw;
+  int32_t training;  // 0 => all kept, scale 1
+  __device__ __forceinline__ uint32_t get(uint32_t dir, uint32_t node, uint32_t w) const {
+    if (!training) return 0xffffffffu;
+    if (words) return words[(size_t(dir) * size_t(num_nodes) + node) * size_t(nw) + w];
+    return keep_word(seed, dir, node, w);
+  }
+  __device__ __forceinline__ float scale() const { return training ? 2.0f : 1.0f; }
+};
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ float4 f4fma(float a, float4 x, float4 acc) {
+  acc.x = fmaf(a, x.x, acc.x);
+  acc.y = fmaf(a, x.y, acc.y);
+  acc.z = fmaf(a, x.z, acc.z);
+  acc.w = fmaf(a, x.w, acc.w);
+  return acc;
+}
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 f4relu(float4 a) {
+  return make_float4(fmaxf(a.x, 0.f), fmaxf(a.y, 0.f), fmaxf(a.z, 0.f), fmaxf(a.w, 0.f));
+}
+
+inline unsigned grid_for(int64_t n, int block) { return unsigned((n + block - 1) / block); }
+
+}  // namespace bgcn

@@ -1,0 +1,444 @@
+// K2 / K10: the dense GEMMs of GCNConv.lin on MFMA (fp32 in, fp32 accumulate).
+//
+// The reference runs lin BEFORE propagate (PyG >= 2.0 GCNConv), so conv1 is the
+// genuine dense (N x 5000) . (5000 x 64) product; its weight gradient is the
+// (64 x N) . (N x 5000) product.  Both directions (TD, BU) read the same X, so the
+// build fuses them: one pass over X against [W1_td ; W1_bu] (128 columns) forward
+// and one pass over X for [dZ1_td | dZ1_bu]^T backward.
+//
+// gfx950 has exact f32-in MFMA (v_mfma_f32_32x32x2_f32, a k-ordered f32 fma chain,
+// 64 FLOP/clk/SIMD = 157 TFLOP/s chip peak).  Tiles are staged global -> VGPR -> LDS
+// (register staging, one LDS double buffer, one barrier per K step; the next tile's
+// global loads are issued before the current tile's MFMAs).
+//
+// MFMA 32x32x2 f32 operand maps (cdna_hip_programming.md section 3): lane l supplies
+// A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31]; D register r of lane l is
+// D[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31].
+#include "bgcn_common.h"
+
+namespace bgcn {
+
+constexpr int BK = 32;
+
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// ============================================================================
+// Y[M, Nc] = X[M, K] . W[Nc, K]^T.   Block tile 64 x 128, 4 waves as 2 x 2,
+// wave tile 32 x 64 (two 32x32 accumulators).  LDS tiles are row-major with a
+// 33-float stride (conflict-free ds_read_b32 for the column-of-rows read).
+// ============================================================================
+// BKM = false: W is [Nc, K] (Y = X W^T, GCNConv.lin forward);
+// BKM = true : W is [K, Nc] (Y = X W, the input gradient dX = dZ W of GCNConv.lin),
+//              staged k-major in LDS.  W1/split are ignored for BKM.
+template <bool VEC, bool BKM>
+__global__ __launch_bounds__(256) void k_gemm_xwt(const float* __restrict__ X, int64_t ldx,
+                                                  const float* __restrict__ W0,
+                                                  const float* __restrict__ W1, int64_t ldw,
+                                                  int64_t split, float* __restrict__ Y,
+                                                  int64_t ldy, int64_t M, int64_t Nc, int64_t K) {
+  constexpr int BM = 64, BN = 128, LS = BK + 1;
+  __shared__ float As[2][BM * LS];
+  __shared__ float Bs[2][BN * LS];  // BKM: [BK][BN] (fits: BK*BN <= BN*LS)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t m0 = int64_t(blockIdx.x) * BM, n0 = int64_t(blockIdx.y) * BN;
+  const int srow = tid >> 3, skq = (tid & 7) * 4;  // staging: row, k offset (float4)
+
+  const float* arow[2];
+  bool aok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int64_t m = m0 + srow + 32 * i;
+    aok[i] = m < M;
+    arow[i] = X + (aok[i] ? m : 0) * ldx;
+  }
+  const float* brow[4];
+  bool bok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int64_t n = n0 + srow + 32 * i;
+    bok[i] = n < Nc;
+    int64_t nn = bok[i] ? n : 0;
+    brow[i] = nn < split ? W0 + nn * ldw : W1 + (nn - split) * ldw;
+  }
+
+  // BKM staging: k = tid/32 + 8 i, n quad (tid%32)*4
+  const int bk_k = tid >> 5, bk_n = (tid & 31) * 4;
+  float4 ra[2], rb[4];
+  auto gload = [&](int64_t k0) {
+    int64_t k = k0 + skq;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (VEC) {
+        ra[i] = (aok[i] && k < K) ? ld4(arow[i] + k) : f4zero();
+      } else {
+        float t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = (aok[i] && k + j < K) ? arow[i][k + j] : 0.f;
+        ra[i] = make_float4(t[0], t[1], t[2], t[3]);
+      }
+    }
+    if constexpr (BKM) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int64_t kk = k0 + bk_k + 8 * i, n = n0 + bk_n;
+        if (VEC) {
+          rb[i] = (kk < K && n < Nc) ? ld4(W0 + kk * ldw + n) : f4zero();
+        } else {
+          float t[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) t[j] = (kk < K && n + j < Nc) ? W0[kk * ldw + n + j] : 0.f;
+          rb[i] = make_float4(t[0], t[1], t[2], t[3]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (VEC) {
+          rb[i] = (bok[i] && k < K) ? ld4(brow[i] + k) : f4zero();
+        } else {
+          float t[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) t[j] = (bok[i] && k + j < K) ? brow[i][k + j] : 0.f;
+          rb[i] = make_float4(t[0], t[1], t[2], t[3]);
+        }
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float* d = &As[buf][(srow + 32 * i) * LS + skq];
+      d[0] = ra[i].x; d[1] = ra[i].y; d[2] = ra[i].z; d[3] = ra[i].w;
+    }
+    if constexpr (BKM) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st4(&Bs[buf][(bk_k + 8 * i) * BN + bk_n], rb[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float* d = &Bs[buf][(srow + 32 * i) * LS + skq];
+        d[0] = rb[i].x; d[1] = rb[i].y; d[2] = rb[i].z; d[3] = rb[i].w;
+      }
+    }
+  };
+
+  f32x16 acc0 = {0}, acc1 = {0};
+  const int h = lane >> 5, r32 = lane & 31;
+  const int nk = int((K + BK - 1) / BK);
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(int64_t(kt + 1) * BK);
+    const float* A = &As[buf][(wr * 32 + r32) * LS + h];
+    if constexpr (BKM) {
+      const float* B0 = &Bs[buf][h * BN + wc * 64 + r32];
+#pragma unroll
+      for (int s = 0; s < BK / 2; ++s) {
+        float a = A[2 * s], b0 = B0[2 * s * BN], b1 = B0[2 * s * BN + 32];
+        acc0 = mfma32x32x2(a, b0, acc0);
+        acc1 = mfma32x32x2(a, b1, acc1);
+      }
+    } else {
+      const float* B0 = &Bs[buf][(wc * 64 + r32) * LS + h];
+      const float* B1 = B0 + 32 * LS;
+#pragma unroll
+      for (int s = 0; s < BK / 2; ++s) {
+        float a = A[2 * s], b0 = B0[2 * s], b1 = B1[2 * s];
+        acc0 = mfma32x32x2(a, b0, acc0);
+        acc1 = mfma32x32x2(a, b1, acc1);
+      }
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    int64_t m = m0 + wr * 32 + acc_row(r, lane);
+    if (m >= M) continue;
+    int64_t n = n0 + wc * 64 + r32;
+    if (n < Nc) Y[m * ldy + n] = acc0[r];
+    if (n + 32 < Nc) Y[m * ldy + n + 32] = acc1[r];
+  }
+}
+
+// ============================================================================
+// Partial C_s[Mc, Nc] = G[Ks, Mc]^T . X[Ks, Nc] over the node chunk Ks of split s.
+// Block tile 128 (Mc) x 64 (Nc), waves 2 x 2 -> wave tile 64 x 32.  Both operands
+// are k-major in memory (rows = nodes) and staged k-major in LDS (no padding: the
+// MFMA read is 32 consecutive floats per half-wave).
+// ============================================================================
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ G, int64_t ldg,
+                                                 const float* __restrict__ X, int64_t ldx,
+                                                 float* __restrict__ part, int64_t Mc, int64_t Nc,
+                                                 int64_t K, int64_t kchunk) {
+  constexpr int BM = 128, BN = 64;
+  __shared__ float Gs[2][BK * BM];
+  __shared__ float Xs[2][BK * BN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t n0 = int64_t(blockIdx.x) * BN, m0 = int64_t(blockIdx.y) * BM;
+  const int64_t kb = int64_t(blockIdx.z) * kchunk;
+  const int64_t ke = min<int64_t>(kb + kchunk, K);
+  float* out = part + int64_t(blockIdx.z) * Mc * Nc;
+
+  // staging maps: G tile 32 nodes x 128 -> 4 float4/thread; X tile 32 x 64 -> 2 float4/thread
+  const int g_node = tid >> 5, g_q = (tid & 31) * 4;
+  const int x_node = tid >> 4, x_q = (tid & 15) * 4;
+  float4 rg[4], rx[2];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t k = k0 + g_node + 8 * i;
+      int64_t m = m0 + g_q;
+      if (VEC) {
+        rg[i] = (k < ke && m < Mc) ? ld4(G + k * ldg + m) : f4zero();
+      } else {
+        float t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = (k < ke && m + j < Mc) ? G[k * ldg + m + j] : 0.f;
+        rg[i] = make_float4(t[0], t[1], t[2], t[3]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int64_t k = k0 + x_node + 16 * i;
+      int64_t n = n0 + x_q;
+      if (VEC) {
+        rx[i] = (k < ke && n < Nc) ? ld4(X + k * ldx + n) : f4zero();
+      } else {
+        float t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = (k < ke && n + j < Nc) ? X[k * ldx + n + j] : 0.f;
+        rx[i] = make_float4(t[0], t[1], t[2], t[3]);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st4(&Gs[buf][(g_node + 8 * i) * BM + g_q], rg[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) st4(&Xs[buf][(x_node + 16 * i) * BN + x_q], rx[i]);
+  };
+
+  f32x16 acc0 = {0}, acc1 = {0};
+  const int h = lane >> 5, r32 = lane & 31;
+  const int nk = int((ke - kb + BK - 1) / BK);
+  if (nk > 0) {
+    gload(kb);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kb + int64_t(kt + 1) * BK);
+    const float* A0 = &Gs[buf][h * BM + wr * 64 + r32];
+    const float* Bp = &Xs[buf][h * BN + wc * 32 + r32];
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      float a0 = A0[2 * s * BM], a1 = A0[2 * s * BM + 32], b = Bp[2 * s * BN];
+      acc0 = mfma32x32x2(a0, b, acc0);
+      acc1 = mfma32x32x2(a1, b, acc1);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    int64_t n = n0 + wc * 32 + r32;
+    if (n >= Nc) continue;
+    int64_t m = m0 + wr * 64 + acc_row(r, lane);
+    if (m < Mc) out[m * Nc + n] = acc0[r];
+    if (m + 32 < Mc) out[(m + 32) * Nc + n] = acc1[r];
+  }
+}
+
+// C[m][n] = sum_s part[s][m][n] (fixed order), rows [0, split) -> C0, the rest -> C1.
+__global__ __launch_bounds__(256) void k_reduce_splits(const float* __restrict__ part, int S,
+                                                       int64_t Mc, int64_t Nc, float* __restrict__ C0,
+                                                       float* __restrict__ C1, int64_t ldc,
+                                                       int64_t split) {
+  int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  int64_t total = Mc * Nc;
+  if (idx >= total) return;
+  float acc = part[idx];
+  for (int s = 1; s < S; ++s) acc += part[int64_t(s) * total + idx];
+  int64_t m = idx / Nc, n = idx % Nc;
+  if (m < split) C0[m * ldc + n] = acc;
+  else C1[(m - split) * ldc + n] = acc;
+}
+
+// ---------------------------------------------------------------- host side
+int tn_splits(int64_t Mc, int64_t Nc, int64_t K) {
+  // aim for ~5 blocks per CU over 256 CUs, never less than 32 nodes per split
+  int64_t tiles = ((Nc + 63) / 64) * ((Mc + 127) / 128);
+  int64_t want = (5 * 256 + tiles - 1) / tiles;
+  int64_t maxs = (K + BK - 1) / BK;
+  int64_t s = want < maxs ? want : maxs;
+  return int(s < 1 ? 1 : (s > 64 ? 64 : s));
+}
+
+size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K) {
+  return size_t(tn_splits(Mc, Nc, K)) * size_t(Mc) * size_t(Nc) * sizeof(float) + 256;
+}
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int gemm_xwt_impl(const float* X, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
+                  int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
+                  hipStream_t stream) {
+  BGCN_CHECK_ARG(X && W0 && Y, "null pointer");
+  BGCN_CHECK_ARG(M >= 0 && Nc > 0 && K > 0, "bad shape");
+  BGCN_CHECK_ARG(ldx >= K && ldw >= K && ldy >= Nc, "bad leading dimension");
+  BGCN_CHECK_ARG(split >= Nc || W1, "W1 required when split < Nc");
+  if (M == 0) return BGCN_OK;
+  bool vec = K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0 && aligned16(X) && aligned16(W0) &&
+             (!W1 || aligned16(W1));
+  dim3 grid(grid_for(M, 64), grid_for(Nc, 128));
+  if (vec)
+    hipLaunchKernelGGL((k_gemm_xwt<true, false>), grid, dim3(256), 0, stream, X, ldx, W0, W1, ldw,
+                       split, Y, ldy, M, Nc, K);
+  else
+    hipLaunchKernelGGL((k_gemm_xwt<false, false>), grid, dim3(256), 0, stream, X, ldx, W0, W1,
+                       ldw, split, Y, ldy, M, Nc, K);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int gemm_xw_impl(const float* X, int64_t ldx, const float* W, int64_t ldw, float* Y, int64_t ldy,
+                 int64_t M, int64_t Nc, int64_t K, hipStream_t stream) {
+  BGCN_CHECK_ARG(X && W && Y, "null pointer");
+  BGCN_CHECK_ARG(M >= 0 && Nc > 0 && K > 0, "bad shape");
+  BGCN_CHECK_ARG(ldx >= K && ldw >= Nc && ldy >= Nc, "bad leading dimension");
+  if (M == 0) return BGCN_OK;
+  bool vec = K % 4 == 0 && Nc % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0 && aligned16(X) &&
+             aligned16(W);
+  dim3 grid(grid_for(M, 64), grid_for(Nc, 128));
+  if (vec)
+    hipLaunchKernelGGL((k_gemm_xwt<true, true>), grid, dim3(256), 0, stream, X, ldx, W,
+                       (const float*)nullptr, ldw, Nc, Y, ldy, M, Nc, K);
+  else
+    hipLaunchKernelGGL((k_gemm_xwt<false, true>), grid, dim3(256), 0, stream, X, ldx, W,
+                       (const float*)nullptr, ldw, Nc, Y, ldy, M, Nc, K);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+// ---------------------------------------------------------------- column sums
+// out[c] = sum_r A[r][c]: bias gradients of the generic GCNConv backward
+// (deterministic two-stage reduction).
+constexpr int kColRows = 256;
+
+__global__ __launch_bounds__(256) void k_colsum_part(const float* __restrict__ A, int64_t lda,
+                                                     int64_t rows, int C,
+                                                     float* __restrict__ part) {
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int64_t r0 = int64_t(blockIdx.x) * kColRows, r1 = min<int64_t>(r0 + kColRows, rows);
+  float acc = 0.f;
+  for (int64_t r = r0; r < r1; ++r) acc += A[r * lda + c];
+  part[int64_t(blockIdx.x) * C + c] = acc;
+}
+
+__global__ void k_colsum_final(const float* __restrict__ part, int P, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float acc = 0.f;
+  for (int p = 0; p < P; ++p) acc += part[int64_t(p) * C + c];
+  out[c] = acc;
+}
+
+size_t colsum_ws_size(int64_t rows, int32_t C) {
+  int64_t P = (rows + kColRows - 1) / kColRows;
+  return size_t(P > 0 ? P : 1) * size_t(C) * sizeof(float) + 256;
+}
+
+int colsum_impl(const float* A, int64_t lda, int64_t rows, int32_t C, float* out, void* ws,
+                size_t ws_bytes, hipStream_t stream) {
+  BGCN_CHECK_ARG(out && C > 0 && rows >= 0 && lda >= C && (rows == 0 || A), "bad arguments");
+  BGCN_CHECK_ARG(ws && ws_bytes >= colsum_ws_size(rows, C), "workspace too small");
+  float* part = static_cast<float*>(ws);
+  int P = int((rows + kColRows - 1) / kColRows);
+  if (P == 0) {
+    BGCN_CHECK_HIP(hipMemsetAsync(out, 0, size_t(C) * sizeof(float), stream));
+    return BGCN_OK;
+  }
+  hipLaunchKernelGGL(k_colsum_part, dim3(unsigned(P), unsigned((C + 255) / 256)), dim3(256), 0,
+                     stream, A, lda, rows, C, part);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_colsum_final, dim3(grid_for(C, 256)), dim3(256), 0, stream, part, P, C,
+                     out);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float* C0, float* C1,
+                 int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
+                 size_t ws_bytes, hipStream_t stream) {
+  BGCN_CHECK_ARG(G && X && C0, "null pointer");
+  BGCN_CHECK_ARG(Mc > 0 && Nc > 0 && K >= 0, "bad shape");
+  BGCN_CHECK_ARG(ldg >= Mc && ldx >= Nc && ldc >= Nc, "bad leading dimension");
+  BGCN_CHECK_ARG(split >= Mc || C1, "C1 required when split < Mc");
+  BGCN_CHECK_ARG(ws && ws_bytes >= tn_ws_size(Mc, Nc, K), "workspace too small");
+  int S = tn_splits(Mc, Nc, K);
+  int64_t kchunk = (K + S - 1) / S;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  if (kchunk == 0) kchunk = BK;
+  S = int((K + kchunk - 1) / kchunk);
+  if (S < 1) S = 1;
+  float* part = static_cast<float*>(ws);
+  bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) &&
+             aligned16(X);
+  dim3 grid(grid_for(Nc, 64), grid_for(Mc, 128), S);
+  if (vec)
+    hipLaunchKernelGGL(k_gemm_tn<true>, grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc, Nc,
+                       K, kchunk);
+  else
+    hipLaunchKernelGGL(k_gemm_tn<false>, grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc, Nc,
+                       K, kchunk);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_reduce_splits, dim3(grid_for(Mc * Nc, 256)), dim3(256), 0, stream, part, S,
+                     Mc, Nc, C0, C1, ldc, split);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+}  // namespace bgcn
+
+extern "C" int bgcn_gemm_xwt(const float* X, int64_t ldx, const float* W0, const float* W1,
+                             int64_t ldw, int64_t split, float* Y, int64_t ldy, int64_t M,
+                             int64_t Nc, int64_t K, bgcn_stream_t stream) {
+  return bgcn::gemm_xwt_impl(X, ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K,
+                             reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int bgcn_gemm_xw(const float* X, int64_t ldx, const float* W, int64_t ldw, float* Y,
+                            int64_t ldy, int64_t M, int64_t Nc, int64_t K, bgcn_stream_t stream) {
+  return bgcn::gemm_xw_impl(X, ldx, W, ldw, Y, ldy, M, Nc, K,
+                            reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t bgcn_colsum_workspace_size(int64_t rows, int32_t C) {
+  return bgcn::colsum_ws_size(rows, C);
+}
+
+extern "C" int bgcn_colsum(const float* A, int64_t lda, int64_t rows, int32_t C, float* out,
+                           void* workspace, size_t workspace_bytes, bgcn_stream_t stream) {
+  return bgcn::colsum_impl(A, lda, rows, C, out, workspace, workspace_bytes,
+                           reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t bgcn_gemm_tn_workspace_size(int64_t Mc, int64_t Nc, int64_t K) {
+  return bgcn::tn_ws_size(Mc, Nc, K);
+}
+
+extern "C" int bgcn_gemm_tn(const float* G, int64_t ldg, const float* X, int64_t ldx, float* C0,
+                            float* C1, int64_t ldc, int64_t split, int64_t Mc, int64_t Nc,
+                            int64_t K, void* workspace, size_t workspace_bytes,
+                            bgcn_stream_t stream) {
+  return bgcn::gemm_tn_impl(G, ldg, X, ldx, C0, C1, ldc, split, Mc, Nc, K, workspace,
+                            workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+}

@@ -1,0 +1,87 @@
+// Host runtime of libbgcn: thread-local error string, ABI version, and the
+// kernel-timing hook bench.py uses to measure the dominant kernel with HIP events
+// on the stream it is launched on.
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "bgcn_common.h"
+
+namespace bgcn {
+
+namespace {
+thread_local std::string g_err;
+
+struct TimingState {
+  bool enabled = false;
+  struct Pair { hipEvent_t a, b; };
+  std::vector<Pair> pending[4];
+  hipEvent_t open[4] = {nullptr, nullptr, nullptr, nullptr};
+  double total_ms[4] = {0, 0, 0, 0};
+  int64_t count[4] = {0, 0, 0, 0};
+};
+thread_local TimingState g_tm;
+}  // namespace
+
+void set_error(const std::string& msg) { g_err = msg; }
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+void timing_begin(int cls, hipStream_t s) {
+  if (!g_tm.enabled || cls < 0 || cls > 3) return;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  (void)hipEventRecord(e, s);
+  g_tm.open[cls] = e;
+}
+
+void timing_end(int cls, hipStream_t s) {
+  if (!g_tm.enabled || cls < 0 || cls > 3 || !g_tm.open[cls]) return;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  (void)hipEventRecord(e, s);
+  g_tm.pending[cls].push_back({g_tm.open[cls], e});
+  g_tm.open[cls] = nullptr;
+}
+
+}  // namespace bgcn
+
+extern "C" int bgcn_abi_version(void) { return BGCN_ABI_VERSION; }
+
+extern "C" const char* bgcn_last_error(void) { return bgcn::g_err.c_str(); }
+
+extern "C" int bgcn_set_kernel_timing(int enable) {
+  auto& t = bgcn::g_tm;
+  t.enabled = enable != 0;
+  for (int c = 0; c < 4; ++c) {
+    t.total_ms[c] = 0;
+    t.count[c] = 0;
+  }
+  return BGCN_OK;
+}
+
+// Synchronises on the recorded events (call outside the timed region).
+extern "C" int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* launches) {
+  auto& t = bgcn::g_tm;
+  if (kernel_class < 0 || kernel_class > 3) return bgcn::fail(BGCN_EINVAL, "bad kernel class");
+  auto& v = t.pending[kernel_class];
+  for (auto& p : v) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) != hipSuccess) return bgcn::fail(BGCN_EHIP, "event sync failed");
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      t.total_ms[kernel_class] += ms;
+      t.count[kernel_class] += 1;
+    }
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  v.clear();
+  if (total_ms) *total_ms = float(t.total_ms[kernel_class]);
+  if (launches) *launches = t.count[kernel_class];
+  return BGCN_OK;
+}

@@ -1,0 +1,340 @@
+"""Autograd operators over the HIP kernels of libbgcn (the hot path of BiGCN).
+
+* :class:`Graph` / :func:`build_graph` - ``gcn_norm`` + ``add_remaining_self_loops`` +
+  CSR (K1), built once per batch and direction, shared by conv1/conv2 forward and
+  backward (the reference recomputes it 4x per step, ``cached=False``).
+* :func:`gcn_conv` - PyG-2.x ``GCNConv.forward`` (lin -> propagate -> +bias) with a
+  HIP backward (K2, K3, K4, K10).
+* :func:`scatter_mean` - ``torch_scatter.scatter_mean`` (K8).
+* :func:`bigcn_encoder` - the fused TD+BU encoder of ``BiGCN.forward``
+  (``model/Twitter/BiGCN_Twitter.py:125-128``), all of K1-K10 on the GPU.
+
+Every function runs on the caller's current HIP stream and never falls back to a
+CPU or PyTorch implementation.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import BiGCNArgs, GraphView, check, ptr, stream_handle, workspace
+
+HID = 64
+
+
+def _dev_check(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.BGCNError("bigcn_amd ops take device tensors (no CPU path)")
+
+
+# ----------------------------------------------------------------------------- K1
+class Graph:
+    """Normalised adjacency of one direction in both CSR orientations.
+
+    ``t_*`` rows are targets (forward aggregation, ``out[i] = sum norm * h[src]``),
+    ``s_*`` rows are sources (the transposed product of the backward pass)."""
+
+    __slots__ = ("num_nodes", "num_edges", "capacity", "t_ptr", "t_row", "t_col", "t_w",
+                 "s_ptr", "s_row", "s_col", "s_w", "status", "_view")
+
+    def view(self) -> GraphView:
+        v = GraphView()
+        v.t_ptr, v.t_row, v.t_col, v.t_w = ptr(self.t_ptr), ptr(self.t_row), ptr(self.t_col), ptr(self.t_w)
+        v.s_ptr, v.s_row, v.s_col, v.s_w = ptr(self.s_ptr), ptr(self.s_row), ptr(self.s_col), ptr(self.s_w)
+        v.capacity = self.capacity
+        return v
+
+    def check(self) -> None:
+        """Host sync: raise IndexError if edge_index held an index outside [0, N)."""
+        if int(self.status.item()) != 0:
+            raise IndexError("edge_index contains an index out of range [0, num_nodes)")
+
+
+def build_graph(edge_index: torch.Tensor, num_nodes: int, edge_weight: Optional[torch.Tensor] = None,
+                degree_on: str = "col", validate: bool = False) -> Graph:
+    _dev_check(edge_index, edge_weight)
+    if edge_index.dim() != 2 or edge_index.size(0) != 2:
+        raise ValueError("edge_index must be [2, E]")
+    ei = edge_index.to(torch.int64).contiguous()
+    ew = None if edge_weight is None else edge_weight.to(torch.float32).contiguous()
+    E, N = int(ei.size(1)), int(num_nodes)
+    dev = ei.device
+    cap = E + N
+    g = Graph()
+    g.num_nodes, g.num_edges, g.capacity = N, E, cap
+    i32 = dict(dtype=torch.int32, device=dev)
+    f32 = dict(dtype=torch.float32, device=dev)
+    g.t_ptr, g.s_ptr = torch.empty(N + 1, **i32), torch.empty(N + 1, **i32)
+    g.t_row, g.t_col, g.t_w = torch.empty(cap, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32)
+    g.s_row, g.s_col, g.s_w = torch.empty(cap, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32)
+    g.status = torch.zeros(1, **i32)
+    L = _lib.lib()
+    ws = workspace(L.bgcn_graph_workspace_size(E, N), dev)
+    check(L.bgcn_build_graph(ptr(ei), ptr(ew), E, N, 0 if degree_on == "col" else 1,
+                             ptr(g.t_ptr), ptr(g.t_row), ptr(g.t_col), ptr(g.t_w),
+                             ptr(g.s_ptr), ptr(g.s_row), ptr(g.s_col), ptr(g.s_w),
+                             ptr(g.status), ptr(ws), ws.numel(), stream_handle()))
+    if validate:
+        g.check()
+    return g
+
+
+# ----------------------------------------------------------------------------- K3/K4
+def spmm(g: Graph, x: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
+         transposed: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``out = A_hat x (+bias)`` (or ``A_hat^T x``); x [N, F] fp32 with F % 4 == 0."""
+    _dev_check(x, bias)
+    N, F = x.shape
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    if out is None:
+        out = torch.empty(N, F, dtype=torch.float32, device=x.device)
+    L = _lib.lib()
+    ws = workspace(L.bgcn_spmm_workspace_size(g.capacity, F), x.device)
+    p = (g.s_ptr, g.s_row, g.s_col, g.s_w) if transposed else (g.t_ptr, g.t_row, g.t_col, g.t_w)
+    check(L.bgcn_spmm(ptr(p[0]), ptr(p[1]), ptr(p[2]), ptr(p[3]), N, g.capacity, ptr(x), x.stride(0),
+                      ptr(out), out.stride(0), F, ptr(bias), 1 if relu else 0, ptr(ws), ws.numel(),
+                      stream_handle()))
+    return out
+
+
+def _pad4(t: torch.Tensor) -> torch.Tensor:
+    """Zero-pad the last dim to a multiple of 4 (spmm works on float4 rows)."""
+    F = t.size(-1)
+    if F % 4 == 0:
+        return t.contiguous()
+    return torch.nn.functional.pad(t, (0, 4 - F % 4)).contiguous()
+
+
+def _linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x [N, K] . w[O, K]^T on MFMA."""
+    N, K = x.shape
+    O = w.size(0)
+    y = torch.empty(N, O, dtype=torch.float32, device=x.device)
+    check(_lib.lib().bgcn_gemm_xwt(ptr(x), x.stride(0), ptr(w), 0, w.stride(0), O, ptr(y), O, N, O, K,
+                                   stream_handle()))
+    return y
+
+
+class _GCNConvFn(torch.autograd.Function):
+    """PyG-2.x GCNConv: out = A_hat (x W^T) + b."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, g: Graph):
+        x = x.contiguous().float()
+        weight = weight.contiguous()
+        z = _pad4(_linear(x, weight))
+        O = weight.size(0)
+        b = None if bias is None else _pad4(bias.view(1, -1)).view(-1)
+        out = spmm(g, z, b)[:, :O]
+        ctx.g = g
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return out.contiguous()
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, weight = ctx.saved_tensors
+        g: Graph = ctx.g
+        L = _lib.lib()
+        N, K = x.shape
+        O = weight.size(0)
+        d = _pad4(dout.float())
+        dz = spmm(g, d, transposed=True)[:, :O].contiguous()   # A_hat^T dout
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(N, K, dtype=torch.float32, device=x.device)
+            check(L.bgcn_gemm_xw(ptr(dz), dz.stride(0), ptr(weight), weight.stride(0), ptr(dx), K,
+                                 N, K, O, stream_handle()))
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty(O, K, dtype=torch.float32, device=x.device)
+            ws = workspace(L.bgcn_gemm_tn_workspace_size(O, K, N), x.device)
+            check(L.bgcn_gemm_tn(ptr(dz), dz.stride(0), ptr(x), x.stride(0), ptr(dw), 0, K, O, O, K,
+                                 N, ptr(ws), ws.numel(), stream_handle()))
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.empty(O, dtype=torch.float32, device=x.device)
+            dd = dout.float().contiguous()
+            ws = workspace(L.bgcn_colsum_workspace_size(N, O), x.device)
+            check(L.bgcn_colsum(ptr(dd), dd.stride(0), N, O, ptr(db), ptr(ws), ws.numel(),
+                                stream_handle()))
+        return dx, dw, db, None
+
+
+def gcn_conv(x: torch.Tensor, edge_index_or_graph, weight: torch.Tensor,
+             bias: Optional[torch.Tensor] = None, edge_weight: Optional[torch.Tensor] = None,
+             degree_on: str = "col") -> torch.Tensor:
+    _dev_check(x, weight, bias)
+    g = edge_index_or_graph
+    if not isinstance(g, Graph):
+        g = build_graph(g, x.size(0), edge_weight, degree_on)
+    return _GCNConvFn.apply(x, weight, bias, g)
+
+
+# ----------------------------------------------------------------------------- K8
+class _ScatterMeanFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, index, B):
+        src = src.contiguous().float()
+        n, C = src.shape
+        out = torch.empty(B, C, dtype=torch.float32, device=src.device)
+        cnt = torch.empty(B, dtype=torch.float32, device=src.device)
+        status = torch.zeros(1, dtype=torch.int32, device=src.device)
+        L = _lib.lib()
+        ws = workspace(L.bgcn_scatter_mean_workspace_size(B), src.device)
+        check(L.bgcn_scatter_mean_fwd(ptr(src), src.stride(0), ptr(index), n, C, B, ptr(out), C,
+                                      ptr(cnt), ptr(status), ptr(ws), ws.numel(), stream_handle()))
+        ctx.save_for_backward(index, cnt)
+        ctx.shape = (n, C, B)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        index, cnt = ctx.saved_tensors
+        n, C, B = ctx.shape
+        dout = dout.contiguous().float()
+        dsrc = torch.empty(n, C, dtype=torch.float32, device=dout.device)
+        check(_lib.lib().bgcn_scatter_mean_bwd(ptr(dout), dout.stride(0), ptr(index), ptr(cnt), n, C, B,
+                                               ptr(dsrc), C, stream_handle()))
+        return dsrc, None, None
+
+
+def scatter_mean(src: torch.Tensor, index: torch.Tensor, dim: int = 0, out=None,
+                 dim_size: Optional[int] = None) -> torch.Tensor:
+    """``torch_scatter.scatter_mean(src, index, dim=0)`` on the GPU.  Like torch_scatter,
+    ``dim_size=None`` means ``index.max() + 1`` (a host sync, as in the reference)."""
+    if dim not in (0, -src.dim()):
+        raise NotImplementedError("scatter_mean: only dim=0 is on the BiGCN path")
+    _dev_check(src, index)
+    index = index.to(torch.int64).contiguous()
+    if dim_size is None:
+        dim_size = int(index.max().item()) + 1 if index.numel() else 0
+    if dim_size == 0:
+        return src.new_zeros((0,) + tuple(src.shape[1:]))
+    shp = src.shape
+    res = _ScatterMeanFn.apply(src.reshape(shp[0], -1), index, int(dim_size))
+    res = res.view((int(dim_size),) + tuple(shp[1:]))
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+# ----------------------------------------------------------------------------- fused encoder
+_PARAM_ORDER = ("td_w1", "td_b1", "td_w2", "td_b2", "bu_w1", "bu_b1", "bu_w2", "bu_b2")
+
+
+class _BiGCNEncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training, seed, keep_words,
+                *params):
+        x = x.contiguous().float()
+        N, F = x.shape
+        dev = x.device
+        L = _lib.lib()
+        a = BiGCNArgs()
+        a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats, a.hid = ptr(x), x.stride(0), N, B, F, HID
+        a.batch, a.rootindex = ptr(batch), ptr(rootindex)
+        a.td, a.bu = td.view(), bu.view()
+        for name, p in zip(_PARAM_ORDER, params):
+            setattr(a, name, ptr(p))
+        a.training, a.seed = int(bool(training)), int(seed) & (2**64 - 1)
+        a.keep_words = ptr(keep_words)
+        tree_ptr = torch.empty(B + 1, dtype=torch.int32, device=dev)
+        h1 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
+        h2 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
+        head = torch.empty(B, 4 * HID, dtype=torch.float32, device=dev)
+        a.tree_ptr, a.h1, a.h2, a.head_in = ptr(tree_ptr), ptr(h1), ptr(h2), ptr(head)
+        ws = workspace(L.bgcn_bigcn_workspace_size(N, B, F, HID), dev)
+        check(L.bgcn_bigcn_forward(ctypes.byref(a), ptr(ws), ws.numel(), stream_handle()))
+        ctx.graphs = (td, bu)
+        ctx.meta = (B, training, seed)
+        ctx.save_for_backward(x, batch, rootindex, keep_words if keep_words is not None else x.new_empty(0),
+                              tree_ptr, h1, h2, *params)
+        ctx.has_keep = keep_words is not None
+        return head
+
+    @staticmethod
+    def backward(ctx, dhead):
+        x, batch, rootindex, keep, tree_ptr, h1, h2, *params = ctx.saved_tensors
+        td, bu = ctx.graphs
+        B, training, seed = ctx.meta
+        N, F = x.shape
+        dev = x.device
+        L = _lib.lib()
+        dhead = dhead.contiguous().float()
+        a = BiGCNArgs()
+        a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats, a.hid = ptr(x), x.stride(0), N, B, F, HID
+        a.batch, a.rootindex = ptr(batch), ptr(rootindex)
+        a.td, a.bu = td.view(), bu.view()
+        for name, p in zip(_PARAM_ORDER, params):
+            setattr(a, name, ptr(p))
+        a.training, a.seed = int(bool(training)), int(seed) & (2**64 - 1)
+        a.keep_words = ptr(keep) if ctx.has_keep else 0
+        a.tree_ptr, a.h1, a.h2, a.dhead_in = ptr(tree_ptr), ptr(h1), ptr(h2), ptr(dhead)
+        grads = [torch.empty_like(p) for p in params]
+        for name, gt in zip(_PARAM_ORDER, grads):
+            setattr(a, name.replace("_w", "_dw").replace("_b", "_db"), ptr(gt))
+        ws = workspace(L.bgcn_bigcn_workspace_size(N, B, F, HID), dev)
+        check(L.bgcn_bigcn_backward(ctypes.byref(a), ptr(ws), ws.numel(), stream_handle()))
+        return (None,) * 9 + tuple(grads)
+
+
+def bigcn_encoder(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, td: Graph, bu: Graph,
+                  num_graphs: int, params, training: bool = False, seed: int = 0,
+                  keep_words: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cat(BU_x, TD_x) [B, 256] of ``BiGCN.forward`` (``BiGCN_Twitter.py:126-128``).
+
+    ``params`` = (td_w1, td_b1, td_w2, td_b2, bu_w1, bu_b1, bu_w2, bu_b2) in the
+    reference layout (``convN.lin.weight [out, in]``, ``convN.bias``).  ``keep_words``
+    optionally injects the dropout draw as packed bits [2, N, ceil((64+F)/32)] int32."""
+    _dev_check(x, batch, rootindex, keep_words, *params)
+    for p in params:
+        if p.dtype != torch.float32 or not p.is_contiguous():
+            raise ValueError("parameters must be contiguous fp32")
+    if keep_words is not None:
+        keep_words = keep_words.contiguous()
+    return _BiGCNEncoderFn.apply(x, batch.to(torch.int64).contiguous(), rootindex.to(torch.int64).contiguous(),
+                                 td, bu, int(num_graphs), bool(training), int(seed), keep_words, *params)
+
+
+def keep_words(seed: int, num_nodes: int, in_feats: int, device) -> torch.Tensor:
+    """Materialise the in-kernel dropout keep bits [2, N, nw] (int32 view of uint32)."""
+    nw = (HID + in_feats + 31) // 32
+    w = torch.empty(2, num_nodes, nw, dtype=torch.int32, device=device)
+    check(_lib.lib().bgcn_keep_words(int(seed) & (2**64 - 1), num_nodes, nw, ptr(w), stream_handle()))
+    return w
+
+
+def unpack_keep(words: torch.Tensor, width: int) -> torch.Tensor:
+    """[..., nw] packed keep words -> [..., width] bool (bit j of word w = column 32w+j)."""
+    w = words.to(torch.int64) & 0xFFFFFFFF
+    bits = torch.arange(32, device=w.device, dtype=torch.int64)
+    m = ((w.unsqueeze(-1) >> bits) & 1).bool()
+    return m.reshape(*words.shape[:-1], -1)[..., :width]
+
+
+def pack_keep(mask: torch.Tensor) -> torch.Tensor:
+    """[..., width] bool -> [..., ceil(width/32)] int32 words."""
+    width = mask.size(-1)
+    nw = (width + 31) // 32
+    pad = nw * 32 - width
+    m = torch.nn.functional.pad(mask.to(torch.int64), (0, pad)).reshape(*mask.shape[:-1], nw, 32)
+    w = (m << torch.arange(32, dtype=torch.int64, device=mask.device)).sum(-1)
+    w = torch.where(w >= 2**31, w - 2**32, w)
+    return w.to(torch.int32)
+
+
+def set_kernel_timing(enable: bool) -> None:
+    check(_lib.lib().bgcn_set_kernel_timing(1 if enable else 0))
+
+
+def kernel_timing(kernel_class: int):
+    """(total_ms, launches) of a kernel class since set_kernel_timing(True) (syncs)."""
+    ms = ctypes.c_float(0.0)
+    n = ctypes.c_int64(0)
+    check(_lib.lib().bgcn_kernel_timing(kernel_class, ctypes.byref(ms), ctypes.byref(n)))
+    return float(ms.value), int(n.value)

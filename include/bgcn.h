@@ -1,0 +1,213 @@
+/*
+ * bgcn.h - C ABI of the MI355X (gfx950) BiGCN message-passing path.
+ *
+ * This is the drop-in boundary of the build.  The reference reaches the hot path
+ * through module-level Python symbols of third-party packages (no plugin system):
+ *
+ *   from torch_geometric.nn import GCNConv      model/Twitter/BiGCN_Twitter.py:15
+ *                                               model/Weibo/BiGCN_Weibo.py:13
+ *   from torch_scatter import scatter_mean      model/Twitter/BiGCN_Twitter.py:6
+ *                                               model/Weibo/BiGCN_Weibo.py:5
+ *
+ * called from TDrumorGCN/BUrumorGCN.forward (BiGCN_Twitter.py:42,56,65,92,105,113).
+ * Each entry point below names the reference operation it replaces.  The Python
+ * mirror (bigcn_amd/) binds these with ctypes; INTEGRATION.md shows the binding a
+ * maintainer of the reference would add.
+ *
+ * Conventions (all entry points):
+ *   - every tensor pointer is a DEVICE pointer owned by the caller; the library
+ *     never allocates or frees caller memory.  Scratch comes from a caller-provided
+ *     workspace whose size is returned by the matching *_workspace_size() call;
+ *   - every call is asynchronous on the given stream, performs no host sync and is
+ *     re-entrant (no global mutable state besides the thread-local error string);
+ *   - return value: 0 = ok, BGCN_EINVAL (-1) = invalid argument / shape,
+ *     BGCN_EHIP (-2) = HIP launch error.  bgcn_last_error() gives a thread-local
+ *     message.  Data-dependent errors (an edge index outside [0, N)) cannot be
+ *     reported synchronously: the offending edge is skipped and *status is set to 1
+ *     on the device (the Python layer raises IndexError, like index_select would).
+ *   - fp32 everywhere (the reference's dtype); rows are row-major with a leading
+ *     dimension ("ld", in elements).
+ */
+#ifndef BGCN_H_
+#define BGCN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
+
+#define BGCN_OK 0
+#define BGCN_EINVAL (-1)
+#define BGCN_EHIP (-2)
+
+#define BGCN_ABI_VERSION 1
+
+/* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
+ * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
+#define BGCN_DEGREE_ON_COL 0
+#define BGCN_DEGREE_ON_ROW 1
+
+/* epilogue flags of bgcn_spmm */
+#define BGCN_EPI_NONE 0
+#define BGCN_EPI_RELU 1
+
+int bgcn_abi_version(void);
+const char* bgcn_last_error(void);
+
+/* --------------------------------------------------------------------------
+ * K1  gcn_norm + add_remaining_self_loops + propagate's index preparation.
+ * Replaces: torch_geometric GCNConv.forward -> gcn_norm (explicit call form at
+ * explain_PHEME.py:62-63), invoked by every GCNConv call of BiGCN_Twitter.py:42,56,92,105.
+ *
+ * edge_index: int64 [2, E] (row 0 = source, row 1 = target), PyG layout.
+ * edge_weight: optional fp32 [E] (NULL = all ones; EBGCN's variant, EBGCN.py:84).
+ * Existing self loops are dropped and one loop (i,i) of weight 1 is appended per node.
+ * Outputs two CSR views of the normalised adjacency (capacity E + N entries each):
+ *   by target  (forward aggregation): t_ptr[N+1], t_row[], t_col[] = source, t_w[]
+ *   by source  (backward, A^T)      : s_ptr[N+1], s_row[], s_col[] = target, s_w[]
+ * Entries of a row keep edge order with the self loop last, which is the summation
+ * order of PyG's scatter-add.  *_row holds the row id of each entry (COO form).
+ * The number of valid entries is t_ptr[N] (= s_ptr[N]), on the device.
+ * -------------------------------------------------------------------------- */
+size_t bgcn_graph_workspace_size(int64_t num_edges, int64_t num_nodes);
+int bgcn_build_graph(const int64_t* edge_index, const float* edge_weight, int64_t num_edges,
+                     int64_t num_nodes, int degree_on,
+                     int32_t* t_ptr, int32_t* t_row, int32_t* t_col, float* t_w,
+                     int32_t* s_ptr, int32_t* s_row, int32_t* s_col, float* s_w,
+                     int32_t* status, void* workspace, size_t workspace_bytes,
+                     bgcn_stream_t stream);
+
+/* --------------------------------------------------------------------------
+ * K3/K4  MessagePassing.propagate(aggr='add') with message norm * x_j, + bias.
+ * Replaces: the gather x[row] * norm + scatter_add to col inside GCNConv
+ * (forward, CSR by target) and its autograd backward (CSR by source).
+ * out[r, :F] = epi( sum_{p in row r} w[p] * in[col[p], :F]  (+ bias) )
+ * Atomic-free and deterministic: the nnz range is split evenly over lane groups
+ * (merge path) and rows that cross a split are combined in a fixed order.
+ * `capacity` = allocated entries (E + N); the valid count is read from ptr[rows].
+ * -------------------------------------------------------------------------- */
+size_t bgcn_spmm_workspace_size(int64_t capacity, int32_t F);
+int bgcn_spmm(const int32_t* ptr, const int32_t* row, const int32_t* col, const float* w,
+              int64_t rows, int64_t capacity, const float* in, int64_t ld_in, float* out,
+              int64_t ld_out, int32_t F, const float* bias, int epilogue,
+              void* workspace, size_t workspace_bytes, bgcn_stream_t stream);
+
+/* --------------------------------------------------------------------------
+ * K2  GCNConv.lin: Y[M, Nc] = X[M, K] * W[Nc, K]^T  (fp32 in, fp32 MFMA accumulate).
+ * Replaces: torch.nn.functional.linear / aten mm inside GCNConv (lin before propagate).
+ * W rows [0, split) come from W0, rows [split, Nc) from W1 (lets TD and BU conv1
+ * share one pass over X: Nc = 128, split = 64).  W1 may be NULL if split >= Nc.
+ * -------------------------------------------------------------------------- */
+int bgcn_gemm_xwt(const float* X, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
+                  int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
+                  bgcn_stream_t stream);
+
+/* Input gradient of GCNConv.lin: Y[M, Nc] = X[M, K] * W[K, Nc]  (dX = dZ * W).
+ * Replaces: the autograd backward of F.linear w.r.t. its input inside GCNConv. */
+int bgcn_gemm_xw(const float* X, int64_t ldx, const float* W, int64_t ldw, float* Y, int64_t ldy,
+                 int64_t M, int64_t Nc, int64_t K, bgcn_stream_t stream);
+
+/* Column sums out[c] = sum_r A[r, c] (bias gradient of GCNConv; deterministic). */
+size_t bgcn_colsum_workspace_size(int64_t rows, int32_t C);
+int bgcn_colsum(const float* A, int64_t lda, int64_t rows, int32_t C, float* out,
+                void* workspace, size_t workspace_bytes, bgcn_stream_t stream);
+
+/* --------------------------------------------------------------------------
+ * K10  weight gradient of GCNConv.lin: C[Mc, Nc] = G[K, Mc]^T * X[K, Nc]
+ * (reduction over the K = node dimension, split over node chunks with partial
+ * slabs in the workspace and a fixed-order reduction: deterministic).
+ * Output rows [0, split) go to C0 (ld ldc), rows [split, Mc) to C1.
+ * -------------------------------------------------------------------------- */
+size_t bgcn_gemm_tn_workspace_size(int64_t Mc, int64_t Nc, int64_t K);
+int bgcn_gemm_tn(const float* G, int64_t ldg, const float* X, int64_t ldx, float* C0, float* C1,
+                 int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K,
+                 void* workspace, size_t workspace_bytes, bgcn_stream_t stream);
+
+/* --------------------------------------------------------------------------
+ * K8  torch_scatter.scatter_mean(src, index, dim=0, dim_size=B)  (fwd and bwd).
+ * Replaces: scatter_mean at BiGCN_Twitter.py:65,113 / BiGCN_Weibo.py:43,73.
+ * index: int64 [n] (any order; values outside [0,B) are ignored and flag *status).
+ * count[B] receives max(count, 1) as fp32 (saved for backward).  A sorted index
+ * (PyG's batch vector) takes a deterministic segmented path, any other order a
+ * float-atomic path; the choice is made on the device (no host sync).
+ * -------------------------------------------------------------------------- */
+size_t bgcn_scatter_mean_workspace_size(int64_t B);
+int bgcn_scatter_mean_fwd(const float* src, int64_t ld_src, const int64_t* index, int64_t n,
+                          int32_t C, int64_t B, float* out, int64_t ld_out, float* count,
+                          int32_t* status, void* workspace, size_t workspace_bytes,
+                          bgcn_stream_t stream);
+int bgcn_scatter_mean_bwd(const float* dout, int64_t ld_dout, const int64_t* index,
+                          const float* count, int64_t n, int32_t C, int64_t B, float* dsrc,
+                          int64_t ld_dsrc, bgcn_stream_t stream);
+
+/* --------------------------------------------------------------------------
+ * Fused bidirectional BiGCN encoder: TDrumorGCN + BUrumorGCN forward/backward
+ * (BiGCN_Twitter.py:26-67 and :77-114, Weibo :22-44 / :52-74), producing the
+ * head input cat(BU_x, TD_x) [B, 256] of BiGCN.forward (:126-128).
+ * The fc / log_softmax / nll head (:129-130, :184) stays in PyTorch.
+ *
+ * Internal layout: per-node matrices are [N, 2*H] with TD in columns [0, H) and
+ * BU in [H, 2H).  Dropout (F.dropout p = 0.5 over the [N, H+F] concat, :54) keep
+ * bits are either generated in-kernel from (seed, direction, node, word) or read
+ * from an injected bitmask keep_words[2][N][nw], nw = ceil((H+F)/32),
+ * bit j of word w = column 32w + j; set bit = keep (x2).
+ * -------------------------------------------------------------------------- */
+typedef struct bgcn_graph_view {
+  const int32_t* t_ptr; const int32_t* t_row; const int32_t* t_col; const float* t_w;
+  const int32_t* s_ptr; const int32_t* s_row; const int32_t* s_col; const float* s_w;
+  int64_t capacity; /* E + N */
+} bgcn_graph_view;
+
+typedef struct bgcn_bigcn_args {
+  /* batch */
+  const float* x; int64_t ldx;   /* [N, F] node features (data.x)          */
+  int64_t num_nodes;             /* N                                       */
+  int64_t num_graphs;            /* B                                       */
+  int64_t in_feats;              /* F (5000 Twitter/Weibo BoW)              */
+  int64_t hid;                   /* H = out_feats = 64                      */
+  const int64_t* batch;          /* [N] sorted tree id per node             */
+  const int64_t* rootindex;      /* [B] GLOBAL root node ids (PyG collate)  */
+  bgcn_graph_view td, bu;        /* graphs of edge_index / BU_edge_index    */
+  /* parameters, reference state_dict layout */
+  const float* td_w1; const float* td_b1; const float* td_w2; const float* td_b2;
+  const float* bu_w1; const float* bu_b1; const float* bu_w2; const float* bu_b2;
+  /* dropout */
+  int training; uint64_t seed; const uint32_t* keep_words; /* NULL = generate */
+  /* saved activations (caller-owned, kept for backward) */
+  int32_t* tree_ptr;             /* [B+1]                                   */
+  float* h1;                     /* [N, 2H] conv1 outputs (pre-relu)        */
+  float* h2;                     /* [N, 2H] conv2 outputs (pre-relu)        */
+  /* forward output */
+  float* head_in;                /* [B, 4H] = cat(BU_x, TD_x)              */
+  /* backward input / outputs */
+  const float* dhead_in;         /* [B, 4H]                                 */
+  float* td_dw1; float* td_db1; float* td_dw2; float* td_db2;
+  float* bu_dw1; float* bu_db1; float* bu_dw2; float* bu_db2;
+} bgcn_bigcn_args;
+
+size_t bgcn_bigcn_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,
+                                 int64_t hid);
+int bgcn_bigcn_forward(const bgcn_bigcn_args* args, void* workspace, size_t workspace_bytes,
+                       bgcn_stream_t stream);
+int bgcn_bigcn_backward(const bgcn_bigcn_args* args, void* workspace, size_t workspace_bytes,
+                        bgcn_stream_t stream);
+
+/* Materialise the in-kernel dropout keep bits (for tests / debugging):
+ * words[dir][n][w] for dir in {0 (TD), 1 (BU)}. */
+int bgcn_keep_words(uint64_t seed, int64_t num_nodes, int32_t num_words, uint32_t* words,
+                    bgcn_stream_t stream);
+
+/* Timing hook for bench.py: HIP-event time (ms) of the last launch of the named
+ * kernel class on this thread, when enabled with bgcn_set_kernel_timing(1).
+ * kernel class 0 = conv1 X*W1^T GEMM, 1 = dW1 GEMM, 2 = conv2 GEMM, 3 = dW2 GEMM. */
+int bgcn_set_kernel_timing(int enable);
+int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BGCN_H_ */

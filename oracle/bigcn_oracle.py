@@ -1,0 +1,256 @@
+"""CPU oracle for the BiGCN bidirectional message-passing path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing under ``bigcn_amd/`` imports this module; only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+use it, and only as the checker / the timed CPU baseline.
+
+What it restates (plain PyTorch, CPU, op for op):
+
+* ``model/Twitter/BiGCN_Twitter.py:19-131`` (TDrumorGCN / BUrumorGCN / BiGCN) and
+  ``model/Weibo/BiGCN_Weibo.py:16-89`` (same math, 2-class ``Net`` head), including
+  the five semantic traps listed in SURVEY.md section 0:
+  detached ``x2 = copy.copy(h1)`` (``BiGCN_Twitter.py:44``), dropout over the whole
+  ``[N, 64+F]`` concat (``:51-54``), global ``rootindex`` (PyG collation), target-degree
+  normalisation with self loops appended after the edges, lin -> propagate -> +bias.
+* The third-party operators the reference calls but does not vendor:
+  ``torch_geometric.nn.GCNConv`` (PyG >= 2.0 semantics, ``gcn_norm`` +
+  ``add_remaining_self_loops`` + ``MessagePassing(aggr='add')``; the PyG 1.x
+  source-degree convention is selectable with ``degree_on='row'``) and
+  ``torch_scatter.scatter_mean`` (sum / count.clamp(min=1), dim_size = index.max()+1).
+* The optimiser of ``BiGCN_Twitter.py:146-153`` / ``:186-189`` (Adam, three groups,
+  BU convs at lr/5, weight_decay as L2 in the gradient).
+
+PARITY PINNING.  torch_geometric / torch_scatter are not installed in this image
+and the reference ships no tests or golden vectors for this arithmetic, so the
+GCNConv / scatter_mean arithmetic here is **parity unpinned** by the reference
+itself: it follows the published PyG-2.x / torch_scatter algorithms (cited per
+function) and is cross-checked against hand-derived closed forms in
+``tests/test_oracle.py``.  The on-disk / in-memory data format IS pinned: the
+fixtures in ``tests/golden/format_*.npz`` were produced by the reference's own
+``Process/getTwittergraph.py:constructMat/getfeature`` (``oracle/gen_golden.py``).
+"""
+from __future__ import annotations
+
+import copy
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+__all__ = [
+    "add_remaining_self_loops", "gcn_norm", "gcn_conv", "scatter_mean",
+    "root_extend", "BiGCNParams", "direction_forward", "bigcn_forward",
+    "bigcn_loss", "make_params", "make_optimizer", "train_step",
+]
+
+
+# ----------------------------------------------------------------------------
+# torch_geometric (>= 2.0) operators, restated
+# ----------------------------------------------------------------------------
+def add_remaining_self_loops(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor],
+                             num_nodes: int, fill_value: float = 1.0, dtype=torch.float32):
+    """PyG ``utils.add_remaining_self_loops`` (called from ``gcn_norm``; the reference
+    reaches it through every ``GCNConv`` call, ``BiGCN_Twitter.py:42,56,92,105``, and
+    names it explicitly at ``explain_PHEME.py:62-63``).
+
+    Existing self loops are removed from the edge list (their weight becomes the
+    loop weight), then one loop ``(i, i)`` per node is appended AFTER the edges.
+    """
+    row, col = edge_index[0], edge_index[1]
+    mask = row != col
+    if edge_weight is None:
+        edge_weight = torch.ones(edge_index.size(1), dtype=dtype)
+    loop_index = torch.arange(num_nodes, dtype=torch.long)
+    loop_weight = torch.full((num_nodes,), fill_value, dtype=edge_weight.dtype)
+    inv = ~mask
+    if bool(inv.any()):
+        loop_weight[row[inv]] = edge_weight[inv]
+    ei = torch.cat([edge_index[:, mask], torch.stack([loop_index, loop_index])], dim=1)
+    ew = torch.cat([edge_weight[mask], loop_weight])
+    return ei, ew
+
+
+def gcn_norm(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor], num_nodes: int,
+             degree_on: str = "col", dtype=torch.float32):
+    """PyG ``nn.conv.gcn_conv.gcn_norm(improved=False, add_self_loops=True,
+    flow='source_to_target')``.  ``degree_on='col'`` is PyG >= 1.6 (target degree);
+    ``'row'`` is PyG 1.3.2 (source degree, the version ``readme.md:28`` pins)."""
+    ei, ew = add_remaining_self_loops(edge_index, edge_weight, num_nodes, dtype=dtype)
+    row, col = ei[0], ei[1]
+    idx = col if degree_on == "col" else row
+    deg = torch.zeros(num_nodes, dtype=ew.dtype).scatter_add_(0, idx, ew)
+    dinv = deg.pow(-0.5)
+    dinv = dinv.masked_fill(dinv == float("inf"), 0.0)
+    norm = dinv[row] * ew * dinv[col]
+    return ei, norm
+
+
+def gcn_conv(x: torch.Tensor, edge_index: torch.Tensor, weight: torch.Tensor,
+             bias: Optional[torch.Tensor], edge_weight: Optional[torch.Tensor] = None,
+             degree_on: str = "col") -> torch.Tensor:
+    """PyG ``GCNConv.forward`` (2.x): ``h = lin(x)`` (``lin.weight [out,in]``, no bias),
+    ``out[i] = sum_{e: col_e = i} norm_e * h[row_e]`` (message = norm * x_j, aggr add,
+    edges in order, self loops last), then ``+ bias``."""
+    n = x.size(0)
+    ei, norm = gcn_norm(edge_index, edge_weight, n, degree_on, dtype=x.dtype)  # PyG passes x.dtype
+    h = x @ weight.t()
+    msg = norm.view(-1, 1) * h.index_select(0, ei[0])
+    out = torch.zeros(n, h.size(1), dtype=h.dtype).index_add_(0, ei[1], msg)
+    if bias is not None:
+        out = out + bias
+    return out
+
+
+# ----------------------------------------------------------------------------
+# torch_scatter.scatter_mean, restated
+# ----------------------------------------------------------------------------
+def scatter_mean(src: torch.Tensor, index: torch.Tensor, dim: int = 0,
+                 dim_size: Optional[int] = None) -> torch.Tensor:
+    """torch_scatter ``scatter_mean(src, index, dim=0)`` (called at
+    ``BiGCN_Twitter.py:65,113``): ``sum / count.clamp(min=1)``, output rows =
+    ``index.max()+1`` unless ``dim_size`` is given."""
+    assert dim == 0
+    if dim_size is None:
+        dim_size = int(index.max()) + 1 if index.numel() else 0
+    out = torch.zeros(dim_size, *src.shape[1:], dtype=src.dtype)
+    out = out.index_add(0, index, src)
+    cnt = torch.zeros(dim_size, dtype=src.dtype).index_add_(0, index, torch.ones(index.numel(), dtype=src.dtype))
+    cnt = cnt.clamp(min=1)
+    return out / cnt.view(-1, *([1] * (src.dim() - 1)))
+
+
+# ----------------------------------------------------------------------------
+# The BiGCN model (BiGCN_Twitter.py:19-131)
+# ----------------------------------------------------------------------------
+def root_extend(src: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor) -> torch.Tensor:
+    """The Python loop of ``BiGCN_Twitter.py:46-50`` / ``:59-63``, kept as a loop."""
+    out = torch.zeros(len(batch), src.size(1), dtype=src.dtype)
+    batch_size = int(max(batch)) + 1
+    for b in range(batch_size):
+        index = torch.eq(batch, b)
+        out[index] = src[rootindex[b]]
+    return out
+
+
+class BiGCNParams(dict):
+    """Parameters keyed exactly like the reference ``state_dict`` (PyG-2.x layout)."""
+
+
+def make_params(in_feats: int = 5000, hid: int = 64, out: int = 64, num_classes: int = 4,
+                seed: int = 0, dtype=torch.float32) -> Dict[str, torch.Tensor]:
+    """glorot-uniform ``lin.weight`` and zero ``bias`` (PyG GCNConv.reset_parameters);
+    ``fc`` as ``torch.nn.Linear`` default init (``BiGCN_Twitter.py:122``).  Biases get
+    small random values so that parity tests exercise the bias path."""
+    g = torch.Generator().manual_seed(seed)
+
+    def glorot(o, i):
+        a = (6.0 / (i + o)) ** 0.5
+        return (torch.rand(o, i, generator=g, dtype=torch.float64) * 2 * a - a).to(dtype)
+
+    p = {}
+    for d in ("TDrumorGCN", "BUrumorGCN"):
+        p[f"{d}.conv1.lin.weight"] = glorot(hid, in_feats)
+        p[f"{d}.conv1.bias"] = (torch.rand(hid, generator=g, dtype=torch.float64) * 0.2 - 0.1).to(dtype)
+        p[f"{d}.conv2.lin.weight"] = glorot(out, hid + in_feats)
+        p[f"{d}.conv2.bias"] = (torch.rand(out, generator=g, dtype=torch.float64) * 0.2 - 0.1).to(dtype)
+    fin = (out + hid) * 2
+    k = 1.0 / fin ** 0.5
+    p["fc.weight"] = ((torch.rand(num_classes, fin, generator=g, dtype=torch.float64) * 2 - 1) * k).to(dtype)
+    p["fc.bias"] = ((torch.rand(num_classes, generator=g, dtype=torch.float64) * 2 - 1) * k).to(dtype)
+    return p
+
+
+def direction_forward(p: Dict[str, torch.Tensor], prefix: str, x: torch.Tensor,
+                      edge_index: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor,
+                      training: bool = False, keep_mask: Optional[torch.Tensor] = None,
+                      degree_on: str = "col", stages: Optional[dict] = None) -> torch.Tensor:
+    """``TDrumorGCN.forward`` (``BiGCN_Twitter.py:26-67``) == ``BUrumorGCN.forward``
+    (``:77-114``) with the direction's edge_index.  ``keep_mask`` ([N, hid+F] bool)
+    injects the dropout draw of ``:54`` (``F.dropout(p=0.5)`` keeps with prob 0.5 and
+    scales by 2); ``None`` in training mode uses torch's own RNG like the reference."""
+    w1, b1 = p[f"{prefix}.conv1.lin.weight"], p[f"{prefix}.conv1.bias"]
+    w2, b2 = p[f"{prefix}.conv2.lin.weight"], p[f"{prefix}.conv2.bias"]
+    x1 = copy.copy(x.float())                                            # :28
+    h = gcn_conv(x, edge_index, w1, b1, degree_on=degree_on)             # :42
+    x2 = copy.copy(h)                                                    # :44  detached leaf
+    h = torch.cat((h, root_extend(x1, batch, rootindex)), 1)             # :46-51
+    h = F.relu(h)                                                        # :53
+    if training:                                                         # :54
+        if keep_mask is None:
+            h = F.dropout(h, training=True)
+        else:
+            h = h * keep_mask.to(h.dtype) * 2.0
+    if stages is not None:
+        stages[f"{prefix}.h1"] = x2.detach().clone()
+        stages[f"{prefix}.a2"] = h.detach().clone()
+    h = gcn_conv(h, edge_index, w2, b2, degree_on=degree_on)             # :56
+    h = F.relu(h)                                                        # :57
+    if stages is not None:
+        stages[f"{prefix}.r1"] = h.detach().clone()
+    h = torch.cat((h, root_extend(x2, batch, rootindex)), 1)             # :59-63
+    out = scatter_mean(h, batch, dim=0)                                  # :65
+    if stages is not None:
+        stages[f"{prefix}.out"] = out.detach().clone()
+    return out
+
+
+def bigcn_forward(p: Dict[str, torch.Tensor], x, td_edge_index, bu_edge_index, batch, rootindex,
+                  training: bool = False, td_mask=None, bu_mask=None, degree_on: str = "col",
+                  stages: Optional[dict] = None) -> torch.Tensor:
+    """``BiGCN.forward`` (``BiGCN_Twitter.py:125-131``): TD first, BU second, concat
+    **BU first** (``:128``), fc, log_softmax."""
+    td = direction_forward(p, "TDrumorGCN", x, td_edge_index, batch, rootindex, training, td_mask,
+                           degree_on, stages)
+    bu = direction_forward(p, "BUrumorGCN", x, bu_edge_index, batch, rootindex, training, bu_mask,
+                           degree_on, stages)
+    h = torch.cat((bu, td), 1)
+    if stages is not None:
+        stages["head_in"] = h.detach().clone()
+    h = F.linear(h, p["fc.weight"], p["fc.bias"])
+    return F.log_softmax(h, dim=1)
+
+
+def bigcn_loss(logp: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """``F.nll_loss(out_labels, Batch_data.y)`` (``BiGCN_Twitter.py:184``)."""
+    return F.nll_loss(logp, y)
+
+
+def make_optimizer(p: Dict[str, torch.Tensor], lr: float = 5e-4, weight_decay: float = 1e-4):
+    """Adam with three groups (``BiGCN_Twitter.py:146-153``): BU conv1/conv2 at lr/5."""
+    bu1 = [p[k] for k in p if k.startswith("BUrumorGCN.conv1.")]
+    bu2 = [p[k] for k in p if k.startswith("BUrumorGCN.conv2.")]
+    base = [p[k] for k in p if not k.startswith("BUrumorGCN.conv")]
+    return torch.optim.Adam([
+        {"params": base},
+        {"params": bu1, "lr": lr / 5},
+        {"params": bu2, "lr": lr / 5},
+    ], lr=lr, weight_decay=weight_decay)
+
+
+def train_step(p: Dict[str, torch.Tensor], opt, batch: dict, training: bool = True,
+               td_mask=None, bu_mask=None, degree_on: str = "col") -> float:
+    """One step of the ``train_GCN`` batch loop (``BiGCN_Twitter.py:183-189``)."""
+    logp = bigcn_forward(p, batch["x"], batch["edge_index"], batch["BU_edge_index"], batch["batch"],
+                         batch["rootindex"], training, td_mask, bu_mask, degree_on)
+    loss = bigcn_loss(logp, batch["y"])
+    opt.zero_grad()
+    loss.backward()
+    val = loss.item()
+    opt.step()
+    return val
+
+
+def params_requiring_grad(p: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    return {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
+
+
+def reference_grads(p: Dict[str, torch.Tensor], batch: dict, training: bool = False,
+                    td_mask=None, bu_mask=None, degree_on: str = "col",
+                    stages: Optional[dict] = None):
+    """Forward + NLL + backward on fresh leaf copies of ``p``; returns (loss, logp, grads)."""
+    q = params_requiring_grad(p)
+    logp = bigcn_forward(q, batch["x"], batch["edge_index"], batch["BU_edge_index"], batch["batch"],
+                         batch["rootindex"], training, td_mask, bu_mask, degree_on, stages)
+    loss = bigcn_loss(logp, batch["y"])
+    loss.backward()
+    return loss.detach(), logp.detach(), {k: v.grad.detach().clone() for k, v in q.items()}

@@ -1,0 +1,227 @@
+"""GPU parity tests of the individual HIP kernels (K1-K4, K8, K10) through the C ABI.
+
+Each kernel is compared against the CPU oracle / a float64 torch restatement on the
+same seeded inputs.  Tolerance (fp32 path vs fp64 reference): |a - b| <= 1e-4 * (|b| + s)
+with s the reference's scale, i.e. the north-star "within 1e-4 fp32"; integer/index
+outputs are compared exactly.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import bigcn_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 1e-4
+
+
+def close(a, b, tol=TOL, what=""):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    scale = float(b.abs().max()) if b.numel() else 1.0
+    err = float((a - b).abs().max()) if b.numel() else 0.0
+    assert err <= tol * max(scale, 1e-30) + 1e-30, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def rand_forest(rng, sizes, star=False):
+    rows, cols, off = [], [], 0
+    for n in sizes:
+        for k in range(1, n):
+            p = 0 if (star or k == 1 or rng.random() < 0.5) else int(rng.integers(1, k))
+            rows.append(off + p)
+            cols.append(off + k)
+        off += n
+    return torch.tensor([rows, cols], dtype=torch.int64), off
+
+
+def dense_adj(ptr, row, col, w, N):
+    """Dense matrix A[row, col] = w from a CSR (row-major by `row`)."""
+    nnz = int(ptr[N])
+    A = torch.zeros(N, N, dtype=torch.float64)
+    A.index_put_((row[:nnz].long(), col[:nnz].long()), w[:nnz].double(), accumulate=True)
+    return A
+
+
+@pytest.mark.parametrize("degree_on", ["col", "row"])
+@pytest.mark.parametrize("star", [False, True])
+def test_build_graph_matches_gcn_norm(degree_on, star):
+    from bigcn_amd.ops import build_graph
+    rng = np.random.default_rng(1)
+    ei, N = rand_forest(rng, [1, 2, 7, 40, 300], star=star)
+    g = build_graph(ei.to(DEV), N, degree_on=degree_on, validate=True)
+    e, w = O.gcn_norm(ei, None, N, degree_on, dtype=torch.float64)
+    ref = torch.zeros(N, N, dtype=torch.float64)
+    ref.index_put_((e[1], e[0]), w, accumulate=True)      # target-major: A[dst, src]
+    t = [x.cpu() for x in (g.t_ptr, g.t_row, g.t_col, g.t_w)]
+    s = [x.cpu() for x in (g.s_ptr, g.s_row, g.s_col, g.s_w)]
+    close(dense_adj(*t, N), ref, 1e-6, "t-csr")
+    close(dense_adj(*s, N), ref.t(), 1e-6, "s-csr")
+    # row structure: self loop last, real entries keep edge order
+    tp = t[0]
+    assert int(tp[N]) == ei.size(1) + N
+    for i in range(0, N, 37):
+        a, b = int(tp[i]), int(tp[i + 1])
+        assert int(t[2][b - 1]) == i and bool((t[1][a:b] == i).all())
+
+
+def test_build_graph_drops_input_self_loops_and_flags_bad_index():
+    from bigcn_amd.ops import build_graph
+    ei = torch.tensor([[0, 1, 1, 2], [1, 1, 2, 0]])
+    g = build_graph(ei.to(DEV), 3)
+    e, w = O.gcn_norm(ei, None, 3, "col", dtype=torch.float64)
+    ref = torch.zeros(3, 3, dtype=torch.float64)
+    ref.index_put_((e[1], e[0]), w, accumulate=True)
+    close(dense_adj(*[x.cpu() for x in (g.t_ptr, g.t_row, g.t_col, g.t_w)], 3), ref, 1e-6)
+    bad = torch.tensor([[0, 5], [1, 0]])
+    with pytest.raises(IndexError):
+        build_graph(bad.to(DEV), 3, validate=True)
+
+
+def test_build_graph_edge_weight():
+    from bigcn_amd.ops import build_graph
+    rng = np.random.default_rng(3)
+    ei, N = rand_forest(rng, [9, 20])
+    ew = torch.rand(ei.size(1), dtype=torch.float64) + 0.1
+    g = build_graph(ei.to(DEV), N, ew.float().to(DEV))
+    e, w = O.gcn_norm(ei, ew, N, "col", dtype=torch.float64)
+    ref = torch.zeros(N, N, dtype=torch.float64)
+    ref.index_put_((e[1], e[0]), w, accumulate=True)
+    close(dense_adj(*[x.cpu() for x in (g.t_ptr, g.t_row, g.t_col, g.t_w)], N), ref, 1e-6)
+
+
+@pytest.mark.parametrize("F", [64, 128, 12, 5000])
+@pytest.mark.parametrize("star", [False, True])
+def test_spmm_forward_and_transpose(F, star):
+    from bigcn_amd.ops import build_graph, spmm
+    rng = np.random.default_rng(F)
+    sizes = [2, 3, 700, 5, 64] if not star else [3000, 2, 33]
+    ei, N = rand_forest(rng, sizes, star=star)
+    g = build_graph(ei.to(DEV), N)
+    e, w = O.gcn_norm(ei, None, N, "col", dtype=torch.float64)
+    A = torch.zeros(N, N, dtype=torch.float64)
+    A.index_put_((e[1], e[0]), w, accumulate=True)
+    x = torch.randn(N, F, dtype=torch.float64)
+    bias = torch.randn(F, dtype=torch.float64)
+    out = spmm(g, x.float().to(DEV), bias.float().to(DEV))
+    close(out, A @ x + bias, what="A x + b")
+    outr = spmm(g, x.float().to(DEV), bias.float().to(DEV), relu=True)
+    close(outr, torch.relu(A @ x + bias), what="relu")
+    outt = spmm(g, x.float().to(DEV), transposed=True)
+    close(outt, A.t() @ x, what="A^T x")
+
+
+def test_spmm_deterministic():
+    from bigcn_amd.ops import build_graph, spmm
+    rng = np.random.default_rng(5)
+    ei, N = rand_forest(rng, [2000, 100, 5], star=True)
+    g = build_graph(ei.to(DEV), N)
+    x = torch.randn(N, 64, device=DEV)
+    a = spmm(g, x, transposed=True)
+    b = spmm(g, x, transposed=True)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,Nc,K", [(1000, 128, 5000), (77, 64, 5064), (130, 20, 37), (5, 128, 8)])
+def test_gemm_xwt(M, Nc, K):
+    from bigcn_amd import _lib
+    from bigcn_amd._lib import check, ptr, stream_handle
+    torch.manual_seed(M)
+    X = torch.randn(M, K, dtype=torch.float64)
+    W = torch.randn(Nc, K, dtype=torch.float64)
+    Xd, Wd = X.float().to(DEV), W.float().to(DEV)
+    Y = torch.empty(M, Nc, device=DEV)
+    split = Nc // 2
+    check(_lib.lib().bgcn_gemm_xwt(ptr(Xd), K, ptr(Wd), ptr(Wd[split:]), K, split, ptr(Y), Nc, M, Nc, K,
+                                   stream_handle()))
+    close(Y, X @ W.t(), 1e-5, "X W^T")
+
+
+@pytest.mark.parametrize("M,Nc,K", [(500, 5000, 64), (33, 13, 7), (64, 128, 128)])
+def test_gemm_xw(M, Nc, K):
+    from bigcn_amd import _lib
+    from bigcn_amd._lib import check, ptr, stream_handle
+    torch.manual_seed(K)
+    X = torch.randn(M, K, dtype=torch.float64)
+    W = torch.randn(K, Nc, dtype=torch.float64)
+    Xd, Wd = X.float().to(DEV), W.float().to(DEV)
+    Y = torch.empty(M, Nc, device=DEV)
+    check(_lib.lib().bgcn_gemm_xw(ptr(Xd), K, ptr(Wd), Nc, ptr(Y), Nc, M, Nc, K, stream_handle()))
+    close(Y, X @ W, 1e-5, "X W")
+
+
+@pytest.mark.parametrize("Mc,Nc,K", [(128, 5000, 3000), (64, 5064, 257), (20, 30, 1000), (128, 64, 5)])
+def test_gemm_tn(Mc, Nc, K):
+    from bigcn_amd import _lib
+    from bigcn_amd._lib import check, ptr, stream_handle, workspace
+    torch.manual_seed(Mc + Nc)
+    G = torch.randn(K, Mc, dtype=torch.float64)
+    X = torch.randn(K, Nc, dtype=torch.float64)
+    Gd, Xd = G.float().to(DEV), X.float().to(DEV)
+    split = Mc // 2
+    C0 = torch.empty(split, Nc, device=DEV)
+    C1 = torch.empty(Mc - split, Nc, device=DEV)
+    L = _lib.lib()
+    ws = workspace(L.bgcn_gemm_tn_workspace_size(Mc, Nc, K), DEV)
+    check(L.bgcn_gemm_tn(ptr(Gd), Mc, ptr(Xd), Nc, ptr(C0), ptr(C1), Nc, split, Mc, Nc, K, ptr(ws),
+                         ws.numel(), stream_handle()))
+    ref = G.t() @ X
+    close(torch.cat([C0, C1]), ref, 1e-5, "G^T X")
+
+
+def test_colsum():
+    from bigcn_amd import _lib
+    from bigcn_amd._lib import check, ptr, stream_handle, workspace
+    A = torch.randn(3001, 70, dtype=torch.float64)
+    Ad = A.float().to(DEV)
+    out = torch.empty(70, device=DEV)
+    L = _lib.lib()
+    ws = workspace(L.bgcn_colsum_workspace_size(3001, 70), DEV)
+    check(L.bgcn_colsum(ptr(Ad), 70, 3001, 70, ptr(out), ptr(ws), ws.numel(), stream_handle()))
+    close(out, A.sum(0), 1e-5)
+
+
+@pytest.mark.parametrize("sorted_index", [True, False])
+def test_scatter_mean(sorted_index):
+    from bigcn_amd import scatter_mean
+    torch.manual_seed(0)
+    n, C, B = 5000, 128, 40
+    idx = torch.randint(0, B, (n,))
+    idx[idx == 7] = 8                      # an empty segment
+    if sorted_index:
+        idx = idx.sort().values
+    src = torch.randn(n, C, dtype=torch.float64, requires_grad=True)
+    ref = O.scatter_mean(src, idx, dim_size=B)
+    ref.backward(torch.ones_like(ref) * torch.arange(C, dtype=torch.float64))
+    s = src.detach().float().to(DEV).requires_grad_(True)
+    out = scatter_mean(s, idx.to(DEV), dim=0, dim_size=B)
+    close(out, ref, what="fwd")
+    out.backward(torch.ones_like(out) * torch.arange(C, device=DEV, dtype=torch.float32))
+    close(s.grad, src.grad, what="bwd")
+
+
+def test_gcnconv_module_fwd_bwd():
+    from bigcn_amd import GCNConv
+    rng = np.random.default_rng(11)
+    ei, N = rand_forest(rng, [50, 3, 200])
+    torch.manual_seed(0)
+    conv = GCNConv(333, 64).to(DEV)
+    with torch.no_grad():
+        conv.bias.uniform_(-0.1, 0.1)
+    assert set(conv.state_dict()) == {"lin.weight", "bias"}
+    x = torch.rand(N, 333, dtype=torch.float64, requires_grad=True)
+    w = conv.lin.weight.detach().double().cpu().requires_grad_(True)
+    b = conv.bias.detach().double().cpu().requires_grad_(True)
+    ref = O.gcn_conv(x, ei, w, b)
+    gout = torch.randn_like(ref)
+    ref.backward(gout)
+    xd = x.detach().float().to(DEV).requires_grad_(True)
+    out = conv(xd, ei.to(DEV))
+    out.backward(gout.float().to(DEV))
+    close(out, ref, what="out")
+    close(xd.grad, x.grad, what="dx")
+    close(conv.lin.weight.grad, w.grad, what="dW")
+    close(conv.bias.grad, b.grad, what="db")
