@@ -1,0 +1,227 @@
+#!/usr/bin/env python
+"""BiGCN training-step benchmark on MI355X (BASELINE.json metric: propagation-trees/s
+fwd+bwd, batch = 128 trees per GPU, 5000-dim features).
+
+    python bench.py [--gpus N --steps K --warmup W --workload twitter15]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one pass of the reference training loop body (``BiGCN_Twitter.py:183-189``) over
+one batch of synthetic trees already resident in HBM: gcn_norm/CSR for TD and BU (K1),
+the fused encoder forward, fc + log_softmax + NLL, backward, the DP gradient all-reduce
+(N > 1) and the Adam step with the reference's three parameter groups.  Batches are
+cycled from a pool of ``--pool`` distinct batches (each larger than the 256 MiB
+Infinity Cache).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "propagation-trees/sec fwd+bwd, batch=128, 5000-dim feats @ 1/2/4/8 MI355X"
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (dense)
+PEAK_HBM_GBS = 8000.0
+
+WORKLOADS = {
+    # BASELINE.json configs[1]: Twitter15 training, batch 128, fp32, 1 x MI355X.  The real
+    # trees are absent (.MISSING_LARGE_BLOBS), so the batch is synthetic in the reference's
+    # format with the tree-size distribution of SURVEY.md 8(d).
+    "twitter15": dict(trees=128, mean=256, sigma=0.8, feats=5000, classes=4, drop=(0.2, 0.2),
+                      desc="Twitter15-shaped synthetic: 128 trees/GPU, LogNormal(0.8) sizes mean 256 "
+                           "clamped [2,8192], 5000-dim BoW x, DropEdge 0.2/0.2, dropout 0.5, fp32"),
+}
+
+KERNEL_CLASSES = {0: "conv1 X.W1^T (TD+BU fused)", 1: "dW1 = dZ1^T X (TD+BU fused)",
+                  2: "conv2 A2.W2^T (generated A2)", 3: "dW2 = dZ2^T A2 (generated A2)"}
+
+
+def kernel_flops(cls: int, N: int, Fd: int) -> float:
+    H = 64
+    if cls in (0, 1):
+        return 2.0 * N * Fd * 2 * H
+    return 2.0 * N * (Fd + H) * H * 2
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_pool(wl, rank, pool, device):
+    from bigcn_amd.data import synth_batch, synth_tree_sizes
+    out = []
+    for i in range(pool):
+        rng = np.random.default_rng(20250205 + 1 + 1000 * rank + i)
+        sizes = synth_tree_sizes(rng, wl["trees"], wl["mean"], wl["sigma"])
+        out.append(synth_batch(rng, sizes, wl["feats"], wl["classes"], *wl["drop"], device=device))
+    return out
+
+
+def cpu_baseline(wl, trees: int, steps: int):
+    """The oracle (op-for-op plain-PyTorch restatement of the reference step) on the
+    host cores: Python root loops, materialised [N, 5064] concat, aten dropout, autograd,
+    Adam with 3 groups."""
+    from bigcn_amd.data import synth_batch, synth_tree_sizes
+    from oracle import bigcn_oracle as O
+    cores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(cores)
+    rng = np.random.default_rng(777)
+    sizes = synth_tree_sizes(rng, trees, wl["mean"], wl["sigma"])
+    b = synth_batch(rng, sizes, wl["feats"], wl["classes"], *wl["drop"], device="cpu")
+    batch = {"x": b.x, "edge_index": b.edge_index, "BU_edge_index": b.BU_edge_index, "batch": b.batch,
+             "rootindex": b.rootindex, "y": b.y}
+    p = {k: v.requires_grad_(True) for k, v in O.make_params(wl["feats"], 64, 64, wl["classes"]).items()}
+    opt = O.make_optimizer(p)
+    O.train_step(p, opt, batch, training=True)        # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        O.train_step(p, opt, batch, training=True)
+    dt = time.perf_counter() - t0
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(trees * steps / dt, 3), "unit": "trees/s", "cores": cores, "kind": "port",
+            "sample": f"{steps} timed steps (+1 warm-up) of {trees} trees ({int(sizes.sum())} nodes), "
+                      f"same tree/feature distribution; oracle/bigcn_oracle.py train_step, torch "
+                      f"{torch.__version__} on {cpu}, {cores} threads; baseline only"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="twitter15", choices=sorted(WORKLOADS))
+    ap.add_argument("--pool", type=int, default=4)
+    ap.add_argument("--cpu-trees", type=int, default=32)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    from bigcn_amd import BiGCN, make_optimizer
+    from bigcn_amd import ops
+    from bigcn_amd.dp import GradBucket, init_from_env
+
+    rank, world, local = init_from_env("nccl")
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    wl = WORKLOADS[args.workload]
+    torch.manual_seed(1234 + rank)
+    pool = make_pool(wl, rank, args.pool, dev)
+    nodes = [b.x.size(0) for b in pool]
+    model = BiGCN(wl["feats"], 64, 64, dev).to(dev)
+    if world > 1:   # identical initial parameters on every rank
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    model.train()
+    opt = make_optimizer(model, fused=True)
+    bucket = GradBucket(model.parameters())
+
+    def step(i):
+        b = pool[i % len(pool)]
+        b.__dict__.pop("_bgcn_graphs", None)          # gcn_norm/CSR rebuilt every step (as GCNConv does)
+        logp = model(b)
+        loss = F.nll_loss(logp, b.y)
+        opt.zero_grad(set_to_none=False)
+        loss.backward()
+        bucket.allreduce_mean()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timing = not args.no_kernel_timing
+    if timing:
+        ops.set_kernel_timing(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+        if rank == 0 and (i + 1) % max(1, args.steps // 4) == 0:
+            log(f"step {i + 1}/{args.steps}")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    kern = {}
+    if timing:
+        ops.set_kernel_timing(False)
+        for c in KERNEL_CLASSES:
+            ms, n = ops.kernel_timing(c)
+            kern[c] = (ms, n)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    final_loss = float(loss.item())
+
+    if rank == 0:
+        trees_total = wl["trees"] * world * args.steps
+        value = trees_total / dt
+        N_avg = float(np.mean([nodes[(args.warmup + i) % len(nodes)] for i in range(args.steps)]))
+        roof = None
+        kernels = {}
+        if kern:
+            best = None
+            for c, (ms, n) in kern.items():
+                if n == 0:
+                    continue
+                avg_ms = ms / n
+                flops = kernel_flops(c, N_avg, wl["feats"])
+                tf = flops / (avg_ms * 1e-3) / 1e12
+                kernels[KERNEL_CLASSES[c]] = {"avg_ms": round(avg_ms, 4), "launches": n,
+                                              "tflops": round(tf, 2)}
+                if best is None or avg_ms > best[1]:
+                    best = (c, avg_ms, tf)
+            if best is not None:
+                roof = {"bound": "mfma", "achieved": round(best[2], 2), "peak": PEAK_FP32_MFMA_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(best[2] / PEAK_FP32_MFMA_TFLOPS, 4),
+                        "traffic": None, "kernel": KERNEL_CLASSES[best[0]],
+                        "flops_per_launch": kernel_flops(best[0], N_avg, wl["feats"])}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline ...")
+            cpu = cpu_baseline(wl, args.cpu_trees, args.cpu_steps)
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "trees/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (reference npz/Batch layout; real Twitter15 trees absent)",
+            "config": {"workload": wl["desc"], "trees_per_gpu": wl["trees"],
+                       "global_batch": wl["trees"] * world, "avg_nodes_per_batch": round(N_avg, 1),
+                       "in_feats": wl["feats"], "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "final_loss": round(final_loss, 5),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

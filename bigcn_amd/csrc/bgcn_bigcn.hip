@@ -26,7 +26,7 @@ int gemm_xwt_impl(const float* X, int64_t ldx, const float* W0, const float* W1,
                   hipStream_t stream);
 int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float* C0, float* C1,
                  int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
-                 size_t ws_bytes, hipStream_t stream);
+                 size_t ws_bytes, hipStream_t stream, int timing_cls);
 size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K);
 int tn_splits(int64_t Mc, int64_t Nc, int64_t K);
 
@@ -558,10 +558,10 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   hipLaunchKernelGGL(k_dw2, dim3(grid_for(H + F, 64), w.S2, 2), dim3(256), 0, s, a->x, a->ldx, F,
                      a->h1, w.dz2, w.node_root, w.dw2_part, N, w.kchunk2, w.S2, keep);
   BGCN_CHECK_LAUNCH();
+  timing_end(3, s);
   hipLaunchKernelGGL(k_reduce_dw2, dim3(grid_for(2 * H * (H + F), 256)), dim3(256), 0, s,
                      w.dw2_part, w.S2, H + F, a->td_dw2, a->bu_dw2);
   BGCN_CHECK_LAUNCH();
-  timing_end(3, s);
   // dH1 through dropout and relu, db1
   hipLaunchKernelGGL(k_dh1, dim3(unsigned(nblk), 2), dim3(256), 0, s, w.dz2, a->h1, a->td_w2,
                      a->bu_w2, H + F, N, kRowsPerBlock, keep, w.dh1, w.colpart);
@@ -573,10 +573,8 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   BGCN_TRY(spmm_dir(a->td, true, N, w.dh1, w.dz1, nullptr, BGCN_EPI_NONE, w, s));
   BGCN_TRY(spmm_dir(a->bu, true, N, w.dh1 + H, w.dz1 + H, nullptr, BGCN_EPI_NONE, w, s));
   // dW1 = [dZ1_td | dZ1_bu]^T X  (one pass over X for both directions)
-  timing_begin(1, s);
   BGCN_TRY(gemm_tn_impl(w.dz1, 2 * H, a->x, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F, N,
-                        w.tn_ws, w.tn_bytes, s));
-  timing_end(1, s);
+                        w.tn_ws, w.tn_bytes, s, 1));
   return BGCN_OK;
 }
 

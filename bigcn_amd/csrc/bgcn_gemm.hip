@@ -377,7 +377,7 @@ int colsum_impl(const float* A, int64_t lda, int64_t rows, int32_t C, float* out
 
 int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float* C0, float* C1,
                  int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
-                 size_t ws_bytes, hipStream_t stream) {
+                 size_t ws_bytes, hipStream_t stream, int timing_cls) {
   BGCN_CHECK_ARG(G && X && C0, "null pointer");
   BGCN_CHECK_ARG(Mc > 0 && Nc > 0 && K >= 0, "bad shape");
   BGCN_CHECK_ARG(ldg >= Mc && ldx >= Nc && ldc >= Nc, "bad leading dimension");
@@ -393,6 +393,7 @@ int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float
   bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) &&
              aligned16(X);
   dim3 grid(grid_for(Nc, 64), grid_for(Mc, 128), S);
+  timing_begin(timing_cls, stream);
   if (vec)
     hipLaunchKernelGGL(k_gemm_tn<true>, grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc, Nc,
                        K, kchunk);
@@ -400,6 +401,7 @@ int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float
     hipLaunchKernelGGL(k_gemm_tn<false>, grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc, Nc,
                        K, kchunk);
   BGCN_CHECK_LAUNCH();
+  timing_end(timing_cls, stream);
   hipLaunchKernelGGL(k_reduce_splits, dim3(grid_for(Mc * Nc, 256)), dim3(256), 0, stream, part, S,
                      Mc, Nc, C0, C1, ldc, split);
   BGCN_CHECK_LAUNCH();
@@ -440,5 +442,5 @@ extern "C" int bgcn_gemm_tn(const float* G, int64_t ldg, const float* X, int64_t
                             int64_t K, void* workspace, size_t workspace_bytes,
                             bgcn_stream_t stream) {
   return bgcn::gemm_tn_impl(G, ldg, X, ldx, C0, C1, ldc, split, Mc, Nc, K, workspace,
-                            workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+                            workspace_bytes, reinterpret_cast<hipStream_t>(stream), -1);
 }
