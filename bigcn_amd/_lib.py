@@ -24,11 +24,15 @@ BGCN_DEGREE_ON_COL = 0
 BGCN_DEGREE_ON_ROW = 1
 BGCN_EPI_NONE = 0
 BGCN_EPI_RELU = 1
+BGCN_FEAT_AUTO = 0
+BGCN_FEAT_DENSE = 1
+BGCN_SPARSE_CAP = 32
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
     "bgcn_abi_version", "bgcn_last_error",
     "bgcn_graph_workspace_size", "bgcn_build_graph",
+    "bgcn_graph_pair_workspace_size", "bgcn_build_graph_pair",
     "bgcn_spmm_workspace_size", "bgcn_spmm",
     "bgcn_gemm_xwt", "bgcn_gemm_xw", "bgcn_gemm_tn_workspace_size", "bgcn_gemm_tn",
     "bgcn_colsum_workspace_size", "bgcn_colsum",
@@ -46,6 +50,13 @@ class GraphView(Structure):
     ]
 
 
+class CsrOut(Structure):
+    _fields_ = [
+        ("t_ptr", c_void_p), ("t_row", c_void_p), ("t_col", c_void_p), ("t_w", c_void_p),
+        ("s_ptr", c_void_p), ("s_row", c_void_p), ("s_col", c_void_p), ("s_w", c_void_p),
+    ]
+
+
 class BiGCNArgs(Structure):
     _fields_ = [
         ("x", c_void_p), ("ldx", c_int64), ("num_nodes", c_int64), ("num_graphs", c_int64),
@@ -54,6 +65,8 @@ class BiGCNArgs(Structure):
         ("td_w1", c_void_p), ("td_b1", c_void_p), ("td_w2", c_void_p), ("td_b2", c_void_p),
         ("bu_w1", c_void_p), ("bu_b1", c_void_p), ("bu_w2", c_void_p), ("bu_b2", c_void_p),
         ("training", c_int), ("seed", c_uint64), ("keep_words", c_void_p),
+        ("feat_mode", c_int), ("x_flags", c_void_p), ("x_nnz", c_void_p), ("x_cols", c_void_p),
+        ("x_vals", c_void_p),
         ("tree_ptr", c_void_p), ("h1", c_void_p), ("h2", c_void_p), ("head_in", c_void_p),
         ("dhead_in", c_void_p),
         ("td_dw1", c_void_p), ("td_db1", c_void_p), ("td_dw2", c_void_p), ("td_db2", c_void_p),
@@ -69,6 +82,10 @@ _SIGS = {
                                  c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_size_t, c_void_p]),
+    "bgcn_graph_pair_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
+    "bgcn_build_graph_pair": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int,
+                                      POINTER(CsrOut), POINTER(CsrOut), c_void_p, c_void_p, c_size_t,
+                                      c_void_p]),
     "bgcn_spmm_workspace_size": (c_size_t, [c_int64, c_int32]),
     "bgcn_spmm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                           c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int, c_void_p,

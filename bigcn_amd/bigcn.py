@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from .conv import GCNConv
-from .ops import Graph, bigcn_encoder, build_graph, scatter_mean
+from .ops import Graph, bigcn_encoder, build_graph_pair, scatter_mean
 
 
 def _graphs(data, degree_on: str = "col"):
@@ -26,8 +26,7 @@ def _graphs(data, degree_on: str = "col"):
     if cache is not None and cache[0] == degree_on:
         return cache[1], cache[2]
     n = data.x.size(0)
-    td = build_graph(data.edge_index, n, degree_on=degree_on)
-    bu = build_graph(data.BU_edge_index, n, degree_on=degree_on)
+    td, bu = build_graph_pair(data.edge_index, data.BU_edge_index, n, degree_on=degree_on)
     try:
         data._bgcn_graphs = (degree_on, td, bu)
     except AttributeError:
@@ -99,6 +98,7 @@ class BiGCN(torch.nn.Module):
         self.fc = torch.nn.Linear((out_feats + hid_feats) * 2, self.num_classes)
         self.device = device
         self.keep_words = None  # optional injected dropout draw (tests)
+        self.feat_mode = "auto"  # "auto": sparse feature path with device-side dense fallback
 
     def encoder_params(self):
         t, b = self.TDrumorGCN, self.BUrumorGCN
@@ -111,7 +111,7 @@ class BiGCN(torch.nn.Module):
             seed = _draw_seed() if self.training else 0
         return bigcn_encoder(data.x, data.batch, data.rootindex, td, bu, _num_graphs(data),
                              self.encoder_params(), training=self.training, seed=seed,
-                             keep_words=self.keep_words)
+                             keep_words=self.keep_words, feat_mode=self.feat_mode)
 
     def forward(self, data, seed=None):
         x = self.encode(data, seed)            # cat(BU_x, TD_x)  (:126-128)

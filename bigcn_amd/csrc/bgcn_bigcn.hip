@@ -12,23 +12,10 @@
 //   out = mean_tree([relu(H2) | H1[root]])   (:57-65; H1[root] is the detached x2)
 // Backward follows SURVEY.md 8(a) "Gradient dataflow": no gradient reaches conv1
 // through the root-extended x2 (copy.copy makes a new leaf, :44).
-#include "bgcn_common.h"
+#include "bgcn_internal.h"
+#include "bgcn_sparse.h"
 
 namespace bgcn {
-
-int spmm_impl(const int32_t* ptr, const int32_t* row, const int32_t* col, const float* w,
-              int64_t rows, int64_t capacity, const float* in, int64_t ld_in, float* out,
-              int64_t ld_out, int32_t F, const float* bias, int epi, void* ws, size_t ws_bytes,
-              hipStream_t stream);
-size_t spmm_ws_size(int64_t capacity, int32_t F);
-int gemm_xwt_impl(const float* X, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
-                  int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
-                  hipStream_t stream);
-int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float* C0, float* C1,
-                 int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
-                 size_t ws_bytes, hipStream_t stream, int timing_cls);
-size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K);
-int tn_splits(int64_t Mc, int64_t Nc, int64_t K);
 
 namespace {
 
@@ -70,7 +57,9 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ X, 
                                                    const int32_t* __restrict__ node_root,
                                                    const float* __restrict__ W2td,
                                                    const float* __restrict__ W2bu,
-                                                   float* __restrict__ Z2, int64_t N, KeepSrc keep) {
+                                                   float* __restrict__ Z2, int64_t N, KeepSrc keep,
+                                                   const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
   constexpr int BM = 64, LS = BK + 1;
   __shared__ float As[2][BM * LS];
   __shared__ float Bs[2][H * LS];
@@ -161,7 +150,9 @@ __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_
                                              const float* __restrict__ dZ2,
                                              const int32_t* __restrict__ node_root,
                                              float* __restrict__ part, int64_t N, int64_t kchunk,
-                                             int S, KeepSrc keep) {
+                                             int S, KeepSrc keep, const int32_t* __restrict__ gate) {
+  // column tile 0 (the relu(H1) block) always runs; the X[root] tiles only on the dense path
+  if (blockIdx.x > 0 && gate_closed(gate)) return;
   constexpr int BN = 64;
   __shared__ float As[2][BK * H];   // [node][o]
   __shared__ float Bs[2][BK * BN];  // [node][c]
@@ -245,12 +236,14 @@ __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_
 }
 
 __global__ void k_reduce_dw2(const float* __restrict__ part, int S, int64_t K2,
-                             float* __restrict__ dw_td, float* __restrict__ dw_bu) {
+                             float* __restrict__ dw_td, float* __restrict__ dw_bu,
+                             const int32_t* __restrict__ gate) {
   int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   int64_t per = int64_t(H) * K2;
   if (idx >= 2 * per) return;
   int d = int(idx / per);
   int64_t e = idx % per;
+  if (e % K2 >= H && gate_closed(gate)) return;   // root columns come from the sparse path
   const float* p = part + int64_t(d) * S * per + e;
   float acc = p[0];
   for (int s = 1; s < S; ++s) acc += p[int64_t(s) * per];
@@ -367,14 +360,24 @@ __global__ __launch_bounds__(256) void k_dh1(const float* __restrict__ dZ2,
     colpart[int64_t(blockIdx.x) * (2 * H) + d * H + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
-// out_td[c] = sum_p colpart[p][c], out_bu[c] = sum_p colpart[p][H + c]  (fixed order)
-__global__ void k_colsum_reduce(const float* __restrict__ colpart, int P,
-                                float* __restrict__ out_td, float* __restrict__ out_bu) {
-  const int c = threadIdx.x;
-  if (c >= 2 * H) return;
+// out_td[c] = sum_p colpart[p][c], out_bu[c] = sum_p colpart[p][H + c]: one block per
+// column, strided partial sums + a fixed LDS tree (deterministic).
+__global__ __launch_bounds__(256) void k_colsum_reduce(const float* __restrict__ colpart, int P,
+                                                       float* __restrict__ out_td,
+                                                       float* __restrict__ out_bu) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
   float acc = 0.f;
-  for (int p = 0; p < P; ++p) acc += colpart[int64_t(p) * (2 * H) + c];
-  if (c < H) out_td[c] = acc; else out_bu[c - H] = acc;
+  for (int p = threadIdx.x; p < P; p += 256) acc += colpart[int64_t(p) * (2 * H) + c];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (c < H) out_td[c] = red[0]; else out_bu[c - H] = red[0];
+  }
 }
 
 __global__ void k_keep_words(uint64_t seed, int64_t N, int nw, uint32_t* __restrict__ words) {
@@ -440,6 +443,7 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
 size_t fused_ws_fixed(int64_t N, int64_t B, int64_t F) {
   Carve c(nullptr, 0);
   carve_fused(c, N, B, F, nullptr);
+  carve_sparse(c, N, B, F, nullptr);
   return c.off;
 }
 
@@ -475,50 +479,92 @@ size_t bigcn_ws_size(int64_t N, int64_t B, int64_t F, int64_t hid) {
   return fused_ws_fixed(N, B, F) + 256 + spmm_ws_size(5 * N + 64, 2 * H);
 }
 
-static int spmm_dir(const bgcn_graph_view& g, bool transposed, int64_t N, const float* in,
-                    float* out, const float* bias, int epi, FusedWs& w, hipStream_t s) {
-  const int32_t* ptr = transposed ? g.s_ptr : g.t_ptr;
-  const int32_t* row = transposed ? g.s_row : g.t_row;
-  const int32_t* col = transposed ? g.s_col : g.t_col;
-  const float* wt = transposed ? g.s_w : g.t_w;
-  BGCN_CHECK_ARG(spmm_ws_size(g.capacity, H) <= w.spmm_bytes, "graph capacity exceeds workspace");
-  return spmm_impl(ptr, row, col, wt, N, g.capacity, in, 2 * H, out, 2 * H, H, bias, epi,
-                   w.spmm_ws, w.spmm_bytes, s);
+// TD (columns [0, H)) and BU (columns [H, 2H)) aggregations of one [N, 2H] matrix in
+// one launch; `transposed` selects A^T (backward).
+static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool transposed,
+                     int64_t N, const float* in, float* out, const float* bias_td,
+                     const float* bias_bu, int epi, FusedWs& w, hipStream_t s) {
+  const size_t half = w.spmm_bytes / 2 / 256 * 256;
+  BGCN_CHECK_ARG(spmm_ws_size(td.capacity, H) <= half && spmm_ws_size(bu.capacity, H) <= half,
+                 "graph capacity exceeds workspace");
+  SpmmBatch sb{};
+  sb.rows = N;
+  sb.F = H;
+  sb.epi = epi;
+  const bgcn_graph_view* g[2] = {&td, &bu};
+  for (int d = 0; d < 2; ++d) {
+    const bgcn_graph_view& v = *g[d];
+    sb.p[d] = SpmmProb{transposed ? v.s_ptr : v.t_ptr, transposed ? v.s_row : v.t_row,
+                       transposed ? v.s_col : v.t_col, transposed ? v.s_w : v.t_w,
+                       in + d * H, 2 * H, out + d * H, 2 * H, d == 0 ? bias_td : bias_bu,
+                       reinterpret_cast<float*>(reinterpret_cast<char*>(w.spmm_ws) + d * half),
+                       spmm_groups(v.capacity)};
+  }
+  return spmm_batch_impl(sb, 2, s);
+}
+
+// Workspace + sparse state of one call.  The sparse path's per-row lists and its
+// overflow flag live in caller-owned buffers (saved from forward to backward).
+static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w, SparseState& sp,
+                 const int32_t*& gate) {
+  const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
+  BGCN_CHECK_ARG(ws && ws_bytes >= bigcn_ws_size(N, B, F, H), "workspace too small");
+  BGCN_CHECK_ARG(a->feat_mode == BGCN_FEAT_DENSE ||
+                     (a->x_flags && a->x_nnz && a->x_cols && a->x_vals),
+                 "sparse feature buffers required unless feat_mode == BGCN_FEAT_DENSE");
+  Carve c(ws, ws_bytes);
+  carve_fused(c, N, B, F, &w);
+  sp.mode = a->feat_mode == BGCN_FEAT_DENSE ? 1 : 0;
+  sp.flags = a->x_flags;
+  sp.nnz = a->x_nnz;
+  sp.cols = a->x_cols;
+  sp.vals = a->x_vals;
+  carve_sparse(c, N, B, F, &sp);
+  BGCN_CHECK_ARG(c.ok(), "workspace too small");
+  w.spmm_bytes = ws_bytes - align_up(c.off, 256) - 256;
+  w.spmm_ws = c.take<float>(1);
+  // dense kernels run when feat_mode == dense (no gate) or when the sparse path overflowed
+  gate = sp.mode == 1 ? nullptr : a->x_flags;
+  return BGCN_OK;
 }
 
 int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->head_in && a->td_w1 && a->bu_w1 && a->td_w2 && a->bu_w2, "null pointer");
   const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
-  BGCN_CHECK_ARG(ws && ws_bytes >= bigcn_ws_size(N, B, F, H), "workspace too small");
-  Carve c(ws, ws_bytes);
   FusedWs w;
-  carve_fused(c, N, B, F, &w);
-  w.spmm_bytes = ws_bytes - align_up(c.off, 256) - 256;
-  w.spmm_ws = c.take<float>(1);
+  SparseState sp{};
+  const int32_t* gate = nullptr;
+  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate));
   KeepSrc keep = make_keep(a);
 
+  if (sp.mode != 1) BGCN_CHECK_HIP(hipMemsetAsync(a->x_flags, 0, 8 * sizeof(int32_t), s));
   hipLaunchKernelGGL(k_tree_ptr, dim3(grid_for(B + 1, 256)), dim3(256), 0, s, a->batch, N, B,
                      a->tree_ptr);
   BGCN_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_node_root, dim3(grid_for(N, 256)), dim3(256), 0, s, a->batch,
                      a->rootindex, N, B, w.node_root);
   BGCN_CHECK_LAUNCH();
-  // conv1 lin, TD and BU in one pass over X
-  timing_begin(0, s);
-  BGCN_TRY(gemm_xwt_impl(a->x, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F, s));
-  timing_end(0, s);
+  // conv1 lin, TD and BU in one pass over X: sparse (compaction + gather) or dense MFMA
+  if (sp.mode != 1) {
+    BGCN_TRY(sparse_transpose(sp, a, s));
+    timing_begin(0, s);
+    BGCN_TRY(sparse_compact_conv1(sp, a->x, a->ldx, w.z1, s));
+    timing_end(0, s);
+  }
+  timing_begin(sp.mode == 1 ? 0 : 4, s);
+  BGCN_TRY(gemm_xwt_impl(a->x, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F, s, gate));
+  timing_end(sp.mode == 1 ? 0 : 4, s);
   // conv1 propagate + bias (pre-relu h1 is saved: it is also the detached x2)
-  BGCN_TRY(spmm_dir(a->td, false, N, w.z1, a->h1, a->td_b1, BGCN_EPI_NONE, w, s));
-  BGCN_TRY(spmm_dir(a->bu, false, N, w.z1 + H, a->h1 + H, a->bu_b1, BGCN_EPI_NONE, w, s));
+  BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z1, a->h1, a->td_b1, a->bu_b1, BGCN_EPI_NONE, w, s));
   // conv2 lin with the root-extended, relu'd, dropped-out A operand generated in-kernel
   timing_begin(2, s);
+  if (sp.mode != 1) BGCN_TRY(sparse_conv2(sp, a->h1, w.node_root, w.z2, keep, s));
   hipLaunchKernelGGL(k_conv2_fwd, dim3(grid_for(N, 64), 2), dim3(256), 0, s, a->x, a->ldx, F,
-                     a->h1, w.node_root, a->td_w2, a->bu_w2, w.z2, N, keep);
+                     a->h1, w.node_root, a->td_w2, a->bu_w2, w.z2, N, keep, gate);
   BGCN_CHECK_LAUNCH();
   timing_end(2, s);
-  BGCN_TRY(spmm_dir(a->td, false, N, w.z2, a->h2, a->td_b2, BGCN_EPI_NONE, w, s));
-  BGCN_TRY(spmm_dir(a->bu, false, N, w.z2 + H, a->h2 + H, a->bu_b2, BGCN_EPI_NONE, w, s));
+  BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z2, a->h2, a->td_b2, a->bu_b2, BGCN_EPI_NONE, w, s));
   hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B), 2), dim3(256), 0, s, a->h1, a->h2,
                      a->tree_ptr, a->rootindex, N, a->head_in);
   BGCN_CHECK_LAUNCH();
@@ -531,12 +577,10 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
                      a->bu_db1 && a->td_db2 && a->bu_db2,
                  "null gradient pointer");
   const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
-  BGCN_CHECK_ARG(ws && ws_bytes >= bigcn_ws_size(N, B, F, H), "workspace too small");
-  Carve c(ws, ws_bytes);
   FusedWs w;
-  carve_fused(c, N, B, F, &w);
-  w.spmm_bytes = ws_bytes - align_up(c.off, 256) - 256;
-  w.spmm_ws = c.take<float>(1);
+  SparseState sp{};
+  const int32_t* gate = nullptr;
+  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate));
   KeepSrc keep = make_keep(a);
   const int64_t nblk = (N + kRowsPerBlock - 1) / kRowsPerBlock;
 
@@ -547,34 +591,41 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   hipLaunchKernelGGL(k_readout_bwd, dim3(unsigned(nblk)), dim3(256), 0, s, a->dhead_in, a->h2,
                      a->batch, a->tree_ptr, N, B, kRowsPerBlock, w.d2, w.colpart);
   BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_colsum_reduce, dim3(1), dim3(128), 0, s, w.colpart, int(nblk), a->td_db2,
+  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, s, w.colpart, int(nblk), a->td_db2,
                      a->bu_db2);
   BGCN_CHECK_LAUNCH();
   // dZ2 = A^T dH2
-  BGCN_TRY(spmm_dir(a->td, true, N, w.d2, w.dz2, nullptr, BGCN_EPI_NONE, w, s));
-  BGCN_TRY(spmm_dir(a->bu, true, N, w.d2 + H, w.dz2 + H, nullptr, BGCN_EPI_NONE, w, s));
-  // dW2 (both directions, generated A2 operand)
+  BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.d2, w.dz2, nullptr, nullptr, BGCN_EPI_NONE, w, s));
+  // dW2 (both directions, generated A2 operand): the relu(H1) columns always by MFMA,
+  // the X[root] columns by MFMA (dense) or from the root non-zeros (sparse, finished
+  // in sparse_dw_cols below)
   timing_begin(3, s);
   hipLaunchKernelGGL(k_dw2, dim3(grid_for(H + F, 64), w.S2, 2), dim3(256), 0, s, a->x, a->ldx, F,
-                     a->h1, w.dz2, w.node_root, w.dw2_part, N, w.kchunk2, w.S2, keep);
+                     a->h1, w.dz2, w.node_root, w.dw2_part, N, w.kchunk2, w.S2, keep, gate);
   BGCN_CHECK_LAUNCH();
   timing_end(3, s);
   hipLaunchKernelGGL(k_reduce_dw2, dim3(grid_for(2 * H * (H + F), 256)), dim3(256), 0, s,
-                     w.dw2_part, w.S2, H + F, a->td_dw2, a->bu_dw2);
+                     w.dw2_part, w.S2, H + F, a->td_dw2, a->bu_dw2, gate);
   BGCN_CHECK_LAUNCH();
+  if (sp.mode != 1) BGCN_TRY(sparse_dw2_root_part(sp, a, w.dz2, keep, s));
   // dH1 through dropout and relu, db1
   hipLaunchKernelGGL(k_dh1, dim3(unsigned(nblk), 2), dim3(256), 0, s, w.dz2, a->h1, a->td_w2,
                      a->bu_w2, H + F, N, kRowsPerBlock, keep, w.dh1, w.colpart);
   BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_colsum_reduce, dim3(1), dim3(128), 0, s, w.colpart, int(nblk), a->td_db1,
+  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, s, w.colpart, int(nblk), a->td_db1,
                      a->bu_db1);
   BGCN_CHECK_LAUNCH();
   // dZ1 = A^T dH1
-  BGCN_TRY(spmm_dir(a->td, true, N, w.dh1, w.dz1, nullptr, BGCN_EPI_NONE, w, s));
-  BGCN_TRY(spmm_dir(a->bu, true, N, w.dh1 + H, w.dz1 + H, nullptr, BGCN_EPI_NONE, w, s));
-  // dW1 = [dZ1_td | dZ1_bu]^T X  (one pass over X for both directions)
+  BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.dh1, w.dz1, nullptr, nullptr, BGCN_EPI_NONE, w, s));
+  // dW1 = [dZ1_td | dZ1_bu]^T X  (one pass over X for both directions) - dense MFMA, or
+  // over the column-sorted non-zeros of X together with the dW2 root columns
+  if (sp.mode != 1) {
+    timing_begin(5, s);
+    BGCN_TRY(sparse_dw_cols(sp, a, w.dz1, w.node_root, keep, s));
+    timing_end(5, s);
+  }
   BGCN_TRY(gemm_tn_impl(w.dz1, 2 * H, a->x, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F, N,
-                        w.tn_ws, w.tn_bytes, s, 1));
+                        w.tn_ws, w.tn_bytes, s, 1, gate));
   return BGCN_OK;
 }
 

@@ -84,7 +84,7 @@ struct KeepSrc {
     if (words) return words[(size_t(dir) * size_t(num_nodes) + node) * size_t(nw) + w];
     return keep_word(seed, dir, node, w);
   }
-  __device__ __forceinline__ float scale() const { return training ? 2.0f : 1.0f; }
+  __host__ __device__ __forceinline__ float scale() const { return training ? 2.0f : 1.0f; }
 };
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -112,5 +112,10 @@ __device__ __forceinline__ float4 f4relu(float4 a) {
 }
 
 inline unsigned grid_for(int64_t n, int block) { return unsigned((n + block - 1) / block); }
+
+// Dense-path gate: the fused encoder runs the dense MFMA kernels only when the sparse
+// feature path is off (gate == nullptr: always run) or has flagged an overflow row
+// (*gate != 0).  Decided on the device, so no host sync.
+__device__ __forceinline__ bool gate_closed(const int32_t* gate) { return gate && *gate == 0; }
 
 }  // namespace bgcn

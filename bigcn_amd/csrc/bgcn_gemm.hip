@@ -14,7 +14,7 @@
 // MFMA 32x32x2 f32 operand maps (cdna_hip_programming.md section 3): lane l supplies
 // A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31]; D register r of lane l is
 // D[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31].
-#include "bgcn_common.h"
+#include "bgcn_internal.h"
 
 namespace bgcn {
 
@@ -35,7 +35,9 @@ __global__ __launch_bounds__(256) void k_gemm_xwt(const float* __restrict__ X, i
                                                   const float* __restrict__ W0,
                                                   const float* __restrict__ W1, int64_t ldw,
                                                   int64_t split, float* __restrict__ Y,
-                                                  int64_t ldy, int64_t M, int64_t Nc, int64_t K) {
+                                                  int64_t ldy, int64_t M, int64_t Nc, int64_t K,
+                                                  const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
   constexpr int BM = 64, BN = 128, LS = BK + 1;
   __shared__ float As[2][BM * LS];
   __shared__ float Bs[2][BN * LS];  // BKM: [BK][BN] (fits: BK*BN <= BN*LS)
@@ -174,7 +176,9 @@ template <bool VEC>
 __global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ G, int64_t ldg,
                                                  const float* __restrict__ X, int64_t ldx,
                                                  float* __restrict__ part, int64_t Mc, int64_t Nc,
-                                                 int64_t K, int64_t kchunk) {
+                                                 int64_t K, int64_t kchunk,
+                                                 const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
   constexpr int BM = 128, BN = 64;
   __shared__ float Gs[2][BK * BM];
   __shared__ float Xs[2][BK * BN];
@@ -260,7 +264,8 @@ __global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ G, in
 __global__ __launch_bounds__(256) void k_reduce_splits(const float* __restrict__ part, int S,
                                                        int64_t Mc, int64_t Nc, float* __restrict__ C0,
                                                        float* __restrict__ C1, int64_t ldc,
-                                                       int64_t split) {
+                                                       int64_t split, const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
   int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   int64_t total = Mc * Nc;
   if (idx >= total) return;
@@ -289,7 +294,7 @@ static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 int gemm_xwt_impl(const float* X, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
                   int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
-                  hipStream_t stream) {
+                  hipStream_t stream, const int32_t* gate) {
   BGCN_CHECK_ARG(X && W0 && Y, "null pointer");
   BGCN_CHECK_ARG(M >= 0 && Nc > 0 && K > 0, "bad shape");
   BGCN_CHECK_ARG(ldx >= K && ldw >= K && ldy >= Nc, "bad leading dimension");
@@ -300,10 +305,10 @@ int gemm_xwt_impl(const float* X, int64_t ldx, const float* W0, const float* W1,
   dim3 grid(grid_for(M, 64), grid_for(Nc, 128));
   if (vec)
     hipLaunchKernelGGL((k_gemm_xwt<true, false>), grid, dim3(256), 0, stream, X, ldx, W0, W1, ldw,
-                       split, Y, ldy, M, Nc, K);
+                       split, Y, ldy, M, Nc, K, gate);
   else
     hipLaunchKernelGGL((k_gemm_xwt<false, false>), grid, dim3(256), 0, stream, X, ldx, W0, W1,
-                       ldw, split, Y, ldy, M, Nc, K);
+                       ldw, split, Y, ldy, M, Nc, K, gate);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -319,10 +324,10 @@ int gemm_xw_impl(const float* X, int64_t ldx, const float* W, int64_t ldw, float
   dim3 grid(grid_for(M, 64), grid_for(Nc, 128));
   if (vec)
     hipLaunchKernelGGL((k_gemm_xwt<true, true>), grid, dim3(256), 0, stream, X, ldx, W,
-                       (const float*)nullptr, ldw, Nc, Y, ldy, M, Nc, K);
+                       (const float*)nullptr, ldw, Nc, Y, ldy, M, Nc, K, (const int32_t*)nullptr);
   else
     hipLaunchKernelGGL((k_gemm_xwt<false, true>), grid, dim3(256), 0, stream, X, ldx, W,
-                       (const float*)nullptr, ldw, Nc, Y, ldy, M, Nc, K);
+                       (const float*)nullptr, ldw, Nc, Y, ldy, M, Nc, K, (const int32_t*)nullptr);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -377,7 +382,7 @@ int colsum_impl(const float* A, int64_t lda, int64_t rows, int32_t C, float* out
 
 int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float* C0, float* C1,
                  int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
-                 size_t ws_bytes, hipStream_t stream, int timing_cls) {
+                 size_t ws_bytes, hipStream_t stream, int timing_cls, const int32_t* gate) {
   BGCN_CHECK_ARG(G && X && C0, "null pointer");
   BGCN_CHECK_ARG(Mc > 0 && Nc > 0 && K >= 0, "bad shape");
   BGCN_CHECK_ARG(ldg >= Mc && ldx >= Nc && ldc >= Nc, "bad leading dimension");
@@ -396,14 +401,14 @@ int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float
   timing_begin(timing_cls, stream);
   if (vec)
     hipLaunchKernelGGL(k_gemm_tn<true>, grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc, Nc,
-                       K, kchunk);
+                       K, kchunk, gate);
   else
     hipLaunchKernelGGL(k_gemm_tn<false>, grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc, Nc,
-                       K, kchunk);
+                       K, kchunk, gate);
   BGCN_CHECK_LAUNCH();
   timing_end(timing_cls, stream);
   hipLaunchKernelGGL(k_reduce_splits, dim3(grid_for(Mc * Nc, 256)), dim3(256), 0, stream, part, S,
-                     Mc, Nc, C0, C1, ldc, split);
+                     Mc, Nc, C0, C1, ldc, split, gate);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -414,7 +419,7 @@ extern "C" int bgcn_gemm_xwt(const float* X, int64_t ldx, const float* W0, const
                              int64_t ldw, int64_t split, float* Y, int64_t ldy, int64_t M,
                              int64_t Nc, int64_t K, bgcn_stream_t stream) {
   return bgcn::gemm_xwt_impl(X, ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K,
-                             reinterpret_cast<hipStream_t>(stream));
+                             reinterpret_cast<hipStream_t>(stream), nullptr);
 }
 
 extern "C" int bgcn_gemm_xw(const float* X, int64_t ldx, const float* W, int64_t ldw, float* Y,
@@ -442,5 +447,5 @@ extern "C" int bgcn_gemm_tn(const float* G, int64_t ldg, const float* X, int64_t
                             int64_t K, void* workspace, size_t workspace_bytes,
                             bgcn_stream_t stream) {
   return bgcn::gemm_tn_impl(G, ldg, X, ldx, C0, C1, ldc, split, Mc, Nc, K, workspace,
-                            workspace_bytes, reinterpret_cast<hipStream_t>(stream), -1);
+                            workspace_bytes, reinterpret_cast<hipStream_t>(stream), -1, nullptr);
 }

@@ -3,212 +3,369 @@
 // Restates PyG >= 2.0 gcn_norm(improved=False, add_self_loops=True,
 // flow='source_to_target') as used by every GCNConv call of the reference
 // (model/Twitter/BiGCN_Twitter.py:42,56,92,105; explicit call form at
-// explain_PHEME.py:62-63), with the PyG 1.3.2 source-degree convention selectable.
+// explain_PHEME.py:62-63), with the PyG 1.3.2 source-degree convention selectable:
+//   * existing self loops are removed and one loop (i, i) per node is appended after
+//     the edges (its weight = the removed loop's weight, else 1);
+//   * deg[i] = sum of edge weights at the target (col) - or source (row) - of i;
+//   * norm_e = deg^-1/2[src] * w_e * deg^-1/2[dst]  (inf -> 0).
 //
-// Plan (deterministic, no float atomics):
-//   1. keys: key_t[e] = target, key_s[e] = source, or N for self loops / invalid
-//      edges (sorted to the end and dropped); value = e.
-//   2. two stable LSD radix sorts (rocPRIM) -> edges grouped by target / by source
-//      in their original order (the order PyG's scatter-add sums them in).
-//   3. per node: segment bounds by binary search, weighted degree, D^-1/2, row
-//      pointers (each row gets one extra slot for its self loop, placed last),
-//      self-loop entries.
-//   4. per sorted edge: CSR entry at position j + key (j = sorted position).
-#include <cstring>
-
-#include <rocprim/rocprim.hpp>
-
+// Both orientations are stable counting sorts of the edge list (entries of a row keep
+// edge order, the self loop last = PyG's scatter-add summation order), built with no
+// float atomics and no general sort:
+//   count (int atomics) -> exclusive scan (3 launches) -> place.
+// Placement: when every key's edges form one contiguous run in edge order (always the
+// case for propagation trees: TD edges are sorted by (parent, child), each child has one
+// parent; BU is the flip) an edge's rank in its row is e - run_start(key).  Otherwise a
+// device-side flag selects the general placement (atomic slots + an O(d) rank per entry
+// that restores edge order).  The choice is made on the device: no host sync.
+//
+// Several graphs are built per launch sequence (blockIdx.y = graph): the fused step
+// builds TD and BU together.
 #include "bgcn_common.h"
 
 namespace bgcn {
 namespace {
 
-__global__ void k_edge_keys(const int64_t* __restrict__ ei, int64_t E, int64_t N,
-                            uint32_t* __restrict__ key_t, uint32_t* __restrict__ key_s,
-                            uint32_t* __restrict__ val, int32_t* __restrict__ status) {
-  int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  int64_t src = ei[e], dst = ei[E + e];
-  bool valid = src >= 0 && src < N && dst >= 0 && dst < N;
-  if (!valid && status) atomicOr(status, 1);
-  bool keep = valid && src != dst;  // existing self loops are replaced by the appended ones
-  key_t[e] = keep ? uint32_t(dst) : uint32_t(N);
-  key_s[e] = keep ? uint32_t(src) : uint32_t(N);
-  val[e] = uint32_t(e);
-}
+constexpr int kMaxGraphs = 2;
+constexpr int kScanThreads = 256, kScanItems = 16, kScanChunk = kScanThreads * kScanItems;
 
-__device__ __forceinline__ int64_t lower_bound_u32(const uint32_t* a, int64_t n, uint32_t x) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (a[mid] < x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// One thread per node i in [0, N].  Thread N only writes the terminal pointers.
-__global__ void k_nodes(const uint32_t* __restrict__ st_keys, const uint32_t* __restrict__ st_vals,
-                        const uint32_t* __restrict__ ss_keys, const uint32_t* __restrict__ ss_vals,
-                        const float* __restrict__ ew, int64_t E, int64_t N, int degree_on,
-                        float* __restrict__ dinv, int32_t* __restrict__ t_ptr,
-                        int32_t* __restrict__ s_ptr) {
-  int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i > N) return;
-  int64_t t0 = lower_bound_u32(st_keys, E, uint32_t(i));
-  int64_t s0 = lower_bound_u32(ss_keys, E, uint32_t(i));
-  t_ptr[i] = int32_t(t0 + i);
-  s_ptr[i] = int32_t(s0 + i);
-  if (i == N) return;
-  const uint32_t* keys = degree_on == BGCN_DEGREE_ON_COL ? st_keys : ss_keys;
-  const uint32_t* vals = degree_on == BGCN_DEGREE_ON_COL ? st_vals : ss_vals;
-  int64_t a = degree_on == BGCN_DEGREE_ON_COL ? t0 : s0;
-  int64_t b = lower_bound_u32(keys, E, uint32_t(i + 1));
-  // scatter_add over the final edge list in order: real edges, then the loop (w=1)
-  float deg = 0.f;
-  if (ew) {
-    for (int64_t j = a; j < b; ++j) deg += ew[vals[j]];
-  } else {
-    for (int64_t j = a; j < b; ++j) deg += 1.f;
-  }
-  deg += 1.f;
-  float d = deg > 0.f ? 1.0f / sqrtf(deg) : 0.f;  // pow(-0.5); inf -> 0
-  if (isinf(d)) d = 0.f;
-  dinv[i] = d;
-}
-
-__global__ void k_self_loops(const int32_t* __restrict__ t_ptr, const int32_t* __restrict__ s_ptr,
-                             const float* __restrict__ dinv, int64_t N,
-                             int32_t* __restrict__ t_row, int32_t* __restrict__ t_col,
-                             float* __restrict__ t_w, int32_t* __restrict__ s_row,
-                             int32_t* __restrict__ s_col, float* __restrict__ s_w) {
-  int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  float d = dinv[i];
-  float w = (d * 1.0f) * d;  // dinv[row] * w * dinv[col]
-  int32_t pt = t_ptr[i + 1] - 1, ps = s_ptr[i + 1] - 1;
-  t_row[pt] = int32_t(i); t_col[pt] = int32_t(i); t_w[pt] = w;
-  s_row[ps] = int32_t(i); s_col[ps] = int32_t(i); s_w[ps] = w;
-}
-
-// One thread per sorted edge position j (both orientations).
-__global__ void k_fill(const int64_t* __restrict__ ei, const float* __restrict__ ew, int64_t E,
-                       int64_t N, const uint32_t* __restrict__ st_keys,
-                       const uint32_t* __restrict__ st_vals, const uint32_t* __restrict__ ss_keys,
-                       const uint32_t* __restrict__ ss_vals, const float* __restrict__ dinv,
-                       int32_t* __restrict__ t_row, int32_t* __restrict__ t_col,
-                       float* __restrict__ t_w, int32_t* __restrict__ s_row,
-                       int32_t* __restrict__ s_col, float* __restrict__ s_w) {
-  int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j >= E) return;
-  uint32_t kt = st_keys[j];
-  if (kt < uint32_t(N)) {
-    uint32_t e = st_vals[j];
-    int64_t src = ei[e];
-    float w = ew ? ew[e] : 1.f;
-    int64_t pos = j + kt;
-    t_row[pos] = int32_t(kt);
-    t_col[pos] = int32_t(src);
-    t_w[pos] = (dinv[src] * w) * dinv[kt];
-  }
-  uint32_t ks = ss_keys[j];
-  if (ks < uint32_t(N)) {
-    uint32_t e = ss_vals[j];
-    int64_t dst = ei[E + e];
-    float w = ew ? ew[e] : 1.f;
-    int64_t pos = j + ks;
-    s_row[pos] = int32_t(ks);
-    s_col[pos] = int32_t(dst);
-    s_w[pos] = (dinv[ks] * w) * dinv[dst];
-  }
-}
-
-int key_bits(int64_t N) {
-  int bits = 1;
-  while ((int64_t(1) << bits) <= N) ++bits;  // keys in [0, N]
-  return bits;
-}
-
-struct GraphWs {
-  uint32_t *key_t, *key_s, *val, *st_keys, *st_vals, *ss_keys, *ss_vals;
+struct GraphIO {
+  const int64_t* ei;
+  const float* ew;
+  int64_t E;
+  int32_t *t_ptr, *t_row, *t_col;
+  float* t_w;
+  int32_t *s_ptr, *s_row, *s_col;
+  float* s_w;
+  int32_t* status;
+  // scratch
+  int32_t *cnt_t, *cnt_s, *cur_t, *cur_s, *loop_eid;  // zero-initialised block
+  int32_t* flags;                                        // [0] runs_t [1] runs_s [2] excluded [3] grouped_t [4] grouped_s
+  int32_t *run_t, *run_s;                                // run start per key
+  int32_t *tmp_t, *tmp_s;                                // general path: eid per slot
+  int32_t* bsum;                                         // [nb][4]: sum_t, sum_s, distinct_t, distinct_s
   float* dinv;
-  void* sort_tmp;
-  size_t sort_bytes;
 };
 
-size_t sort_tmp_bytes(int64_t E, int64_t N) {
-  size_t bytes = 0;
-  if (E == 0) return 0;
-  (void)rocprim::radix_sort_pairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                            (uint32_t*)nullptr, (uint32_t*)nullptr, size_t(E), 0, key_bits(N));
-  return bytes;
+struct GraphBatch {
+  GraphIO g[kMaxGraphs];
+  int64_t N;
+  int degree_on;
+};
+
+__device__ __forceinline__ bool edge_kept(const int64_t* ei, int64_t E, int64_t N, int64_t e,
+                                          int64_t& src, int64_t& dst, bool& valid) {
+  src = ei[e];
+  dst = ei[E + e];
+  valid = src >= 0 && src < N && dst >= 0 && dst < N;
+  return valid && src != dst;
 }
 
-size_t carve_graph_ws(Carve& c, int64_t E, int64_t N, GraphWs* g) {
-  size_t e = size_t(E > 0 ? E : 1);
-  GraphWs t;
-  t.key_t = c.take<uint32_t>(e);
-  t.key_s = c.take<uint32_t>(e);
-  t.val = c.take<uint32_t>(e);
-  t.st_keys = c.take<uint32_t>(e);
-  t.st_vals = c.take<uint32_t>(e);
-  t.ss_keys = c.take<uint32_t>(e);
-  t.ss_vals = c.take<uint32_t>(e);
-  t.dinv = c.take<float>(size_t(N > 0 ? N : 1));
-  t.sort_bytes = sort_tmp_bytes(E, N);
-  t.sort_tmp = c.take<char>(t.sort_bytes > 0 ? t.sort_bytes : 1);
-  if (g) *g = t;
+__global__ void k_count(GraphBatch gb) {
+  GraphIO& G = gb.g[blockIdx.y];
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= G.E) return;
+  const int64_t N = gb.N;
+  int64_t src, dst;
+  bool valid;
+  bool keep = edge_kept(G.ei, G.E, N, e, src, dst, valid);
+  if (!valid) {
+    if (G.status) atomicOr(G.status, 1);
+    atomicOr(&G.flags[2], 1);
+    return;
+  }
+  if (!keep) {  // an input self loop: removed, its weight becomes the loop weight (last wins)
+    atomicMax(&G.loop_eid[src], int32_t(e + 1));
+    atomicOr(&G.flags[2], 1);
+    return;
+  }
+  atomicAdd(&G.cnt_t[dst], 1);
+  atomicAdd(&G.cnt_s[src], 1);
+  int64_t psrc = -1, pdst = -1;
+  if (e > 0) {
+    bool pv;
+    edge_kept(G.ei, G.E, N, e - 1, psrc, pdst, pv);
+  }
+  if (e == 0 || pdst != dst) {
+    G.run_t[dst] = int32_t(e);
+    atomicAdd(&G.flags[0], 1);
+  }
+  if (e == 0 || psrc != src) {
+    G.run_s[src] = int32_t(e);
+    atomicAdd(&G.flags[1], 1);
+  }
+}
+
+// block partial sums of (cnt + 1) and of (cnt > 0) over [0, N)
+__global__ __launch_bounds__(kScanThreads) void k_scan_blocks(GraphBatch gb) {
+  GraphIO& G = gb.g[blockIdx.y];
+  const int64_t N = gb.N;
+  const int64_t base = int64_t(blockIdx.x) * kScanChunk;
+  int st = 0, ss = 0, dt = 0, ds = 0;
+  for (int k = 0; k < kScanItems; ++k) {
+    int64_t i = base + int64_t(k) * kScanThreads + threadIdx.x;
+    if (i < N) {
+      int ct = G.cnt_t[i], cs = G.cnt_s[i];
+      st += ct + 1; ss += cs + 1; dt += ct > 0; ds += cs > 0;
+    }
+  }
+  __shared__ int red[4][kScanThreads];
+  red[0][threadIdx.x] = st; red[1][threadIdx.x] = ss; red[2][threadIdx.x] = dt; red[3][threadIdx.x] = ds;
+  __syncthreads();
+  for (int o = kScanThreads / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int q = 0; q < 4; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) G.bsum[int64_t(blockIdx.x) * 4 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// exclusive scan of the block sums (one block per graph); grouped flags
+__global__ __launch_bounds__(kScanThreads) void k_scan_top(GraphBatch gb, int nb) {
+  GraphIO& G = gb.g[blockIdx.y];
+  __shared__ int sh[2][kScanThreads];
+  __shared__ int carry[2];
+  __shared__ int dist[2];
+  if (threadIdx.x < 2) { carry[threadIdx.x] = 0; dist[threadIdx.x] = 0; }
+  __syncthreads();
+  for (int c0 = 0; c0 < nb; c0 += kScanThreads) {
+    int b = c0 + threadIdx.x;
+    int vt = b < nb ? G.bsum[b * 4 + 0] : 0, vs = b < nb ? G.bsum[b * 4 + 1] : 0;
+    int dt = b < nb ? G.bsum[b * 4 + 2] : 0, ds = b < nb ? G.bsum[b * 4 + 3] : 0;
+    sh[0][threadIdx.x] = vt; sh[1][threadIdx.x] = vs;
+    __syncthreads();
+    for (int o = 1; o < kScanThreads; o <<= 1) {   // Hillis-Steele inclusive scan
+      int a0 = threadIdx.x >= o ? sh[0][threadIdx.x - o] : 0;
+      int a1 = threadIdx.x >= o ? sh[1][threadIdx.x - o] : 0;
+      __syncthreads();
+      sh[0][threadIdx.x] += a0; sh[1][threadIdx.x] += a1;
+      __syncthreads();
+    }
+    if (b < nb) {   // exclusive offsets, reuse the bsum slots 0/1
+      G.bsum[b * 4 + 0] = carry[0] + sh[0][threadIdx.x] - vt;
+      G.bsum[b * 4 + 1] = carry[1] + sh[1][threadIdx.x] - vs;
+    }
+    atomicAdd(&dist[0], dt);
+    atomicAdd(&dist[1], ds);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      carry[0] += sh[0][kScanThreads - 1];
+      carry[1] += sh[1][kScanThreads - 1];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    bool clean = G.flags[2] == 0;
+    G.flags[3] = (clean && G.flags[0] == dist[0]) ? 1 : 0;
+    G.flags[4] = (clean && G.flags[1] == dist[1]) ? 1 : 0;
+  }
+}
+
+// row pointers: ptr[i] = offset + local exclusive scan of (cnt + 1); ptr[N] = total
+__global__ __launch_bounds__(kScanThreads) void k_scan_write(GraphBatch gb) {
+  GraphIO& G = gb.g[blockIdx.y];
+  const int64_t N = gb.N;
+  const int64_t base = int64_t(blockIdx.x) * kScanChunk + int64_t(threadIdx.x) * kScanItems;
+  // thread-contiguous items for the write pass
+  int vt[kScanItems], vs[kScanItems];
+  int st = 0, ss = 0;
+  for (int k = 0; k < kScanItems; ++k) {
+    int64_t i = base + k;
+    vt[k] = i < N ? G.cnt_t[i] + 1 : 0;
+    vs[k] = i < N ? G.cnt_s[i] + 1 : 0;
+    st += vt[k]; ss += vs[k];
+  }
+  __shared__ int sh[2][kScanThreads];
+  sh[0][threadIdx.x] = st; sh[1][threadIdx.x] = ss;
+  __syncthreads();
+  for (int o = 1; o < kScanThreads; o <<= 1) {
+    int a0 = threadIdx.x >= o ? sh[0][threadIdx.x - o] : 0;
+    int a1 = threadIdx.x >= o ? sh[1][threadIdx.x - o] : 0;
+    __syncthreads();
+    sh[0][threadIdx.x] += a0; sh[1][threadIdx.x] += a1;
+    __syncthreads();
+  }
+  int ot = G.bsum[int64_t(blockIdx.x) * 4 + 0] + sh[0][threadIdx.x] - st;
+  int os = G.bsum[int64_t(blockIdx.x) * 4 + 1] + sh[1][threadIdx.x] - ss;
+  for (int k = 0; k < kScanItems; ++k) {
+    int64_t i = base + k;
+    if (i < N) { G.t_ptr[i] = ot; G.s_ptr[i] = os; }
+    if (i == N) { G.t_ptr[N] = ot; G.s_ptr[N] = os; }
+    ot += vt[k]; os += vs[k];
+  }
+}
+
+// grouped: direct placement.  general: atomic slot + eid (ordered by k_fill_rank).
+__global__ void k_fill(GraphBatch gb) {
+  GraphIO& G = gb.g[blockIdx.y];
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= G.E) return;
+  int64_t src, dst;
+  bool valid;
+  if (!edge_kept(G.ei, G.E, gb.N, e, src, dst, valid)) return;
+  const float w = G.ew ? G.ew[e] : 1.f;
+  if (G.flags[3]) {
+    int64_t p = G.t_ptr[dst] + (e - G.run_t[dst]);
+    G.t_row[p] = int32_t(dst); G.t_col[p] = int32_t(src); G.t_w[p] = w;
+  } else {
+    int64_t p = G.t_ptr[dst] + atomicAdd(&G.cur_t[dst], 1);
+    G.tmp_t[p] = int32_t(e);
+  }
+  if (G.flags[4]) {
+    int64_t p = G.s_ptr[src] + (e - G.run_s[src]);
+    G.s_row[p] = int32_t(src); G.s_col[p] = int32_t(dst); G.s_w[p] = w;
+  } else {
+    int64_t p = G.s_ptr[src] + atomicAdd(&G.cur_s[src], 1);
+    G.tmp_s[p] = int32_t(e);
+  }
+}
+
+// general path only: rank = number of entries of the row with a smaller edge id
+__global__ void k_fill_rank(GraphBatch gb) {
+  GraphIO& G = gb.g[blockIdx.y];
+  if (G.flags[3] && G.flags[4]) return;
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= G.E) return;
+  int64_t src, dst;
+  bool valid;
+  if (!edge_kept(G.ei, G.E, gb.N, e, src, dst, valid)) return;
+  const float w = G.ew ? G.ew[e] : 1.f;
+  if (!G.flags[3]) {
+    int64_t a = G.t_ptr[dst], n = G.cnt_t[dst];
+    int r = 0;
+    for (int64_t q = 0; q < n; ++q) r += G.tmp_t[a + q] < e;
+    G.t_row[a + r] = int32_t(dst); G.t_col[a + r] = int32_t(src); G.t_w[a + r] = w;
+  }
+  if (!G.flags[4]) {
+    int64_t a = G.s_ptr[src], n = G.cnt_s[src];
+    int r = 0;
+    for (int64_t q = 0; q < n; ++q) r += G.tmp_s[a + q] < e;
+    G.s_row[a + r] = int32_t(src); G.s_col[a + r] = int32_t(dst); G.s_w[a + r] = w;
+  }
+}
+
+// self loops (raw loop weight) + degree + D^-1/2
+__global__ void k_nodes(GraphBatch gb) {
+  GraphIO& G = gb.g[blockIdx.y];
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= gb.N) return;
+  const int le = G.loop_eid[i];
+  const float lw = (le > 0 && G.ew) ? G.ew[le - 1] : 1.f;
+  const int64_t pt = G.t_ptr[i + 1] - 1, ps = G.s_ptr[i + 1] - 1;
+  G.t_row[pt] = int32_t(i); G.t_col[pt] = int32_t(i); G.t_w[pt] = lw;
+  G.s_row[ps] = int32_t(i); G.s_col[ps] = int32_t(i); G.s_w[ps] = lw;
+  // scatter_add over the final edge list in order (real edges, then the loop)
+  const bool col = gb.degree_on == BGCN_DEGREE_ON_COL;
+  const int64_t a = col ? G.t_ptr[i] : G.s_ptr[i];
+  const float* wr = col ? G.t_w : G.s_w;
+  float deg = 0.f;
+  for (int64_t p = a; p < (col ? pt : ps); ++p) deg += wr[p];
+  deg += lw;
+  float d = 1.0f / sqrtf(deg);  // pow(-0.5)
+  if (isinf(d)) d = 0.f;
+  G.dinv[i] = d;
+}
+
+__global__ void k_normalize(GraphBatch gb) {
+  GraphIO& G = gb.g[blockIdx.y];
+  const int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= int64_t(G.t_ptr[gb.N])) return;
+  // dinv[row] * w * dinv[col] with row = source, col = target (PyG order)
+  G.t_w[p] = (G.dinv[G.t_col[p]] * G.t_w[p]) * G.dinv[G.t_row[p]];
+  G.s_w[p] = (G.dinv[G.s_row[p]] * G.s_w[p]) * G.dinv[G.s_col[p]];
+}
+
+struct Scratch {
+  size_t zero_off, zero_bytes;
+};
+
+size_t carve(Carve& c, int64_t E, int64_t N, GraphIO* G) {
+  const size_t n = size_t(N > 0 ? N : 1), cap = size_t(E + N > 0 ? E + N : 1);
+  const int64_t nb = (N + 1 + kScanChunk - 1) / kScanChunk;
+  GraphIO t{};
+  // zero-initialised block first (one memset)
+  t.cnt_t = c.take<int32_t>(n);
+  t.cnt_s = c.take<int32_t>(n);
+  t.cur_t = c.take<int32_t>(n);
+  t.cur_s = c.take<int32_t>(n);
+  t.loop_eid = c.take<int32_t>(n);
+  t.flags = c.take<int32_t>(8);
+  t.run_t = c.take<int32_t>(n);
+  t.run_s = c.take<int32_t>(n);
+  t.tmp_t = c.take<int32_t>(cap);
+  t.tmp_s = c.take<int32_t>(cap);
+  t.bsum = c.take<int32_t>(size_t(nb) * 4);
+  t.dinv = c.take<float>(n);
+  if (G) *G = t;
   return c.off;
 }
 
 }  // namespace
 
-int build_graph_impl(const int64_t* ei, const float* ew, int64_t E, int64_t N, int degree_on,
-                     int32_t* t_ptr, int32_t* t_row, int32_t* t_col, float* t_w, int32_t* s_ptr,
-                     int32_t* s_row, int32_t* s_col, float* s_w, int32_t* status, void* ws,
-                     size_t ws_bytes, hipStream_t stream) {
-  BGCN_CHECK_ARG(N > 0 && N < (int64_t(1) << 31) - 1, "num_nodes out of range");
-  BGCN_CHECK_ARG(E >= 0 && E + N < (int64_t(1) << 31), "num_edges out of range");
-  BGCN_CHECK_ARG(degree_on == BGCN_DEGREE_ON_COL || degree_on == BGCN_DEGREE_ON_ROW,
-                 "degree_on must be 0 (col) or 1 (row)");
-  BGCN_CHECK_ARG(t_ptr && t_row && t_col && t_w && s_ptr && s_row && s_col && s_w,
-                 "null output pointer");
-  BGCN_CHECK_ARG(E == 0 || ei, "null edge_index");
-  Carve c(ws, ws_bytes);
-  GraphWs g;
-  carve_graph_ws(c, E, N, &g);
-  BGCN_CHECK_ARG(c.ok() && ws, "workspace too small");
-  const int blk = 256;
-  if (E > 0) {
-    hipLaunchKernelGGL(k_edge_keys, dim3(grid_for(E, blk)), dim3(blk), 0, stream, ei, E, N,
-                       g.key_t, g.key_s, g.val, status);
-    BGCN_CHECK_LAUNCH();
-    int bits = key_bits(N);
-    size_t tb = g.sort_bytes;
-    BGCN_CHECK_HIP(rocprim::radix_sort_pairs(g.sort_tmp, tb, g.key_t, g.st_keys, g.val,
-                                             g.st_vals, size_t(E), 0, bits, stream));
-    tb = g.sort_bytes;
-    BGCN_CHECK_HIP(rocprim::radix_sort_pairs(g.sort_tmp, tb, g.key_s, g.ss_keys, g.val,
-                                             g.ss_vals, size_t(E), 0, bits, stream));
-  }
-  hipLaunchKernelGGL(k_nodes, dim3(grid_for(N + 1, blk)), dim3(blk), 0, stream, g.st_keys,
-                     g.st_vals, g.ss_keys, g.ss_vals, ew, E, N, degree_on, g.dinv, t_ptr, s_ptr);
-  BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_self_loops, dim3(grid_for(N, blk)), dim3(blk), 0, stream, t_ptr, s_ptr,
-                     g.dinv, N, t_row, t_col, t_w, s_row, s_col, s_w);
-  BGCN_CHECK_LAUNCH();
-  if (E > 0) {
-    hipLaunchKernelGGL(k_fill, dim3(grid_for(E, blk)), dim3(blk), 0, stream, ei, ew, E, N,
-                       g.st_keys, g.st_vals, g.ss_keys, g.ss_vals, g.dinv, t_row, t_col, t_w,
-                       s_row, s_col, s_w);
-    BGCN_CHECK_LAUNCH();
-  }
-  return BGCN_OK;
-}
-
 size_t graph_ws_size(int64_t E, int64_t N) {
   Carve c(nullptr, 0);
-  carve_graph_ws(c, E, N, nullptr);
+  carve(c, E, N, nullptr);
   return c.off + 256;
+}
+
+struct GraphArgs {
+  const int64_t* ei; const float* ew; int64_t E;
+  int32_t *t_ptr, *t_row, *t_col; float* t_w;
+  int32_t *s_ptr, *s_row, *s_col; float* s_w;
+  int32_t* status; void* ws; size_t ws_bytes;
+};
+
+int build_graphs_impl(const GraphArgs* ga, int count, int64_t N, int degree_on, hipStream_t s) {
+  BGCN_CHECK_ARG(count >= 1 && count <= kMaxGraphs, "1 or 2 graphs per call");
+  BGCN_CHECK_ARG(N > 0 && N < (int64_t(1) << 31) - 1, "num_nodes out of range");
+  BGCN_CHECK_ARG(degree_on == BGCN_DEGREE_ON_COL || degree_on == BGCN_DEGREE_ON_ROW,
+                 "degree_on must be 0 (col) or 1 (row)");
+  GraphBatch gb{};
+  gb.N = N;
+  gb.degree_on = degree_on;
+  int64_t Emax = 0;
+  for (int k = 0; k < count; ++k) {
+    const GraphArgs& a = ga[k];
+    BGCN_CHECK_ARG(a.E >= 0 && a.E + N < (int64_t(1) << 31), "num_edges out of range");
+    BGCN_CHECK_ARG(a.t_ptr && a.t_row && a.t_col && a.t_w && a.s_ptr && a.s_row && a.s_col && a.s_w,
+                   "null output pointer");
+    BGCN_CHECK_ARG(a.E == 0 || a.ei, "null edge_index");
+    BGCN_CHECK_ARG(a.ws && a.ws_bytes >= graph_ws_size(a.E, N), "workspace too small");
+    Carve c(a.ws, a.ws_bytes);
+    GraphIO& G = gb.g[k];
+    carve(c, a.E, N, &G);
+    G.ei = a.ei; G.ew = a.ew; G.E = a.E;
+    G.t_ptr = a.t_ptr; G.t_row = a.t_row; G.t_col = a.t_col; G.t_w = a.t_w;
+    G.s_ptr = a.s_ptr; G.s_row = a.s_row; G.s_col = a.s_col; G.s_w = a.s_w;
+    G.status = a.status;
+    const size_t zero_bytes = reinterpret_cast<char*>(G.run_t) - reinterpret_cast<char*>(G.cnt_t);
+    BGCN_CHECK_HIP(hipMemsetAsync(G.cnt_t, 0, zero_bytes, s));
+    Emax = a.E > Emax ? a.E : Emax;
+  }
+  const unsigned gy = unsigned(count);
+  const int blk = 256;
+  const int64_t nb = (N + 1 + kScanChunk - 1) / kScanChunk;
+  if (Emax > 0) {
+    hipLaunchKernelGGL(k_count, dim3(grid_for(Emax, blk), gy), dim3(blk), 0, s, gb);
+    BGCN_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(k_scan_blocks, dim3(unsigned(nb), gy), dim3(kScanThreads), 0, s, gb);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_scan_top, dim3(1, gy), dim3(kScanThreads), 0, s, gb, int(nb));
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_scan_write, dim3(unsigned(nb), gy), dim3(kScanThreads), 0, s, gb);
+  BGCN_CHECK_LAUNCH();
+  if (Emax > 0) {
+    hipLaunchKernelGGL(k_fill, dim3(grid_for(Emax, blk), gy), dim3(blk), 0, s, gb);
+    BGCN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_fill_rank, dim3(grid_for(Emax, blk), gy), dim3(blk), 0, s, gb);
+    BGCN_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(k_nodes, dim3(grid_for(N, blk), gy), dim3(blk), 0, s, gb);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_normalize, dim3(grid_for(Emax + N, blk), gy), dim3(blk), 0, s, gb);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
 }
 
 }  // namespace bgcn
@@ -223,7 +380,30 @@ extern "C" int bgcn_build_graph(const int64_t* edge_index, const float* edge_wei
                                 int32_t* s_ptr, int32_t* s_row, int32_t* s_col, float* s_w,
                                 int32_t* status, void* workspace, size_t workspace_bytes,
                                 bgcn_stream_t stream) {
-  return bgcn::build_graph_impl(edge_index, edge_weight, num_edges, num_nodes, degree_on, t_ptr,
-                                t_row, t_col, t_w, s_ptr, s_row, s_col, s_w, status, workspace,
-                                workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+  bgcn::GraphArgs a{edge_index, edge_weight, num_edges, t_ptr, t_row, t_col, t_w,
+                    s_ptr, s_row, s_col, s_w, status, workspace, workspace_bytes};
+  return bgcn::build_graphs_impl(&a, 1, num_nodes, degree_on, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t bgcn_graph_pair_workspace_size(int64_t td_num_edges, int64_t bu_num_edges,
+                                                int64_t num_nodes) {
+  int64_t e = td_num_edges > bu_num_edges ? td_num_edges : bu_num_edges;
+  return 2 * bgcn::align_up(bgcn::graph_ws_size(e, num_nodes), 256);
+}
+
+extern "C" int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_num_edges,
+                                     const int64_t* bu_edge_index, int64_t bu_num_edges,
+                                     int64_t num_nodes, int degree_on, const bgcn_csr_out* td,
+                                     const bgcn_csr_out* bu, int32_t* status, void* workspace,
+                                     size_t workspace_bytes, bgcn_stream_t stream) {
+  using bgcn::GraphArgs;
+  if (!td || !bu) return bgcn::fail(BGCN_EINVAL, "null csr descriptor");
+  const size_t half = workspace_bytes / 2 / 256 * 256;
+  char* ws = static_cast<char*>(workspace);
+  GraphArgs a[2] = {
+      {td_edge_index, nullptr, td_num_edges, td->t_ptr, td->t_row, td->t_col, td->t_w, td->s_ptr,
+       td->s_row, td->s_col, td->s_w, status, ws, half},
+      {bu_edge_index, nullptr, bu_num_edges, bu->t_ptr, bu->t_row, bu->t_col, bu->t_w, bu->s_ptr,
+       bu->s_row, bu->s_col, bu->s_w, status, ws ? ws + half : nullptr, half}};
+  return bgcn::build_graphs_impl(a, 2, num_nodes, degree_on, reinterpret_cast<hipStream_t>(stream));
 }

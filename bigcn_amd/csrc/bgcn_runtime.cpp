@@ -1,4 +1,4 @@
-// Host runtime of libbgcn: thread-local error string, ABI version, and the
+// Host runtime of libbgcn: thread-local error string, ABI version, and the (process-global)
 // kernel-timing hook bench.py uses to measure the dominant kernel with HIP events
 // on the stream it is launched on.
 #include <hip/hip_runtime.h>
@@ -12,17 +12,21 @@
 namespace bgcn {
 
 namespace {
+constexpr int kTimingClasses = 8;
 thread_local std::string g_err;
 
 struct TimingState {
   bool enabled = false;
   struct Pair { hipEvent_t a, b; };
-  std::vector<Pair> pending[4];
-  hipEvent_t open[4] = {nullptr, nullptr, nullptr, nullptr};
-  double total_ms[4] = {0, 0, 0, 0};
-  int64_t count[4] = {0, 0, 0, 0};
+  std::vector<Pair> pending[kTimingClasses];
+  hipEvent_t open[kTimingClasses] = {};
+  double total_ms[kTimingClasses] = {};
+  int64_t count[kTimingClasses] = {};
 };
-thread_local TimingState g_tm;
+// process-global: the fused backward runs on autograd's device thread, the forward on
+// the caller's thread; both record into the same state
+TimingState g_tm;
+std::mutex g_tm_mu;
 }  // namespace
 
 void set_error(const std::string& msg) { g_err = msg; }
@@ -33,7 +37,8 @@ int fail(int code, const std::string& msg) {
 }
 
 void timing_begin(int cls, hipStream_t s) {
-  if (!g_tm.enabled || cls < 0 || cls > 3) return;
+  if (!g_tm.enabled || cls < 0 || cls >= kTimingClasses) return;
+  std::lock_guard<std::mutex> lk(g_tm_mu);
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return;
   (void)hipEventRecord(e, s);
@@ -41,7 +46,9 @@ void timing_begin(int cls, hipStream_t s) {
 }
 
 void timing_end(int cls, hipStream_t s) {
-  if (!g_tm.enabled || cls < 0 || cls > 3 || !g_tm.open[cls]) return;
+  if (!g_tm.enabled || cls < 0 || cls >= kTimingClasses) return;
+  std::lock_guard<std::mutex> lk(g_tm_mu);
+  if (!g_tm.open[cls]) return;
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return;
   (void)hipEventRecord(e, s);
@@ -56,9 +63,10 @@ extern "C" int bgcn_abi_version(void) { return BGCN_ABI_VERSION; }
 extern "C" const char* bgcn_last_error(void) { return bgcn::g_err.c_str(); }
 
 extern "C" int bgcn_set_kernel_timing(int enable) {
+  std::lock_guard<std::mutex> lk(bgcn::g_tm_mu);
   auto& t = bgcn::g_tm;
   t.enabled = enable != 0;
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < bgcn::kTimingClasses; ++c) {
     t.total_ms[c] = 0;
     t.count[c] = 0;
   }
@@ -67,8 +75,9 @@ extern "C" int bgcn_set_kernel_timing(int enable) {
 
 // Synchronises on the recorded events (call outside the timed region).
 extern "C" int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* launches) {
+  std::lock_guard<std::mutex> lk(bgcn::g_tm_mu);
   auto& t = bgcn::g_tm;
-  if (kernel_class < 0 || kernel_class > 3) return bgcn::fail(BGCN_EINVAL, "bad kernel class");
+  if (kernel_class < 0 || kernel_class >= bgcn::kTimingClasses) return bgcn::fail(BGCN_EINVAL, "bad kernel class");
   auto& v = t.pending[kernel_class];
   for (auto& p : v) {
     float ms = 0.f;

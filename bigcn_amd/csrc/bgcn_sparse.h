@@ -1,0 +1,41 @@
+// Sparse-feature path of the fused encoder (see bgcn_sparse.hip).
+#pragma once
+
+#include "bgcn_common.h"
+
+namespace bgcn {
+
+constexpr int kCap = 32;     // max non-zeros per feature row on the sparse path
+constexpr int kChunk = 256;  // nodes per work item of the dW2 root-column pass
+
+struct SparseState {
+  int mode;        // 0 auto, 1 dense (sparse kernels idle), 2 sparse preferred (same as auto)
+  int64_t N, F, B;
+  // saved with the activations (caller-owned)
+  int32_t* flags;  // [0] = some row has > kCap non-zeros -> dense path
+  int32_t* nnz;    // [N]
+  int32_t* cols;   // [N][kCap]
+  float* vals;     // [N][kCap]
+  // step scratch
+  float* w1t;      // [F][128]     = [W1_td ; W1_bu]^T
+  float* w2t;      // [2][64+F][64] = W2_d^T
+  int max_items;
+  int32_t *item_tree, *item_chunk, *tree_item0;
+  float* root_part;  // [2][max_items][kCap][64]
+  uint32_t *key_in, *val_in, *key_out, *val_out;  // [N*kCap] CSC sort
+  int32_t *col_start, *col_end;                    // [F]
+  void* sort_tmp;
+  size_t sort_bytes;
+};
+
+size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S);
+int sparse_transpose(SparseState& S, const bgcn_bigcn_args* a, hipStream_t s);
+int sparse_compact_conv1(SparseState& S, const float* X, int64_t ldx, float* Z1, hipStream_t s);
+int sparse_conv2(SparseState& S, const float* H1, const int32_t* node_root, float* Z2, KeepSrc keep,
+                 hipStream_t s);
+int sparse_dw2_root_part(SparseState& S, const bgcn_bigcn_args* a, const float* dZ2, KeepSrc keep,
+                         hipStream_t s);
+int sparse_dw_cols(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1,
+                   const int32_t* node_root, KeepSrc keep, hipStream_t s);
+
+}  // namespace bgcn

@@ -1,0 +1,455 @@
+// Sparse-feature path of the fused BiGCN encoder.
+//
+// The reference's node features are bag-of-words counts (Process/getTwittergraph.py:
+// 67-72: x[n, 5000] holds the "idx:count" pairs of one post, ~10-20 non-zeros) stored
+// dense.  Every product with X or with the root-extended X[root] is exact when the
+// zero entries are skipped (x * w == 0 for x == 0), so this path reads the dense X from
+// HBM exactly once per step, compacts every row to an ELL list (col, val) of at most
+// kCap entries, and evaluates
+//   conv1        Z1[i]         = sum_s val_s * W1^T[col_s]                      (K2)
+//   conv2        Z2_d[i]       = sum_{k<64} a_ik W2_d^T[k] + sum_{s in root(i)} a_is W2_d^T[64+col_s]
+//   dW2 (root)   dW2_d[:,64+c] = sum_{b: c in root_b} 2 relu(x_rb,c) sum_{i in b} keep_i[64+c] dZ2_d[i]
+//   dW1          dW1[:, c]     = sum_{i: x_ic != 0} x_ic dZ1[i]                 (K10)
+// (a_ik = keep * 2 * relu(.)), every sum in a fixed order (deterministic).  dW1 and the
+// dW2 root columns come out of one pass over the column-sorted (CSC) non-zeros of X.
+// A row with more than kCap non-zeros sets a device flag that switches the whole batch
+// to the dense MFMA path (identical results); every kernel of both paths checks the flag
+// on the device, so the choice costs no host sync.
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "bgcn_sparse.h"
+
+namespace bgcn {
+namespace {
+
+constexpr int H = 64;
+
+__device__ __forceinline__ bool use_sparse(const SparseState& S) { return S.mode != 1 && S.flags[0] == 0; }
+
+// ---------------------------------------------------------------- weight transposes
+// W1T[c][d*64 + o] = W1_d[o][c] (c < F) and W2T_d[k][o] = W2_d[o][k] (k < 64+F):
+// 32 x 32 tiles through LDS; blockIdx.z: 0/1 = W1 td/bu, 2/3 = W2 td/bu.
+__global__ __launch_bounds__(256) void k_transpose_weights(SparseState S, const float* __restrict__ w1td,
+                                                           const float* __restrict__ w1bu,
+                                                           const float* __restrict__ w2td,
+                                                           const float* __restrict__ w2bu) {
+  if (!use_sparse(S)) return;
+  __shared__ float tile[32][33];
+  const int z = blockIdx.z;
+  const int64_t K = z < 2 ? S.F : S.F + H;
+  const float* src = z == 0 ? w1td : z == 1 ? w1bu : z == 2 ? w2td : w2bu;
+  const int64_t k0 = int64_t(blockIdx.x) * 32;
+  const int o0 = blockIdx.y * 32;
+  if (k0 >= K) return;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int r = ty; r < 32; r += 8) {
+    const int64_t k = k0 + tx;
+    tile[r][tx] = k < K ? src[int64_t(o0 + r) * K + k] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int64_t k = k0 + r;
+    if (k >= K) continue;
+    if (z < 2) S.w1t[k * (2 * H) + z * H + o0 + tx] = tile[tx][r];
+    else S.w2t[(int64_t(z - 2) * K + k) * H + o0 + tx] = tile[tx][r];
+  }
+}
+
+// ---------------------------------------------------------------- X compaction + conv1
+// One wave per row: stream the dense row (float4 per lane, 4 x 1 KiB in flight),
+// compact the non-zeros in (chunk, component, lane) order, then
+// Z1[i] = sum val * W1T[col] with each lane owning 2 of the 128 outputs.
+__global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const float* __restrict__ X,
+                                                       int64_t ldx, float* __restrict__ Z1) {
+  __shared__ int32_t s_col[4][kCap];
+  __shared__ float s_val[4][kCap];
+  if (S.mode == 1) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = int64_t(blockIdx.x) * 4 + wave;
+  if (i >= S.N) return;
+  const float* row = X + i * ldx;
+  const int nq = int(S.F / 4);   // float4 per row (F % 4 == 0)
+  int cnt = 0;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int q0 = 0; q0 < nq; q0 += 4 * 64) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = q0 + u * 64 + lane;
+      v[u] = q < nq ? ld4(row + int64_t(q) * 4) : f4zero();
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bool nz = e[c] != 0.f;
+        const uint64_t m = __ballot(nz);
+        const int pos = cnt + __popcll(m & lt);
+        if (nz && pos < kCap) {
+          s_col[wave][pos] = (q0 + u * 64 + lane) * 4 + c;
+          s_val[wave][pos] = e[c];
+        }
+        cnt += __popcll(m);
+      }
+    }
+  }
+  if (lane == 0) S.nnz[i] = cnt;
+  if (cnt > kCap) {
+    if (lane == 0) atomicOr(&S.flags[0], 1);
+    return;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes have landed
+  __builtin_amdgcn_wave_barrier();
+  if (lane < cnt) {
+    S.cols[i * kCap + lane] = s_col[wave][lane];
+    S.vals[i * kCap + lane] = s_val[wave][lane];
+  }
+  float2 acc = make_float2(0.f, 0.f);
+  for (int s0 = 0; s0 < cnt; s0 += 8) {
+    float2 w[8];
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int s = s0 + u;
+      const bool ok = s < cnt;
+      x[u] = ok ? s_val[wave][s] : 0.f;
+      w[u] = ok ? *reinterpret_cast<const float2*>(S.w1t + int64_t(s_col[wave][s]) * (2 * H) + 2 * lane)
+                : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      acc.x = fmaf(x[u], w[u].x, acc.x);
+      acc.y = fmaf(x[u], w[u].y, acc.y);
+    }
+  }
+  *reinterpret_cast<float2*>(Z1 + i * (2 * H) + 2 * lane) = acc;
+}
+
+// ---------------------------------------------------------------- conv2 forward
+// Block = (64 nodes, direction); W2T_d[0:64] staged in LDS; 16 lanes x float4 per node.
+__global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float* __restrict__ H1,
+                                                      const int32_t* __restrict__ node_root,
+                                                      float* __restrict__ Z2, KeepSrc keep) {
+  if (!use_sparse(S)) return;
+  __shared__ float4 wl[H][H / 4];   // W2T_d[k][o]
+  const int d = blockIdx.y;
+  const int64_t K2 = S.F + H;
+  const float* w2t = S.w2t + int64_t(d) * K2 * H;
+  for (int e = threadIdx.x; e < H * H / 4; e += 256) wl[e / (H / 4)][e % (H / 4)] = ld4(w2t + e * 4);
+  __syncthreads();
+  const int lane = threadIdx.x & 15, grp = threadIdx.x >> 4;   // 16 nodes per pass
+  const float sc = keep.scale();
+  const int base_lane = (threadIdx.x & 63) & ~15;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int64_t i = int64_t(blockIdx.x) * 64 + pass * 16 + grp;
+    if (i >= S.N) break;
+    const float4 h4 = ld4(H1 + i * (2 * H) + d * H + lane * 4);  // lane holds H1[i][4l .. 4l+3]
+    const uint32_t w0 = keep.get(uint32_t(d), uint32_t(i), 0u);
+    const uint32_t w1 = keep.get(uint32_t(d), uint32_t(i), 1u);
+    float4 acc = f4zero();
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const float hv = (k & 3) == 0 ? h4.x : (k & 3) == 1 ? h4.y : (k & 3) == 2 ? h4.z : h4.w;
+      const float hk = __shfl(hv, base_lane + (k >> 2), 64);
+      const uint32_t wd = k < 32 ? w0 : w1;
+      const float a = ((wd >> (k & 31)) & 1u) ? sc * fmaxf(hk, 0.f) : 0.f;
+      acc = f4fma(a, wl[k][lane], acc);
+    }
+    const int64_t r = node_root[i];
+    const int rn = S.nnz[r];
+    for (int s0 = 0; s0 < rn; s0 += 4) {
+      float4 wv[4];
+      float av[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int s = s0 + u;
+        const bool ok = s < rn;
+        const uint32_t k = ok ? uint32_t(H + S.cols[r * kCap + s]) : 0u;
+        const float v = ok ? S.vals[r * kCap + s] : 0.f;
+        const uint32_t wd = ok ? keep.get(uint32_t(d), uint32_t(i), k >> 5) : 0u;
+        av[u] = ((wd >> (k & 31)) & 1u) ? sc * fmaxf(v, 0.f) : 0.f;
+        wv[u] = ok ? ld4(w2t + int64_t(k) * H + lane * 4) : f4zero();
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = f4fma(av[u], wv[u], acc);
+    }
+    st4(Z2 + i * (2 * H) + d * H + lane * 4, acc);
+  }
+}
+
+// ---------------------------------------------------------------- dW2 root columns, part 1
+// Work item = (tree b, chunk of <= kChunk nodes of b), blockIdx.y = direction:
+// part[d][item][s][o] = sum_{i in chunk} keep_i[64 + col_s] * dZ2_d[i][o] for the root's
+// non-zeros s (the 2 relu(x) factor is applied in k_dw_cols).
+__global__ __launch_bounds__(256) void k_items(SparseState S, const int32_t* __restrict__ tree_ptr) {
+  if (!use_sparse(S) || threadIdx.x != 0 || blockIdx.x != 0) return;
+  int it = 0;
+  for (int64_t b = 0; b < S.B; ++b) {
+    S.tree_item0[b] = it;
+    const int n = tree_ptr[b + 1] - tree_ptr[b];
+    const int chunks = (n + kChunk - 1) / kChunk;
+    for (int q = 0; q < chunks && it < S.max_items; ++q, ++it) {
+      S.item_tree[it] = int32_t(b);
+      S.item_chunk[it] = q;
+    }
+  }
+  S.tree_item0[S.B] = it;
+}
+
+__global__ __launch_bounds__(256) void k_dw2_root_part(SparseState S, const float* __restrict__ dZ2,
+                                                       const int32_t* __restrict__ tree_ptr,
+                                                       const int64_t* __restrict__ rootindex,
+                                                       KeepSrc keep) {
+  if (!use_sparse(S)) return;
+  const int item = blockIdx.x;
+  if (item >= S.tree_item0[S.B]) return;
+  __shared__ uint32_t bits[kChunk];
+  __shared__ float red[4][kCap][H];
+  const int d = blockIdx.y;
+  const int b = S.item_tree[item];
+  const int64_t beg = int64_t(tree_ptr[b]) + int64_t(S.item_chunk[item]) * kChunk;
+  const int64_t end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
+  const int64_t r = rootindex[b];
+  const int rn = S.nnz[r];
+  for (int t = threadIdx.x; t < kChunk; t += 256) {
+    uint32_t m = 0;
+    const int64_t i = beg + t;
+    if (i < end) {
+      for (int s = 0; s < rn; ++s) {
+        const uint32_t k = uint32_t(H + S.cols[r * kCap + s]);
+        m |= ((keep.get(uint32_t(d), uint32_t(i), k >> 5) >> (k & 31)) & 1u) << s;
+      }
+    }
+    bits[t] = m;
+  }
+  __syncthreads();
+  const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;   // 64 outputs x 4 node slices
+  float acc[kCap];
+#pragma unroll
+  for (int s = 0; s < kCap; ++s) acc[s] = 0.f;
+  for (int64_t i = beg + sl; i < end; i += 4) {
+    const float g = dZ2[i * (2 * H) + d * H + o];
+    const uint32_t m = bits[i - beg];
+#pragma unroll
+    for (int s = 0; s < kCap; ++s) acc[s] += ((m >> s) & 1u) ? g : 0.f;
+  }
+#pragma unroll
+  for (int s = 0; s < kCap; ++s) red[sl][s][o] = acc[s];
+  __syncthreads();
+  float* out = S.root_part + (int64_t(d) * S.max_items + item) * (kCap * H);
+  for (int e = threadIdx.x; e < kCap * H; e += 256) {
+    const int s = e / H, oo = e % H;
+    out[e] = (red[0][s][oo] + red[1][s][oo]) + (red[2][s][oo] + red[3][s][oo]);
+  }
+}
+
+// ---------------------------------------------------------------- CSC of X
+__global__ void k_csc_keys(SparseState S) {
+  if (!use_sparse(S)) return;
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= S.N * kCap) return;
+  const int64_t i = t / kCap;
+  const int s = int(t % kCap);
+  S.key_in[t] = s < S.nnz[i] ? uint32_t(S.cols[t]) : uint32_t(S.F);
+  S.val_in[t] = uint32_t(t);
+}
+
+__global__ void k_col_bounds(SparseState S) {
+  if (!use_sparse(S)) return;
+  const int64_t u = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t n = S.N * kCap;
+  if (u >= n) return;
+  const uint32_t k = S.key_out[u];
+  if (k >= uint32_t(S.F)) return;
+  if (u == 0 || S.key_out[u - 1] != k) S.col_start[k] = int32_t(u);
+  if (u == n - 1 || S.key_out[u + 1] != k) S.col_end[k] = int32_t(u + 1);
+}
+
+// ---------------------------------------------------------------- dW1 + dW2 root columns
+// One wave per column c (16 columns per 1024-thread block), the column's non-zeros in
+// row order, 64 at a time (lane l loads entry l), 8 dZ1 rows in flight:
+//   dW1[:, c]       += x_ic * dZ1[i]                      (lane: outputs 2l, 2l+1)
+//   dW2_d[:, 64+c]  += 2 relu(x_ic) * sum_items part_d    (i a root; lane: output l)
+__global__ __launch_bounds__(1024) void k_dw_cols(SparseState S, const float* __restrict__ dZ1,
+                                                  const int32_t* __restrict__ node_root,
+                                                  const int64_t* __restrict__ batch,
+                                                  float* __restrict__ dw1_td, float* __restrict__ dw1_bu,
+                                                  float* __restrict__ dw2_td, float* __restrict__ dw2_bu,
+                                                  float scale) {
+  if (!use_sparse(S)) return;
+  __shared__ float t1[2 * H][17];
+  __shared__ float t2[2][H][17];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t c = int64_t(blockIdx.x) * 16 + wave;
+  float2 a1 = make_float2(0.f, 0.f);
+  float a2[2] = {0.f, 0.f};
+  if (c < S.F) {
+    const int64_t beg = S.col_start[c], end = S.col_end[c];
+    for (int64_t u0 = beg; u0 < end; u0 += 64) {
+      const int64_t u = u0 + lane;
+      const bool ok = u < end;
+      const uint32_t slot = ok ? S.val_out[u] : 0u;
+      const float x_l = ok ? S.vals[slot] : 0.f;
+      const int32_t i_l = int32_t(slot / kCap);
+      const int32_t s_l = int32_t(slot % kCap);
+      const bool root_l = ok && node_root[i_l] == i_l;
+      const int n = int(min<int64_t>(64, end - u0));
+      const uint64_t roots = __ballot(root_l);
+      for (int j0 = 0; j0 < n; j0 += 8) {
+        float2 g[8];
+        float x[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          const int j = j0 + v;
+          const int32_t i = __shfl(i_l, j < 64 ? j : 0, 64);
+          x[v] = j < n ? __shfl(x_l, j < 64 ? j : 0, 64) : 0.f;
+          g[v] = j < n ? *reinterpret_cast<const float2*>(dZ1 + int64_t(i) * (2 * H) + 2 * lane)
+                       : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          a1.x = fmaf(x[v], g[v].x, a1.x);
+          a1.y = fmaf(x[v], g[v].y, a1.y);
+        }
+      }
+      // root rows (rare): dW2 root columns, in row (= tree) order
+      uint64_t m = roots;
+      while (m) {
+        const int j = __builtin_ctzll(m);
+        m &= m - 1;
+        const int32_t i = __shfl(i_l, j, 64);
+        const int32_t s = __shfl(s_l, j, 64);
+        const float xv = __shfl(x_l, j, 64);
+        const int b = int(batch[i]);
+        const float f = scale * fmaxf(xv, 0.f);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          float sum = 0.f;
+          for (int it = S.tree_item0[b]; it < S.tree_item0[b + 1]; ++it)
+            sum += S.root_part[(int64_t(d) * S.max_items + it) * (kCap * H) + s * H + lane];
+          a2[d] = fmaf(f, sum, a2[d]);
+        }
+      }
+    }
+  }
+  t1[2 * lane][wave] = a1.x;
+  t1[2 * lane + 1][wave] = a1.y;
+  t2[0][lane][wave] = a2[0];
+  t2[1][lane][wave] = a2[1];
+  __syncthreads();
+  // coalesced stores: 16 consecutive columns per output row
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 x 64
+  const int64_t cc = int64_t(blockIdx.x) * 16 + tx;
+  if (cc < S.F) {
+    const int64_t K2 = S.F + H;
+    for (int o = ty; o < 2 * H; o += 64) {
+      float* dst = o < H ? dw1_td + int64_t(o) * S.F : dw1_bu + int64_t(o - H) * S.F;
+      dst[cc] = t1[o][tx];
+    }
+    for (int o = ty; o < H; o += 64) {
+      dw2_td[int64_t(o) * K2 + H + cc] = t2[0][o][tx];
+      dw2_bu[int64_t(o) * K2 + H + cc] = t2[1][o][tx];
+    }
+  }
+}
+
+size_t sort_bytes(int64_t n, int64_t F) {
+  size_t bytes = 0;
+  int bits = 1;
+  while ((int64_t(1) << bits) <= F) ++bits;
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (uint32_t*)nullptr, (uint32_t*)nullptr, size_t(n), 0, bits);
+  return bytes;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host side
+size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
+  SparseState t{};
+  t.N = N;
+  t.F = F;
+  t.B = B;
+  t.max_items = int(N / kChunk + B + 1);
+  t.w1t = c.take<float>(size_t(F) * 2 * H);
+  t.w2t = c.take<float>(size_t(2) * (F + H) * H);
+  t.item_tree = c.take<int32_t>(size_t(t.max_items));
+  t.item_chunk = c.take<int32_t>(size_t(t.max_items));
+  t.tree_item0 = c.take<int32_t>(size_t(B + 1));
+  t.root_part = c.take<float>(size_t(2) * t.max_items * kCap * H);
+  const size_t slots = size_t(N) * kCap;
+  t.key_in = c.take<uint32_t>(slots);
+  t.val_in = c.take<uint32_t>(slots);
+  t.key_out = c.take<uint32_t>(slots);
+  t.val_out = c.take<uint32_t>(slots);
+  t.col_start = c.take<int32_t>(size_t(F));
+  t.col_end = c.take<int32_t>(size_t(F));
+  t.sort_bytes = sort_bytes(int64_t(slots), F);
+  t.sort_tmp = c.take<char>(t.sort_bytes + 16);
+  if (S) {
+    t.mode = S->mode;
+    t.flags = S->flags;
+    t.nnz = S->nnz;
+    t.cols = S->cols;
+    t.vals = S->vals;
+    *S = t;
+  }
+  return c.off;
+}
+
+int sparse_transpose(SparseState& S, const bgcn_bigcn_args* a, hipStream_t s) {
+  dim3 grid(unsigned((S.F + H + 31) / 32), 2, 4);
+  hipLaunchKernelGGL(k_transpose_weights, grid, dim3(256), 0, s, S, a->td_w1, a->bu_w1, a->td_w2,
+                     a->bu_w2);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int sparse_compact_conv1(SparseState& S, const float* X, int64_t ldx, float* Z1, hipStream_t s) {
+  hipLaunchKernelGGL(k_compact_conv1, dim3(grid_for(S.N, 4)), dim3(256), 0, s, S, X, ldx, Z1);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int sparse_conv2(SparseState& S, const float* H1, const int32_t* node_root, float* Z2, KeepSrc keep,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(k_conv2_sparse, dim3(grid_for(S.N, 64), 2), dim3(256), 0, s, S, H1, node_root,
+                     Z2, keep);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int sparse_dw2_root_part(SparseState& S, const bgcn_bigcn_args* a, const float* dZ2, KeepSrc keep,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_items, dim3(1), dim3(64), 0, s, S, a->tree_ptr);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_dw2_root_part, dim3(unsigned(S.max_items), 2), dim3(256), 0, s, S, dZ2,
+                     a->tree_ptr, a->rootindex, keep);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int sparse_dw_cols(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1,
+                   const int32_t* node_root, KeepSrc keep, hipStream_t s) {
+  const int64_t slots = S.N * kCap;
+  hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(slots, 256)), dim3(256), 0, s, S);
+  BGCN_CHECK_LAUNCH();
+  int bits = 1;
+  while ((int64_t(1) << bits) <= S.F) ++bits;
+  size_t tb = S.sort_bytes;
+  BGCN_CHECK_HIP(rocprim::radix_sort_pairs(S.sort_tmp, tb, S.key_in, S.key_out, S.val_in, S.val_out,
+                                           size_t(slots), 0, bits, s));
+  BGCN_CHECK_HIP(hipMemsetAsync(S.col_start, 0, size_t(S.F) * sizeof(int32_t), s));
+  BGCN_CHECK_HIP(hipMemsetAsync(S.col_end, 0, size_t(S.F) * sizeof(int32_t), s));
+  hipLaunchKernelGGL(k_col_bounds, dim3(grid_for(slots, 256)), dim3(256), 0, s, S);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_dw_cols, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, dZ1, node_root,
+                     a->batch, a->td_dw1, a->bu_dw1, a->td_dw2, a->bu_dw2, keep.scale());
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+}  // namespace bgcn

@@ -54,15 +54,7 @@ class Graph:
             raise IndexError("edge_index contains an index out of range [0, num_nodes)")
 
 
-def build_graph(edge_index: torch.Tensor, num_nodes: int, edge_weight: Optional[torch.Tensor] = None,
-                degree_on: str = "col", validate: bool = False) -> Graph:
-    _dev_check(edge_index, edge_weight)
-    if edge_index.dim() != 2 or edge_index.size(0) != 2:
-        raise ValueError("edge_index must be [2, E]")
-    ei = edge_index.to(torch.int64).contiguous()
-    ew = None if edge_weight is None else edge_weight.to(torch.float32).contiguous()
-    E, N = int(ei.size(1)), int(num_nodes)
-    dev = ei.device
+def _alloc_graph(E: int, N: int, dev, status=None) -> Graph:
     cap = E + N
     g = Graph()
     g.num_nodes, g.num_edges, g.capacity = N, E, cap
@@ -71,7 +63,52 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, edge_weight: Optional[
     g.t_ptr, g.s_ptr = torch.empty(N + 1, **i32), torch.empty(N + 1, **i32)
     g.t_row, g.t_col, g.t_w = torch.empty(cap, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32)
     g.s_row, g.s_col, g.s_w = torch.empty(cap, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32)
-    g.status = torch.zeros(1, **i32)
+    g.status = torch.zeros(1, **i32) if status is None else status
+    return g
+
+
+def _csr_out(g: Graph) -> _lib.CsrOut:
+    c = _lib.CsrOut()
+    c.t_ptr, c.t_row, c.t_col, c.t_w = ptr(g.t_ptr), ptr(g.t_row), ptr(g.t_col), ptr(g.t_w)
+    c.s_ptr, c.s_row, c.s_col, c.s_w = ptr(g.s_ptr), ptr(g.s_row), ptr(g.s_col), ptr(g.s_w)
+    return c
+
+
+def _check_ei(edge_index: torch.Tensor) -> torch.Tensor:
+    if edge_index.dim() != 2 or edge_index.size(0) != 2:
+        raise ValueError("edge_index must be [2, E]")
+    return edge_index.to(torch.int64).contiguous()
+
+
+def build_graph_pair(td_edge_index: torch.Tensor, bu_edge_index: torch.Tensor, num_nodes: int,
+                     degree_on: str = "col", validate: bool = False):
+    """TD and BU graphs of one batch in one launch sequence (the fused step's K1)."""
+    _dev_check(td_edge_index, bu_edge_index)
+    td_ei, bu_ei = _check_ei(td_edge_index), _check_ei(bu_edge_index)
+    N = int(num_nodes)
+    dev = td_ei.device
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    td = _alloc_graph(int(td_ei.size(1)), N, dev, status)
+    bu = _alloc_graph(int(bu_ei.size(1)), N, dev, status)
+    L = _lib.lib()
+    ws = workspace(L.bgcn_graph_pair_workspace_size(td.num_edges, bu.num_edges, N), dev)
+    a, b = _csr_out(td), _csr_out(bu)
+    check(L.bgcn_build_graph_pair(ptr(td_ei), td.num_edges, ptr(bu_ei), bu.num_edges, N,
+                                  0 if degree_on == "col" else 1, ctypes.byref(a), ctypes.byref(b),
+                                  ptr(status), ptr(ws), ws.numel(), stream_handle()))
+    if validate:
+        td.check()
+    return td, bu
+
+
+def build_graph(edge_index: torch.Tensor, num_nodes: int, edge_weight: Optional[torch.Tensor] = None,
+                degree_on: str = "col", validate: bool = False) -> Graph:
+    _dev_check(edge_index, edge_weight)
+    ei = _check_ei(edge_index)
+    ew = None if edge_weight is None else edge_weight.to(torch.float32).contiguous()
+    E, N = int(ei.size(1)), int(num_nodes)
+    dev = ei.device
+    g = _alloc_graph(E, N, dev)
     L = _lib.lib()
     ws = workspace(L.bgcn_graph_workspace_size(E, N), dev)
     check(L.bgcn_build_graph(ptr(ei), ptr(ew), E, N, 0 if degree_on == "col" else 1,
@@ -227,22 +264,39 @@ def scatter_mean(src: torch.Tensor, index: torch.Tensor, dim: int = 0, out=None,
 _PARAM_ORDER = ("td_w1", "td_b1", "td_w2", "td_b2", "bu_w1", "bu_b1", "bu_w2", "bu_b2")
 
 
+_FEAT_MODES = {"auto": _lib.BGCN_FEAT_AUTO, "sparse": _lib.BGCN_FEAT_AUTO, "dense": _lib.BGCN_FEAT_DENSE}
+
+
+def _fill_args(a: BiGCNArgs, x, batch, rootindex, td, bu, B, training, seed, keep, feat_mode, xs, params):
+    N, F = x.shape
+    a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats, a.hid = ptr(x), x.stride(0), N, B, F, HID
+    a.batch, a.rootindex = ptr(batch), ptr(rootindex)
+    a.td, a.bu = td.view(), bu.view()
+    for name, p in zip(_PARAM_ORDER, params):
+        setattr(a, name, ptr(p))
+    a.training, a.seed = int(bool(training)), int(seed) & (2**64 - 1)
+    a.keep_words = ptr(keep)
+    a.feat_mode = feat_mode
+    if xs is not None:
+        a.x_flags, a.x_nnz, a.x_cols, a.x_vals = (ptr(t) for t in xs)
+
+
 class _BiGCNEncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training, seed, keep_words,
-                *params):
+                feat_mode, *params):
         x = x.contiguous().float()
         N, F = x.shape
         dev = x.device
         L = _lib.lib()
+        xs = None
+        if feat_mode != _lib.BGCN_FEAT_DENSE:
+            cap = _lib.BGCN_SPARSE_CAP
+            xs = (torch.empty(8, dtype=torch.int32, device=dev), torch.empty(N, dtype=torch.int32, device=dev),
+                  torch.empty(N * cap, dtype=torch.int32, device=dev),
+                  torch.empty(N * cap, dtype=torch.float32, device=dev))
         a = BiGCNArgs()
-        a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats, a.hid = ptr(x), x.stride(0), N, B, F, HID
-        a.batch, a.rootindex = ptr(batch), ptr(rootindex)
-        a.td, a.bu = td.view(), bu.view()
-        for name, p in zip(_PARAM_ORDER, params):
-            setattr(a, name, ptr(p))
-        a.training, a.seed = int(bool(training)), int(seed) & (2**64 - 1)
-        a.keep_words = ptr(keep_words)
+        _fill_args(a, x, batch, rootindex, td, bu, B, training, seed, keep_words, feat_mode, xs, params)
         tree_ptr = torch.empty(B + 1, dtype=torch.int32, device=dev)
         h1 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
         h2 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
@@ -251,46 +305,45 @@ class _BiGCNEncoderFn(torch.autograd.Function):
         ws = workspace(L.bgcn_bigcn_workspace_size(N, B, F, HID), dev)
         check(L.bgcn_bigcn_forward(ctypes.byref(a), ptr(ws), ws.numel(), stream_handle()))
         ctx.graphs = (td, bu)
-        ctx.meta = (B, training, seed)
-        ctx.save_for_backward(x, batch, rootindex, keep_words if keep_words is not None else x.new_empty(0),
-                              tree_ptr, h1, h2, *params)
+        ctx.meta = (B, training, seed, feat_mode)
+        empty = x.new_empty(0)
+        ctx.save_for_backward(x, batch, rootindex, keep_words if keep_words is not None else empty,
+                              tree_ptr, h1, h2, *(xs if xs is not None else (empty,) * 4), *params)
         ctx.has_keep = keep_words is not None
         return head
 
     @staticmethod
     def backward(ctx, dhead):
-        x, batch, rootindex, keep, tree_ptr, h1, h2, *params = ctx.saved_tensors
+        x, batch, rootindex, keep, tree_ptr, h1, h2, xf, xn, xc, xv, *params = ctx.saved_tensors
         td, bu = ctx.graphs
-        B, training, seed = ctx.meta
+        B, training, seed, feat_mode = ctx.meta
         N, F = x.shape
         dev = x.device
         L = _lib.lib()
         dhead = dhead.contiguous().float()
         a = BiGCNArgs()
-        a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats, a.hid = ptr(x), x.stride(0), N, B, F, HID
-        a.batch, a.rootindex = ptr(batch), ptr(rootindex)
-        a.td, a.bu = td.view(), bu.view()
-        for name, p in zip(_PARAM_ORDER, params):
-            setattr(a, name, ptr(p))
-        a.training, a.seed = int(bool(training)), int(seed) & (2**64 - 1)
-        a.keep_words = ptr(keep) if ctx.has_keep else 0
+        xs = None if feat_mode == _lib.BGCN_FEAT_DENSE else (xf, xn, xc, xv)
+        _fill_args(a, x, batch, rootindex, td, bu, B, training, seed, keep if ctx.has_keep else None,
+                   feat_mode, xs, params)
         a.tree_ptr, a.h1, a.h2, a.dhead_in = ptr(tree_ptr), ptr(h1), ptr(h2), ptr(dhead)
         grads = [torch.empty_like(p) for p in params]
         for name, gt in zip(_PARAM_ORDER, grads):
             setattr(a, name.replace("_w", "_dw").replace("_b", "_db"), ptr(gt))
         ws = workspace(L.bgcn_bigcn_workspace_size(N, B, F, HID), dev)
         check(L.bgcn_bigcn_backward(ctypes.byref(a), ptr(ws), ws.numel(), stream_handle()))
-        return (None,) * 9 + tuple(grads)
+        return (None,) * 10 + tuple(grads)
 
 
 def bigcn_encoder(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, td: Graph, bu: Graph,
                   num_graphs: int, params, training: bool = False, seed: int = 0,
-                  keep_words: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  keep_words: Optional[torch.Tensor] = None, feat_mode: str = "auto") -> torch.Tensor:
     """cat(BU_x, TD_x) [B, 256] of ``BiGCN.forward`` (``BiGCN_Twitter.py:126-128``).
 
     ``params`` = (td_w1, td_b1, td_w2, td_b2, bu_w1, bu_b1, bu_w2, bu_b2) in the
     reference layout (``convN.lin.weight [out, in]``, ``convN.bias``).  ``keep_words``
-    optionally injects the dropout draw as packed bits [2, N, ceil((64+F)/32)] int32."""
+    optionally injects the dropout draw as packed bits [2, N, ceil((64+F)/32)] int32.
+    ``feat_mode``: "auto" (sparse feature path, dense MFMA fallback decided on the
+    device) or "dense" (always the dense MFMA kernels)."""
     _dev_check(x, batch, rootindex, keep_words, *params)
     for p in params:
         if p.dtype != torch.float32 or not p.is_contiguous():
@@ -298,7 +351,8 @@ def bigcn_encoder(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor,
     if keep_words is not None:
         keep_words = keep_words.contiguous()
     return _BiGCNEncoderFn.apply(x, batch.to(torch.int64).contiguous(), rootindex.to(torch.int64).contiguous(),
-                                 td, bu, int(num_graphs), bool(training), int(seed), keep_words, *params)
+                                 td, bu, int(num_graphs), bool(training), int(seed), keep_words,
+                                 _FEAT_MODES[feat_mode], *params)
 
 
 def keep_words(seed: int, num_nodes: int, in_feats: int, device) -> torch.Tensor:

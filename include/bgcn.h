@@ -71,6 +71,9 @@ const char* bgcn_last_error(void);
  *   by source  (backward, A^T)      : s_ptr[N+1], s_row[], s_col[] = target, s_w[]
  * Entries of a row keep edge order with the self loop last, which is the summation
  * order of PyG's scatter-add.  *_row holds the row id of each entry (COO form).
+ * Deterministic (no float atomics): counting sort with a run-based placement when each
+ * key's edges are contiguous (always true for propagation trees), else an ordered
+ * general placement; the choice is made on the device.
  * The number of valid entries is t_ptr[N] (= s_ptr[N]), on the device.
  * -------------------------------------------------------------------------- */
 size_t bgcn_graph_workspace_size(int64_t num_edges, int64_t num_nodes);
@@ -80,6 +83,19 @@ int bgcn_build_graph(const int64_t* edge_index, const float* edge_weight, int64_
                      int32_t* s_ptr, int32_t* s_row, int32_t* s_col, float* s_w,
                      int32_t* status, void* workspace, size_t workspace_bytes,
                      bgcn_stream_t stream);
+
+/* Both directions of one batch in one launch sequence (the fused step's TD graph of
+ * edge_index and BU graph of BU_edge_index; dataset.py:80-90).  No edge weights. */
+typedef struct bgcn_csr_out {
+  int32_t* t_ptr; int32_t* t_row; int32_t* t_col; float* t_w;
+  int32_t* s_ptr; int32_t* s_row; int32_t* s_col; float* s_w;
+} bgcn_csr_out;
+size_t bgcn_graph_pair_workspace_size(int64_t td_num_edges, int64_t bu_num_edges, int64_t num_nodes);
+int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_num_edges,
+                          const int64_t* bu_edge_index, int64_t bu_num_edges, int64_t num_nodes,
+                          int degree_on, const bgcn_csr_out* td, const bgcn_csr_out* bu,
+                          int32_t* status, void* workspace, size_t workspace_bytes,
+                          bgcn_stream_t stream);
 
 /* --------------------------------------------------------------------------
  * K3/K4  MessagePassing.propagate(aggr='add') with message norm * x_j, + bias.
@@ -162,6 +178,15 @@ typedef struct bgcn_graph_view {
   int64_t capacity; /* E + N */
 } bgcn_graph_view;
 
+/* Feature path of the fused encoder.  AUTO: X is read once and every row compacted to
+ * at most BGCN_SPARSE_CAP (col, val) pairs; products with X / X[root] then skip the zero
+ * entries (exact: bag-of-words rows hold ~10-20 non-zeros of 5000).  If any row holds
+ * more, the batch falls back to the dense MFMA kernels on the device (no host sync).
+ * DENSE: always the dense MFMA kernels. */
+#define BGCN_FEAT_AUTO 0
+#define BGCN_FEAT_DENSE 1
+#define BGCN_SPARSE_CAP 32
+
 typedef struct bgcn_bigcn_args {
   /* batch */
   const float* x; int64_t ldx;   /* [N, F] node features (data.x)          */
@@ -177,6 +202,12 @@ typedef struct bgcn_bigcn_args {
   const float* bu_w1; const float* bu_b1; const float* bu_w2; const float* bu_b2;
   /* dropout */
   int training; uint64_t seed; const uint32_t* keep_words; /* NULL = generate */
+  /* feature path (AUTO needs the four buffers below; they are saved for backward) */
+  int feat_mode;
+  int32_t* x_flags;              /* [8] ([0] != 0: a row overflowed -> dense)  */
+  int32_t* x_nnz;                /* [N]                                     */
+  int32_t* x_cols;               /* [N][BGCN_SPARSE_CAP]                    */
+  float* x_vals;                 /* [N][BGCN_SPARSE_CAP]                    */
   /* saved activations (caller-owned, kept for backward) */
   int32_t* tree_ptr;             /* [B+1]                                   */
   float* h1;                     /* [N, 2H] conv1 outputs (pre-relu)        */

@@ -35,23 +35,24 @@ def close(a, b, tol=TOL, what=""):
     assert err <= tol * max(scale, 1e-12), f"{what}: max err {err:.3e} vs scale {scale:.3e}"
 
 
-def gpu_step(b, p, training, keep_words=None, degree_on="col", seed=0):
-    """Fused encoder + torch head on the GPU; returns (logp, loss, grads)."""
+def gpu_step(b, p, training, keep_words=None, degree_on="col", seed=0, mode="auto"):
+    """Fused encoder + torch head on the GPU; returns (logp, loss, grads, head)."""
     from bigcn_amd.ops import bigcn_encoder, build_graph
     q = {k: v.float().to(DEV).contiguous().requires_grad_(True) for k, v in p.items()}
     N = b.x.size(0)
     td = build_graph(b.edge_index, N, degree_on=degree_on, validate=True)
     bu = build_graph(b.BU_edge_index, N, degree_on=degree_on, validate=True)
     head = bigcn_encoder(b.x, b.batch, b.rootindex, td, bu, b.num_graphs, [q[k] for k in ENC_KEYS],
-                         training=training, seed=seed, keep_words=keep_words)
+                         training=training, seed=seed, keep_words=keep_words, feat_mode=mode)
     logp = F.log_softmax(F.linear(head, q["fc.weight"], q["fc.bias"]), dim=1)
     loss = F.nll_loss(logp, b.y)
     loss.backward()
     return logp, loss, {k: v.grad for k, v in q.items()}, head
 
 
+@pytest.mark.parametrize("mode", ["auto", "dense"])
 @pytest.mark.parametrize("name", GOLDEN)
-def test_fused_matches_golden(name):
+def test_fused_matches_golden(name, mode):
     from bigcn_amd.ops import pack_keep
     g = load_golden(name)
     b = golden_batch(g, DEV)
@@ -60,7 +61,7 @@ def test_fused_matches_golden(name):
     kw = None
     if training:
         kw = torch.stack([pack_keep(torch.as_tensor(g["td_keep"])), pack_keep(torch.as_tensor(g["bu_keep"]))]).to(DEV)
-    logp, loss, grads, head = gpu_step(b, p, training, kw, str(g["degree_on"]))
+    logp, loss, grads, head = gpu_step(b, p, training, kw, str(g["degree_on"]), mode=mode)
     close(head, g["stage:head_in"], what="head_in")
     close(logp, g["logp"], what="logp")
     close(loss, g["loss"], what="loss")
@@ -84,8 +85,9 @@ def _oracle(b, p, training, td_mask=None, bu_mask=None):
     return logp, loss, grads, st
 
 
+@pytest.mark.parametrize("mode", ["auto", "dense"])
 @pytest.mark.parametrize("training", [False, True])
-def test_fused_midsize_5000_features(training):
+def test_fused_midsize_5000_features(training, mode):
     """B = 12 trees (~120 nodes each), F = 5000: the real feature width, in-kernel dropout
     mask materialised for the oracle."""
     from bigcn_amd.ops import keep_words, unpack_keep
@@ -101,7 +103,7 @@ def test_fused_midsize_5000_features(training):
         frac = float(m.float().mean())
         assert 0.49 < frac < 0.51, frac
         assert not torch.equal(m[0], m[1])
-    logp, loss, grads, head = gpu_step(b, p, training, None, seed=seed)
+    logp, loss, grads, head = gpu_step(b, p, training, None, seed=seed, mode=mode)
     rlogp, rloss, rgrads, st = _oracle(b, p, training, *masks)
     close(head, st["head_in"], what="head_in")
     close(logp, rlogp, what="logp")
@@ -109,19 +111,51 @@ def test_fused_midsize_5000_features(training):
         close(grads[k], rgrads[k], what=k)
 
 
-def test_fused_is_deterministic_full_size():
+@pytest.mark.parametrize("mode", ["auto", "dense"])
+def test_fused_is_deterministic_full_size(mode):
     """Full Twitter15-shaped batch (B = 128, mean 256 nodes, F = 5000): two runs of the
     training step give bitwise-identical outputs and gradients (atomic-free kernels)."""
     b = _synth(22, 128, 256)
     p = O.make_params(5000, 64, 64, 4, seed=6)
-    r1 = gpu_step(b, p, True, None, seed=99)
-    r2 = gpu_step(b, p, True, None, seed=99)
+    r1 = gpu_step(b, p, True, None, seed=99, mode=mode)
+    r2 = gpu_step(b, p, True, None, seed=99, mode=mode)
     assert torch.equal(r1[0], r2[0])
     for k in r1[2]:
         assert torch.equal(r1[2][k], r2[2][k]), k
-    r3 = gpu_step(b, p, True, None, seed=100)   # another draw changes the result
+    r3 = gpu_step(b, p, True, None, seed=100, mode=mode)   # another draw changes the result
     assert not torch.equal(r1[0], r3[0])
     assert torch.isfinite(r1[1])
+
+
+def test_sparse_and_dense_paths_agree_full_size():
+    """The sparse feature path and the dense MFMA path compute the same step (fp32
+    rounding only) on a full Twitter15-shaped batch."""
+    b = _synth(25, 128, 256)
+    p = O.make_params(5000, 64, 64, 4, seed=8)
+    rs = gpu_step(b, p, True, None, seed=5, mode="auto")
+    rd = gpu_step(b, p, True, None, seed=5, mode="dense")
+    close(rs[3], rd[3], what="head")
+    for k in rs[2]:
+        close(rs[2][k], rd[2][k], what=k)
+
+
+@pytest.mark.parametrize("dense_rows", [1, 200])
+def test_sparse_overflow_falls_back_to_dense(dense_rows):
+    """Rows with more than 32 non-zeros switch the batch to the dense path on the device:
+    results still match the oracle."""
+    from bigcn_amd.ops import keep_words, unpack_keep
+    b = _synth(26, 6, 60, F=512)
+    g = torch.Generator().manual_seed(3)
+    rows = torch.randperm(b.x.size(0), generator=g)[:dense_rows]
+    b.x[rows.to(DEV)] = torch.rand(dense_rows, 512, generator=g).to(DEV)
+    p = O.make_params(512, 64, 64, 4, seed=9)
+    N = b.x.size(0)
+    m = unpack_keep(keep_words(7, N, 512, DEV).cpu(), 64 + 512)
+    logp, loss, grads, head = gpu_step(b, p, True, None, seed=7, mode="auto")
+    rlogp, _, rgrads, st = _oracle(b, p, True, m[0], m[1])
+    close(logp, rlogp, what="logp")
+    for k in p:
+        close(grads[k], rgrads[k], what=k)
 
 
 def test_model_module_matches_oracle_and_state_dict():

@@ -68,6 +68,32 @@ def test_build_graph_matches_gcn_norm(degree_on, star):
         assert int(t[2][b - 1]) == i and bool((t[1][a:b] == i).all())
 
 
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_build_graph_pair_matches_single(shuffle):
+    """Paired TD/BU build == two single builds, bit for bit; grouped (tree order) and
+    general (shuffled edge order) placement both restore edge order in every row."""
+    from bigcn_amd.ops import build_graph, build_graph_pair
+    rng = np.random.default_rng(7)
+    ei, N = rand_forest(rng, [3, 50, 1, 600, 9], star=False)
+    order = np.lexsort((ei[1].numpy(), ei[0].numpy()))           # reference order (parent, child)
+    td = ei[:, torch.as_tensor(order)]
+    if shuffle:
+        td = td[:, torch.as_tensor(rng.permutation(td.size(1)))]
+    bu = td.flip(0)
+    a, b = build_graph_pair(td.to(DEV), bu.to(DEV), N, validate=True)
+    for g, e in ((a, td), (b, bu)):
+        s = build_graph(e.to(DEV), N)
+        for k in ("t_ptr", "t_row", "t_col", "t_w", "s_ptr", "s_row", "s_col", "s_w"):
+            n = int(s.t_ptr[N])
+            assert torch.equal(getattr(g, k)[:n + 1] if "ptr" in k else getattr(g, k)[:n],
+                               getattr(s, k)[:n + 1] if "ptr" in k else getattr(s, k)[:n]), k
+        # rows keep edge order: the sources of target row i appear as in `e`
+        tp, tc = s.t_ptr.cpu(), s.t_col.cpu()
+        for i in range(0, N, 53):
+            want = e[0][e[1] == i].tolist() + [i]
+            assert tc[int(tp[i]):int(tp[i + 1])].tolist() == want
+
+
 def test_build_graph_drops_input_self_loops_and_flags_bad_index():
     from bigcn_amd.ops import build_graph
     ei = torch.tensor([[0, 1, 1, 2], [1, 1, 2, 0]])
