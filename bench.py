@@ -43,15 +43,34 @@ WORKLOADS = {
                            "clamped [2,8192], 5000-dim BoW x, DropEdge 0.2/0.2, dropout 0.5, fp32"),
 }
 
-KERNEL_CLASSES = {0: "conv1 X.W1^T (TD+BU fused)", 1: "dW1 = dZ1^T X (TD+BU fused)",
-                  2: "conv2 A2.W2^T (generated A2)", 3: "dW2 = dZ2^T A2 (generated A2)"}
+# kernel classes timed by libbgcn's HIP-event hook (bgcn_set_kernel_timing)
+KERNEL_CLASSES = {
+    "dense": {0: "conv1 X.W1^T MFMA (TD+BU fused)", 1: "dW1 = dZ1^T X MFMA (TD+BU fused)",
+              2: "conv2 A2.W2^T MFMA (generated A2)", 3: "dW2 = dZ2^T A2 MFMA (generated A2)"},
+    "auto": {0: "k_compact_conv1: X read + BoW compaction + conv1 gather", 2: "conv2 (sparse root gather)",
+             3: "dW2 relu(H1) block MFMA", 5: "dW1 + dW2 root columns over CSC(X)"},
+}
+SPARSE_CAP = 32
 
 
-def kernel_flops(cls: int, N: int, Fd: int) -> float:
+def kernel_work(mode: str, cls: int, N: float, Fd: int):
+    """(bound, algorithmic units per launch): FLOPs for MFMA kernels, bytes for HBM ones."""
     H = 64
+    if mode == "auto":
+        if cls == 0:   # dense X read once + Z1 [N,128] + the compacted lists written
+            return "hbm", N * Fd * 4.0 + N * 2 * H * 4.0 + N * (SPARSE_CAP * 8.0 + 4.0)
+        if cls == 2:   # H1 [N,128] read + Z2 [N,128] written (gathers of W2^T rows hit L2)
+            return "hbm", N * 2 * H * 4.0 * 2
+        if cls == 3:   # the relu(H1) block of dW2, both directions, reduction over N
+            return "mfma", 2.0 * N * H * H * 2
+        if cls == 5:   # ELL + CSC slots + dZ1 [N,128] read, dW1 + dW2 root columns written
+            return "hbm", N * SPARSE_CAP * 12.0 + N * 2 * H * 4.0 + 4.0 * Fd * (2 * H + 2 * H)
+        return None, 0.0
     if cls in (0, 1):
-        return 2.0 * N * Fd * 2 * H
-    return 2.0 * N * (Fd + H) * H * 2
+        return "mfma", 2.0 * N * Fd * 2 * H
+    if cls in (2, 3):
+        return "mfma", 2.0 * N * (Fd + H) * H * 2
+    return None, 0.0
 
 
 def log(*a):
@@ -114,11 +133,16 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--feat-mode", default="auto", choices=["auto", "dense"],
+                    help="auto: sparse feature path with device-side dense fallback; dense: MFMA only")
+    ap.add_argument("--compare-dense", type=int, default=1,
+                    help="at N=1 also time the dense MFMA path and report it beside the main line")
     args = ap.parse_args()
 
-    from bigcn_amd import BiGCN, make_optimizer
+    from bigcn_amd import BiGCN
     from bigcn_amd import ops
     from bigcn_amd.dp import GradBucket, init_from_env
+    from bigcn_amd.optim import bigcn_adam
 
     rank, world, local = init_from_env("nccl")
     if world != args.gpus:
@@ -134,75 +158,93 @@ def main():
         for p in model.parameters():
             dist.broadcast(p.data, 0)
     model.train()
-    opt = make_optimizer(model, fused=True)
-    bucket = GradBucket(model.parameters())
+    opt = bigcn_adam(model)                             # reference groups, one fused launch
+    bucket = GradBucket(opt.params())                   # same parameter order as opt
 
     def step(i):
         b = pool[i % len(pool)]
         b.__dict__.pop("_bgcn_graphs", None)          # gcn_norm/CSR rebuilt every step (as GCNConv does)
         logp = model(b)
         loss = F.nll_loss(logp, b.y)
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad()
         loss.backward()
-        bucket.allreduce_mean()
-        opt.step()
+        if world > 1:                                   # RCCL sum of the flat bucket, mean folded in
+            opt.step(grads=bucket.reduce_sum(), grad_scale=1.0 / world)
+        else:
+            opt.step()
         return loss
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    timing = not args.no_kernel_timing
-    if timing:
-        ops.set_kernel_timing(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(args.warmup + i)
-        if rank == 0 and (i + 1) % max(1, args.steps // 4) == 0:
-            log(f"step {i + 1}/{args.steps}")
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    kern = {}
-    if timing:
-        ops.set_kernel_timing(False)
-        for c in KERNEL_CLASSES:
-            ms, n = ops.kernel_timing(c)
-            kern[c] = (ms, n)
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    final_loss = float(loss.item())
+    def run(mode: str, steps: int, warmup: int):
+        model.feat_mode = mode
+        for i in range(warmup):
+            step(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        timing = not args.no_kernel_timing
+        if timing:
+            ops.set_kernel_timing(True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            loss = step(warmup + i)
+            if rank == 0 and (i + 1) % max(1, steps // 4) == 0:
+                log(f"[{mode}] step {i + 1}/{steps}")
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        kern = {}
+        if timing:
+            ops.set_kernel_timing(False)
+            for c in KERNEL_CLASSES[mode]:
+                kern[c] = ops.kernel_timing(c)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        N_avg = float(np.mean([nodes[(warmup + i) % len(nodes)] for i in range(steps)]))
+        roof, kernels, best = None, {}, None
+        for c, (ms, n) in kern.items():
+            if n == 0:
+                continue
+            avg_ms = ms / n
+            bound, work = kernel_work(mode, c, N_avg, wl["feats"])
+            ent = {"avg_ms": round(avg_ms, 4), "launches": n}
+            if bound == "mfma":
+                ent["tflops"] = round(work / (avg_ms * 1e-3) / 1e12, 2)
+            elif bound == "hbm":
+                ent["gbs"] = round(work / (avg_ms * 1e-3) / 1e9, 1)
+            kernels[KERNEL_CLASSES[mode][c]] = ent
+            if bound is not None and (best is None or avg_ms > best[1]):
+                best = (c, avg_ms, bound, work)
+        if best is not None:
+            c, avg_ms, bound, work = best
+            if bound == "mfma":
+                ach = work / (avg_ms * 1e-3) / 1e12
+                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
+                        "traffic": None, "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
+                        "avg_ms": round(avg_ms, 4)}
+            else:
+                ach = work / (avg_ms * 1e-3) / 1e9
+                roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+                        "kernel": KERNEL_CLASSES[mode][c], "bytes_per_launch": work,
+                        "avg_ms": round(avg_ms, 4)}
+        value = wl["trees"] * world * steps / dt
+        return {"value": value, "dt": dt, "N_avg": N_avg, "roof": roof, "kernels": kernels,
+                "loss": float(loss.item())}
 
+    main_res = run(args.feat_mode, args.steps, args.warmup)
+    dense_res = None
+    if world == 1 and args.feat_mode != "dense" and args.compare_dense:
+        dense_res = run("dense", max(3, args.steps // 2), 2)
     if rank == 0:
-        trees_total = wl["trees"] * world * args.steps
-        value = trees_total / dt
-        N_avg = float(np.mean([nodes[(args.warmup + i) % len(nodes)] for i in range(args.steps)]))
-        roof = None
-        kernels = {}
-        if kern:
-            best = None
-            for c, (ms, n) in kern.items():
-                if n == 0:
-                    continue
-                avg_ms = ms / n
-                flops = kernel_flops(c, N_avg, wl["feats"])
-                tf = flops / (avg_ms * 1e-3) / 1e12
-                kernels[KERNEL_CLASSES[c]] = {"avg_ms": round(avg_ms, 4), "launches": n,
-                                              "tflops": round(tf, 2)}
-                if best is None or avg_ms > best[1]:
-                    best = (c, avg_ms, tf)
-            if best is not None:
-                roof = {"bound": "mfma", "achieved": round(best[2], 2), "peak": PEAK_FP32_MFMA_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(best[2] / PEAK_FP32_MFMA_TFLOPS, 4),
-                        "traffic": None, "kernel": KERNEL_CLASSES[best[0]],
-                        "flops_per_launch": kernel_flops(best[0], N_avg, wl["feats"])}
+        value, dt, N_avg = main_res["value"], main_res["dt"], main_res["N_avg"]
+        roof, kernels, final_loss = main_res["roof"], main_res["kernels"], main_res["loss"]
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
@@ -212,11 +254,16 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (reference npz/Batch layout; real Twitter15 trees absent)",
-            "config": {"workload": wl["desc"], "trees_per_gpu": wl["trees"],
+            "config": {"workload": wl["desc"], "trees_per_gpu": wl["trees"], "feat_path": args.feat_mode,
                        "global_batch": wl["trees"] * world, "avg_nodes_per_batch": round(N_avg, 1),
                        "in_feats": wl["feats"], "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "final_loss": round(final_loss, 5),
+            "feat_mode": args.feat_mode,
         }
+        if dense_res is not None:
+            out["dense_path"] = {"value": round(dense_res["value"], 2), "unit": "trees/s",
+                                 "ms_per_step": round(dense_res["dt"] / max(3, args.steps // 2) * 1e3, 4),
+                                 "roofline": dense_res["roof"], "kernels": dense_res["kernels"]}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_colsum_workspace_size", "bgcn_colsum",
     "bgcn_scatter_mean_workspace_size", "bgcn_scatter_mean_fwd", "bgcn_scatter_mean_bwd",
     "bgcn_bigcn_workspace_size", "bgcn_bigcn_forward", "bgcn_bigcn_backward",
-    "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing",
+    "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_adam_step",
 )
 
 
@@ -110,6 +110,7 @@ _SIGS = {
     "bgcn_bigcn_forward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
     "bgcn_bigcn_backward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
     "bgcn_keep_words": (c_int, [c_uint64, c_int64, c_int32, c_void_p, c_void_p]),
+    "bgcn_adam_step": (c_int, [c_void_p, c_void_p]),
     "bgcn_set_kernel_timing": (c_int, [c_int]),
     "bgcn_kernel_timing": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),
 }

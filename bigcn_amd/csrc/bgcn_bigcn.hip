@@ -150,9 +150,13 @@ __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_
                                              const float* __restrict__ dZ2,
                                              const int32_t* __restrict__ node_root,
                                              float* __restrict__ part, int64_t N, int64_t kchunk,
-                                             int S, KeepSrc keep, const int32_t* __restrict__ gate) {
-  // column tile 0 (the relu(H1) block) always runs; the X[root] tiles only on the dense path
-  if (blockIdx.x > 0 && gate_closed(gate)) return;
+                                             int S, KeepSrc keep, const int32_t* __restrict__ gate,
+                                             int want_dense, int64_t ldp) {
+  // Two launch configurations share this kernel: the dense path's full grid (all 64+F
+  // columns, few node splits; want_dense = 1) and the sparse path's relu(H1) block only
+  // (column tile 0, many node splits, partial rows of ldp = 64; want_dense = 0).  Only
+  // the configuration of the path selected on the device does any work.
+  if (dense_active(gate) != (want_dense != 0)) return;
   constexpr int BN = 64;
   __shared__ float As[2][BK * H];   // [node][o]
   __shared__ float Bs[2][BK * BN];  // [node][c]
@@ -226,28 +230,31 @@ __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
   }
-  float* out = part + (int64_t(d) * S + split) * (H * K2);
+  float* out = part + (int64_t(d) * S + split) * (H * ldp);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     int64_t c = c0 + wc * 32 + r32;
     int o = wr * 32 + acc_row(r, lane);
-    if (c < K2) out[int64_t(o) * K2 + c] = acc[r];
+    if (c < ldp) out[int64_t(o) * ldp + c] = acc[r];
   }
 }
 
-__global__ void k_reduce_dw2(const float* __restrict__ part, int S, int64_t K2,
+// dW2_d[o][c] = sum_s part[d][s][o][c] (fixed order) for c < ldp; the dense config
+// reduces all 64+F columns, the sparse config the relu(H1) block (the root columns come
+// from sparse_dw_cols).
+__global__ void k_reduce_dw2(const float* __restrict__ part, int S, int64_t ldp, int64_t K2,
                              float* __restrict__ dw_td, float* __restrict__ dw_bu,
-                             const int32_t* __restrict__ gate) {
+                             const int32_t* __restrict__ gate, int want_dense) {
+  if (dense_active(gate) != (want_dense != 0)) return;
   int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  int64_t per = int64_t(H) * K2;
+  int64_t per = int64_t(H) * ldp;
   if (idx >= 2 * per) return;
   int d = int(idx / per);
   int64_t e = idx % per;
-  if (e % K2 >= H && gate_closed(gate)) return;   // root columns come from the sparse path
   const float* p = part + int64_t(d) * S * per + e;
   float acc = p[0];
   for (int s = 1; s < S; ++s) acc += p[int64_t(s) * per];
-  (d == 0 ? dw_td : dw_bu)[e] = acc;
+  (d == 0 ? dw_td : dw_bu)[(e / ldp) * K2 + e % ldp] = acc;
 }
 
 // ---------------------------------------------------------------- readout
@@ -401,6 +408,7 @@ struct FusedWs {
   float* dw2_part;                        // [2][S2][H][H+F]
   float* tn_ws; size_t tn_bytes;
   int S2; int64_t kchunk2;
+  int Sh; int64_t kchunkh;
 };
 
 int dw2_splits(int64_t N, int64_t F) {
@@ -432,7 +440,12 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   t.kchunk2 = kc;
   t.S2 = int((N + kc - 1) / kc);
   if (t.S2 < 1) t.S2 = 1;
-  t.dw2_part = c.take<float>(size_t(2) * t.S2 * H * (H + F));
+  // sparse path: relu(H1) block of dW2 over 256-node splits (partial rows of 64)
+  t.kchunkh = 256;
+  t.Sh = int((N + t.kchunkh - 1) / t.kchunkh);
+  if (t.Sh < 1) t.Sh = 1;
+  const size_t dense_part = size_t(2) * t.S2 * H * (H + F), sparse_part = size_t(2) * t.Sh * H * H;
+  t.dw2_part = c.take<float>(dense_part > sparse_part ? dense_part : sparse_part);
   t.tn_bytes = tn_ws_size(2 * H, F, N);
   t.tn_ws = c.take<float>(t.tn_bytes / sizeof(float) + 1);
   if (w) *w = t;
@@ -514,7 +527,7 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
                  "sparse feature buffers required unless feat_mode == BGCN_FEAT_DENSE");
   Carve c(ws, ws_bytes);
   carve_fused(c, N, B, F, &w);
-  sp.mode = a->feat_mode == BGCN_FEAT_DENSE ? 1 : 0;
+  sp.mode = (a->feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxF) ? 1 : 0;
   sp.flags = a->x_flags;
   sp.nnz = a->x_nnz;
   sp.cols = a->x_cols;
@@ -601,12 +614,22 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   // in sparse_dw_cols below)
   timing_begin(3, s);
   hipLaunchKernelGGL(k_dw2, dim3(grid_for(H + F, 64), w.S2, 2), dim3(256), 0, s, a->x, a->ldx, F,
-                     a->h1, w.dz2, w.node_root, w.dw2_part, N, w.kchunk2, w.S2, keep, gate);
+                     a->h1, w.dz2, w.node_root, w.dw2_part, N, w.kchunk2, w.S2, keep, gate, 1, H + F);
   BGCN_CHECK_LAUNCH();
+  if (sp.mode != 1) {
+    hipLaunchKernelGGL(k_dw2, dim3(1, w.Sh, 2), dim3(256), 0, s, a->x, a->ldx, F, a->h1, w.dz2,
+                       w.node_root, w.dw2_part, N, w.kchunkh, w.Sh, keep, gate, 0, int64_t(H));
+    BGCN_CHECK_LAUNCH();
+  }
   timing_end(3, s);
   hipLaunchKernelGGL(k_reduce_dw2, dim3(grid_for(2 * H * (H + F), 256)), dim3(256), 0, s,
-                     w.dw2_part, w.S2, H + F, a->td_dw2, a->bu_dw2, gate);
+                     w.dw2_part, w.S2, H + F, H + F, a->td_dw2, a->bu_dw2, gate, 1);
   BGCN_CHECK_LAUNCH();
+  if (sp.mode != 1) {
+    hipLaunchKernelGGL(k_reduce_dw2, dim3(grid_for(2 * H * H, 256)), dim3(256), 0, s, w.dw2_part,
+                       w.Sh, int64_t(H), H + F, a->td_dw2, a->bu_dw2, gate, 0);
+    BGCN_CHECK_LAUNCH();
+  }
   if (sp.mode != 1) BGCN_TRY(sparse_dw2_root_part(sp, a, w.dz2, keep, s));
   // dH1 through dropout and relu, db1
   hipLaunchKernelGGL(k_dh1, dim3(unsigned(nblk), 2), dim3(256), 0, s, w.dz2, a->h1, a->td_w2,

@@ -117,5 +117,6 @@ inline unsigned grid_for(int64_t n, int block) { return unsigned((n + block - 1)
 // feature path is off (gate == nullptr: always run) or has flagged an overflow row
 // (*gate != 0).  Decided on the device, so no host sync.
 __device__ __forceinline__ bool gate_closed(const int32_t* gate) { return gate && *gate == 0; }
+__device__ __forceinline__ bool dense_active(const int32_t* gate) { return !gate_closed(gate); }
 
 }  // namespace bgcn

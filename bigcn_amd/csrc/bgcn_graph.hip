@@ -256,10 +256,14 @@ __global__ void k_nodes(GraphBatch gb) {
   G.s_row[ps] = int32_t(i); G.s_col[ps] = int32_t(i); G.s_w[ps] = lw;
   // scatter_add over the final edge list in order (real edges, then the loop)
   const bool col = gb.degree_on == BGCN_DEGREE_ON_COL;
-  const int64_t a = col ? G.t_ptr[i] : G.s_ptr[i];
-  const float* wr = col ? G.t_w : G.s_w;
   float deg = 0.f;
-  for (int64_t p = a; p < (col ? pt : ps); ++p) deg += wr[p];
+  if (G.ew) {
+    const int64_t a = col ? G.t_ptr[i] : G.s_ptr[i];
+    const float* wr = col ? G.t_w : G.s_w;
+    for (int64_t p = a; p < (col ? pt : ps); ++p) deg += wr[p];
+  } else {
+    deg = float(col ? G.cnt_t[i] : G.cnt_s[i]);   // unit weights: the count (exact in fp32)
+  }
   deg += lw;
   float d = 1.0f / sqrtf(deg);  // pow(-0.5)
   if (isinf(d)) d = 0.f;

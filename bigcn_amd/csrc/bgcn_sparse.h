@@ -22,11 +22,14 @@ struct SparseState {
   int max_items;
   int32_t *item_tree, *item_chunk, *tree_item0;
   float* root_part;  // [2][max_items][kCap][64]
-  uint32_t *key_in, *val_in, *key_out, *val_out;  // [N*kCap] CSC sort
-  int32_t *col_start, *col_end;                    // [F]
-  void* sort_tmp;
-  size_t sort_bytes;
+  int32_t* hist;        // [R][F] per-row-block column counts -> prefixes (R = N / kRowBlock)
+  int32_t* col_total;   // [F]
+  int32_t *col_start, *col_end;  // [F]
+  uint32_t* csc_slot;   // [N*kCap] slots (i*kCap + s) grouped by column, rows in order
 };
+
+constexpr int kRowBlock = 256;          // rows per block of the CSC counting sort
+constexpr int64_t kSparseMaxF = 16384;  // LDS bound of the CSC kernels (2 x 4 B x F)
 
 size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S);
 int sparse_transpose(SparseState& S, const bgcn_bigcn_args* a, hipStream_t s);

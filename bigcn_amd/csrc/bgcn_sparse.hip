@@ -17,7 +17,7 @@
 // on the device, so the choice costs no host sync.
 #include <cstring>
 
-#include <rocprim/rocprim.hpp>
+
 
 #include "bgcn_sparse.h"
 
@@ -184,19 +184,38 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
 // Work item = (tree b, chunk of <= kChunk nodes of b), blockIdx.y = direction:
 // part[d][item][s][o] = sum_{i in chunk} keep_i[64 + col_s] * dZ2_d[i][o] for the root's
 // non-zeros s (the 2 relu(x) factor is applied in k_dw_cols).
-__global__ __launch_bounds__(256) void k_items(SparseState S, const int32_t* __restrict__ tree_ptr) {
-  if (!use_sparse(S) || threadIdx.x != 0 || blockIdx.x != 0) return;
-  int it = 0;
-  for (int64_t b = 0; b < S.B; ++b) {
-    S.tree_item0[b] = it;
-    const int n = tree_ptr[b + 1] - tree_ptr[b];
-    const int chunks = (n + kChunk - 1) / kChunk;
-    for (int q = 0; q < chunks && it < S.max_items; ++q, ++it) {
-      S.item_tree[it] = int32_t(b);
-      S.item_chunk[it] = q;
+// one block: items per tree = ceil(n_b / kChunk), exclusive scan over trees (1024 at a
+// time with a carry), then every tree writes its item descriptors.
+__global__ __launch_bounds__(1024) void k_items(SparseState S, const int32_t* __restrict__ tree_ptr) {
+  if (!use_sparse(S)) return;
+  __shared__ int sh[1024];
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < S.B; b0 += 1024) {
+    const int64_t b = b0 + threadIdx.x;
+    const int chunks = b < S.B ? (tree_ptr[b + 1] - tree_ptr[b] + kChunk - 1) / kChunk : 0;
+    sh[threadIdx.x] = chunks;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int v = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+      __syncthreads();
+      sh[threadIdx.x] += v;
+      __syncthreads();
     }
+    const int first = carry + sh[threadIdx.x] - chunks;
+    if (b < S.B) {
+      S.tree_item0[b] = first < S.max_items ? first : S.max_items;
+      for (int q = 0; q < chunks && first + q < S.max_items; ++q) {
+        S.item_tree[first + q] = int32_t(b);
+        S.item_chunk[first + q] = q;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += sh[1023];
+    __syncthreads();
   }
-  S.tree_item0[S.B] = it;
+  if (threadIdx.x == 0) S.tree_item0[S.B] = carry < S.max_items ? carry : S.max_items;
 }
 
 __global__ __launch_bounds__(256) void k_dw2_root_part(SparseState S, const float* __restrict__ dZ2,
@@ -247,25 +266,122 @@ __global__ __launch_bounds__(256) void k_dw2_root_part(SparseState S, const floa
 }
 
 // ---------------------------------------------------------------- CSC of X
-__global__ void k_csc_keys(SparseState S) {
+// Stable counting sort of the non-zeros by column (rows stay in order inside a column):
+//   k_csc_hist    per row block (kRowBlock rows): column histogram in LDS -> hist[r][c]
+//   k_csc_prefix  per column: exclusive prefix over the row blocks, column totals
+//   k_csc_place   per row block: column starts (LDS scan of the totals) + the block's
+//                 prefix, then the rows in order, 8 at a time, rank inside the batch
+// No float atomics, no general sort; deterministic.
+__global__ __launch_bounds__(256) void k_csc_hist(SparseState S) {
   if (!use_sparse(S)) return;
-  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= S.N * kCap) return;
-  const int64_t i = t / kCap;
-  const int s = int(t % kCap);
-  S.key_in[t] = s < S.nnz[i] ? uint32_t(S.cols[t]) : uint32_t(S.F);
-  S.val_in[t] = uint32_t(t);
+  extern __shared__ __attribute__((aligned(16))) int32_t hsm[];   // [F]
+  for (int64_t c = threadIdx.x; c < S.F; c += 256) hsm[c] = 0;
+  __syncthreads();
+  const int64_t r0 = int64_t(blockIdx.x) * kRowBlock;
+  for (int t = threadIdx.x; t < kRowBlock * kCap; t += 256) {
+    const int64_t i = r0 + t / kCap;
+    const int s = t % kCap;
+    if (i < S.N && s < S.nnz[i]) atomicAdd(&hsm[S.cols[i * kCap + s]], 1);
+  }
+  __syncthreads();
+  int32_t* out = S.hist + int64_t(blockIdx.x) * S.F;
+  for (int64_t c = threadIdx.x; c < S.F; c += 256) out[c] = hsm[c];
 }
 
-__global__ void k_col_bounds(SparseState S) {
+// 64 columns x 4 row-block quarters per block; hist[r][c] becomes the exclusive prefix
+__global__ __launch_bounds__(256) void k_csc_prefix(SparseState S, int R) {
   if (!use_sparse(S)) return;
-  const int64_t u = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int64_t n = S.N * kCap;
-  if (u >= n) return;
-  const uint32_t k = S.key_out[u];
-  if (k >= uint32_t(S.F)) return;
-  if (u == 0 || S.key_out[u - 1] != k) S.col_start[k] = int32_t(u);
-  if (u == n - 1 || S.key_out[u + 1] != k) S.col_end[k] = int32_t(u + 1);
+  __shared__ int32_t part[4][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t c = int64_t(blockIdx.x) * 64 + cl;
+  const int rq = (R + 3) / 4, rb = q * rq, re = min(R, rb + rq);
+  int32_t sum = 0;
+  if (c < S.F)
+    for (int r = rb; r < re; ++r) sum += S.hist[int64_t(r) * S.F + c];
+  part[q][cl] = sum;
+  __syncthreads();
+  int32_t run = 0;
+  for (int qq = 0; qq < q; ++qq) run += part[qq][cl];
+  if (c < S.F) {
+    for (int r = rb; r < re; ++r) {
+      const int32_t v = S.hist[int64_t(r) * S.F + c];
+      S.hist[int64_t(r) * S.F + c] = run;
+      run += v;
+    }
+    if (q == 3) S.col_total[c] = run;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
+  if (!use_sparse(S)) return;
+  extern __shared__ __attribute__((aligned(16))) int32_t psm[];   // [F] counters, [F] row masks
+  int32_t* cnt = psm;
+  uint32_t* rows = reinterpret_cast<uint32_t*>(psm + S.F);
+  __shared__ int32_t wsum[256];
+  // column starts: exclusive scan of col_total (each thread a contiguous run of columns)
+  const int64_t F = S.F;
+  const int64_t per = (F + 255) / 256;
+  const int64_t c0 = threadIdx.x * per, c1 = min<int64_t>(F, c0 + per);
+  int32_t local = 0;
+  for (int64_t c = c0; c < c1; ++c) local += S.col_total[c];
+  wsum[threadIdx.x] = local;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int32_t v = threadIdx.x >= o ? wsum[threadIdx.x - o] : 0;
+    __syncthreads();
+    wsum[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int32_t run = wsum[threadIdx.x] - local;
+  const int32_t* pre = S.hist + int64_t(blockIdx.x) * F;
+  for (int64_t c = c0; c < c1; ++c) {
+    const int32_t t = S.col_total[c];
+    cnt[c] = run + pre[c];
+    rows[c] = 0u;
+    if (blockIdx.x == 0) { S.col_start[c] = run; S.col_end[c] = run + t; }
+    run += t;
+  }
+  __syncthreads();
+  // rows of the block in order, 32 rows (= 1024 slots, 4 per thread) per batch.  The
+  // columns of one row are distinct, so an entry's rank among the batch's entries of
+  // its column = the number of earlier batch rows holding that column: an OR of row bits
+  // per column (order-independent) + popcount.
+  const int64_t r0 = int64_t(blockIdx.x) * kRowBlock;
+  constexpr int kBatchRows = 32;
+  for (int b = 0; b < kRowBlock; b += kBatchRows) {
+    int32_t col[4];
+    int rr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = threadIdx.x + 256 * k;
+      rr[k] = t / kCap;
+      const int64_t i = r0 + b + rr[k];
+      const int s = t % kCap;
+      col[k] = (i < S.N && s < S.nnz[i]) ? S.cols[i * kCap + s] : -1;
+      if (col[k] >= 0) atomicOr(&rows[col[k]], 1u << rr[k]);
+    }
+    __syncthreads();
+    int rank[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      rank[k] = -1;
+      if (col[k] >= 0) {
+        const uint32_t m = rows[col[k]];
+        rank[k] = __popc(m & ((1u << rr[k]) - 1u));
+        const int64_t i = r0 + b + rr[k];
+        S.csc_slot[cnt[col[k]] + rank[k]] = uint32_t(i * kCap + (threadIdx.x + 256 * k) % kCap);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (rank[k] == 0) {   // the batch's first entry of a column advances its counter
+        cnt[col[k]] += __popc(rows[col[k]]);
+        rows[col[k]] = 0u;
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------- dW1 + dW2 root columns
@@ -291,7 +407,7 @@ __global__ __launch_bounds__(1024) void k_dw_cols(SparseState S, const float* __
     for (int64_t u0 = beg; u0 < end; u0 += 64) {
       const int64_t u = u0 + lane;
       const bool ok = u < end;
-      const uint32_t slot = ok ? S.val_out[u] : 0u;
+      const uint32_t slot = ok ? S.csc_slot[u] : 0u;
       const float x_l = ok ? S.vals[slot] : 0.f;
       const int32_t i_l = int32_t(slot / kCap);
       const int32_t s_l = int32_t(slot % kCap);
@@ -356,15 +472,6 @@ __global__ __launch_bounds__(1024) void k_dw_cols(SparseState S, const float* __
   }
 }
 
-size_t sort_bytes(int64_t n, int64_t F) {
-  size_t bytes = 0;
-  int bits = 1;
-  while ((int64_t(1) << bits) <= F) ++bits;
-  (void)rocprim::radix_sort_pairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                  (uint32_t*)nullptr, (uint32_t*)nullptr, size_t(n), 0, bits);
-  return bytes;
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------- host side
@@ -381,14 +488,12 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   t.tree_item0 = c.take<int32_t>(size_t(B + 1));
   t.root_part = c.take<float>(size_t(2) * t.max_items * kCap * H);
   const size_t slots = size_t(N) * kCap;
-  t.key_in = c.take<uint32_t>(slots);
-  t.val_in = c.take<uint32_t>(slots);
-  t.key_out = c.take<uint32_t>(slots);
-  t.val_out = c.take<uint32_t>(slots);
+  const size_t R = size_t((N + kRowBlock - 1) / kRowBlock);
+  t.hist = c.take<int32_t>(R * size_t(F));
+  t.col_total = c.take<int32_t>(size_t(F));
   t.col_start = c.take<int32_t>(size_t(F));
   t.col_end = c.take<int32_t>(size_t(F));
-  t.sort_bytes = sort_bytes(int64_t(slots), F);
-  t.sort_tmp = c.take<char>(t.sort_bytes + 16);
+  t.csc_slot = c.take<uint32_t>(slots);
   if (S) {
     t.mode = S->mode;
     t.flags = S->flags;
@@ -424,7 +529,7 @@ int sparse_conv2(SparseState& S, const float* H1, const int32_t* node_root, floa
 
 int sparse_dw2_root_part(SparseState& S, const bgcn_bigcn_args* a, const float* dZ2, KeepSrc keep,
                          hipStream_t s) {
-  hipLaunchKernelGGL(k_items, dim3(1), dim3(64), 0, s, S, a->tree_ptr);
+  hipLaunchKernelGGL(k_items, dim3(1), dim3(1024), 0, s, S, a->tree_ptr);
   BGCN_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_dw2_root_part, dim3(unsigned(S.max_items), 2), dim3(256), 0, s, S, dZ2,
                      a->tree_ptr, a->rootindex, keep);
@@ -434,17 +539,12 @@ int sparse_dw2_root_part(SparseState& S, const bgcn_bigcn_args* a, const float* 
 
 int sparse_dw_cols(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1,
                    const int32_t* node_root, KeepSrc keep, hipStream_t s) {
-  const int64_t slots = S.N * kCap;
-  hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(slots, 256)), dim3(256), 0, s, S);
+  const int R = int((S.N + kRowBlock - 1) / kRowBlock);
+  hipLaunchKernelGGL(k_csc_hist, dim3(unsigned(R)), dim3(256), size_t(S.F) * sizeof(int32_t), s, S);
   BGCN_CHECK_LAUNCH();
-  int bits = 1;
-  while ((int64_t(1) << bits) <= S.F) ++bits;
-  size_t tb = S.sort_bytes;
-  BGCN_CHECK_HIP(rocprim::radix_sort_pairs(S.sort_tmp, tb, S.key_in, S.key_out, S.val_in, S.val_out,
-                                           size_t(slots), 0, bits, s));
-  BGCN_CHECK_HIP(hipMemsetAsync(S.col_start, 0, size_t(S.F) * sizeof(int32_t), s));
-  BGCN_CHECK_HIP(hipMemsetAsync(S.col_end, 0, size_t(S.F) * sizeof(int32_t), s));
-  hipLaunchKernelGGL(k_col_bounds, dim3(grid_for(slots, 256)), dim3(256), 0, s, S);
+  hipLaunchKernelGGL(k_csc_prefix, dim3(grid_for(S.F, 64)), dim3(256), 0, s, S, R);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_csc_place, dim3(unsigned(R)), dim3(256), size_t(2 * S.F) * sizeof(int32_t), s, S);
   BGCN_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_dw_cols, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, dZ1, node_root,
                      a->batch, a->td_dw1, a->bu_dw1, a->td_dw2, a->bu_dw2, keep.scale());

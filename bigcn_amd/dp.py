@@ -2,15 +2,16 @@
 
 The reference is single-device (``BiGCN_Twitter.py:367``).  Trees are independent,
 so the batch shards with no halo exchange: each rank builds its own graphs and runs
-the fused encoder on its own 128 trees; the only exchange is one all-reduce of the
-flat fp32 gradient bucket (1,289,476 params = 5.16 MB for the Twitter model) per
-step over RCCL (torch.distributed backend "nccl" on ROCm) / gloo on CPU, followed by
-the same Adam step on every rank.
+the fused encoder on its own 128 trees; the only exchange is one all-reduce (sum) of
+the flat fp32 gradient bucket (1,289,476 params = 5.16 MB for the Twitter model) per
+step over RCCL (torch.distributed backend "nccl" on ROCm) / gloo on CPU.  The mean
+(÷ world) is folded into the fused Adam step (``grad_scale``), which reads the reduced
+bucket in place, so every rank applies the identical update.
 """
 from __future__ import annotations
 
 import os
-from typing import Iterable, List
+from typing import Iterable, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -38,29 +39,30 @@ class GradBucket:
 
     def __init__(self, params: Iterable[torch.nn.Parameter]):
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
+        self.numels = [p.numel() for p in self.params]
         dev = self.params[0].device
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.flat = torch.zeros(sum(self.numels), dtype=torch.float32, device=dev)
+
+    def world(self, group=None) -> int:
+        return dist.get_world_size(group) if dist.is_initialized() else 1
+
+    def reduce_sum(self, group=None) -> List[torch.Tensor]:
+        """Concatenate the grads (one copy kernel), all-reduce SUM in place, and return
+        views of the reduced bucket in parameter order (the caller divides by world)."""
+        grads = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(n, device=self.flat.device)
+                 for p, n in zip(self.params, self.numels)]
+        torch.cat(grads, out=self.flat)
+        if dist.is_initialized() and self.world(group) > 1:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+        return [v.view_as(p) for v, p in zip(torch.split(self.flat, self.numels), self.params)]
 
     def allreduce_mean(self, group=None) -> None:
-        """grads <- mean over ranks of grads (sum all-reduce, then / world)."""
-        if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        """In-place mean of p.grad over ranks (for torch optimisers)."""
+        world = self.world(group)
+        if world == 1:
             return
-        world = dist.get_world_size(group)
-        off = 0
-        for p in self.params:
-            n = p.numel()
-            if p.grad is None:
-                self.flat[off:off + n].zero_()
-            else:
-                self.flat[off:off + n].copy_(p.grad.view(-1))
-            off += n
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
-        self.flat.div_(world)
-        off = 0
-        for p in self.params:
-            n = p.numel()
+        views = self.reduce_sum(group)
+        for p, v in zip(self.params, views):
             if p.grad is None:
                 p.grad = torch.empty_like(p)
-            p.grad.view(-1).copy_(self.flat[off:off + n])
-            off += n
+            p.grad.copy_(v).div_(world)

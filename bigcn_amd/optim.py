@@ -1,0 +1,107 @@
+"""Fused Adam for the BiGCN training loop (one HIP launch per step).
+
+Mirrors ``torch.optim.Adam([{base}, {BU conv1, lr/5}, {BU conv2, lr/5}], lr=5e-4,
+weight_decay=1e-4)`` of ``model/Twitter/BiGCN_Twitter.py:146-153`` (step at ``:189``):
+same update rule (amsgrad off, weight decay as L2 in the gradient), same parameter
+groups and learning rates, kernel ``bgcn_adam_step`` in ``csrc/bgcn_optim.hip``.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Iterable, List, Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream_handle
+
+MAX_TENSORS = 16
+
+
+class _AdamTensor(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_int64), ("lr", ctypes.c_float)]
+
+
+class AdamArgs(ctypes.Structure):
+    _fields_ = [("t", _AdamTensor * MAX_TENSORS), ("block_start", ctypes.c_int64 * MAX_TENSORS),
+                ("count", ctypes.c_int), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+                ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
+                ("bias_correction1", ctypes.c_float), ("bias_correction2_sqrt", ctypes.c_float),
+                ("grad_scale", ctypes.c_float)]
+
+
+class FusedAdam:
+    """``param_groups``: list of dicts {"params": [...], "lr": float} (torch layout)."""
+
+    def __init__(self, param_groups: Sequence[dict], lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0):
+        self.param_groups = []
+        for g in param_groups:
+            ps = [p for p in g["params"]]
+            self.param_groups.append({"params": ps, "lr": g.get("lr", lr)})
+        self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
+        self.step_count = 0
+        self.state = {}
+        n = sum(len(g["params"]) for g in self.param_groups)
+        if n > MAX_TENSORS:
+            raise ValueError(f"FusedAdam handles at most {MAX_TENSORS} tensors")
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.dtype != torch.float32 or not p.is_contiguous():
+                    raise ValueError("FusedAdam: contiguous fp32 parameters only")
+                self.state[p] = (torch.zeros_like(p), torch.zeros_like(p))
+
+    def params(self) -> List[torch.nn.Parameter]:
+        return [p for g in self.param_groups for p in g["params"]]
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        for p in self.params():
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
+
+    @torch.no_grad()
+    def step(self, grads: Optional[Sequence[torch.Tensor]] = None, grad_scale: float = 1.0) -> None:
+        """``grads`` overrides ``p.grad`` (e.g. views of a reduced flat DP bucket)."""
+        self.step_count += 1
+        t = self.step_count
+        b1, b2 = self.betas
+        a = AdamArgs()
+        a.beta1, a.beta2, a.eps, a.weight_decay = b1, b2, self.eps, self.weight_decay
+        a.bias_correction1 = 1.0 - b1 ** t
+        a.bias_correction2_sqrt = math.sqrt(1.0 - b2 ** t)
+        a.grad_scale = grad_scale
+        k = 0
+        keep = []
+        gi = 0
+        for g in self.param_groups:
+            for p in g["params"]:
+                gr = grads[gi] if grads is not None else p.grad
+                gi += 1
+                if gr is None:
+                    continue
+                gr = gr.contiguous()
+                keep.append(gr)
+                m, v = self.state[p]
+                e = a.t[k]
+                e.param, e.grad, e.exp_avg, e.exp_avg_sq = ptr(p), ptr(gr), ptr(m), ptr(v)
+                e.numel, e.lr = p.numel(), g["lr"]
+                k += 1
+        a.count = k
+        if k:
+            check(_lib.lib().bgcn_adam_step(ctypes.addressof(a), stream_handle()))
+
+
+def bigcn_adam(model, lr: float = 5e-4, weight_decay: float = 1e-4) -> FusedAdam:
+    """The reference's optimiser (``BiGCN_Twitter.py:146-153``) on FusedAdam."""
+    bu_ids = {id(p) for p in model.BUrumorGCN.conv1.parameters()}
+    bu_ids |= {id(p) for p in model.BUrumorGCN.conv2.parameters()}
+    base = [p for p in model.parameters() if id(p) not in bu_ids]
+    return FusedAdam([
+        {"params": base},
+        {"params": list(model.BUrumorGCN.conv1.parameters()), "lr": lr / 5},
+        {"params": list(model.BUrumorGCN.conv2.parameters()), "lr": lr / 5},
+    ], lr=lr, weight_decay=weight_decay)

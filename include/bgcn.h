@@ -227,6 +227,28 @@ int bgcn_bigcn_forward(const bgcn_bigcn_args* args, void* workspace, size_t work
 int bgcn_bigcn_backward(const bgcn_bigcn_args* args, void* workspace, size_t workspace_bytes,
                         bgcn_stream_t stream);
 
+/* --------------------------------------------------------------------------
+ * Optimiser step of the training loop: torch.optim.Adam with the reference's three
+ * parameter groups (BiGCN_Twitter.py:146-153, step at :189) as ONE fused launch.
+ * amsgrad = False; weight_decay is L2 added to the gradient (torch Adam semantics).
+ * grad_scale multiplies every gradient first (1/world for a summed DP bucket).
+ * bias_correction1 = 1 - beta1^t, bias_correction2_sqrt = sqrt(1 - beta2^t).
+ * block_start is scratch filled by the library.
+ * -------------------------------------------------------------------------- */
+#define BGCN_ADAM_MAX_TENSORS 16
+typedef struct bgcn_adam_tensor {
+  float* param; const float* grad; float* exp_avg; float* exp_avg_sq;
+  int64_t numel; float lr;
+} bgcn_adam_tensor;
+typedef struct bgcn_adam_args {
+  bgcn_adam_tensor t[BGCN_ADAM_MAX_TENSORS];
+  int64_t block_start[BGCN_ADAM_MAX_TENSORS];
+  int count;
+  float beta1, beta2, eps, weight_decay;
+  float bias_correction1, bias_correction2_sqrt, grad_scale;
+} bgcn_adam_args;
+int bgcn_adam_step(const bgcn_adam_args* args, bgcn_stream_t stream);
+
 /* Materialise the in-kernel dropout keep bits (for tests / debugging):
  * words[dir][n][w] for dir in {0 (TD), 1 (BU)}. */
 int bgcn_keep_words(uint64_t seed, int64_t num_nodes, int32_t num_words, uint32_t* words,
