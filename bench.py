@@ -135,11 +135,14 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--feat-mode", default="auto", choices=["auto", "dense"],
                     help="auto: sparse feature path with device-side dense fallback; dense: MFMA only")
+    ap.add_argument("--path", default="fused", choices=["fused", "autograd"],
+                    help="fused: FusedTrainStep (one native call per step); autograd: per-op "
+                         "drop-in modules + loss.backward()")
     ap.add_argument("--compare-dense", type=int, default=1,
                     help="at N=1 also time the dense MFMA path and report it beside the main line")
     args = ap.parse_args()
 
-    from bigcn_amd import BiGCN
+    from bigcn_amd import BiGCN, FusedTrainStep
     from bigcn_amd import ops
     from bigcn_amd.dp import GradBucket, init_from_env
     from bigcn_amd.optim import bigcn_adam
@@ -158,11 +161,19 @@ def main():
         for p in model.parameters():
             dist.broadcast(p.data, 0)
     model.train()
+    # the step runs on its own stream: the fused encoder forks independent branches onto
+    # libbgcn's auxiliary stream, which needs a non-default stream to wait on the device
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
     opt = bigcn_adam(model)                             # reference groups, one fused launch
     bucket = GradBucket(opt.params())                   # same parameter order as opt
 
+    fused = FusedTrainStep(model, opt)                  # bgcn_train_step + all-reduce + Adam
+
     def step(i):
         b = pool[i % len(pool)]
+        if args.path == "fused":                        # K1 + fwd + head + loss + bwd in one call
+            return fused(b)
         b.__dict__.pop("_bgcn_graphs", None)          # gcn_norm/CSR rebuilt every step (as GCNConv does)
         logp = model(b)
         loss = F.nll_loss(logp, b.y)
@@ -175,6 +186,10 @@ def main():
         return loss
 
     def run(mode: str, steps: int, warmup: int):
+        with torch.cuda.stream(stream):
+            return run_on_stream(mode, steps, warmup)
+
+    def run_on_stream(mode: str, steps: int, warmup: int):
         model.feat_mode = mode
         for i in range(warmup):
             step(i)
@@ -258,7 +273,7 @@ def main():
                        "global_batch": wl["trees"] * world, "avg_nodes_per_batch": round(N_avg, 1),
                        "in_feats": wl["feats"], "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "final_loss": round(final_loss, 5),
-            "feat_mode": args.feat_mode,
+            "feat_mode": args.feat_mode, "step_path": args.path,
         }
         if dense_res is not None:
             out["dense_path"] = {"value": round(dense_res["value"], 2), "unit": "trees/s",

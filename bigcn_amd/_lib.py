@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_scatter_mean_workspace_size", "bgcn_scatter_mean_fwd", "bgcn_scatter_mean_bwd",
     "bgcn_bigcn_workspace_size", "bgcn_bigcn_forward", "bgcn_bigcn_backward",
     "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_adam_step",
+    "bgcn_train_step_workspace_size", "bgcn_train_step",
 )
 
 
@@ -71,6 +72,23 @@ class BiGCNArgs(Structure):
         ("dhead_in", c_void_p),
         ("td_dw1", c_void_p), ("td_db1", c_void_p), ("td_dw2", c_void_p), ("td_db2", c_void_p),
         ("bu_dw1", c_void_p), ("bu_db1", c_void_p), ("bu_dw2", c_void_p), ("bu_db2", c_void_p),
+        ("save_for_backward", c_int32),
+    ]
+
+
+BGCN_STEP_PARAMS = 10
+
+
+class StepArgs(Structure):
+    """bgcn_step_args (include/bgcn.h)."""
+    _fields_ = [
+        ("x", c_void_p), ("ldx", c_int64), ("num_nodes", c_int64), ("num_graphs", c_int64),
+        ("in_feats", c_int64), ("num_classes", c_int64), ("batch", c_void_p), ("rootindex", c_void_p),
+        ("y", c_void_p), ("td_edge_index", c_void_p), ("td_num_edges", c_int64),
+        ("bu_edge_index", c_void_p), ("bu_num_edges", c_int64), ("degree_on", c_int32),
+        ("training", c_int32), ("seed", c_uint64), ("feat_mode", c_int32),
+        ("params", c_void_p * BGCN_STEP_PARAMS), ("grads", c_void_p * BGCN_STEP_PARAMS),
+        ("loss", c_void_p), ("logp", c_void_p), ("status", c_void_p),
     ]
 
 
@@ -111,6 +129,8 @@ _SIGS = {
     "bgcn_bigcn_backward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
     "bgcn_keep_words": (c_int, [c_uint64, c_int64, c_int32, c_void_p, c_void_p]),
     "bgcn_adam_step": (c_int, [c_void_p, c_void_p]),
+    "bgcn_train_step_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64, c_int64, c_int64]),
+    "bgcn_train_step": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_set_kernel_timing": (c_int, [c_int]),
     "bgcn_kernel_timing": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),
 }

@@ -241,130 +241,209 @@ __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_
 
 // dW2_d[o][c] = sum_s part[d][s][o][c] (fixed order) for c < ldp; the dense config
 // reduces all 64+F columns, the sparse config the relu(H1) block (the root columns come
-// from sparse_dw_cols).
-__global__ void k_reduce_dw2(const float* __restrict__ part, int S, int64_t ldp, int64_t K2,
-                             float* __restrict__ dw_td, float* __restrict__ dw_bu,
-                             const int32_t* __restrict__ gate, int want_dense) {
+// from sparse_dw_cols).  A block owns 64 consecutive outputs; its 4 waves take splits
+// s = q (mod 4), four loads in flight each, combined in wave order: deterministic.
+// Grid-stride over output tiles, so a small grid retires cheaply when the gate skips it.
+__global__ __launch_bounds__(256) void k_reduce_dw2(const float* __restrict__ part, int S,
+                                                    int64_t ldp, int64_t K2,
+                                                    float* __restrict__ dw_td,
+                                                    float* __restrict__ dw_bu,
+                                                    const int32_t* __restrict__ gate,
+                                                    int want_dense) {
   if (dense_active(gate) != (want_dense != 0)) return;
-  int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  int64_t per = int64_t(H) * ldp;
-  if (idx >= 2 * per) return;
-  int d = int(idx / per);
-  int64_t e = idx % per;
-  const float* p = part + int64_t(d) * S * per + e;
-  float acc = p[0];
-  for (int s = 1; s < S; ++s) acc += p[int64_t(s) * per];
-  (d == 0 ? dw_td : dw_bu)[(e / ldp) * K2 + e % ldp] = acc;
+  __shared__ float red[4][64];
+  const int64_t per = int64_t(H) * ldp;
+  const int64_t ntiles = (2 * per + 63) / 64;
+  const int q = threadIdx.x >> 6, t = threadIdx.x & 63;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t idx = tile * 64 + t;
+    const bool valid = idx < 2 * per;
+    const int d = valid ? int(idx / per) : 0;
+    const int64_t e = valid ? idx % per : 0;
+    const float* p = part + int64_t(d) * S * per + e;
+    float acc = 0.f;
+    int s = q;
+    if (valid) {
+      for (; s + 12 < S; s += 16) {
+        const float v0 = p[int64_t(s) * per], v1 = p[int64_t(s + 4) * per];
+        const float v2 = p[int64_t(s + 8) * per], v3 = p[int64_t(s + 12) * per];
+        acc += v0; acc += v1; acc += v2; acc += v3;
+      }
+      for (; s < S; s += 4) acc += p[int64_t(s) * per];
+    }
+    red[q][t] = acc;
+    __syncthreads();
+    if (q == 0 && valid)
+      (d == 0 ? dw_td : dw_bu)[(e / ldp) * K2 + e % ldp] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------- readout
 // head_in[b] = [BU: mean(relu(H2_bu)) | H1_bu[root] , TD: mean(relu(H2_td)) | H1_td[root]]
-// One block per (tree, direction): 16 row slices x 16 lanes x float4.
-__global__ __launch_bounds__(256) void k_readout_fwd(const float* __restrict__ H1,
-                                                     const float* __restrict__ H2,
-                                                     const int32_t* __restrict__ tree_ptr,
-                                                     const int64_t* __restrict__ rootindex,
-                                                     int64_t N, float* __restrict__ head) {
-  __shared__ float4 red[2][16][16];
+// One 1024-thread block per (tree, direction): 64 row slices x 16 lanes x float4, eight
+// independent row loads in flight per slice, then a fixed-order two-level LDS reduction
+// (deterministic).  The root half is the mean of identical copies, i.e. H1[root] itself
+// (the reference's root_extend is a detached copy, BiGCN_Twitter.py:42-47, so it has no
+// backward).
+constexpr int kReadSlices = 64;
+__global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ H1,
+                                                      const float* __restrict__ H2,
+                                                      const int32_t* __restrict__ tree_ptr,
+                                                      const int64_t* __restrict__ rootindex,
+                                                      int64_t N, float* __restrict__ head) {
+  __shared__ float4 red[kReadSlices][16];
+  __shared__ float4 red2[8][16];
   const int b = blockIdx.x, d = blockIdx.y;
   const int lane = threadIdx.x & 15, slice = threadIdx.x >> 4;
   const int64_t beg = tree_ptr[b], end = tree_ptr[b + 1];
-  const int64_t root = rootindex[b];
-  const float4 hr = (end > beg && root >= 0 && root < N)
-                        ? ld4(H1 + root * (2 * H) + d * H + lane * 4) : f4zero();
-  float4 s1 = f4zero(), s2 = f4zero();
-  for (int64_t i = beg + slice; i < end; i += 16) {
-    s1 = f4add(s1, f4relu(ld4(H2 + i * (2 * H) + d * H + lane * 4)));
-    s2 = f4add(s2, hr);
+  const float* src = H2 + d * H + lane * 4;
+  float4 s = f4zero();
+  int64_t i = beg + slice;
+  for (; i + 7 * kReadSlices < end; i += 8 * kReadSlices) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld4(src + (i + u * kReadSlices) * (2 * H));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = f4add(s, f4relu(v[u]));
   }
-  red[0][slice][lane] = s1;
-  red[1][slice][lane] = s2;
+  for (; i < end; i += kReadSlices) s = f4add(s, f4relu(ld4(src + i * (2 * H))));
+  red[slice][lane] = s;
   __syncthreads();
-  if (slice < 2) {
-    float4 acc = red[slice][0][lane];
-    for (int q = 1; q < 16; ++q) acc = f4add(acc, red[slice][q][lane]);
-    float cnt = float(end - beg > 0 ? end - beg : 1);
+  if (threadIdx.x < 128) {
+    const int g = threadIdx.x >> 4;
+    float4 acc = red[g * 8][lane];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) acc = f4add(acc, red[g * 8 + q][lane]);
+    red2[g][lane] = acc;
+  }
+  __syncthreads();
+  const int base = (d == 1 ? 0 : 2 * H) + lane * 4;  // BU first (:128)
+  if (threadIdx.x < 16) {
+    float4 acc = red2[0][lane];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) acc = f4add(acc, red2[q][lane]);
+    const float cnt = float(end - beg > 0 ? end - beg : 1);
     acc = make_float4(acc.x / cnt, acc.y / cnt, acc.z / cnt, acc.w / cnt);
-    const int off = (d == 1 ? 0 : 2 * H) + slice * H + lane * 4;  // BU first (:128)
-    st4(head + int64_t(b) * (4 * H) + off, acc);
+    st4(head + int64_t(b) * (4 * H) + base, acc);
+  } else if (threadIdx.x < 32) {
+    const int64_t root = rootindex[b];
+    const float4 hr = (end > beg && root >= 0 && root < N)
+                          ? ld4(H1 + root * (2 * H) + d * H + lane * 4) : f4zero();
+    st4(head + int64_t(b) * (4 * H) + base + H, hr);
   }
 }
 
 // dH2[i][d*H + f] = dhead[b(i)][r1 block of d][f] / cnt_b * [H2 > 0]; block partial
-// column sums -> colpart[blk][2H].  256 threads = 2 row phases x 128 columns.
+// column sums -> colpart[blk][2H].  256 threads = 8 row phases x 32 lanes x float4; a
+// block covers kReadBwdRows rows, every thread's rows are loaded before use.
+constexpr int kReadBwdRows = 64;
 __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dhead,
                                                      const float* __restrict__ H2,
                                                      const int64_t* __restrict__ batch,
                                                      const int32_t* __restrict__ tree_ptr,
-                                                     int64_t N, int64_t B, int rows_per_block,
+                                                     int64_t N, int64_t B,
                                                      float* __restrict__ dH2,
                                                      float* __restrict__ colpart) {
-  __shared__ float red[256];
-  const int c = threadIdx.x & 127, ph = threadIdx.x >> 7;
-  const int d = c / H, f = c % H;
+  constexpr int kPer = kReadBwdRows / 8;
+  __shared__ float4 red[8][32];
+  const int l = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  const int c = l * 4, d = c / H, f = c % H;
   const int hoff = (d == 1 ? 0 : 2 * H) + f;
-  const int64_t r0 = int64_t(blockIdx.x) * rows_per_block;
-  const int64_t r1 = min<int64_t>(r0 + rows_per_block, N);
-  float cs = 0.f;
-  for (int64_t i = r0 + ph; i < r1; i += 2) {
-    int64_t b = batch[i];
-    float g = 0.f;
-    if (b >= 0 && b < B) {
-      float cnt = float(max(tree_ptr[b + 1] - tree_ptr[b], 1));
-      float h2 = H2[i * (2 * H) + c];
-      g = h2 > 0.f ? dhead[b * (4 * H) + hoff] / cnt : 0.f;
-    }
-    dH2[i * (2 * H) + c] = g;
-    cs += g;
+  const int64_t r0 = int64_t(blockIdx.x) * kReadBwdRows;
+  int64_t bt[kPer];
+  float4 h2[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t i = r0 + ph + 8 * u;
+    bt[u] = i < N ? batch[i] : -1;
+    h2[u] = i < N ? ld4(H2 + i * (2 * H) + c) : f4zero();
   }
-  red[threadIdx.x] = cs;
+  float4 cs = f4zero();
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t i = r0 + ph + 8 * u;
+    const int64_t b = bt[u];
+    float4 g = f4zero();
+    if (b >= 0 && b < B) {
+      const float cnt = float(max(tree_ptr[b + 1] - tree_ptr[b], 1));
+      const float4 dh = ld4(dhead + b * (4 * H) + hoff);
+      g.x = h2[u].x > 0.f ? dh.x / cnt : 0.f;
+      g.y = h2[u].y > 0.f ? dh.y / cnt : 0.f;
+      g.z = h2[u].z > 0.f ? dh.z / cnt : 0.f;
+      g.w = h2[u].w > 0.f ? dh.w / cnt : 0.f;
+    }
+    if (i < N) st4(dH2 + i * (2 * H) + c, g);
+    cs = f4add(cs, g);
+  }
+  red[ph][l] = cs;
   __syncthreads();
-  if (ph == 0) colpart[int64_t(blockIdx.x) * (2 * H) + c] = red[c] + red[c + 128];
+  if (ph == 0) {
+    float4 acc = red[0][l];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) acc = f4add(acc, red[q][l]);
+    st4(colpart + int64_t(blockIdx.x) * (2 * H) + c, acc);
+  }
 }
 
 // dH1[i][d*H + c] = (dZ2_d[i] . W2_d[:, c]) * keep(d,i,c) * s * [H1 > 0], c < H,
-// + block partial column sums.  Block: 4 nodes x 64 columns per step, both directions
-// handled by blockIdx.y; W2_d[:, :H] staged in LDS.
+// + block partial column sums.  A 64-row x 64-column tile per (block, direction) on the
+// fp32 MFMA (32x32x2): four waves as 2 row halves x 2 column halves, K = H = 64 in 32
+// steps.  The K order is permuted (lane half h owns k in [32h, 32h+32)) so each lane's
+// dZ2 operand is one contiguous 128-byte run; W2 rows come straight from L2.
+constexpr int kDh1Rows = 64;
 __global__ __launch_bounds__(256) void k_dh1(const float* __restrict__ dZ2,
                                              const float* __restrict__ H1,
                                              const float* __restrict__ W2td,
                                              const float* __restrict__ W2bu, int64_t ldw2,
-                                             int64_t N, int rows_per_block, KeepSrc keep,
+                                             int64_t N, KeepSrc keep,
                                              float* __restrict__ dH1, float* __restrict__ colpart) {
-  __shared__ float Ws[H * (H + 1)];
-  __shared__ float dz[4][H];
-  __shared__ float red[4][H];
+  __shared__ float red[2][H];
   const int d = blockIdx.y;
   const float* W2 = d == 0 ? W2td : W2bu;
-  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
-  for (int e = threadIdx.x; e < H * H; e += 256) {
-    int o = e / H, cc = e % H;
-    Ws[o * (H + 1) + cc] = W2[int64_t(o) * ldw2 + cc];
+  const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int rh = wid & 1, ch = wid >> 1;
+  const int r = l & 31, h = l >> 5;
+  const int64_t row0 = int64_t(blockIdx.x) * kDh1Rows + rh * 32;
+  const int c = ch * 32 + r;  // output column of this lane (within H)
+
+  float a[32], bv[32];
+  const int64_t ia = row0 + r;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 v = ia < N ? ld4(dZ2 + ia * (2 * H) + d * H + 32 * h + 4 * q) : f4zero();
+    a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
   }
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) bv[kk] = W2[int64_t(32 * h + kk) * ldw2 + c];
+  float hv[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    hv[q] = i < N ? H1[i * (2 * H) + d * H + c] : 0.f;
+  }
+  f32x16 acc = {};
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) acc = mfma32x32x2(a[kk], bv[kk], acc);
+
   const float sc = keep.scale();
-  const int64_t r0 = int64_t(blockIdx.x) * rows_per_block;
-  const int64_t r1 = min<int64_t>(r0 + rows_per_block, N);
   float cs = 0.f;
-  for (int64_t base = r0; base < r1; base += 4) {
-    const int64_t i = base + q;
-    __syncthreads();
-    dz[q][c] = i < r1 ? dZ2[i * (2 * H) + d * H + c] : 0.f;
-    __syncthreads();
-    if (i < r1) {
-      float acc = 0.f;
-#pragma unroll 16
-      for (int o = 0; o < H; ++o) acc = fmaf(dz[q][o], Ws[o * (H + 1) + c], acc);
-      uint32_t wd = keep.get(uint32_t(d), uint32_t(i), uint32_t(c / 32));
-      float h1 = H1[i * (2 * H) + d * H + c];
-      float g = (((wd >> (c & 31)) & 1u) && h1 > 0.f) ? acc * sc : 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    if (i < N) {
+      const uint32_t wd = keep.get(uint32_t(d), uint32_t(i), uint32_t(c >> 5));
+      const float g = (((wd >> (c & 31)) & 1u) && hv[q] > 0.f) ? acc[q] * sc : 0.f;
       dH1[i * (2 * H) + d * H + c] = g;
       cs += g;
     }
   }
-  red[q][c] = cs;
+  cs += __shfl_xor(cs, 32);
+  if (h == 0) red[rh][c] = cs;
   __syncthreads();
-  if (q == 0)
-    colpart[int64_t(blockIdx.x) * (2 * H) + d * H + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  if (threadIdx.x < H)
+    colpart[int64_t(blockIdx.x) * (2 * H) + d * H + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x];
 }
 
 // out_td[c] = sum_p colpart[p][c], out_bu[c] = sum_p colpart[p][H + c]: one block per
@@ -398,7 +477,6 @@ __global__ void k_keep_words(uint64_t seed, int64_t N, int nw, uint32_t* __restr
 }
 
 // ---------------------------------------------------------------- workspace
-constexpr int kRowsPerBlock = 128;
 
 struct FusedWs {
   int32_t* node_root;
@@ -431,7 +509,8 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   t.dz2 = c.take<float>(nm);
   t.dh1 = c.take<float>(nm);
   t.dz1 = c.take<float>(nm);
-  const int64_t nblk = (N + kRowsPerBlock - 1) / kRowsPerBlock;
+  const int64_t nblk = std::max((N + kDh1Rows - 1) / kDh1Rows,
+                                 (N + kReadBwdRows - 1) / kReadBwdRows);
   t.colpart = c.take<float>(size_t(nblk) * 2 * H);
   t.S2 = dw2_splits(N, F);
   int64_t kc = (N + t.S2 - 1) / t.S2;
@@ -541,7 +620,14 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
   return BGCN_OK;
 }
 
-int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s) {
+// Forward.  Main stream: node maps, conv1 (sparse compaction + gather, or dense MFMA),
+// propagate, conv2, propagate, readout.  When a backward follows, the CSC of X for dW1
+// is built on auxiliary lane 0 right after the compaction, overlapped with the
+// latency-bound second half of the forward, and joined before returning.  graph_lane
+// >= 0: the caller is building the TD/BU graphs on that lane (bgcn_train_step), joined
+// just before their first use.
+int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
+                       int graph_lane) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->head_in && a->td_w1 && a->bu_w1 && a->td_w2 && a->bu_w2, "null pointer");
   const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
@@ -550,8 +636,9 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
   const int32_t* gate = nullptr;
   BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate));
   KeepSrc keep = make_keep(a);
+  const bool sparse = sp.mode != 1;
 
-  if (sp.mode != 1) BGCN_CHECK_HIP(hipMemsetAsync(a->x_flags, 0, 8 * sizeof(int32_t), s));
+  if (sparse) BGCN_CHECK_HIP(hipMemsetAsync(a->x_flags, 0, 8 * sizeof(int32_t), s));
   hipLaunchKernelGGL(k_tree_ptr, dim3(grid_for(B + 1, 256)), dim3(256), 0, s, a->batch, N, B,
                      a->tree_ptr);
   BGCN_CHECK_LAUNCH();
@@ -559,31 +646,44 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
                      a->rootindex, N, B, w.node_root);
   BGCN_CHECK_LAUNCH();
   // conv1 lin, TD and BU in one pass over X: sparse (compaction + gather) or dense MFMA
-  if (sp.mode != 1) {
+  bool forked = false;
+  if (sparse) {
     BGCN_TRY(sparse_transpose(sp, a, s));
     timing_begin(0, s);
     BGCN_TRY(sparse_compact_conv1(sp, a->x, a->ldx, w.z1, s));
     timing_end(0, s);
+    BGCN_TRY(sparse_items(sp, a->tree_ptr, s));
+    if (a->save_for_backward) {
+      hipStream_t x;
+      BGCN_TRY(aux_fork(s, 0, &x));
+      BGCN_TRY(sparse_csc(sp, x));
+      forked = true;
+    }
   }
-  timing_begin(sp.mode == 1 ? 0 : 4, s);
+  timing_begin(sparse ? 4 : 0, s);
   BGCN_TRY(gemm_xwt_impl(a->x, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F, s, gate));
-  timing_end(sp.mode == 1 ? 0 : 4, s);
+  timing_end(sparse ? 4 : 0, s);
   // conv1 propagate + bias (pre-relu h1 is saved: it is also the detached x2)
+  if (graph_lane >= 0) BGCN_TRY(aux_join(s, graph_lane));  // graphs built on that lane
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z1, a->h1, a->td_b1, a->bu_b1, BGCN_EPI_NONE, w, s));
   // conv2 lin with the root-extended, relu'd, dropped-out A operand generated in-kernel
   timing_begin(2, s);
-  if (sp.mode != 1) BGCN_TRY(sparse_conv2(sp, a->h1, w.node_root, w.z2, keep, s));
+  if (sparse) BGCN_TRY(sparse_conv2(sp, a->h1, a->tree_ptr, a->rootindex, w.z2, keep, s));
   hipLaunchKernelGGL(k_conv2_fwd, dim3(grid_for(N, 64), 2), dim3(256), 0, s, a->x, a->ldx, F,
                      a->h1, w.node_root, a->td_w2, a->bu_w2, w.z2, N, keep, gate);
   BGCN_CHECK_LAUNCH();
   timing_end(2, s);
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z2, a->h2, a->td_b2, a->bu_b2, BGCN_EPI_NONE, w, s));
-  hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B), 2), dim3(256), 0, s, a->h1, a->h2,
+  hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B), 2), dim3(1024), 0, s, a->h1, a->h2,
                      a->tree_ptr, a->rootindex, N, a->head_in);
   BGCN_CHECK_LAUNCH();
+  if (forked) BGCN_TRY(aux_join(s, 0));
   return BGCN_OK;
 }
 
+// Backward, given the forward's workspace.  After dZ2 the step splits into two
+// independent chains: dW2 (auxiliary stream) and dH1 -> dZ1 (main stream); they join
+// before the pass over the CSC of X that writes dW1 and the dW2 root columns.
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->dhead_in && a->td_dw1 && a->bu_dw1 && a->td_dw2 && a->bu_dw2 && a->td_db1 &&
@@ -595,60 +695,64 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   const int32_t* gate = nullptr;
   BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate));
   KeepSrc keep = make_keep(a);
-  const int64_t nblk = (N + kRowsPerBlock - 1) / kRowsPerBlock;
+  const bool sparse = sp.mode != 1;
 
-  hipLaunchKernelGGL(k_node_root, dim3(grid_for(N, 256)), dim3(256), 0, s, a->batch,
-                     a->rootindex, N, B, w.node_root);
-  BGCN_CHECK_LAUNCH();
   // readout + relu' -> dH2, db2
-  hipLaunchKernelGGL(k_readout_bwd, dim3(unsigned(nblk)), dim3(256), 0, s, a->dhead_in, a->h2,
-                     a->batch, a->tree_ptr, N, B, kRowsPerBlock, w.d2, w.colpart);
+  const int64_t nblk_r = (N + kReadBwdRows - 1) / kReadBwdRows;
+  hipLaunchKernelGGL(k_readout_bwd, dim3(unsigned(nblk_r)), dim3(256), 0, s, a->dhead_in, a->h2,
+                     a->batch, a->tree_ptr, N, B, w.d2, w.colpart);
   BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, s, w.colpart, int(nblk), a->td_db2,
+  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, s, w.colpart, int(nblk_r), a->td_db2,
                      a->bu_db2);
   BGCN_CHECK_LAUNCH();
   // dZ2 = A^T dH2
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.d2, w.dz2, nullptr, nullptr, BGCN_EPI_NONE, w, s));
-  // dW2 (both directions, generated A2 operand): the relu(H1) columns always by MFMA,
-  // the X[root] columns by MFMA (dense) or from the root non-zeros (sparse, finished
-  // in sparse_dw_cols below)
-  timing_begin(3, s);
-  hipLaunchKernelGGL(k_dw2, dim3(grid_for(H + F, 64), w.S2, 2), dim3(256), 0, s, a->x, a->ldx, F,
+
+  // ---- auxiliary chain: dW2 (both directions, generated A2 operand).  The relu(H1)
+  // columns always by MFMA; the X[root] columns by MFMA (dense) or from the root
+  // non-zeros (sparse, finished in sparse_dw_cols below).
+  hipStream_t x;
+  BGCN_TRY(aux_fork(s, 0, &x));
+  timing_begin(3, x);
+  hipLaunchKernelGGL(k_dw2, dim3(grid_for(H + F, 64), w.S2, 2), dim3(256), 0, x, a->x, a->ldx, F,
                      a->h1, w.dz2, w.node_root, w.dw2_part, N, w.kchunk2, w.S2, keep, gate, 1, H + F);
   BGCN_CHECK_LAUNCH();
-  if (sp.mode != 1) {
-    hipLaunchKernelGGL(k_dw2, dim3(1, w.Sh, 2), dim3(256), 0, s, a->x, a->ldx, F, a->h1, w.dz2,
+  if (sparse) {
+    hipLaunchKernelGGL(k_dw2, dim3(1, w.Sh, 2), dim3(256), 0, x, a->x, a->ldx, F, a->h1, w.dz2,
                        w.node_root, w.dw2_part, N, w.kchunkh, w.Sh, keep, gate, 0, int64_t(H));
     BGCN_CHECK_LAUNCH();
   }
-  timing_end(3, s);
-  hipLaunchKernelGGL(k_reduce_dw2, dim3(grid_for(2 * H * (H + F), 256)), dim3(256), 0, s,
-                     w.dw2_part, w.S2, H + F, H + F, a->td_dw2, a->bu_dw2, gate, 1);
+  timing_end(3, x);
+  hipLaunchKernelGGL(k_reduce_dw2, dim3(std::min<unsigned>(grid_for(2 * H * (H + F), 64), 1024)),
+                     dim3(256), 0, x, w.dw2_part, w.S2, H + F, H + F, a->td_dw2, a->bu_dw2, gate, 1);
   BGCN_CHECK_LAUNCH();
-  if (sp.mode != 1) {
-    hipLaunchKernelGGL(k_reduce_dw2, dim3(grid_for(2 * H * H, 256)), dim3(256), 0, s, w.dw2_part,
+  if (sparse) {
+    hipLaunchKernelGGL(k_reduce_dw2, dim3(grid_for(2 * H * H, 64)), dim3(256), 0, x, w.dw2_part,
                        w.Sh, int64_t(H), H + F, a->td_dw2, a->bu_dw2, gate, 0);
     BGCN_CHECK_LAUNCH();
+    BGCN_TRY(sparse_dw2_root_part(sp, a->tree_ptr, w.dz2, x));
+    if (!a->save_for_backward) BGCN_TRY(sparse_csc(sp, x));
   }
-  if (sp.mode != 1) BGCN_TRY(sparse_dw2_root_part(sp, a, w.dz2, keep, s));
-  // dH1 through dropout and relu, db1
-  hipLaunchKernelGGL(k_dh1, dim3(unsigned(nblk), 2), dim3(256), 0, s, w.dz2, a->h1, a->td_w2,
-                     a->bu_w2, H + F, N, kRowsPerBlock, keep, w.dh1, w.colpart);
+
+  // ---- main chain: dH1 through dropout and relu, db1, dZ1 = A^T dH1
+  const int64_t nblk_h = (N + kDh1Rows - 1) / kDh1Rows;
+  hipLaunchKernelGGL(k_dh1, dim3(unsigned(nblk_h), 2), dim3(256), 0, s, w.dz2, a->h1, a->td_w2,
+                     a->bu_w2, H + F, N, keep, w.dh1, w.colpart);
   BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, s, w.colpart, int(nblk), a->td_db1,
+  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, s, w.colpart, int(nblk_h), a->td_db1,
                      a->bu_db1);
   BGCN_CHECK_LAUNCH();
-  // dZ1 = A^T dH1
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.dh1, w.dz1, nullptr, nullptr, BGCN_EPI_NONE, w, s));
+  BGCN_TRY(aux_join(s, 0));
   // dW1 = [dZ1_td | dZ1_bu]^T X  (one pass over X for both directions) - dense MFMA, or
   // over the column-sorted non-zeros of X together with the dW2 root columns
-  if (sp.mode != 1) {
+  if (sparse) {
     timing_begin(5, s);
     BGCN_TRY(sparse_dw_cols(sp, a, w.dz1, w.node_root, keep, s));
     timing_end(5, s);
   }
   BGCN_TRY(gemm_tn_impl(w.dz1, 2 * H, a->x, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F, N,
-                        w.tn_ws, w.tn_bytes, s, 1, gate));
+                        w.tn_ws, w.tn_bytes, s, sparse ? 6 : 1, gate));
   return BGCN_OK;
 }
 
@@ -669,7 +773,7 @@ extern "C" size_t bgcn_bigcn_workspace_size(int64_t num_nodes, int64_t num_graph
 extern "C" int bgcn_bigcn_forward(const bgcn_bigcn_args* args, void* workspace,
                                   size_t workspace_bytes, bgcn_stream_t stream) {
   return bgcn::bigcn_forward_impl(args, workspace, workspace_bytes,
-                                  reinterpret_cast<hipStream_t>(stream));
+                                  reinterpret_cast<hipStream_t>(stream), -1);
 }
 extern "C" int bgcn_bigcn_backward(const bgcn_bigcn_args* args, void* workspace,
                                    size_t workspace_bytes, bgcn_stream_t stream) {

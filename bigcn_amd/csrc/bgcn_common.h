@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 #include <string>
 
 #include "../../include/bgcn.h"
@@ -51,6 +53,15 @@ struct Carve {
   }
   bool ok() const { return off <= cap; }
 };
+
+// Auxiliary streams ("lanes") of the current device for independent branches of the
+// fused step: aux_fork sets *branch to lane's stream after making it wait for the work
+// queued on `main` so far; aux_join makes `main` wait for everything queued on the lane.
+// On the legacy null stream (whose cross-stream waits synchronise the host) *branch =
+// main and the branch runs inline.
+constexpr int kAuxLanes = 2;
+int aux_fork(hipStream_t main, int lane, hipStream_t* branch);
+int aux_join(hipStream_t main, int lane);
 
 // kernel timing hook (bench.py): record HIP events around a launch of a class
 void timing_begin(int cls, hipStream_t s);

@@ -266,14 +266,15 @@ __global__ __launch_bounds__(256) void k_reduce_splits(const float* __restrict__
                                                        float* __restrict__ C1, int64_t ldc,
                                                        int64_t split, const int32_t* __restrict__ gate) {
   if (gate_closed(gate)) return;
-  int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  int64_t total = Mc * Nc;
-  if (idx >= total) return;
-  float acc = part[idx];
-  for (int s = 1; s < S; ++s) acc += part[int64_t(s) * total + idx];
-  int64_t m = idx / Nc, n = idx % Nc;
-  if (m < split) C0[m * ldc + n] = acc;
-  else C1[(m - split) * ldc + n] = acc;
+  const int64_t total = Mc * Nc;
+  for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += int64_t(gridDim.x) * blockDim.x) {
+    float acc = part[idx];
+    for (int s = 1; s < S; ++s) acc += part[int64_t(s) * total + idx];
+    const int64_t m = idx / Nc, n = idx % Nc;
+    if (m < split) C0[m * ldc + n] = acc;
+    else C1[(m - split) * ldc + n] = acc;
+  }
 }
 
 // ---------------------------------------------------------------- host side
@@ -407,7 +408,7 @@ int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float
                        K, kchunk, gate);
   BGCN_CHECK_LAUNCH();
   timing_end(timing_cls, stream);
-  hipLaunchKernelGGL(k_reduce_splits, dim3(grid_for(Mc * Nc, 256)), dim3(256), 0, stream, part, S,
+  hipLaunchKernelGGL(k_reduce_splits, dim3(std::min<unsigned>(grid_for(Mc * Nc, 256), 1024)), dim3(256), 0, stream, part, S,
                      Mc, Nc, C0, C1, ldc, split, gate);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;

@@ -27,7 +27,7 @@ namespace bgcn {
 namespace {
 
 constexpr int kMaxGraphs = 2;
-constexpr int kScanThreads = 256, kScanItems = 16, kScanChunk = kScanThreads * kScanItems;
+constexpr int kScanThreads = 256, kScanItems = 4, kScanChunk = kScanThreads * kScanItems;
 
 struct GraphIO {
   const int64_t* ei;
@@ -61,38 +61,42 @@ __device__ __forceinline__ bool edge_kept(const int64_t* ei, int64_t E, int64_t 
   return valid && src != dst;
 }
 
-__global__ void k_count(GraphBatch gb) {
+// Run-start counters are wave-aggregated (ballot + popcount, one atomic per wave): in a
+// propagation tree nearly every edge starts a run, and per-edge atomics on one address
+// serialise.
+__global__ __launch_bounds__(256) void k_count(GraphBatch gb) {
   GraphIO& G = gb.g[blockIdx.y];
   const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (e >= G.E) return;
   const int64_t N = gb.N;
-  int64_t src, dst;
-  bool valid;
-  bool keep = edge_kept(G.ei, G.E, N, e, src, dst, valid);
-  if (!valid) {
-    if (G.status) atomicOr(G.status, 1);
-    atomicOr(&G.flags[2], 1);
-    return;
+  bool start_t = false, start_s = false;
+  if (e < G.E) {
+    int64_t src, dst;
+    bool valid;
+    const bool keep = edge_kept(G.ei, G.E, N, e, src, dst, valid);
+    if (!valid) {
+      if (G.status) atomicOr(G.status, 1);
+      atomicOr(&G.flags[2], 1);
+    } else if (!keep) {  // an input self loop: removed, its weight becomes the loop weight
+      atomicMax(&G.loop_eid[src], int32_t(e + 1));  // (last wins)
+      atomicOr(&G.flags[2], 1);
+    } else {
+      atomicAdd(&G.cnt_t[dst], 1);
+      atomicAdd(&G.cnt_s[src], 1);
+      int64_t psrc = -1, pdst = -1;
+      if (e > 0) {
+        bool pv;
+        edge_kept(G.ei, G.E, N, e - 1, psrc, pdst, pv);
+      }
+      start_t = e == 0 || pdst != dst;
+      start_s = e == 0 || psrc != src;
+      if (start_t) G.run_t[dst] = int32_t(e);
+      if (start_s) G.run_s[src] = int32_t(e);
+    }
   }
-  if (!keep) {  // an input self loop: removed, its weight becomes the loop weight (last wins)
-    atomicMax(&G.loop_eid[src], int32_t(e + 1));
-    atomicOr(&G.flags[2], 1);
-    return;
-  }
-  atomicAdd(&G.cnt_t[dst], 1);
-  atomicAdd(&G.cnt_s[src], 1);
-  int64_t psrc = -1, pdst = -1;
-  if (e > 0) {
-    bool pv;
-    edge_kept(G.ei, G.E, N, e - 1, psrc, pdst, pv);
-  }
-  if (e == 0 || pdst != dst) {
-    G.run_t[dst] = int32_t(e);
-    atomicAdd(&G.flags[0], 1);
-  }
-  if (e == 0 || psrc != src) {
-    G.run_s[src] = int32_t(e);
-    atomicAdd(&G.flags[1], 1);
+  const int nt = __popcll(__ballot(start_t)), ns = __popcll(__ballot(start_s));
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    if (nt) atomicAdd(&G.flags[0], nt);
+    if (ns) atomicAdd(&G.flags[1], ns);
   }
 }
 

@@ -46,4 +46,14 @@ int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float
 size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K);
 int tn_splits(int64_t Mc, int64_t Nc, int64_t K);
 
+// ---- fused encoder (bgcn_bigcn.hip); graph_lane: see bigcn_forward_impl
+size_t bigcn_ws_size(int64_t N, int64_t B, int64_t F, int64_t hid);
+int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
+                       int graph_lane);
+int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s);
+
+// ---- one training step (bgcn_step.hip)
+size_t train_step_ws_size(int64_t N, int64_t B, int64_t F, int64_t C, int64_t Etd, int64_t Ebu);
+int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStream_t s);
+
 }  // namespace bgcn

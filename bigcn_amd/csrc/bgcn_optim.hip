@@ -14,35 +14,50 @@
 namespace bgcn {
 namespace {
 
-constexpr int kChunkElems = 256 * 4 * 4;  // elements per block (256 threads x 4 float4)
+constexpr int kChunkElems = 256 * 4;  // elements per block (256 threads x one float4)
+
+struct AdamConst {
+  float b1, b2, wd, eps, step, inv_bc2, gs;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float gr, float& m, float& v,
+                                          const AdamConst& c) {
+  const float g = gr * c.gs + c.wd * p;
+  m = fmaf(1.0f - c.b1, g - m, m);            // exp_avg.lerp_(grad, 1 - beta1)
+  v = fmaf(1.0f - c.b2, g * g, v * c.b2);     // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+  const float denom = sqrtf(v) * c.inv_bc2 + c.eps;
+  p = p - c.step * (m / denom);
+}
 
 __global__ __launch_bounds__(256) void k_adam(bgcn_adam_args a) {
   // locate this block's tensor (at most BGCN_ADAM_MAX_TENSORS, uniform scan)
   int k = 0;
   while (k + 1 < a.count && int64_t(blockIdx.x) >= a.block_start[k + 1]) ++k;
   const bgcn_adam_tensor& T = a.t[k];
-  const int64_t base = (int64_t(blockIdx.x) - a.block_start[k]) * kChunkElems;
-  const float b1 = a.beta1, b2 = a.beta2, wd = a.weight_decay, eps = a.eps;
-  const float step = T.lr / a.bias_correction1;
-  const float inv_bc2 = 1.0f / a.bias_correction2_sqrt;
-  for (int u = 0; u < 4; ++u) {
-    const int64_t e0 = base + (int64_t(u) * 256 + threadIdx.x) * 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t e = e0 + j;
-      if (e >= T.numel) break;
-      float p = T.param[e];
-      const float g = T.grad[e] * a.grad_scale + wd * p;
-      float m = T.exp_avg[e];
-      float v = T.exp_avg_sq[e];
-      m = fmaf(1.0f - b1, g - m, m);          // exp_avg.lerp_(grad, 1 - beta1)
-      v = fmaf(1.0f - b2, g * g, v * b2);     // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-      const float denom = sqrtf(v) * inv_bc2 + eps;
-      p = p - step * (m / denom);
-      T.param[e] = p;
-      T.exp_avg[e] = m;
-      T.exp_avg_sq[e] = v;
-    }
+  const AdamConst c{a.beta1, a.beta2, a.weight_decay, a.eps, T.lr / a.bias_correction1,
+                    1.0f / a.bias_correction2_sqrt, a.grad_scale};
+  const int64_t e0 = (int64_t(blockIdx.x) - a.block_start[k]) * kChunkElems + threadIdx.x * 4;
+  const bool vec = ((reinterpret_cast<uintptr_t>(T.param) | reinterpret_cast<uintptr_t>(T.grad) |
+                     reinterpret_cast<uintptr_t>(T.exp_avg) |
+                     reinterpret_cast<uintptr_t>(T.exp_avg_sq)) & 15u) == 0;
+  if (vec && e0 + 4 <= T.numel) {
+    float4 p = ld4(T.param + e0), g = ld4(T.grad + e0);
+    float4 m = ld4(T.exp_avg + e0), v = ld4(T.exp_avg_sq + e0);
+    adam_elem(p.x, g.x, m.x, v.x, c);
+    adam_elem(p.y, g.y, m.y, v.y, c);
+    adam_elem(p.z, g.z, m.z, v.z, c);
+    adam_elem(p.w, g.w, m.w, v.w, c);
+    st4(T.param + e0, p);
+    st4(T.exp_avg + e0, m);
+    st4(T.exp_avg_sq + e0, v);
+    return;
+  }
+  for (int64_t e = e0; e < e0 + 4 && e < T.numel; ++e) {
+    float p = T.param[e], m = T.exp_avg[e], v = T.exp_avg_sq[e];
+    adam_elem(p, T.grad[e], m, v, c);
+    T.param[e] = p;
+    T.exp_avg[e] = m;
+    T.exp_avg_sq[e] = v;
   }
 }
 

@@ -1,6 +1,7 @@
-// Host runtime of libbgcn: thread-local error string, ABI version, and the (process-global)
-// kernel-timing hook bench.py uses to measure the dominant kernel with HIP events
-// on the stream it is launched on.
+// Host runtime of libbgcn: thread-local error string, ABI version, the per-device auxiliary
+// stream of the fused step's independent branches, and the (process-global) kernel-timing
+// hook bench.py uses to measure the dominant kernel with HIP events on the stream it is
+// launched on.
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -27,6 +28,31 @@ struct TimingState {
 // the caller's thread; both record into the same state
 TimingState g_tm;
 std::mutex g_tm_mu;
+
+// auxiliary streams ("lanes") + fork/join events per device (created on first use)
+constexpr int kMaxDevices = 64;
+struct AuxState {
+  hipStream_t stream[kAuxLanes] = {};
+  hipEvent_t fork[kAuxLanes] = {}, join[kAuxLanes] = {};
+};
+AuxState g_aux[kMaxDevices];
+std::mutex g_aux_mu;
+
+AuxState* aux_state(int lane) {
+  int dev = 0;
+  if (lane < 0 || lane >= kAuxLanes) return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+  AuxState& a = g_aux[dev];
+  if (!a.stream[lane]) {
+    hipStream_t st;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&a.fork[lane], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&a.join[lane], hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+    a.stream[lane] = st;
+  }
+  return &a;
+}
 }  // namespace
 
 void set_error(const std::string& msg) { g_err = msg; }
@@ -56,6 +82,28 @@ void timing_end(int cls, hipStream_t s) {
   g_tm.open[cls] = nullptr;
 }
 
+int aux_fork(hipStream_t main, int lane, hipStream_t* branch) {
+  *branch = main;
+  if (!main) return BGCN_OK;  // legacy null stream: the branch runs inline (bgcn_common.h)
+  std::lock_guard<std::mutex> lk(g_aux_mu);
+  AuxState* a = aux_state(lane);
+  if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
+  BGCN_CHECK_HIP(hipEventRecord(a->fork[lane], main));
+  BGCN_CHECK_HIP(hipStreamWaitEvent(a->stream[lane], a->fork[lane], 0));
+  *branch = a->stream[lane];
+  return BGCN_OK;
+}
+
+int aux_join(hipStream_t main, int lane) {
+  if (!main) return BGCN_OK;
+  std::lock_guard<std::mutex> lk(g_aux_mu);
+  AuxState* a = aux_state(lane);
+  if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
+  BGCN_CHECK_HIP(hipEventRecord(a->join[lane], a->stream[lane]));
+  BGCN_CHECK_HIP(hipStreamWaitEvent(main, a->join[lane], 0));
+  return BGCN_OK;
+}
+
 }  // namespace bgcn
 
 extern "C" int bgcn_abi_version(void) { return BGCN_ABI_VERSION; }
@@ -69,6 +117,15 @@ extern "C" int bgcn_set_kernel_timing(int enable) {
   for (int c = 0; c < bgcn::kTimingClasses; ++c) {
     t.total_ms[c] = 0;
     t.count[c] = 0;
+    if (!t.enabled) continue;       // disabling keeps the pending events for readout
+    for (auto& p : t.pending[c]) {  // enabling drops events of classes nobody read out
+      (void)hipEventSynchronize(p.b);
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    t.pending[c].clear();
+    if (t.open[c]) (void)hipEventDestroy(t.open[c]);
+    t.open[c] = nullptr;
   }
   return BGCN_OK;
 }

@@ -129,56 +129,120 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const floa
 }
 
 // ---------------------------------------------------------------- conv2 forward
-// Block = (64 nodes, direction); W2T_d[0:64] staged in LDS; 16 lanes x float4 per node.
+// conv2 lin on the sparse path, one work item (<= kChunk nodes of one tree) per block:
+//   Z2_d[i] = [keep * 2 relu(H1_d[i]) | kept_d(i, s)] . [W2_d^T[0:64] ; Wr_b]
+//   Wr_b[s] = 2 relu(x_root,col_s) W2_d^T[64 + col_s]      (s < nnz(root), else 0)
+// i.e. one [nodes x 96] x [96 x 64] product on the fp32 MFMA per item, with the
+// dropout-masked relu(H1) and the per-node root keep bits (0/1) generated in registers
+// and the tree's root block of W2^T staged in LDS.  The root keep masks are stored in
+// S.rbits for the dW2 root columns of the backward.  K order is permuted per lane half
+// (half h owns k in [48h, 48h + 48)), B rows padded to 66 floats so the two halves read
+// disjoint LDS banks.
+constexpr int kC2K = 2 * H / 4 * 3;  // 96 = 64 relu(H1) columns + 32 root slots
+constexpr int kC2Ld = H + 2;
 __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float* __restrict__ H1,
-                                                      const int32_t* __restrict__ node_root,
+                                                      const int32_t* __restrict__ tree_ptr,
+                                                      const int64_t* __restrict__ rootindex,
                                                       float* __restrict__ Z2, KeepSrc keep) {
   if (!use_sparse(S)) return;
-  __shared__ float4 wl[H][H / 4];   // W2T_d[k][o]
+  const int item = blockIdx.x;
+  if (item >= S.tree_item0[S.B]) return;
+  __shared__ float Bs[kC2K * kC2Ld];
+  __shared__ uint32_t rk[kCap];
   const int d = blockIdx.y;
+  const int b = S.item_tree[item];
+  const int64_t beg = int64_t(tree_ptr[b]) + int64_t(S.item_chunk[item]) * kChunk;
+  const int64_t end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
+  const int64_t r = rootindex[b];
+  const int rn = S.nnz[r];
+  const float sc = keep.scale();
   const int64_t K2 = S.F + H;
   const float* w2t = S.w2t + int64_t(d) * K2 * H;
-  for (int e = threadIdx.x; e < H * H / 4; e += 256) wl[e / (H / 4)][e % (H / 4)] = ld4(w2t + e * 4);
+  if (threadIdx.x < kCap)
+    rk[threadIdx.x] = threadIdx.x < rn ? uint32_t(H + S.cols[r * kCap + threadIdx.x]) : 0u;
+  for (int e = threadIdx.x; e < H * (H / 4); e += 256) {
+    const int k = e >> 4, q = (e & 15) * 4;
+    const float4 v = ld4(w2t + int64_t(k) * H + q);
+    float* dst = &Bs[k * kC2Ld + q];
+    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+  }
+  for (int e = threadIdx.x; e < kCap * (H / 4); e += 256) {
+    const int s = e >> 4, q = (e & 15) * 4;
+    float4 v = f4zero();
+    if (s < rn) {
+      const float av = sc * fmaxf(S.vals[r * kCap + s], 0.f);
+      const float4 w = ld4(w2t + int64_t(H + S.cols[r * kCap + s]) * H + q);
+      v = make_float4(av * w.x, av * w.y, av * w.z, av * w.w);
+    }
+    float* dst = &Bs[(H + s) * kC2Ld + q];
+    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+  }
   __syncthreads();
-  const int lane = threadIdx.x & 15, grp = threadIdx.x >> 4;   // 16 nodes per pass
-  const float sc = keep.scale();
-  const int base_lane = (threadIdx.x & 63) & ~15;
-  for (int pass = 0; pass < 4; ++pass) {
-    const int64_t i = int64_t(blockIdx.x) * 64 + pass * 16 + grp;
-    if (i >= S.N) break;
-    const float4 h4 = ld4(H1 + i * (2 * H) + d * H + lane * 4);  // lane holds H1[i][4l .. 4l+3]
-    const uint32_t w0 = keep.get(uint32_t(d), uint32_t(i), 0u);
-    const uint32_t w1 = keep.get(uint32_t(d), uint32_t(i), 1u);
-    float4 acc = f4zero();
+
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
+  for (int t = wv; t < kChunk / 32; t += 4) {
+    const int64_t i0 = beg + 32 * t;
+    if (i0 >= end) break;
+    const int64_t i = i0 + r32;
+    const bool ok = i < end;
+    const float* hrow = H1 + (ok ? i : beg) * (2 * H) + d * H;
+    const uint32_t w0 = ok ? keep.get(uint32_t(d), uint32_t(i), 0u) : 0u;
+    const uint32_t w1 = ok ? keep.get(uint32_t(d), uint32_t(i), 1u) : 0u;
+    float a[48];
+    if (h == 0) {
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const float hv = (k & 3) == 0 ? h4.x : (k & 3) == 1 ? h4.y : (k & 3) == 2 ? h4.z : h4.w;
-      const float hk = __shfl(hv, base_lane + (k >> 2), 64);
-      const uint32_t wd = k < 32 ? w0 : w1;
-      const float a = ((wd >> (k & 31)) & 1u) ? sc * fmaxf(hk, 0.f) : 0.f;
-      acc = f4fma(a, wl[k][lane], acc);
-    }
-    const int64_t r = node_root[i];
-    const int rn = S.nnz[r];
-    for (int s0 = 0; s0 < rn; s0 += 4) {
-      float4 wv[4];
-      float av[4];
+      for (int q = 0; q < 12; ++q) {
+        const float4 v = ld4(hrow + 4 * q);
+        const float ve[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int s = s0 + u;
-        const bool ok = s < rn;
-        const uint32_t k = ok ? uint32_t(H + S.cols[r * kCap + s]) : 0u;
-        const float v = ok ? S.vals[r * kCap + s] : 0.f;
-        const uint32_t wd = ok ? keep.get(uint32_t(d), uint32_t(i), k >> 5) : 0u;
-        av[u] = ((wd >> (k & 31)) & 1u) ? sc * fmaxf(v, 0.f) : 0.f;
-        wv[u] = ok ? ld4(w2t + int64_t(k) * H + lane * 4) : f4zero();
+        for (int e = 0; e < 4; ++e) {
+          const int k = 4 * q + e;
+          const uint32_t bit = k < 32 ? (w0 >> k) & 1u : (w1 >> (k - 32)) & 1u;
+          a[k] = bit ? sc * fmaxf(ve[e], 0.f) : 0.f;
+        }
       }
+    } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc = f4fma(av[u], wv[u], acc);
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = ld4(hrow + 48 + 4 * q);
+        const float ve[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = 48 + 4 * q + e;
+          a[k - 48] = ((w1 >> (k - 32)) & 1u) ? sc * fmaxf(ve[e], 0.f) : 0.f;
+        }
+      }
+      uint32_t m = 0;
+#pragma unroll
+      for (int s = 0; s < kCap; ++s) {
+        uint32_t bit = 0;
+        if (s < rn && ok) {
+          const uint32_t k = rk[s];
+          bit = (keep.get(uint32_t(d), uint32_t(i), k >> 5) >> (k & 31)) & 1u;
+        }
+        m |= bit << s;
+        a[16 + s] = bit ? 1.f : 0.f;
+      }
+      if (ok) S.rbits[int64_t(d) * S.N + i] = m;
     }
-    st4(Z2 + i * (2 * H) + d * H + lane * 4, acc);
+    f32x16 acc0 = {}, acc1 = {};
+    const float* bp = &Bs[(48 * h) * kC2Ld + r32];
+#pragma unroll
+    for (int kk = 0; kk < 48; ++kk) {
+      acc0 = mfma32x32x2(a[kk], bp[kk * kC2Ld], acc0);
+      acc1 = mfma32x32x2(a[kk], bp[kk * kC2Ld + 32], acc1);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t ii = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (ii < end) {
+        Z2[ii * (2 * H) + d * H + r32] = acc0[q];
+        Z2[ii * (2 * H) + d * H + 32 + r32] = acc1[q];
+      }
+    }
   }
 }
+
 
 // ---------------------------------------------------------------- dW2 root columns, part 1
 // Work item = (tree b, chunk of <= kChunk nodes of b), blockIdx.y = direction:
@@ -219,9 +283,7 @@ __global__ __launch_bounds__(1024) void k_items(SparseState S, const int32_t* __
 }
 
 __global__ __launch_bounds__(256) void k_dw2_root_part(SparseState S, const float* __restrict__ dZ2,
-                                                       const int32_t* __restrict__ tree_ptr,
-                                                       const int64_t* __restrict__ rootindex,
-                                                       KeepSrc keep) {
+                                                       const int32_t* __restrict__ tree_ptr) {
   if (!use_sparse(S)) return;
   const int item = blockIdx.x;
   if (item >= S.tree_item0[S.B]) return;
@@ -231,29 +293,31 @@ __global__ __launch_bounds__(256) void k_dw2_root_part(SparseState S, const floa
   const int b = S.item_tree[item];
   const int64_t beg = int64_t(tree_ptr[b]) + int64_t(S.item_chunk[item]) * kChunk;
   const int64_t end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
-  const int64_t r = rootindex[b];
-  const int rn = S.nnz[r];
+  // root keep masks of the forward's conv2 (bit s = root non-zero s kept for node i)
   for (int t = threadIdx.x; t < kChunk; t += 256) {
-    uint32_t m = 0;
     const int64_t i = beg + t;
-    if (i < end) {
-      for (int s = 0; s < rn; ++s) {
-        const uint32_t k = uint32_t(H + S.cols[r * kCap + s]);
-        m |= ((keep.get(uint32_t(d), uint32_t(i), k >> 5) >> (k & 31)) & 1u) << s;
-      }
-    }
-    bits[t] = m;
+    bits[t] = i < end ? S.rbits[int64_t(d) * S.N + i] : 0u;
   }
   __syncthreads();
   const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;   // 64 outputs x 4 node slices
   float acc[kCap];
 #pragma unroll
   for (int s = 0; s < kCap; ++s) acc[s] = 0.f;
-  for (int64_t i = beg + sl; i < end; i += 4) {
-    const float g = dZ2[i * (2 * H) + d * H + o];
-    const uint32_t m = bits[i - beg];
+  // eight independent dZ2 loads in flight per thread (a chunk row is 256 B apart)
+  for (int64_t i0 = beg + sl; i0 < end; i0 += 32) {
+    float g[8];
 #pragma unroll
-    for (int s = 0; s < kCap; ++s) acc[s] += ((m >> s) & 1u) ? g : 0.f;
+    for (int u = 0; u < 8; ++u) {
+      const int64_t i = i0 + 4 * u;
+      g[u] = i < end ? dZ2[i * (2 * H) + d * H + o] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t i = i0 + 4 * u;
+      const uint32_t m = i < end ? bits[i - beg] : 0u;
+#pragma unroll
+      for (int s = 0; s < kCap; ++s) acc[s] += ((m >> s) & 1u) ? g[u] : 0.f;
+    }
   }
 #pragma unroll
   for (int s = 0; s < kCap; ++s) red[sl][s][o] = acc[s];
@@ -494,6 +558,7 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   t.col_start = c.take<int32_t>(size_t(F));
   t.col_end = c.take<int32_t>(size_t(F));
   t.csc_slot = c.take<uint32_t>(slots);
+  t.rbits = c.take<uint32_t>(size_t(2) * N);
   if (S) {
     t.mode = S->mode;
     t.flags = S->flags;
@@ -519,26 +584,28 @@ int sparse_compact_conv1(SparseState& S, const float* X, int64_t ldx, float* Z1,
   return BGCN_OK;
 }
 
-int sparse_conv2(SparseState& S, const float* H1, const int32_t* node_root, float* Z2, KeepSrc keep,
-                 hipStream_t s) {
-  hipLaunchKernelGGL(k_conv2_sparse, dim3(grid_for(S.N, 64), 2), dim3(256), 0, s, S, H1, node_root,
-                     Z2, keep);
+int sparse_items(SparseState& S, const int32_t* tree_ptr, hipStream_t s) {
+  hipLaunchKernelGGL(k_items, dim3(1), dim3(1024), 0, s, S, tree_ptr);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
 
-int sparse_dw2_root_part(SparseState& S, const bgcn_bigcn_args* a, const float* dZ2, KeepSrc keep,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_items, dim3(1), dim3(1024), 0, s, S, a->tree_ptr);
+int sparse_conv2(SparseState& S, const float* H1, const int32_t* tree_ptr, const int64_t* rootindex,
+                 float* Z2, KeepSrc keep, hipStream_t s) {
+  hipLaunchKernelGGL(k_conv2_sparse, dim3(unsigned(S.max_items), 2), dim3(256), 0, s, S, H1,
+                     tree_ptr, rootindex, Z2, keep);
   BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int sparse_dw2_root_part(SparseState& S, const int32_t* tree_ptr, const float* dZ2, hipStream_t s) {
   hipLaunchKernelGGL(k_dw2_root_part, dim3(unsigned(S.max_items), 2), dim3(256), 0, s, S, dZ2,
-                     a->tree_ptr, a->rootindex, keep);
+                     tree_ptr);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
 
-int sparse_dw_cols(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1,
-                   const int32_t* node_root, KeepSrc keep, hipStream_t s) {
+int sparse_csc(SparseState& S, hipStream_t s) {
   const int R = int((S.N + kRowBlock - 1) / kRowBlock);
   hipLaunchKernelGGL(k_csc_hist, dim3(unsigned(R)), dim3(256), size_t(S.F) * sizeof(int32_t), s, S);
   BGCN_CHECK_LAUNCH();
@@ -546,6 +613,11 @@ int sparse_dw_cols(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1,
   BGCN_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_csc_place, dim3(unsigned(R)), dim3(256), size_t(2 * S.F) * sizeof(int32_t), s, S);
   BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int sparse_dw_cols(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1,
+                   const int32_t* node_root, KeepSrc keep, hipStream_t s) {
   hipLaunchKernelGGL(k_dw_cols, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, dZ1, node_root,
                      a->batch, a->td_dw1, a->bu_dw1, a->td_dw2, a->bu_dw2, keep.scale());
   BGCN_CHECK_LAUNCH();

@@ -50,15 +50,20 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
   const int fo = lane * 4;
   const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
 
-  // entry k of the chunk lives in lane k of the group
+  // entry k of the chunk lives in lane k of the group.  Whether the first row started
+  // before the chunk / the last row runs past it is read off the neighbouring entries
+  // (row[p0-1], row[p1]) - loaded alongside the chunk, so no dependent ptr[] loads.
   const bool mine = lane < n;
   const int32_t r_l = mine ? P.row[p0 + lane] : -1;
   const int32_t c_l = mine ? P.col[p0 + lane] : 0;
   const float w_l = mine ? P.w[p0 + lane] : 0.f;
+  const int32_t prev_row = p0 > 0 ? P.row[p0 - 1] : -1;
+  const int32_t next_row = p1 < nnz ? P.row[p1] : -1;
   const int base_lane = ((threadIdx.x & 63) / LANES) * LANES;  // group's first lane in the wave
 
   float4 acc = f4zero();
   int32_t cur = -1;
+  bool cur_head = false;  // cur started before p0
   for (int k0 = 0; k0 < n; k0 += 8) {
     float4 v[8];
     int32_t rr[8];
@@ -79,9 +84,10 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
       if (r != cur) {
         if (cur >= 0) {
           // `cur` ended inside this chunk (a later entry belongs to another row)
-          if (P.ptr[cur] >= p0) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+          if (!cur_head) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
           else st4(P.part + (g * 2 + 0) * (LANES * 4) + fo, acc);
         }
+        cur_head = cur < 0 && r == prev_row;
         cur = r;
         acc = f4zero();
       }
@@ -89,10 +95,55 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
     }
   }
   if (cur >= 0) {
-    const int64_t rs = P.ptr[cur], re = P.ptr[cur + 1];
-    if (rs >= p0 && re <= p1) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
-    else if (rs < p0) st4(P.part + (g * 2 + 0) * (LANES * 4) + fo, acc);  // head (may also extend past p1)
+    const bool ends = next_row != cur;
+    if (!cur_head && ends) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+    else if (cur_head) st4(P.part + (g * 2 + 0) * (LANES * 4) + fo, acc);  // head (may also extend past p1)
     else st4(P.part + (g * 2 + 1) * (LANES * 4) + fo, acc);               // tail
+  }
+}
+
+// Fixup, one block per chunk boundary g*NPG (g >= 1), F <= 128: if the row containing
+// entry g*NPG started before it and this is the row's last chunk, sum its partials
+// tail[g0], head[g0+1..g1] and write the row.  A BU star root spans hundreds of chunks,
+// so the partial list is split over 256/LANES sub-groups (sub-group s takes items
+// s, s+SG, ...) and combined in a fixed order: deterministic.
+template <int LANES>
+__global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
+  constexpr int SG = 256 / LANES;
+  __shared__ float4 red[SG][LANES];
+  const SpmmProb& P = sb.p[blockIdx.y];
+  const int64_t g = int64_t(blockIdx.x) + 1;
+  if (g >= P.ngroups) return;
+  const int64_t nnz = P.ptr[sb.rows];
+  const int64_t pb = g * NPG;
+  if (pb >= nnz) return;
+  const int32_t r = P.row[pb];
+  if (P.row[pb - 1] != r) return;            // row starts at the boundary: no crossing
+  const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
+  const int64_t g0 = rs / NPG, g1 = (re - 1) / NPG;
+  if (g1 != g) return;                       // only the row's last chunk does the fixup
+  const int s = threadIdx.x / LANES, fo = (threadIdx.x % LANES) * 4;
+  const int64_t m = g1 - g0 + 1;             // item 0 = tail[g0], item j = head[g0 + j]
+  float4 acc = f4zero();
+  int64_t j = s;
+  for (; j + 3 * SG < m; j += 4 * SG) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t jj = j + u * SG;
+      v[u] = ld4(P.part + ((g0 + jj) * 2 + (jj == 0 ? 1 : 0)) * (LANES * 4) + fo);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = f4add(acc, v[u]);
+  }
+  for (; j < m; j += SG) acc = f4add(acc, ld4(P.part + ((g0 + j) * 2 + (j == 0 ? 1 : 0)) * (LANES * 4) + fo));
+  red[s][threadIdx.x % LANES] = acc;
+  __syncthreads();
+  if (s == 0) {
+    float4 t = red[0][threadIdx.x];
+#pragma unroll
+    for (int q = 1; q < SG; ++q) t = f4add(t, red[q][threadIdx.x]);
+    st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(t, P.bias ? ld4(P.bias + fo) : f4zero(), sb.epi));
   }
 }
 
@@ -143,12 +194,15 @@ __global__ __launch_bounds__(256) void k_spmm_wide(SpmmBatch sb) {
     s_w[threadIdx.x] = v ? P.w[p] : 0.f;
   }
   __syncthreads();
+  const int32_t prev_row = p0 > 0 ? P.row[p0 - 1] : -1;
+  const int32_t next_row = p1 < nnz ? P.row[p1] : -1;
   const int F = sb.F;
   const int fo = blockIdx.y * 1024 + threadIdx.x * 4;
   const bool act = fo < F;
   const float4 bv = (P.bias && act) ? ld4(P.bias + fo) : f4zero();
   float4 acc = f4zero();
   int32_t cur = -1;
+  bool cur_head = false;
   for (int k0 = 0; k0 < n; k0 += 8) {
     float4 v[8];
 #pragma unroll
@@ -163,9 +217,10 @@ __global__ __launch_bounds__(256) void k_spmm_wide(SpmmBatch sb) {
       const int32_t r = s_r[k];
       if (r != cur) {
         if (cur >= 0 && act) {
-          if (P.ptr[cur] >= p0) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+          if (!cur_head) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
           else st4(P.part + (g * 2 + 0) * int64_t(F) + fo, acc);
         }
+        cur_head = cur < 0 && r == prev_row;
         cur = r;
         acc = f4zero();
       }
@@ -173,9 +228,9 @@ __global__ __launch_bounds__(256) void k_spmm_wide(SpmmBatch sb) {
     }
   }
   if (cur >= 0 && act) {
-    const int64_t rs = P.ptr[cur], re = P.ptr[cur + 1];
-    if (rs >= p0 && re <= p1) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
-    else if (rs < p0) st4(P.part + (g * 2 + 0) * int64_t(F) + fo, acc);
+    const bool ends = next_row != cur;
+    if (!cur_head && ends) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+    else if (cur_head) st4(P.part + (g * 2 + 0) * int64_t(F) + fo, acc);
     else st4(P.part + (g * 2 + 1) * int64_t(F) + fo, acc);
   }
 }
@@ -211,12 +266,14 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
     constexpr int L = 16;
     hipLaunchKernelGGL(k_spmm_narrow<L>, dim3(grid_for(gmax, 256 / L), gy), dim3(256), 0, stream, sb);
     BGCN_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_spmm_fixup<L>, dim3(grid_for(gmax, 256 / L), gy), dim3(256), 0, stream, sb);
+    if (gmax > 1)
+      hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(unsigned(gmax - 1), gy), dim3(256), 0, stream, sb);
   } else if (F == 128) {
     constexpr int L = 32;
     hipLaunchKernelGGL(k_spmm_narrow<L>, dim3(grid_for(gmax, 256 / L), gy), dim3(256), 0, stream, sb);
     BGCN_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_spmm_fixup<L>, dim3(grid_for(gmax, 256 / L), gy), dim3(256), 0, stream, sb);
+    if (gmax > 1)
+      hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(unsigned(gmax - 1), gy), dim3(256), 0, stream, sb);
   } else {
     hipLaunchKernelGGL(k_spmm_wide, dim3(unsigned(gmax), unsigned((F + 1023) / 1024), gy), dim3(256),
                        0, stream, sb);

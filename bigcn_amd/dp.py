@@ -42,6 +42,17 @@ class GradBucket:
         self.numels = [p.numel() for p in self.params]
         dev = self.params[0].device
         self.flat = torch.zeros(sum(self.numels), dtype=torch.float32, device=dev)
+        self._views = [v.view_as(p) for v, p in zip(torch.split(self.flat, self.numels), self.params)]
+
+    def views(self) -> List[torch.Tensor]:
+        """Persistent per-parameter views of the flat bucket (parameter order): kernels
+        can write gradients straight into them (bgcn_train_step)."""
+        return self._views
+
+    def allreduce_sum_(self, group=None) -> None:
+        """In-place SUM of the bucket over ranks (one RCCL all-reduce; no-op at world 1)."""
+        if dist.is_initialized() and self.world(group) > 1:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
 
     def world(self, group=None) -> int:
         return dist.get_world_size(group) if dist.is_initialized() else 1
@@ -52,9 +63,8 @@ class GradBucket:
         grads = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(n, device=self.flat.device)
                  for p, n in zip(self.params, self.numels)]
         torch.cat(grads, out=self.flat)
-        if dist.is_initialized() and self.world(group) > 1:
-            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
-        return [v.view_as(p) for v, p in zip(torch.split(self.flat, self.numels), self.params)]
+        self.allreduce_sum_(group)
+        return self._views
 
     def allreduce_mean(self, group=None) -> None:
         """In-place mean of p.grad over ranks (for torch optimisers)."""

@@ -302,8 +302,11 @@ class _BiGCNEncoderFn(torch.autograd.Function):
         h2 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
         head = torch.empty(B, 4 * HID, dtype=torch.float32, device=dev)
         a.tree_ptr, a.h1, a.h2, a.head_in = ptr(tree_ptr), ptr(h1), ptr(h2), ptr(head)
+        a.save_for_backward = 1 if any(ctx.needs_input_grad) else 0
         ws = workspace(L.bgcn_bigcn_workspace_size(N, B, F, HID), dev)
         check(L.bgcn_bigcn_forward(ctypes.byref(a), ptr(ws), ws.numel(), stream_handle()))
+        ctx.ws = ws if a.save_for_backward else None   # forward -> backward state (bgcn.h)
+        ctx.save_flag = a.save_for_backward
         ctx.graphs = (td, bu)
         ctx.meta = (B, training, seed, feat_mode)
         empty = x.new_empty(0)
@@ -329,7 +332,11 @@ class _BiGCNEncoderFn(torch.autograd.Function):
         grads = [torch.empty_like(p) for p in params]
         for name, gt in zip(_PARAM_ORDER, grads):
             setattr(a, name.replace("_w", "_dw").replace("_b", "_db"), ptr(gt))
-        ws = workspace(L.bgcn_bigcn_workspace_size(N, B, F, HID), dev)
+        a.save_for_backward = ctx.save_flag
+        ws = ctx.ws
+        ctx.ws = None
+        if ws is None:
+            raise RuntimeError("bigcn_encoder: backward called twice or without a saved forward")
         check(L.bgcn_bigcn_backward(ctypes.byref(a), ptr(ws), ws.numel(), stream_handle()))
         return (None,) * 10 + tuple(grads)
 

@@ -18,8 +18,10 @@
  *   - every tensor pointer is a DEVICE pointer owned by the caller; the library
  *     never allocates or frees caller memory.  Scratch comes from a caller-provided
  *     workspace whose size is returned by the matching *_workspace_size() call;
- *   - every call is asynchronous on the given stream, performs no host sync and is
- *     re-entrant (no global mutable state besides the thread-local error string);
+ *   - every call is asynchronous on the given stream and performs no host sync.  Global
+ *     state: the thread-local error string, the opt-in kernel-timing hook, and one
+ *     auxiliary HIP stream per device (created on first use) that the fused encoder
+ *     forks independent branches onto and joins back before returning;
  *   - return value: 0 = ok, BGCN_EINVAL (-1) = invalid argument / shape,
  *     BGCN_EHIP (-2) = HIP launch error.  bgcn_last_error() gives a thread-local
  *     message.  Data-dependent errors (an edge index outside [0, N)) cannot be
@@ -218,14 +220,63 @@ typedef struct bgcn_bigcn_args {
   const float* dhead_in;         /* [B, 4H]                                 */
   float* td_dw1; float* td_db1; float* td_dw2; float* td_db2;
   float* bu_dw1; float* bu_db1; float* bu_dw2; float* bu_db2;
+  /* 1: a backward will follow - the forward also builds backward-only state (the CSC
+   * of X for dW1) on the library's auxiliary stream, overlapped with the forward */
+  int32_t save_for_backward;
 } bgcn_bigcn_args;
 
+/* The workspace carries state from the forward to the backward (node -> root map,
+ * tree work items, root keep masks, CSC of X): pass the backward the SAME workspace,
+ * unmodified, and the same args as the forward (plus dhead_in and the gradient
+ * pointers).  Both calls may use the library's per-device auxiliary stream for
+ * independent branches; every branch is joined back into `stream` before the call's
+ * work on `stream` ends, so the caller sees ordinary single-stream semantics. */
 size_t bgcn_bigcn_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,
                                  int64_t hid);
 int bgcn_bigcn_forward(const bgcn_bigcn_args* args, void* workspace, size_t workspace_bytes,
                        bgcn_stream_t stream);
 int bgcn_bigcn_backward(const bgcn_bigcn_args* args, void* workspace, size_t workspace_bytes,
                         bgcn_stream_t stream);
+
+/* --------------------------------------------------------------------------
+ * One training step up to the optimiser, as ONE call (the loop body of
+ * BiGCN_Twitter.py:183-188): K1 for TD and BU (gcn_norm + CSR, auxiliary lane,
+ * overlapped with the pass over X), the fused encoder forward, the head
+ * fc -> log_softmax (:129-130) and nll_loss mean (:186), and the complete backward.
+ * Every gradient is WRITTEN (not accumulated), so grads[] may point into a flat
+ * data-parallel bucket; the all-reduce and bgcn_adam_step follow.  Parameter order:
+ * td_w1 td_b1 td_w2 td_b2 bu_w1 bu_b1 bu_w2 bu_b2 fc_w [C, 256] fc_b [C] (the
+ * reference state_dict layout).  *status (optional, zeroed by the call): bit 0 = an
+ * edge index outside [0, N) (skipped), bit 1 = a label outside [0, C) (ignored).
+ * -------------------------------------------------------------------------- */
+#define BGCN_STEP_PARAMS 10
+typedef struct bgcn_step_args {
+  const float* x; int64_t ldx;   /* [N, F] node features                     */
+  int64_t num_nodes;             /* N                                        */
+  int64_t num_graphs;            /* B                                        */
+  int64_t in_feats;              /* F                                        */
+  int64_t num_classes;           /* C in [1, 16] (Twitter 4, Weibo 2)        */
+  const int64_t* batch;          /* [N] sorted tree id per node              */
+  const int64_t* rootindex;      /* [B] global root node ids                 */
+  const int64_t* y;              /* [B] labels                               */
+  const int64_t* td_edge_index; int64_t td_num_edges;   /* [2, E_td]         */
+  const int64_t* bu_edge_index; int64_t bu_num_edges;   /* [2, E_bu]         */
+  int32_t degree_on;             /* BGCN_DEGREE_ON_COL / _ROW                */
+  int32_t training;              /* dropout on/off                           */
+  uint64_t seed;                 /* dropout draw                             */
+  int32_t feat_mode;             /* BGCN_FEAT_AUTO / _DENSE                  */
+  const float* params[BGCN_STEP_PARAMS];
+  float* grads[BGCN_STEP_PARAMS];
+  float* loss;                   /* [1] mean NLL                             */
+  float* logp;                   /* [B, C] log-probabilities, or NULL        */
+  int32_t* status;               /* [1] or NULL                              */
+} bgcn_step_args;
+
+size_t bgcn_train_step_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,
+                                      int64_t num_classes, int64_t td_num_edges,
+                                      int64_t bu_num_edges);
+int bgcn_train_step(const bgcn_step_args* args, void* workspace, size_t workspace_bytes,
+                    bgcn_stream_t stream);
 
 /* --------------------------------------------------------------------------
  * Optimiser step of the training loop: torch.optim.Adam with the reference's three
@@ -254,9 +305,13 @@ int bgcn_adam_step(const bgcn_adam_args* args, bgcn_stream_t stream);
 int bgcn_keep_words(uint64_t seed, int64_t num_nodes, int32_t num_words, uint32_t* words,
                     bgcn_stream_t stream);
 
-/* Timing hook for bench.py: HIP-event time (ms) of the last launch of the named
- * kernel class on this thread, when enabled with bgcn_set_kernel_timing(1).
- * kernel class 0 = conv1 X*W1^T GEMM, 1 = dW1 GEMM, 2 = conv2 GEMM, 3 = dW2 GEMM. */
+/* Timing hook for bench.py: accumulated HIP-event time (ms) and launch count of a
+ * kernel class of the fused encoder since bgcn_set_kernel_timing(1) (process-wide;
+ * events are recorded on the launch stream).  Classes:
+ *   0 conv1 (dense: X*W1^T MFMA; auto: k_compact_conv1)  1 dW1 dense MFMA
+ *   2 conv2 (dense MFMA + sparse root gather)            3 dW2 relu(H1) block MFMA
+ *   4 gated dense conv1 fallback (auto)                  5 dW1 + dW2 root columns over CSC(X)
+ *   6 gated dense dW1 fallback (auto) */
 int bgcn_set_kernel_timing(int enable);
 int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* launches);
 

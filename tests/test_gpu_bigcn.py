@@ -127,6 +127,29 @@ def test_fused_is_deterministic_full_size(mode):
     assert torch.isfinite(r1[1])
 
 
+@pytest.mark.parametrize("mode", ["auto", "dense"])
+def test_aux_stream_branches_match_inline(mode):
+    """On a non-default stream the fused step forks independent branches (the CSC of X,
+    the dW2 chain) onto the library's auxiliary stream; on the legacy null stream they
+    run inline.  Both schedules give bitwise-identical results, also when the caller's
+    stream is busy with unrelated work queued ahead of the step."""
+    b = _synth(23, 64, 256)
+    p = O.make_params(5000, 64, 64, 4, seed=7)
+    r0 = gpu_step(b, p, True, None, seed=11, mode=mode)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        big = torch.randn(4096, 4096, device=DEV)
+        for _ in range(4):
+            big = big @ big * 1e-3                     # keeps the stream busy ahead of the step
+        r1 = gpu_step(b, p, True, None, seed=11, mode=mode)
+    torch.cuda.synchronize()
+    assert torch.equal(r0[0], r1[0])
+    for k in r0[2]:
+        assert torch.equal(r0[2][k], r1[2][k]), k
+
+
 def test_sparse_and_dense_paths_agree_full_size():
     """The sparse feature path and the dense MFMA path compute the same step (fp32
     rounding only) on a full Twitter15-shaped batch."""

@@ -1,0 +1,136 @@
+"""GPU parity of the one-call training step (bgcn_train_step via FusedTrainStep).
+
+Oracle: ``oracle/bigcn_oracle.py`` (CPU fp64 restatement of BiGCN_Twitter.py:183-189)
+with the in-kernel dropout draw materialised by ``keep_words``; tolerance 1e-4 of
+each tensor's max magnitude (fp32 kernels vs fp64 oracle)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import bigcn_oracle as O
+from test_gpu_bigcn import DEV, _oracle, _synth, close
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ["TDrumorGCN.conv1.lin.weight", "TDrumorGCN.conv1.bias", "TDrumorGCN.conv2.lin.weight",
+        "TDrumorGCN.conv2.bias", "BUrumorGCN.conv1.lin.weight", "BUrumorGCN.conv1.bias",
+        "BUrumorGCN.conv2.lin.weight", "BUrumorGCN.conv2.bias", "fc.weight", "fc.bias"]
+
+
+def _model(p, mode="auto", classes=4):
+    from bigcn_amd import BiGCN, Net
+    m = (BiGCN if classes == 4 else Net)(p["TDrumorGCN.conv1.lin.weight"].shape[1], 64, 64).to(DEV)
+    m.load_state_dict({k: v.float() for k, v in p.items()})
+    m.feat_mode = mode
+    return m
+
+
+@pytest.mark.parametrize("mode", ["auto", "dense"])
+@pytest.mark.parametrize("training", [False, True])
+def test_train_step_matches_oracle(training, mode):
+    from bigcn_amd import FusedTrainStep
+    from bigcn_amd.ops import keep_words, unpack_keep
+    b = _synth(31, 16, 150, root_random=True)
+    p = O.make_params(5000, 64, 64, 4, seed=12)
+    m = _model(p, mode)
+    m.train(training)
+    step = FusedTrainStep(m)
+    N = b.x.size(0)
+    seed = 424242
+    logp = torch.empty(b.num_graphs, 4, device=DEV)
+    loss = step.forward_backward(b, seed=seed, logp=logp)
+    masks = (None, None)
+    if training:
+        mk = unpack_keep(keep_words(seed, N, 5000, DEV).cpu(), 64 + 5000)
+        masks = (mk[0], mk[1])
+    rlogp, rloss, rgrads, _ = _oracle(b, p, training, *masks)
+    close(logp, rlogp, what="logp")
+    close(loss, rloss, what="loss")
+    g = step.grads()
+    for k, prm in zip(KEYS, step.step_params):
+        close(g[prm], rgrads[k], what=k)
+    step.check_status()
+
+
+@pytest.mark.parametrize("mode", ["auto", "dense"])
+def test_train_step_matches_autograd_path(mode):
+    """The one-call step and the per-op autograd path compute the same step."""
+    from bigcn_amd import FusedTrainStep
+    b = _synth(32, 64, 256)
+    p = O.make_params(5000, 64, 64, 4, seed=13)
+    m = _model(p, mode)
+    m.train()
+    step = FusedTrainStep(m)
+    loss = step.forward_backward(b, seed=77)
+    fused = {k: v.clone() for k, v in step.grads().items()}
+    m.zero_grad()
+    ref = F.nll_loss(m(b, seed=77), b.y)
+    ref.backward()
+    close(loss, ref, what="loss")
+    for prm, gv in fused.items():
+        close(gv, prm.grad, what=str(tuple(prm.shape)))
+
+
+def test_train_step_adam_matches_torch_adam():
+    """Three full steps: the fused Adam (reference groups, grad_scale path) applied to the
+    step's gradients equals torch.optim.Adam (fp32, same groups) fed the same gradients."""
+    from bigcn_amd import FusedTrainStep, make_optimizer
+    b = _synth(33, 8, 100)
+    p = O.make_params(5000, 64, 64, 4, seed=14)
+    m = _model(p)
+    m.train()
+    step = FusedTrainStep(m)
+    shadow = _model(p)
+    topt = make_optimizer(shadow)
+    for it in range(3):
+        step.forward_backward(b, seed=1000 + it)
+        for sp, prm in zip(shadow.parameters(), m.parameters()):
+            sp.grad = step.grads()[prm].clone()
+        topt.step()
+        step.opt.step(grads=step.bucket.views(), grad_scale=1.0)
+    for (k, v), (k2, v2) in zip(m.state_dict().items(), shadow.state_dict().items()):
+        assert k == k2
+        close(v, v2, tol=1e-6, what=k)
+
+
+def test_train_step_weibo_head_and_determinism():
+    """Net (2 classes): two identical calls are bitwise equal; the step matches the oracle."""
+    from bigcn_amd import FusedTrainStep
+    b = _synth(34, 32, 200)
+    b.y = b.y % 2
+    p = O.make_params(5000, 64, 64, 2, seed=15)
+    m = _model(p, classes=2)
+    m.train()
+    step = FusedTrainStep(m)
+    l1 = step.forward_backward(b, seed=5)
+    g1 = [v.clone() for v in step.grads().values()]
+    l2 = step.forward_backward(b, seed=5)
+    g2 = list(step.grads().values())
+    assert torch.equal(l1, l2)
+    for a, c in zip(g1, g2):
+        assert torch.equal(a, c)
+    m.eval()
+    loss = step.forward_backward(b)
+    _, rloss, rgrads, _ = _oracle(b, p, False)
+    close(loss, rloss, what="loss")
+    for k, prm in zip(KEYS, step.step_params):
+        close(step.grads()[prm], rgrads[k], what=k)
+
+
+def test_train_step_reports_bad_inputs():
+    from bigcn_amd import FusedTrainStep
+    b = _synth(35, 4, 30)
+    p = O.make_params(5000, 64, 64, 4, seed=16)
+    step = FusedTrainStep(_model(p))
+    b.y = b.y.clone()
+    b.y[0] = 7
+    step.forward_backward(b, seed=1)
+    with pytest.raises(IndexError, match="label"):
+        step.check_status()
+    b = _synth(35, 4, 30)
+    b.edge_index = b.edge_index.clone()
+    b.edge_index[1, 0] = b.x.size(0) + 5
+    step.forward_backward(b, seed=1)
+    with pytest.raises(IndexError, match="edge_index"):
+        step.check_status()
