@@ -191,14 +191,26 @@ def main():
 
     def run_on_stream(mode: str, steps: int, warmup: int):
         model.feat_mode = mode
+        timing = not args.no_kernel_timing
+        # warm-up: every kernel class timed, to find the dominant one; the timed loop
+        # then records events only around that class (2 events per step)
+        if timing:
+            ops.set_kernel_timing(True)
         for i in range(warmup):
             step(i)
         torch.cuda.synchronize()
+        warm = {}
+        if timing:
+            ops.set_kernel_timing(False)
+            for c in KERNEL_CLASSES[mode]:
+                ms, n = ops.kernel_timing(c)
+                if n:
+                    warm[c] = ms / n
         if world > 1:
             dist.barrier()
-        timing = not args.no_kernel_timing
-        if timing:
-            ops.set_kernel_timing(True)
+        dominant = [max(warm, key=warm.get)] if warm else []
+        if timing and dominant:
+            ops.set_kernel_timing(True, dominant)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -212,28 +224,33 @@ def main():
             dist.barrier()
         dt = time.perf_counter() - t0
         kern = {}
-        if timing:
+        if timing and dominant:
             ops.set_kernel_timing(False)
-            for c in KERNEL_CLASSES[mode]:
-                kern[c] = ops.kernel_timing(c)
+            kern[dominant[0]] = ops.kernel_timing(dominant[0])
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         N_avg = float(np.mean([nodes[(warmup + i) % len(nodes)] for i in range(steps)]))
+        N_warm = float(np.mean([nodes[i % len(nodes)] for i in range(max(warmup, 1))]))
         roof, kernels, best = None, {}, None
-        for c, (ms, n) in kern.items():
+        per_class = {c: (ms, n, "timed loop") for c, (ms, n) in kern.items()}
+        for c, avg in warm.items():
+            if c not in per_class:
+                per_class[c] = (avg * warmup, warmup, "warm-up")
+        for c, (ms, n, where) in per_class.items():
             if n == 0:
                 continue
             avg_ms = ms / n
-            bound, work = kernel_work(mode, c, N_avg, wl["feats"])
-            ent = {"avg_ms": round(avg_ms, 4), "launches": n}
+            n_nodes = N_avg if where == "timed loop" else N_warm
+            bound, work = kernel_work(mode, c, n_nodes, wl["feats"])
+            ent = {"avg_ms": round(avg_ms, 4), "launches": n, "measured": where}
             if bound == "mfma":
                 ent["tflops"] = round(work / (avg_ms * 1e-3) / 1e12, 2)
             elif bound == "hbm":
                 ent["gbs"] = round(work / (avg_ms * 1e-3) / 1e9, 1)
             kernels[KERNEL_CLASSES[mode][c]] = ent
-            if bound is not None and (best is None or avg_ms > best[1]):
+            if bound is not None and where == "timed loop":
                 best = (c, avg_ms, bound, work)
         if best is not None:
             c, avg_ms, bound, work = best

@@ -622,7 +622,7 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
 
 // Forward.  Main stream: node maps, conv1 (sparse compaction + gather, or dense MFMA),
 // propagate, conv2, propagate, readout.  When a backward follows, the CSC of X for dW1
-// is built on auxiliary lane 0 right after the compaction, overlapped with the
+// is built on the auxiliary lane right after conv1's lin, overlapped with the
 // latency-bound second half of the forward, and joined before returning.  graph_lane
 // >= 0: the caller is building the TD/BU graphs on that lane (bgcn_train_step), joined
 // just before their first use.
@@ -653,18 +653,20 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
     BGCN_TRY(sparse_compact_conv1(sp, a->x, a->ldx, w.z1, s));
     timing_end(0, s);
     BGCN_TRY(sparse_items(sp, a->tree_ptr, s));
-    if (a->save_for_backward) {
-      hipStream_t x;
-      BGCN_TRY(aux_fork(s, 0, &x));
-      BGCN_TRY(sparse_csc(sp, x));
-      forked = true;
-    }
   }
   timing_begin(sparse ? 4 : 0, s);
   BGCN_TRY(gemm_xwt_impl(a->x, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F, s, gate));
   timing_end(sparse ? 4 : 0, s);
+  // the graphs (built on graph_lane by bgcn_train_step) are needed from here on; the
+  // join comes before the CSC fork so that it never waits for the CSC
+  if (graph_lane >= 0) BGCN_TRY(aux_join(s, graph_lane));
+  if (sparse && a->save_for_backward) {
+    hipStream_t x;
+    BGCN_TRY(aux_fork(s, kLaneSide, &x));
+    BGCN_TRY(sparse_csc(sp, x));
+    forked = true;
+  }
   // conv1 propagate + bias (pre-relu h1 is saved: it is also the detached x2)
-  if (graph_lane >= 0) BGCN_TRY(aux_join(s, graph_lane));  // graphs built on that lane
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z1, a->h1, a->td_b1, a->bu_b1, BGCN_EPI_NONE, w, s));
   // conv2 lin with the root-extended, relu'd, dropped-out A operand generated in-kernel
   timing_begin(2, s);
@@ -677,7 +679,7 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
   hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B), 2), dim3(1024), 0, s, a->h1, a->h2,
                      a->tree_ptr, a->rootindex, N, a->head_in);
   BGCN_CHECK_LAUNCH();
-  if (forked) BGCN_TRY(aux_join(s, 0));
+  if (forked) BGCN_TRY(aux_join(s, kLaneSide));
   return BGCN_OK;
 }
 
@@ -712,7 +714,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   // columns always by MFMA; the X[root] columns by MFMA (dense) or from the root
   // non-zeros (sparse, finished in sparse_dw_cols below).
   hipStream_t x;
-  BGCN_TRY(aux_fork(s, 0, &x));
+  BGCN_TRY(aux_fork(s, kLaneSide, &x));
   timing_begin(3, x);
   hipLaunchKernelGGL(k_dw2, dim3(grid_for(H + F, 64), w.S2, 2), dim3(256), 0, x, a->x, a->ldx, F,
                      a->h1, w.dz2, w.node_root, w.dw2_part, N, w.kchunk2, w.S2, keep, gate, 1, H + F);
@@ -743,7 +745,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
                      a->bu_db1);
   BGCN_CHECK_LAUNCH();
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.dh1, w.dz1, nullptr, nullptr, BGCN_EPI_NONE, w, s));
-  BGCN_TRY(aux_join(s, 0));
+  BGCN_TRY(aux_join(s, kLaneSide));
   // dW1 = [dZ1_td | dZ1_bu]^T X  (one pass over X for both directions) - dense MFMA, or
   // over the column-sorted non-zeros of X together with the dW2 root columns
   if (sparse) {

@@ -58,8 +58,12 @@ struct Carve {
 // fused step: aux_fork sets *branch to lane's stream after making it wait for the work
 // queued on `main` so far; aux_join makes `main` wait for everything queued on the lane.
 // On the legacy null stream (whose cross-stream waits synchronise the host) *branch =
-// main and the branch runs inline.
-constexpr int kAuxLanes = 2;
+// main and the branch runs inline.  One lane is used: HIP maps streams onto a few
+// hardware queues (GPU_MAX_HW_QUEUES) and measured, only one extra stream reliably got a
+// queue of its own; the branches are ordered so that sharing it costs nothing (the
+// train step's graph build finishes on it long before the CSC of X is queued behind).
+constexpr int kAuxLanes = 1;
+constexpr int kLaneSide = 0;
 int aux_fork(hipStream_t main, int lane, hipStream_t* branch);
 int aux_join(hipStream_t main, int lane);
 

@@ -1,9 +1,10 @@
 // Host runtime of libbgcn: thread-local error string, ABI version, the per-device auxiliary
-// stream of the fused step's independent branches, and the (process-global) kernel-timing
+// streams ("lanes") of the fused step's independent branches, and the (process-global) kernel-timing
 // hook bench.py uses to measure the dominant kernel with HIP events on the stream it is
 // launched on.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -18,11 +19,13 @@ thread_local std::string g_err;
 
 struct TimingState {
   bool enabled = false;
+  unsigned mask = 0;  // bit c: class c is timed
   struct Pair { hipEvent_t a, b; };
   std::vector<Pair> pending[kTimingClasses];
   hipEvent_t open[kTimingClasses] = {};
   double total_ms[kTimingClasses] = {};
   int64_t count[kTimingClasses] = {};
+  std::vector<hipEvent_t> free_events;  // recycled after readout: no create in the timed loop
 };
 // process-global: the fused backward runs on autograd's device thread, the forward on
 // the caller's thread; both record into the same state
@@ -38,18 +41,22 @@ struct AuxState {
 AuxState g_aux[kMaxDevices];
 std::mutex g_aux_mu;
 
+// All lanes of a device are created together, on first use.
 AuxState* aux_state(int lane) {
   int dev = 0;
   if (lane < 0 || lane >= kAuxLanes) return nullptr;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
   AuxState& a = g_aux[dev];
-  if (!a.stream[lane]) {
-    hipStream_t st;
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&a.fork[lane], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&a.join[lane], hipEventDisableTiming) != hipSuccess)
-      return nullptr;
-    a.stream[lane] = st;
+  if (!a.stream[kAuxLanes - 1]) {
+    for (int k = 0; k < kAuxLanes; ++k) {
+      if (a.stream[k]) continue;
+      hipStream_t st;
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+      if (hipEventCreateWithFlags(&a.fork[k], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&a.join[k], hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+      a.stream[k] = st;
+    }
   }
   return &a;
 }
@@ -62,29 +69,48 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+hipEvent_t take_event() {  // caller holds g_tm_mu
+  if (!g_tm.free_events.empty()) {
+    hipEvent_t e = g_tm.free_events.back();
+    g_tm.free_events.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+
 void timing_begin(int cls, hipStream_t s) {
-  if (!g_tm.enabled || cls < 0 || cls >= kTimingClasses) return;
+  if (!g_tm.enabled || cls < 0 || cls >= kTimingClasses || !((g_tm.mask >> cls) & 1u)) return;
   std::lock_guard<std::mutex> lk(g_tm_mu);
-  hipEvent_t e;
-  if (hipEventCreate(&e) != hipSuccess) return;
+  hipEvent_t e = take_event();
+  if (!e) return;
   (void)hipEventRecord(e, s);
   g_tm.open[cls] = e;
 }
 
 void timing_end(int cls, hipStream_t s) {
-  if (!g_tm.enabled || cls < 0 || cls >= kTimingClasses) return;
+  if (!g_tm.enabled || cls < 0 || cls >= kTimingClasses || !((g_tm.mask >> cls) & 1u)) return;
   std::lock_guard<std::mutex> lk(g_tm_mu);
   if (!g_tm.open[cls]) return;
-  hipEvent_t e;
-  if (hipEventCreate(&e) != hipSuccess) return;
+  hipEvent_t e = take_event();
+  if (!e) return;
   (void)hipEventRecord(e, s);
   g_tm.pending[cls].push_back({g_tm.open[cls], e});
   g_tm.open[cls] = nullptr;
 }
 
+// BGCN_SERIAL=1 in the environment runs every branch inline (A/B measurements)
+bool serial_branches() {
+  static const bool v = [] {
+    const char* e = std::getenv("BGCN_SERIAL");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 int aux_fork(hipStream_t main, int lane, hipStream_t* branch) {
   *branch = main;
-  if (!main) return BGCN_OK;  // legacy null stream: the branch runs inline (bgcn_common.h)
+  if (!main || serial_branches()) return BGCN_OK;  // inline (see bgcn_common.h)
   std::lock_guard<std::mutex> lk(g_aux_mu);
   AuxState* a = aux_state(lane);
   if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
@@ -95,7 +121,7 @@ int aux_fork(hipStream_t main, int lane, hipStream_t* branch) {
 }
 
 int aux_join(hipStream_t main, int lane) {
-  if (!main) return BGCN_OK;
+  if (!main || serial_branches()) return BGCN_OK;
   std::lock_guard<std::mutex> lk(g_aux_mu);
   AuxState* a = aux_state(lane);
   if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
@@ -114,18 +140,25 @@ extern "C" int bgcn_set_kernel_timing(int enable) {
   std::lock_guard<std::mutex> lk(bgcn::g_tm_mu);
   auto& t = bgcn::g_tm;
   t.enabled = enable != 0;
+  t.mask = unsigned(enable);
   for (int c = 0; c < bgcn::kTimingClasses; ++c) {
     t.total_ms[c] = 0;
     t.count[c] = 0;
     if (!t.enabled) continue;       // disabling keeps the pending events for readout
     for (auto& p : t.pending[c]) {  // enabling drops events of classes nobody read out
       (void)hipEventSynchronize(p.b);
-      (void)hipEventDestroy(p.a);
-      (void)hipEventDestroy(p.b);
+      t.free_events.push_back(p.a);
+      t.free_events.push_back(p.b);
     }
     t.pending[c].clear();
-    if (t.open[c]) (void)hipEventDestroy(t.open[c]);
+    if (t.open[c]) (void)hipEventSynchronize(t.open[c]), t.free_events.push_back(t.open[c]);
     t.open[c] = nullptr;
+  }
+  // pre-create events so that the timed loop only records (hipEventCreate is not free)
+  while (t.enabled && t.free_events.size() < 1024) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) break;
+    t.free_events.push_back(e);
   }
   return BGCN_OK;
 }
@@ -143,8 +176,8 @@ extern "C" int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* la
       t.total_ms[kernel_class] += ms;
       t.count[kernel_class] += 1;
     }
-    (void)hipEventDestroy(p.a);
-    (void)hipEventDestroy(p.b);
+    t.free_events.push_back(p.a);
+    t.free_events.push_back(p.b);
   }
   v.clear();
   if (total_ms) *total_ms = float(t.total_ms[kernel_class]);

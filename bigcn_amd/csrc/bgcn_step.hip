@@ -5,9 +5,9 @@
 //       loss = F.nll_loss(out_labels, Batch_data.y)          :186
 //       optimizer.zero_grad(); loss.backward()               :187-188
 //
-// K1 (gcn_norm + CSR of TD and BU) runs on auxiliary lane 1, overlapped with the
-// encoder's pass over X on the caller's stream; the CSC of X (lane 0) overlaps the
-// second half of the forward; the dW2 chain (lane 0) overlaps dH1 -> dZ1.  The head
+// K1 (gcn_norm + CSR of TD and BU) runs on the auxiliary lane, overlapped with the
+// encoder's pass over X on the caller's stream; then the CSC of X (same lane) overlaps
+// the second half of the forward, and the dW2 chain overlaps dH1 -> dZ1.  The head
 // (fc -> log_softmax -> nll mean, BiGCN_Twitter.py:129-130,186) and its backward are
 // two small kernels.  Every parameter gradient is written (not accumulated), so the
 // caller's buffers can be views of a flat data-parallel bucket; the all-reduce and
@@ -174,6 +174,8 @@ bgcn_graph_view view_of(const bgcn_csr_out& g, int64_t cap) {
 
 }  // namespace
 
+static int train_step_body(const bgcn_step_args* a, StepWs& w, hipStream_t s);
+
 size_t train_step_ws_size(int64_t N, int64_t B, int64_t F, int64_t C, int64_t Etd, int64_t Ebu) {
   Carve c(nullptr, 0);
   return carve_step(c, N, B, F, C, Etd, Ebu, nullptr) + 256;
@@ -194,11 +196,17 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
   Carve c(ws, ws_bytes);
   carve_step(c, N, B, F, C, a->td_num_edges, a->bu_num_edges, &w);
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
+  return train_step_body(a, w, s);
+}
+
+static int train_step_body(const bgcn_step_args* a, StepWs& w, hipStream_t s) {
+  const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats, C = a->num_classes;
   if (a->status) BGCN_CHECK_HIP(hipMemsetAsync(a->status, 0, sizeof(int32_t), s));
 
-  // K1 for both directions on lane 1 (joined by the encoder before the first propagate)
+  // K1 for both directions on the side lane (joined by the encoder right after its pass
+  // over X, before the CSC of X is queued on the same lane), overlapped with that pass
   hipStream_t g;
-  BGCN_TRY(aux_fork(s, 1, &g));
+  BGCN_TRY(aux_fork(s, kLaneSide, &g));
   BGCN_TRY(bgcn_build_graph_pair(a->td_edge_index, a->td_num_edges, a->bu_edge_index,
                                  a->bu_num_edges, N, a->degree_on, &w.td, &w.bu, a->status, w.gws,
                                  w.gws_bytes, reinterpret_cast<bgcn_stream_t>(g)));
@@ -217,7 +225,7 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
   e.td_dw1 = a->grads[0]; e.td_db1 = a->grads[1]; e.td_dw2 = a->grads[2]; e.td_db2 = a->grads[3];
   e.bu_dw1 = a->grads[4]; e.bu_db1 = a->grads[5]; e.bu_dw2 = a->grads[6]; e.bu_db2 = a->grads[7];
   e.save_for_backward = 1;
-  BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, g == s ? -1 : 1));
+  BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, g == s ? -1 : kLaneSide));
 
   hipLaunchKernelGGL(k_head_fwd, dim3(grid_for(B, 4)), dim3(256), 0, s, w.head, a->params[8],
                      a->params[9], a->y, B, int(C), a->logp, w.dz, w.loss_row, w.dhead, a->status);

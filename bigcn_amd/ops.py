@@ -389,8 +389,12 @@ def pack_keep(mask: torch.Tensor) -> torch.Tensor:
     return w.to(torch.int32)
 
 
-def set_kernel_timing(enable: bool) -> None:
-    check(_lib.lib().bgcn_set_kernel_timing(1 if enable else 0))
+def set_kernel_timing(enable, classes=None) -> None:
+    """Enable (all classes, or the iterable ``classes``) / disable the kernel-timing hook."""
+    mask = 0
+    if enable:
+        mask = 0xFF if classes is None else sum(1 << int(c) for c in classes)
+    check(_lib.lib().bgcn_set_kernel_timing(mask))
 
 
 def kernel_timing(kernel_class: int):

@@ -19,9 +19,10 @@
  *     never allocates or frees caller memory.  Scratch comes from a caller-provided
  *     workspace whose size is returned by the matching *_workspace_size() call;
  *   - every call is asynchronous on the given stream and performs no host sync.  Global
- *     state: the thread-local error string, the opt-in kernel-timing hook, and one
- *     auxiliary HIP stream per device (created on first use) that the fused encoder
- *     forks independent branches onto and joins back before returning;
+ *     state: the thread-local error string, the opt-in kernel-timing hook, and three
+ *     auxiliary HIP streams ("lanes") per device (created on first use) that the fused
+ *     encoder and train step fork independent branches onto and join back into the
+ *     caller's stream before returning (inline on the legacy null stream);
  *   - return value: 0 = ok, BGCN_EINVAL (-1) = invalid argument / shape,
  *     BGCN_EHIP (-2) = HIP launch error.  bgcn_last_error() gives a thread-local
  *     message.  Data-dependent errors (an edge index outside [0, N)) cannot be
@@ -306,8 +307,9 @@ int bgcn_keep_words(uint64_t seed, int64_t num_nodes, int32_t num_words, uint32_
                     bgcn_stream_t stream);
 
 /* Timing hook for bench.py: accumulated HIP-event time (ms) and launch count of a
- * kernel class of the fused encoder since bgcn_set_kernel_timing(1) (process-wide;
- * events are recorded on the launch stream).  Classes:
+ * kernel class of the fused encoder since bgcn_set_kernel_timing(mask) (process-wide;
+ * events are recorded on the launch stream; mask bit c enables class c, 0 disables and
+ * keeps the recorded events for bgcn_kernel_timing).  Classes:
  *   0 conv1 (dense: X*W1^T MFMA; auto: k_compact_conv1)  1 dW1 dense MFMA
  *   2 conv2 (dense MFMA + sparse root gather)            3 dW2 relu(H1) block MFMA
  *   4 gated dense conv1 fallback (auto)                  5 dW1 + dW2 root columns over CSC(X)

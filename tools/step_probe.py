@@ -21,9 +21,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--null-stream", action="store_true")
+    ap.add_argument("--path", default="fused", choices=["fused", "autograd"])
     args = ap.parse_args()
     import bench
-    from bigcn_amd import BiGCN
+    from bigcn_amd import BiGCN, FusedTrainStep
     from bigcn_amd.optim import bigcn_adam
     dev = torch.device("cuda", 0)
     wl = bench.WORKLOADS["twitter15"]
@@ -34,8 +35,13 @@ def main():
     stream = torch.cuda.current_stream() if args.null_stream else torch.cuda.Stream(dev)
     torch.cuda.synchronize()
 
+    fused = FusedTrainStep(model, opt)
+
     def step(i):
         b = pool[i % len(pool)]
+        if args.path == "fused":
+            fused(b)
+            return
         b.__dict__.pop("_bgcn_graphs", None)
         logp = model(b)
         loss = F.nll_loss(logp, b.y)
