@@ -174,27 +174,28 @@ __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_
   const int bn = tid >> 3, bc = (tid & 7) * 8;
   float4 ra[2], gb[2];
   uint32_t gw = 0;
+  // unconditional loads from clamped nodes / columns, zeroed by select (see k_dh1)
   auto gload = [&](int64_t k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      int64_t node = k0 + an + 16 * i;
-      ra[i] = node < ke ? ld4(dZ2 + node * (2 * H) + d * H + aq) : f4zero();
+      const int64_t node = k0 + an + 16 * i;
+      const float4 v = ld4(dZ2 + min<int64_t>(node, ke - 1) * (2 * H) + d * H + aq);
+      ra[i] = node < ke ? v : f4zero();
     }
-    int64_t node = k0 + bn;
-    bool ok = node < ke;
-    int64_t c = c0 + bc;
-    gw = ok ? keep.get(uint32_t(d), uint32_t(node), uint32_t(c / 32)) : 0u;
-    const float* xr = X + int64_t(ok ? node_root[node] : 0) * ldx;
-    const float* h1 = H1 + (ok ? node : 0) * (2 * H) + d * H;
+    const int64_t node = k0 + bn;
+    const bool ok = node < ke;
+    const int64_t nc = min<int64_t>(node, ke - 1);
+    const int64_t c = c0 + bc;
+    gw = keep.get(uint32_t(d), uint32_t(nc), uint32_t(c / 32));
+    gw = ok ? gw : 0u;
+    const int32_t root = node_root[nc];
+    const float* xr = X + int64_t(root < 0 ? 0 : root) * ldx;
+    const float* h1 = H1 + nc * (2 * H) + d * H;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      int64_t cc = c + 4 * j;
-      float4 v = f4zero();
-      if (ok) {
-        if (cc < H) v = ld4(h1 + cc);
-        else if (cc < K2) v = ld4(xr + (cc - H));
-      }
-      gb[j] = v;
+      const int64_t cc = min<int64_t>(c + 4 * j, K2 - 4);
+      const float4 v = ld4(cc < H ? h1 + cc : xr + (cc - H));
+      gb[j] = (ok && c + 4 * j < K2) ? v : f4zero();
     }
   };
   auto sstore = [&](int buf) {
@@ -351,28 +352,35 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
   const int c = l * 4, d = c / H, f = c % H;
   const int hoff = (d == 1 ? 0 : 2 * H) + f;
   const int64_t r0 = int64_t(blockIdx.x) * kReadBwdRows;
+  // unconditional loads from clamped rows / trees (see k_dh1), selects afterwards
   int64_t bt[kPer];
   float4 h2[kPer];
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
-    const int64_t i = r0 + ph + 8 * u;
-    bt[u] = i < N ? batch[i] : -1;
-    h2[u] = i < N ? ld4(H2 + i * (2 * H) + c) : f4zero();
+    const int64_t i = min<int64_t>(r0 + ph + 8 * u, N - 1);
+    bt[u] = batch[i];
+    h2[u] = ld4(H2 + i * (2 * H) + c);
+  }
+  int32_t t0[kPer], t1[kPer];
+  float4 dh[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t b = min<int64_t>(max<int64_t>(bt[u], 0), B - 1);
+    t0[u] = tree_ptr[b];
+    t1[u] = tree_ptr[b + 1];
+    dh[u] = ld4(dhead + b * (4 * H) + hoff);
   }
   float4 cs = f4zero();
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
     const int64_t i = r0 + ph + 8 * u;
-    const int64_t b = bt[u];
-    float4 g = f4zero();
-    if (b >= 0 && b < B) {
-      const float cnt = float(max(tree_ptr[b + 1] - tree_ptr[b], 1));
-      const float4 dh = ld4(dhead + b * (4 * H) + hoff);
-      g.x = h2[u].x > 0.f ? dh.x / cnt : 0.f;
-      g.y = h2[u].y > 0.f ? dh.y / cnt : 0.f;
-      g.z = h2[u].z > 0.f ? dh.z / cnt : 0.f;
-      g.w = h2[u].w > 0.f ? dh.w / cnt : 0.f;
-    }
+    const bool ok = i < N && bt[u] >= 0 && bt[u] < B;
+    const float cnt = float(max(t1[u] - t0[u], 1));
+    float4 g;
+    g.x = ok && h2[u].x > 0.f ? dh[u].x / cnt : 0.f;
+    g.y = ok && h2[u].y > 0.f ? dh[u].y / cnt : 0.f;
+    g.z = ok && h2[u].z > 0.f ? dh[u].z / cnt : 0.f;
+    g.w = ok && h2[u].w > 0.f ? dh[u].w / cnt : 0.f;
     if (i < N) st4(dH2 + i * (2 * H) + c, g);
     cs = f4add(cs, g);
   }
@@ -407,20 +415,25 @@ __global__ __launch_bounds__(256) void k_dh1(const float* __restrict__ dZ2,
   const int64_t row0 = int64_t(blockIdx.x) * kDh1Rows + rh * 32;
   const int c = ch * 32 + r;  // output column of this lane (within H)
 
+  // Every load is unconditional from a clamped (in-bounds) row: rows past N compute
+  // values that are never stored, and the loads stay independent (a guarded load
+  // compiles to a branch with its own wait).
   float a[32], bv[32];
-  const int64_t ia = row0 + r;
+  const int64_t ia = min<int64_t>(row0 + r, N - 1);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const float4 v = ia < N ? ld4(dZ2 + ia * (2 * H) + d * H + 32 * h + 4 * q) : f4zero();
+    const float4 v = ld4(dZ2 + ia * (2 * H) + d * H + 32 * h + 4 * q);
     a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
   }
 #pragma unroll
   for (int kk = 0; kk < 32; ++kk) bv[kk] = W2[int64_t(32 * h + kk) * ldw2 + c];
   float hv[16];
+  uint32_t wd[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-    hv[q] = i < N ? H1[i * (2 * H) + d * H + c] : 0.f;
+    const int64_t i = min<int64_t>(row0 + (q & 3) + 8 * (q >> 2) + 4 * h, N - 1);
+    hv[q] = H1[i * (2 * H) + d * H + c];
+    wd[q] = keep.get(uint32_t(d), uint32_t(i), uint32_t(c >> 5));
   }
   f32x16 acc = {};
 #pragma unroll
@@ -431,9 +444,8 @@ __global__ __launch_bounds__(256) void k_dh1(const float* __restrict__ dZ2,
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    const float g = (((wd[q] >> (c & 31)) & 1u) && hv[q] > 0.f) ? acc[q] * sc : 0.f;
     if (i < N) {
-      const uint32_t wd = keep.get(uint32_t(d), uint32_t(i), uint32_t(c >> 5));
-      const float g = (((wd >> (c & 31)) & 1u) && hv[q] > 0.f) ? acc[q] * sc : 0.f;
       dH1[i * (2 * H) + d * H + c] = g;
       cs += g;
     }

@@ -111,6 +111,11 @@ __device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+// streaming (non-temporal) 16-byte load: data read once, kept out of the caches' LRU
+__device__ __forceinline__ float4 ld4_nt(const float* p) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 __device__ __forceinline__ float4 f4fma(float a, float4 x, float4 acc) {
   acc.x = fmaf(a, x.x, acc.x);

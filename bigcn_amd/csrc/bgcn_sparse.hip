@@ -58,9 +58,12 @@ __global__ __launch_bounds__(256) void k_transpose_weights(SparseState S, const 
 }
 
 // ---------------------------------------------------------------- X compaction + conv1
-// One wave per row: stream the dense row (float4 per lane, 4 x 1 KiB in flight),
-// compact the non-zeros in (chunk, component, lane) order, then
-// Z1[i] = sum val * W1T[col] with each lane owning 2 of the 128 outputs.
+// One wave per row.  The whole row is requested up front (kRowChunks float4 per lane:
+// 20 KiB of a 5000-wide row in flight per wave) so HBM sees deep, independent streams;
+// then the non-zeros are compacted in ascending column order - a float4 group that is
+// all zero across the wave (the common case for bag-of-words rows) costs one ballot -
+// and Z1[i] = sum val * W1T[col] with each lane owning 2 of the 128 outputs.
+constexpr int kRowChunks = 20;  // float4 per lane per pass (F <= 5120 in one pass)
 __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const float* __restrict__ X,
                                                        int64_t ldx, float* __restrict__ Z1) {
   __shared__ int32_t s_col[4][kCap];
@@ -73,27 +76,34 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const floa
   const int nq = int(S.F / 4);   // float4 per row (F % 4 == 0)
   int cnt = 0;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int q0 = 0; q0 < nq; q0 += 4 * 64) {
-    float4 v[4];
+  for (int q0 = 0; q0 < nq; q0 += kRowChunks * 64) {
+    float4 v[kRowChunks];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kRowChunks; ++u) {
       const int q = q0 + u * 64 + lane;
-      v[u] = q < nq ? ld4(row + int64_t(q) * 4) : f4zero();
+      v[u] = q < nq ? ld4_nt(row + int64_t(q) * 4) : f4zero();
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kRowChunks; ++u) {
+      const bool n0 = v[u].x != 0.f, n1 = v[u].y != 0.f, n2 = v[u].z != 0.f, n3 = v[u].w != 0.f;
+      if (__ballot(n0 || n1 || n2 || n3) == 0ull) continue;   // wave-uniform skip
+      const uint64_t m0 = __ballot(n0), m1 = __ballot(n1), m2 = __ballot(n2), m3 = __ballot(n3);
+      // ascending column order: lanes below me contribute all their non-zeros first
+      int pos = cnt + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+      const int col0 = (q0 + u * 64 + lane) * 4;
       const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      const bool nz[4] = {n0, n1, n2, n3};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const bool nz = e[c] != 0.f;
-        const uint64_t m = __ballot(nz);
-        const int pos = cnt + __popcll(m & lt);
-        if (nz && pos < kCap) {
-          s_col[wave][pos] = (q0 + u * 64 + lane) * 4 + c;
-          s_val[wave][pos] = e[c];
+        if (nz[c]) {
+          if (pos < kCap) {
+            s_col[wave][pos] = col0 + c;
+            s_val[wave][pos] = e[c];
+          }
+          ++pos;
         }
-        cnt += __popcll(m);
       }
+      cnt += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
     }
   }
   if (lane == 0) S.nnz[i] = cnt;
@@ -158,6 +168,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   const float sc = keep.scale();
   const int64_t K2 = S.F + H;
   const float* w2t = S.w2t + int64_t(d) * K2 * H;
+  // B fill with unconditional loads (clamped slot / column; see k_dh1), selects after
   if (threadIdx.x < kCap)
     rk[threadIdx.x] = threadIdx.x < rn ? uint32_t(H + S.cols[r * kCap + threadIdx.x]) : 0u;
   for (int e = threadIdx.x; e < H * (H / 4); e += 256) {
@@ -168,14 +179,13 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   }
   for (int e = threadIdx.x; e < kCap * (H / 4); e += 256) {
     const int s = e >> 4, q = (e & 15) * 4;
-    float4 v = f4zero();
-    if (s < rn) {
-      const float av = sc * fmaxf(S.vals[r * kCap + s], 0.f);
-      const float4 w = ld4(w2t + int64_t(H + S.cols[r * kCap + s]) * H + q);
-      v = make_float4(av * w.x, av * w.y, av * w.z, av * w.w);
-    }
+    const int64_t slot = r * kCap + s;              // always inside the row's ELL list
+    const int32_t col = min(max(S.cols[slot], 0), int32_t(S.F - 1));
+    const float val = S.vals[slot];
+    const float4 w = ld4(w2t + int64_t(H + col) * H + q);
+    const float av = s < rn ? sc * fmaxf(val, 0.f) : 0.f;
     float* dst = &Bs[(H + s) * kC2Ld + q];
-    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+    dst[0] = av * w.x; dst[1] = av * w.y; dst[2] = av * w.z; dst[3] = av * w.w;
   }
   __syncthreads();
 
@@ -186,45 +196,32 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
     const int64_t i = i0 + r32;
     const bool ok = i < end;
     const float* hrow = H1 + (ok ? i : beg) * (2 * H) + d * H;
-    const uint32_t w0 = ok ? keep.get(uint32_t(d), uint32_t(i), 0u) : 0u;
-    const uint32_t w1 = ok ? keep.get(uint32_t(d), uint32_t(i), 1u) : 0u;
+    const uint32_t w0 = keep.get(uint32_t(d), uint32_t(ok ? i : beg), 0u);
+    const uint32_t w1 = keep.get(uint32_t(d), uint32_t(ok ? i : beg), 1u);
+    // lane half h supplies k = 48h + kk: H1 columns [48h, 64) then (h = 1) the 32 root
+    // slots.  Both halves run the same straight-line code (clamped column, selects).
     float a[48];
-    if (h == 0) {
 #pragma unroll
-      for (int q = 0; q < 12; ++q) {
-        const float4 v = ld4(hrow + 4 * q);
-        const float ve[4] = {v.x, v.y, v.z, v.w};
+    for (int q = 0; q < 12; ++q) {
+      const int col = min(48 * h + 4 * q, H - 4);
+      const float4 v = ld4(hrow + col);
+      const float ve[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = 4 * q + e;
-          const uint32_t bit = k < 32 ? (w0 >> k) & 1u : (w1 >> (k - 32)) & 1u;
-          a[k] = bit ? sc * fmaxf(ve[e], 0.f) : 0.f;
-        }
+      for (int e = 0; e < 4; ++e) {
+        const int k = 48 * h + 4 * q + e;
+        const uint32_t bit = k < 32 ? (w0 >> (k & 31)) & 1u : (w1 >> (k & 31)) & 1u;
+        a[4 * q + e] = bit ? sc * fmaxf(ve[e], 0.f) : 0.f;   // used when k < 64
       }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = ld4(hrow + 48 + 4 * q);
-        const float ve[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = 48 + 4 * q + e;
-          a[k - 48] = ((w1 >> (k - 32)) & 1u) ? sc * fmaxf(ve[e], 0.f) : 0.f;
-        }
-      }
-      uint32_t m = 0;
-#pragma unroll
-      for (int s = 0; s < kCap; ++s) {
-        uint32_t bit = 0;
-        if (s < rn && ok) {
-          const uint32_t k = rk[s];
-          bit = (keep.get(uint32_t(d), uint32_t(i), k >> 5) >> (k & 31)) & 1u;
-        }
-        m |= bit << s;
-        a[16 + s] = bit ? 1.f : 0.f;
-      }
-      if (ok) S.rbits[int64_t(d) * S.N + i] = m;
     }
+    uint32_t m = 0;
+#pragma unroll
+    for (int s = 0; s < kCap; ++s) {
+      const uint32_t k = rk[s];
+      const uint32_t bit = (s < rn) ? (keep.get(uint32_t(d), uint32_t(ok ? i : beg), k >> 5) >> (k & 31)) & 1u : 0u;
+      m |= bit << s;
+      if (h == 1) a[16 + s] = bit ? 1.f : 0.f;
+    }
+    if (h == 1 && ok) S.rbits[int64_t(d) * S.N + i] = m;
     f32x16 acc0 = {}, acc1 = {};
     const float* bp = &Bs[(48 * h) * kC2Ld + r32];
 #pragma unroll
@@ -282,97 +279,162 @@ __global__ __launch_bounds__(1024) void k_items(SparseState S, const int32_t* __
   if (threadIdx.x == 0) S.tree_item0[S.B] = carry < S.max_items ? carry : S.max_items;
 }
 
+// dW2 root-column partials per work item (<= kChunk nodes of one tree), on the MFMA:
+//   part[s][o] = sum_{i in item} kept_d(i, s) * dZ2_d[i][o]      (s < 32 root slots)
+// a [32 x nodes] x [nodes x 64] product with the 0/1 keep masks of the forward (S.rbits)
+// as A.  Each wave takes 64 of the item's nodes (lane half h owns 32 of them: permuted
+// K); the four waves' partials are combined in a fixed order.
 __global__ __launch_bounds__(256) void k_dw2_root_part(SparseState S, const float* __restrict__ dZ2,
                                                        const int32_t* __restrict__ tree_ptr) {
   if (!use_sparse(S)) return;
   const int item = blockIdx.x;
   if (item >= S.tree_item0[S.B]) return;
   __shared__ uint32_t bits[kChunk];
-  __shared__ float red[4][kCap][H];
+  __shared__ float red[4][kCap * H];
   const int d = blockIdx.y;
   const int b = S.item_tree[item];
   const int64_t beg = int64_t(tree_ptr[b]) + int64_t(S.item_chunk[item]) * kChunk;
   const int64_t end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
-  // root keep masks of the forward's conv2 (bit s = root non-zero s kept for node i)
   for (int t = threadIdx.x; t < kChunk; t += 256) {
     const int64_t i = beg + t;
     bits[t] = i < end ? S.rbits[int64_t(d) * S.N + i] : 0u;
   }
   __syncthreads();
-  const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;   // 64 outputs x 4 node slices
-  float acc[kCap];
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
+  const int64_t n0 = beg + wv * 64 + 32 * h;
+  f32x16 acc0 = {}, acc1 = {};
+  if (beg + wv * 64 < end) {
 #pragma unroll
-  for (int s = 0; s < kCap; ++s) acc[s] = 0.f;
-  // eight independent dZ2 loads in flight per thread (a chunk row is 256 B apart)
-  for (int64_t i0 = beg + sl; i0 < end; i0 += 32) {
-    float g[8];
+    for (int half = 0; half < 2; ++half) {
+      float b0[16], b1[16], av[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t i = i0 + 4 * u;
-      g[u] = i < end ? dZ2[i * (2 * H) + d * H + o] : 0.f;
-    }
+      for (int kk = 0; kk < 16; ++kk) {
+        const int64_t node = n0 + half * 16 + kk;
+        const bool ok = node < end;
+        const float* zr = dZ2 + (ok ? node : beg) * (2 * H) + d * H;
+        b0[kk] = ok ? zr[r32] : 0.f;
+        b1[kk] = ok ? zr[32 + r32] : 0.f;
+        av[kk] = (ok && ((bits[node - beg] >> r32) & 1u)) ? 1.f : 0.f;
+      }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t i = i0 + 4 * u;
-      const uint32_t m = i < end ? bits[i - beg] : 0u;
-#pragma unroll
-      for (int s = 0; s < kCap; ++s) acc[s] += ((m >> s) & 1u) ? g[u] : 0.f;
+      for (int kk = 0; kk < 16; ++kk) {
+        acc0 = mfma32x32x2(av[kk], b0[kk], acc0);
+        acc1 = mfma32x32x2(av[kk], b1[kk], acc1);
+      }
     }
   }
 #pragma unroll
-  for (int s = 0; s < kCap; ++s) red[sl][s][o] = acc[s];
+  for (int q = 0; q < 16; ++q) {
+    const int sl = (q & 3) + 8 * (q >> 2) + 4 * h;
+    red[wv][sl * H + r32] = acc0[q];
+    red[wv][sl * H + 32 + r32] = acc1[q];
+  }
   __syncthreads();
   float* out = S.root_part + (int64_t(d) * S.max_items + item) * (kCap * H);
-  for (int e = threadIdx.x; e < kCap * H; e += 256) {
-    const int s = e / H, oo = e % H;
-    out[e] = (red[0][s][oo] + red[1][s][oo]) + (red[2][s][oo] + red[3][s][oo]);
-  }
+  for (int e = threadIdx.x; e < kCap * H; e += 256)
+    out[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
 }
 
 // ---------------------------------------------------------------- CSC of X
 // Stable counting sort of the non-zeros by column (rows stay in order inside a column):
-//   k_csc_hist    per row block (kRowBlock rows): column histogram in LDS -> hist[r][c]
-//   k_csc_prefix  per column: exclusive prefix over the row blocks, column totals
-//   k_csc_place   per row block: column starts (LDS scan of the totals) + the block's
-//                 prefix, then the rows in order, 8 at a time, rank inside the batch
-// No float atomics, no general sort; deterministic.
-__global__ __launch_bounds__(256) void k_csc_hist(SparseState S) {
+//   k_csc_hist     per row block (kRowBlock rows, a thread per row): column histogram
+//                  in LDS -> hist[r][c]
+//   k_csc_prefix   per column: exclusive prefix over the row blocks, column totals
+//   k_csc_colscan  one block: column starts/ends = exclusive scan of the totals
+//   k_csc_place    per row block: start + the block's prefix, then the rows in order,
+//                  32 at a time, rank inside the batch from per-column row bitmasks
+// No float atomics, no general sort; deterministic.  Every global load is issued
+// unconditionally (clamped index, select afterwards) so the loads of a thread overlap.
+__global__ __launch_bounds__(kRowBlock) void k_csc_hist(SparseState S) {
   if (!use_sparse(S)) return;
   extern __shared__ __attribute__((aligned(16))) int32_t hsm[];   // [F]
-  for (int64_t c = threadIdx.x; c < S.F; c += 256) hsm[c] = 0;
-  __syncthreads();
-  const int64_t r0 = int64_t(blockIdx.x) * kRowBlock;
-  for (int t = threadIdx.x; t < kRowBlock * kCap; t += 256) {
-    const int64_t i = r0 + t / kCap;
-    const int s = t % kCap;
-    if (i < S.N && s < S.nnz[i]) atomicAdd(&hsm[S.cols[i * kCap + s]], 1);
+  for (int64_t c = threadIdx.x; c < S.F; c += kRowBlock) hsm[c] = 0;
+  const int64_t i = int64_t(blockIdx.x) * kRowBlock + threadIdx.x;
+  const int64_t ic = min<int64_t>(i, S.N - 1);
+  const int n = i < S.N ? min(S.nnz[ic], kCap) : 0;
+  int32_t cl[kCap];
+#pragma unroll
+  for (int q = 0; q < kCap / 4; ++q) {
+    const int4 v = *reinterpret_cast<const int4*>(S.cols + ic * kCap + 4 * q);
+    cl[4 * q] = v.x; cl[4 * q + 1] = v.y; cl[4 * q + 2] = v.z; cl[4 * q + 3] = v.w;
   }
   __syncthreads();
+#pragma unroll
+  for (int s = 0; s < kCap; ++s)
+    if (s < n) atomicAdd(&hsm[cl[s]], 1);
+  __syncthreads();
   int32_t* out = S.hist + int64_t(blockIdx.x) * S.F;
-  for (int64_t c = threadIdx.x; c < S.F; c += 256) out[c] = hsm[c];
+  for (int64_t c = threadIdx.x; c < S.F; c += kRowBlock) out[c] = hsm[c];
 }
 
 // 64 columns x 4 row-block quarters per block; hist[r][c] becomes the exclusive prefix
+// of column c over row blocks < r.  Loads in groups of 8 (independent).
 __global__ __launch_bounds__(256) void k_csc_prefix(SparseState S, int R) {
   if (!use_sparse(S)) return;
   __shared__ int32_t part[4][64];
   const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int64_t c = int64_t(blockIdx.x) * 64 + cl;
+  const int64_t c = min<int64_t>(int64_t(blockIdx.x) * 64 + cl, S.F - 1);
+  const bool live = int64_t(blockIdx.x) * 64 + cl < S.F;
   const int rq = (R + 3) / 4, rb = q * rq, re = min(R, rb + rq);
   int32_t sum = 0;
-  if (c < S.F)
-    for (int r = rb; r < re; ++r) sum += S.hist[int64_t(r) * S.F + c];
+  for (int r0 = rb; r0 < re; r0 += 8) {
+    int32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = S.hist[int64_t(min(r0 + u, re - 1)) * S.F + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sum += r0 + u < re ? v[u] : 0;
+  }
   part[q][cl] = sum;
   __syncthreads();
   int32_t run = 0;
   for (int qq = 0; qq < q; ++qq) run += part[qq][cl];
-  if (c < S.F) {
-    for (int r = rb; r < re; ++r) {
-      const int32_t v = S.hist[int64_t(r) * S.F + c];
-      S.hist[int64_t(r) * S.F + c] = run;
-      run += v;
+  for (int r0 = rb; r0 < re; r0 += 8) {
+    int32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = S.hist[int64_t(min(r0 + u, re - 1)) * S.F + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (live && r0 + u < re) S.hist[int64_t(r0 + u) * S.F + c] = run;
+      run += r0 + u < re ? v[u] : 0;
     }
-    if (q == 3) S.col_total[c] = run;
+  }
+  if (live && q == 3) S.col_total[c] = run;
+}
+
+// column starts: exclusive scan of col_total, one 1024-thread block (thread = run of
+// consecutive columns, block scan of the run sums)
+__global__ __launch_bounds__(1024) void k_csc_colscan(SparseState S) {
+  if (!use_sparse(S)) return;
+  __shared__ int32_t wsum[1024];
+  const int64_t F = S.F;
+  const int64_t per = (F + 1023) / 1024;
+  const int64_t c0 = threadIdx.x * per;
+  constexpr int kMaxPer = kSparseMaxF / 1024;
+  int32_t v[kMaxPer];
+  int32_t local = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) {
+    const int64_t c = c0 + k;
+    v[k] = (k < per && c < F) ? S.col_total[min<int64_t>(c, F - 1)] : 0;
+    local += v[k];
+  }
+  wsum[threadIdx.x] = local;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int32_t t = threadIdx.x >= o ? wsum[threadIdx.x - o] : 0;
+    __syncthreads();
+    wsum[threadIdx.x] += t;
+    __syncthreads();
+  }
+  int32_t run = wsum[threadIdx.x] - local;
+#pragma unroll
+  for (int k = 0; k < kMaxPer; ++k) {
+    const int64_t c = c0 + k;
+    if (k < per && c < F) {
+      S.col_start[c] = run;
+      S.col_end[c] = run + v[k];
+    }
+    run += v[k];
   }
 }
 
@@ -381,67 +443,76 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
   extern __shared__ __attribute__((aligned(16))) int32_t psm[];   // [F] counters, [F] row masks
   int32_t* cnt = psm;
   uint32_t* rows = reinterpret_cast<uint32_t*>(psm + S.F);
-  __shared__ int32_t wsum[256];
-  // column starts: exclusive scan of col_total (each thread a contiguous run of columns)
   const int64_t F = S.F;
-  const int64_t per = (F + 255) / 256;
-  const int64_t c0 = threadIdx.x * per, c1 = min<int64_t>(F, c0 + per);
-  int32_t local = 0;
-  for (int64_t c = c0; c < c1; ++c) local += S.col_total[c];
-  wsum[threadIdx.x] = local;
-  __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
-    const int32_t v = threadIdx.x >= o ? wsum[threadIdx.x - o] : 0;
-    __syncthreads();
-    wsum[threadIdx.x] += v;
-    __syncthreads();
-  }
-  int32_t run = wsum[threadIdx.x] - local;
   const int32_t* pre = S.hist + int64_t(blockIdx.x) * F;
-  for (int64_t c = c0; c < c1; ++c) {
-    const int32_t t = S.col_total[c];
-    cnt[c] = run + pre[c];
-    rows[c] = 0u;
-    if (blockIdx.x == 0) { S.col_start[c] = run; S.col_end[c] = run + t; }
-    run += t;
+  for (int64_t c0 = threadIdx.x; c0 < F; c0 += 4 * 256) {
+    int32_t st[4], pr[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t c = min<int64_t>(c0 + 256 * u, F - 1);
+      st[u] = S.col_start[c];
+      pr[u] = pre[c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t c = c0 + 256 * u;
+      if (c < F) {
+        cnt[c] = st[u] + pr[u];
+        rows[c] = 0u;
+      }
+    }
+  }
+  // all of the block's entries up front: thread t holds entries t + 256k (k < 32) of
+  // the row block = slot t % 32 of rows (t / 32) + 8k
+  const int64_t r0 = int64_t(blockIdx.x) * kRowBlock;
+  const int s = threadIdx.x % kCap;
+  constexpr int kPer = kRowBlock * kCap / 256;   // 32
+  int32_t col[kPer], nn[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {   // issue all 64 loads first ...
+    const int64_t ic = min<int64_t>(r0 + threadIdx.x / kCap + 8 * k, S.N - 1);
+    nn[k] = S.nnz[ic];
+    col[k] = S.cols[ic * kCap + s];
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {   // ... then mask the padding slots
+    const int64_t i = r0 + threadIdx.x / kCap + 8 * k;
+    col[k] = (i < S.N && s < nn[k]) ? col[k] : -1;
   }
   __syncthreads();
   // rows of the block in order, 32 rows (= 1024 slots, 4 per thread) per batch.  The
   // columns of one row are distinct, so an entry's rank among the batch's entries of
-  // its column = the number of earlier batch rows holding that column: an OR of row bits
-  // per column (order-independent) + popcount.
-  const int64_t r0 = int64_t(blockIdx.x) * kRowBlock;
+  // its column = the number of earlier batch rows holding that column: an OR of row
+  // bits per column (order-independent) + popcount.
   constexpr int kBatchRows = 32;
-  for (int b = 0; b < kRowBlock; b += kBatchRows) {
-    int32_t col[4];
-    int rr[4];
+#pragma unroll
+  for (int bt = 0; bt < kRowBlock / kBatchRows; ++bt) {
+    int rr[4], rank[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int t = threadIdx.x + 256 * k;
-      rr[k] = t / kCap;
-      const int64_t i = r0 + b + rr[k];
-      const int s = t % kCap;
-      col[k] = (i < S.N && s < S.nnz[i]) ? S.cols[i * kCap + s] : -1;
-      if (col[k] >= 0) atomicOr(&rows[col[k]], 1u << rr[k]);
+      rr[k] = threadIdx.x / kCap + 8 * k;   // row within the batch
+      const int32_t cc = col[4 * bt + k];
+      if (cc >= 0) atomicOr(&rows[cc], 1u << rr[k]);
     }
     __syncthreads();
-    int rank[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      const int32_t cc = col[4 * bt + k];
       rank[k] = -1;
-      if (col[k] >= 0) {
-        const uint32_t m = rows[col[k]];
+      if (cc >= 0) {
+        const uint32_t m = rows[cc];
         rank[k] = __popc(m & ((1u << rr[k]) - 1u));
-        const int64_t i = r0 + b + rr[k];
-        S.csc_slot[cnt[col[k]] + rank[k]] = uint32_t(i * kCap + (threadIdx.x + 256 * k) % kCap);
+        const int64_t i = r0 + bt * kBatchRows + rr[k];
+        S.csc_slot[cnt[cc] + rank[k]] = uint32_t(i * kCap + s);
       }
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      const int32_t cc = col[4 * bt + k];
       if (rank[k] == 0) {   // the batch's first entry of a column advances its counter
-        cnt[col[k]] += __popc(rows[col[k]]);
-        rows[col[k]] = 0u;
+        cnt[cc] += __popc(rows[cc]);
+        rows[cc] = 0u;
       }
     }
     __syncthreads();
@@ -471,8 +542,9 @@ __global__ __launch_bounds__(1024) void k_dw_cols(SparseState S, const float* __
     for (int64_t u0 = beg; u0 < end; u0 += 64) {
       const int64_t u = u0 + lane;
       const bool ok = u < end;
-      const uint32_t slot = ok ? S.csc_slot[u] : 0u;
-      const float x_l = ok ? S.vals[slot] : 0.f;
+      const uint32_t slot = S.csc_slot[ok ? u : beg];   // clamped: loads stay unconditional
+      const float xv_l = S.vals[slot];
+      const float x_l = ok ? xv_l : 0.f;
       const int32_t i_l = int32_t(slot / kCap);
       const int32_t s_l = int32_t(slot % kCap);
       const bool root_l = ok && node_root[i_l] == i_l;
@@ -485,9 +557,8 @@ __global__ __launch_bounds__(1024) void k_dw_cols(SparseState S, const float* __
         for (int v = 0; v < 8; ++v) {
           const int j = j0 + v;
           const int32_t i = __shfl(i_l, j < 64 ? j : 0, 64);
-          x[v] = j < n ? __shfl(x_l, j < 64 ? j : 0, 64) : 0.f;
-          g[v] = j < n ? *reinterpret_cast<const float2*>(dZ1 + int64_t(i) * (2 * H) + 2 * lane)
-                       : make_float2(0.f, 0.f);
+          x[v] = j < n ? __shfl(x_l, j < 64 ? j : 0, 64) : 0.f;   // x = 0 masks the tail
+          g[v] = *reinterpret_cast<const float2*>(dZ1 + int64_t(i) * (2 * H) + 2 * lane);
         }
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
@@ -607,9 +678,11 @@ int sparse_dw2_root_part(SparseState& S, const int32_t* tree_ptr, const float* d
 
 int sparse_csc(SparseState& S, hipStream_t s) {
   const int R = int((S.N + kRowBlock - 1) / kRowBlock);
-  hipLaunchKernelGGL(k_csc_hist, dim3(unsigned(R)), dim3(256), size_t(S.F) * sizeof(int32_t), s, S);
+  hipLaunchKernelGGL(k_csc_hist, dim3(unsigned(R)), dim3(kRowBlock), size_t(S.F) * sizeof(int32_t), s, S);
   BGCN_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_csc_prefix, dim3(grid_for(S.F, 64)), dim3(256), 0, s, S, R);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_csc_colscan, dim3(1), dim3(1024), 0, s, S);
   BGCN_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_csc_place, dim3(unsigned(R)), dim3(256), size_t(2 * S.F) * sizeof(int32_t), s, S);
   BGCN_CHECK_LAUNCH();

@@ -75,7 +75,10 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
       const int32_t ck = __shfl(c_l, src, 64);
       ww[u] = __shfl(w_l, src, 64);
       rr[u] = rk;
-      v[u] = rk >= 0 ? ld4(P.in + int64_t(ck) * P.ld_in + fo) : f4zero();
+      // unconditional gather (ck = 0 for padding entries): a guarded load would compile
+      // to a branch with its own wait and serialise the eight loads
+      const float4 t = ld4(P.in + int64_t(ck) * P.ld_in + fo);
+      v[u] = rk >= 0 ? t : f4zero();
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -208,7 +211,8 @@ __global__ __launch_bounds__(256) void k_spmm_wide(SpmmBatch sb) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int k = k0 + u;
-      v[u] = (k < n && act) ? ld4(P.in + int64_t(s_c[k]) * P.ld_in + fo) : f4zero();
+      const float4 t = ld4(P.in + int64_t(s_c[k < NPG ? k : 0]) * P.ld_in + (act ? fo : 0));
+      v[u] = (k < n && act) ? t : f4zero();
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
