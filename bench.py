@@ -51,6 +51,24 @@ KERNEL_CLASSES = {
              3: "dW2 relu(H1) block MFMA", 5: "dW1 + dW2 root columns over CSC(X)"},
 }
 SPARSE_CAP = 32
+# rocprofv3 kernel symbol of each timed class (for the PMC traffic lookup)
+ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1", ("auto", 2): "bgcn::k_conv2_sparse",
+                 ("auto", 3): "bgcn::k_dw2", ("auto", 5): "bgcn::k_dw_cols",
+                 ("dense", 0): "bgcn::k_gemm_xwt<true, false>", ("dense", 1): "bgcn::k_gemm_tn<true>",
+                 ("dense", 2): "bgcn::k_conv2_fwd", ("dense", 3): "bgcn::k_dw2"}
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_traffic(mode: str, cls: int):
+    """HBM bytes per launch of a kernel class from the committed PMC passes
+    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, same bench workload), or None."""
+    name = ROCPROF_NAMES.get((mode, cls))
+    try:
+        with open(PMC_FILE) as f:
+            k = json.load(f)["kernels"].get(name)
+    except (OSError, ValueError):
+        return None
+    return None if k is None else round(float(k["hbm_bytes"]), 0)
 
 
 def kernel_work(mode: str, cls: int, N: float, Fd: int):
@@ -130,7 +148,7 @@ def main():
     ap.add_argument("--workload", default="twitter15", choices=sorted(WORKLOADS))
     ap.add_argument("--pool", type=int, default=4)
     ap.add_argument("--cpu-trees", type=int, default=32)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--feat-mode", default="auto", choices=["auto", "dense"],
@@ -258,12 +276,12 @@ def main():
                 ach = work / (avg_ms * 1e-3) / 1e12
                 roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
-                        "traffic": None, "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
+                        "traffic": pmc_traffic(mode, c), "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
             else:
                 ach = work / (avg_ms * 1e-3) / 1e9
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(mode, c),
                         "kernel": KERNEL_CLASSES[mode][c], "bytes_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
         value = wl["trees"] * world * steps / dt
