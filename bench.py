@@ -140,6 +140,35 @@ def cpu_baseline(wl, trees: int, steps: int):
                       f"{torch.__version__} on {cpu}, {cores} threads; baseline only"}
 
 
+def aggregation_bench(b, iters: int = 10):
+    """BASELINE north_star's standalone aggregation target: out = A_hat . X at the full
+    5000-dim width (the algebraically equivalent order of GCNConv's propagate; the fused
+    step aggregates 64-wide rows).  Algorithmic bytes:
+    2*N*F*4 + 4*(N+1) + 8*(E+N)  (inputs read once, outputs written once, CSR)."""
+    from bigcn_amd import ops
+    N, Fd = b.x.shape
+    res = {}
+    for name, ei in (("td", b.edge_index), ("bu", b.BU_edge_index)):
+        g = ops.build_graph(ei, N)
+        out = torch.empty(N, Fd, dtype=torch.float32, device=b.x.device)
+        for _ in range(2):
+            ops.spmm(g, b.x, out=out)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(iters):
+            ops.spmm(g, b.x, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        E = int(ei.size(1))
+        nbytes = 2.0 * N * Fd * 4 + 4.0 * (N + 1) + 8.0 * (E + N)
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        res[name] = {"avg_ms": round(ms, 4), "bytes": nbytes, "achieved": round(gbs, 1),
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4)}
+    return {"kernel": "bgcn_spmm F=5000 (A_hat . X), one pool batch", "N": N, "F": Fd, **res}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +185,8 @@ def main():
     ap.add_argument("--path", default="fused", choices=["fused", "autograd"],
                     help="fused: FusedTrainStep (one native call per step); autograd: per-op "
                          "drop-in modules + loss.backward()")
+    ap.add_argument("--aggregation", type=int, default=1,
+                    help="at N=1 also time the standalone 5000-wide aggregation A_hat . X")
     ap.add_argument("--compare-dense", type=int, default=1,
                     help="at N=1 also time the dense MFMA path and report it beside the main line")
     args = ap.parse_args()
@@ -292,6 +323,9 @@ def main():
     dense_res = None
     if world == 1 and args.feat_mode != "dense" and args.compare_dense:
         dense_res = run("dense", max(3, args.steps // 2), 2)
+    agg = None
+    if world == 1 and args.aggregation:
+        agg = aggregation_bench(pool[0])
     if rank == 0:
         value, dt, N_avg = main_res["value"], main_res["dt"], main_res["N_avg"]
         roof, kernels, final_loss = main_res["roof"], main_res["kernels"], main_res["loss"]
@@ -310,6 +344,8 @@ def main():
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "final_loss": round(final_loss, 5),
             "feat_mode": args.feat_mode, "step_path": args.path,
         }
+        if agg is not None:
+            out["aggregation_5000"] = agg
         if dense_res is not None:
             out["dense_path"] = {"value": round(dense_res["value"], 2), "unit": "trees/s",
                                  "ms_per_step": round(dense_res["dt"] / max(3, args.steps // 2) * 1e3, 4),

@@ -602,7 +602,7 @@ static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool 
                        transposed ? v.s_col : v.t_col, transposed ? v.s_w : v.t_w,
                        in + d * H, 2 * H, out + d * H, 2 * H, d == 0 ? bias_td : bias_bu,
                        reinterpret_cast<float*>(reinterpret_cast<char*>(w.spmm_ws) + d * half),
-                       spmm_groups(v.capacity)};
+                       spmm_groups(v.capacity, H)};
   }
   return spmm_batch_impl(sb, 2, s);
 }

@@ -28,7 +28,7 @@ struct SpmmBatch {
 };
 
 int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream);
-int64_t spmm_groups(int64_t capacity);
+int64_t spmm_groups(int64_t capacity, int32_t F);
 size_t spmm_ws_size(int64_t capacity, int32_t F);
 int spmm_impl(const int32_t* ptr, const int32_t* row, const int32_t* col, const float* w,
               int64_t rows, int64_t capacity, const float* in, int64_t ld_in, float* out,

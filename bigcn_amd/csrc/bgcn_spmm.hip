@@ -150,85 +150,65 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
   }
 }
 
-// One lane group per chunk boundary g*NPG (g >= 1): if the row containing entry
-// g*NPG started before it and this is the row's last chunk, sum tail[g0] +
-// head[g0+1..g] (chunk order) and write the row.
-template <int LANES>
-__global__ __launch_bounds__(256) void k_spmm_fixup(SpmmBatch sb) {
-  const SpmmProb& P = sb.p[blockIdx.y];
-  constexpr int GPB = 256 / LANES;
-  const int lane = threadIdx.x % LANES;
-  const int64_t g = int64_t(blockIdx.x) * GPB + threadIdx.x / LANES;
-  if (g < 1 || g >= P.ngroups) return;
-  const int64_t nnz = P.ptr[sb.rows];
-  const int64_t pb = g * NPG;
-  if (pb >= nnz) return;
-  const int32_t r = P.row[pb];
-  const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
-  if (rs >= pb) return;                      // row starts at the boundary: no crossing
-  const int64_t g0 = rs / NPG, g1 = (re - 1) / NPG;
-  if (g1 != g) return;                       // only the row's last chunk does the fixup
-  const int F = sb.F;
-  for (int fo = lane * 4; fo < F; fo += LANES * 4) {
-    float4 acc = ld4(P.part + (g0 * 2 + 1) * int64_t(F) + fo);
-    for (int64_t q = g0 + 1; q <= g1; ++q) acc = f4add(acc, ld4(P.part + (q * 2 + 0) * int64_t(F) + fo));
-    st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(acc, P.bias ? ld4(P.bias + fo) : f4zero(), sb.epi));
-  }
-}
-
-// Wide kernel: block = one chunk of NPG entries, blockIdx.y = 1024-float slice,
-// blockIdx.z = problem.
+// Wide kernel (F > 128, e.g. the 5000-dim A_hat . X): a block = one chunk of NPGW
+// entries x one 1024-float slice of F (blockIdx.y); 256 threads x float4 read every
+// neighbour row slice fully coalesced, kWideDepth rows in flight.  Large chunks keep the partial
+// rows (each F floats) few: a 1500-child BU star root crosses ~6 chunk boundaries.
+constexpr int NPGW = 256;
+constexpr int kWideSlice = 1024;
+constexpr int kWideDepth = 16;  // neighbour rows in flight per thread
 __global__ __launch_bounds__(256) void k_spmm_wide(SpmmBatch sb) {
   const SpmmProb& P = sb.p[blockIdx.z];
-  __shared__ int32_t s_r[NPG], s_c[NPG];
-  __shared__ float s_w[NPG];
+  __shared__ int32_t s_r[NPGW], s_c[NPGW];
+  __shared__ float s_w[NPGW];
   const int64_t g = blockIdx.x;
   if (g >= P.ngroups) return;
   const int64_t nnz = P.ptr[sb.rows];
-  const int64_t p0 = g * NPG;
+  const int64_t p0 = g * NPGW;
   if (p0 >= nnz) return;
-  const int64_t p1 = min<int64_t>(p0 + NPG, nnz);
+  const int64_t p1 = min<int64_t>(p0 + NPGW, nnz);
   const int n = int(p1 - p0);
-  if (threadIdx.x < NPG) {
-    const int64_t p = p0 + threadIdx.x;
-    const bool v = p < p1;
-    s_r[threadIdx.x] = v ? P.row[p] : -1;
-    s_c[threadIdx.x] = v ? P.col[p] : 0;
-    s_w[threadIdx.x] = v ? P.w[p] : 0.f;
+  {
+    const int64_t p = min<int64_t>(p0 + threadIdx.x, nnz - 1);   // clamped, unconditional
+    const int32_t r = P.row[p], c = P.col[p];
+    const float w = P.w[p];
+    const bool v = threadIdx.x < n;
+    s_r[threadIdx.x] = v ? r : -1;
+    s_c[threadIdx.x] = v ? c : 0;
+    s_w[threadIdx.x] = v ? w : 0.f;
   }
-  __syncthreads();
   const int32_t prev_row = p0 > 0 ? P.row[p0 - 1] : -1;
   const int32_t next_row = p1 < nnz ? P.row[p1] : -1;
+  __syncthreads();
   const int F = sb.F;
-  const int fo = blockIdx.y * 1024 + threadIdx.x * 4;
+  const int fo = blockIdx.y * kWideSlice + threadIdx.x * 4;
   const bool act = fo < F;
+  const int foc = act ? fo : 0;
   const float4 bv = (P.bias && act) ? ld4(P.bias + fo) : f4zero();
   float4 acc = f4zero();
   int32_t cur = -1;
   bool cur_head = false;
-  for (int k0 = 0; k0 < n; k0 += 8) {
-    float4 v[8];
+  for (int k0 = 0; k0 < n; k0 += kWideDepth) {
+    float4 v[kWideDepth];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int k = k0 + u;
-      const float4 t = ld4(P.in + int64_t(s_c[k < NPG ? k : 0]) * P.ld_in + (act ? fo : 0));
-      v[u] = (k < n && act) ? t : f4zero();
-    }
+    for (int u = 0; u < kWideDepth; ++u)   // k0 + u < NPGW: padding entries read row 0
+      v[u] = ld4(P.in + int64_t(s_c[k0 + u]) * P.ld_in + foc);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < kWideDepth; ++u) {
       const int k = k0 + u;
-      if (k >= n) break;
-      const int32_t r = s_r[k];
-      if (r != cur) {
-        if (cur >= 0 && act) {
-          if (!cur_head) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
-          else st4(P.part + (g * 2 + 0) * int64_t(F) + fo, acc);
+      const int32_t r = s_r[k];          // -1 past n: padding, skipped
+      if (r >= 0) {
+        if (r != cur) {
+          if (cur >= 0 && act) {
+            if (!cur_head) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+            else st4(P.part + (g * 2 + 0) * int64_t(F) + fo, acc);
+          }
+          cur_head = cur < 0 && r == prev_row;
+          cur = r;
+          acc = f4zero();
         }
-        cur_head = cur < 0 && r == prev_row;
-        cur = r;
-        acc = f4zero();
+        acc = f4fma(s_w[k], v[u], acc);
       }
-      acc = f4fma(s_w[k], v[u], acc);
     }
   }
   if (cur >= 0 && act) {
@@ -239,10 +219,44 @@ __global__ __launch_bounds__(256) void k_spmm_wide(SpmmBatch sb) {
   }
 }
 
+// Wide fixup: one block per (chunk boundary g*NPGW, 1024-float slice): if the row at the
+// boundary started before it and this is its last chunk, sum tail[g0] + head[g0+1..g]
+// in chunk order (four loads in flight) and write the row.
+__global__ __launch_bounds__(256) void k_spmm_fixup_wide(SpmmBatch sb) {
+  const SpmmProb& P = sb.p[blockIdx.z];
+  const int64_t g = int64_t(blockIdx.x) + 1;
+  if (g >= P.ngroups) return;
+  const int64_t nnz = P.ptr[sb.rows];
+  const int64_t pb = g * NPGW;
+  if (pb >= nnz) return;
+  const int32_t r = P.row[pb];
+  if (P.row[pb - 1] != r) return;
+  const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
+  const int64_t g0 = rs / NPGW, g1 = (re - 1) / NPGW;
+  if (g1 != g) return;
+  const int F = sb.F;
+  const int fo = blockIdx.y * kWideSlice + threadIdx.x * 4;
+  if (fo >= F) return;
+  float4 acc = ld4(P.part + (g0 * 2 + 1) * int64_t(F) + fo);
+  int64_t q = g0 + 1;
+  for (; q + 3 <= g1; q += 4) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld4(P.part + ((q + u) * 2 + 0) * int64_t(F) + fo);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = f4add(acc, v[u]);
+  }
+  for (; q <= g1; ++q) acc = f4add(acc, ld4(P.part + (q * 2 + 0) * int64_t(F) + fo));
+  st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(acc, P.bias ? ld4(P.bias + fo) : f4zero(), sb.epi));
+}
+
 }  // namespace
 
+// chunk size of the kernel family spmm_batch_impl picks for width F
+static int npg_for(int32_t F) { return (F == 64 || F == 128) ? NPG : NPGW; }
+
 size_t spmm_ws_size(int64_t capacity, int32_t F) {
-  const int64_t ngroups = (capacity + NPG - 1) / NPG;
+  const int64_t ngroups = (capacity + npg_for(F) - 1) / npg_for(F);
   return size_t(ngroups) * 2 * size_t(F) * sizeof(float) + 256;
 }
 
@@ -279,10 +293,11 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
     if (gmax > 1)
       hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(unsigned(gmax - 1), gy), dim3(256), 0, stream, sb);
   } else {
-    hipLaunchKernelGGL(k_spmm_wide, dim3(unsigned(gmax), unsigned((F + 1023) / 1024), gy), dim3(256),
-                       0, stream, sb);
+    const unsigned slices = unsigned((F + kWideSlice - 1) / kWideSlice);
+    hipLaunchKernelGGL(k_spmm_wide, dim3(unsigned(gmax), slices, gy), dim3(256), 0, stream, sb);
     BGCN_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_spmm_fixup<64>, dim3(grid_for(gmax, 4), gy), dim3(256), 0, stream, sb);
+    if (gmax > 1)
+      hipLaunchKernelGGL(k_spmm_fixup_wide, dim3(unsigned(gmax - 1), slices, gy), dim3(256), 0, stream, sb);
   }
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
@@ -299,11 +314,11 @@ int spmm_impl(const int32_t* ptr, const int32_t* row, const int32_t* col, const 
   sb.F = F;
   sb.epi = epi;
   sb.p[0] = SpmmProb{ptr, row, col, w, in, ld_in, out, ld_out, bias, static_cast<float*>(ws),
-                     (capacity + NPG - 1) / NPG};
+                     (capacity + npg_for(F) - 1) / npg_for(F)};
   return spmm_batch_impl(sb, 1, stream);
 }
 
-int64_t spmm_groups(int64_t capacity) { return (capacity + NPG - 1) / NPG; }
+int64_t spmm_groups(int64_t capacity, int32_t F) { return (capacity + npg_for(F) - 1) / npg_for(F); }
 
 }  // namespace bgcn
 
