@@ -48,12 +48,12 @@ KERNEL_CLASSES = {
     "dense": {0: "conv1 X.W1^T MFMA (TD+BU fused)", 1: "dW1 = dZ1^T X MFMA (TD+BU fused)",
               2: "conv2 A2.W2^T MFMA (generated A2)", 3: "dW2 = dZ2^T A2 MFMA (generated A2)"},
     "auto": {0: "k_compact_conv1: X read + BoW compaction + conv1 gather", 2: "conv2 (sparse root gather)",
-             3: "dW2 relu(H1) block MFMA", 5: "dW1 + dW2 root columns over CSC(X)"},
+             3: "dW2 relu(H1) block MFMA", 5: "dW1 over CSC(X)"},
 }
 SPARSE_CAP = 32
 # rocprofv3 kernel symbol of each timed class (for the PMC traffic lookup)
 ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1", ("auto", 2): "bgcn::k_conv2_sparse",
-                 ("auto", 3): "bgcn::k_dw2", ("auto", 5): "bgcn::k_dw_cols",
+                 ("auto", 3): "bgcn::k_dw2", ("auto", 5): "bgcn::k_dw1_cols",
                  ("dense", 0): "bgcn::k_gemm_xwt<true, false>", ("dense", 1): "bgcn::k_gemm_tn<true>",
                  ("dense", 2): "bgcn::k_conv2_fwd", ("dense", 3): "bgcn::k_dw2"}
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
@@ -81,8 +81,8 @@ def kernel_work(mode: str, cls: int, N: float, Fd: int):
             return "hbm", N * 2 * H * 4.0 * 2
         if cls == 3:   # the relu(H1) block of dW2, both directions, reduction over N
             return "mfma", 2.0 * N * H * H * 2
-        if cls == 5:   # ELL + CSC slots + dZ1 [N,128] read, dW1 + dW2 root columns written
-            return "hbm", N * SPARSE_CAP * 12.0 + N * 2 * H * 4.0 + 4.0 * Fd * (2 * H + 2 * H)
+        if cls == 5:   # ELL + CSC slots + dZ1 [N,128] read once, dW1 [128, F] written
+            return "hbm", N * SPARSE_CAP * 12.0 + N * 2 * H * 4.0 + 4.0 * Fd * 2 * H
         return None, 0.0
     if cls in (0, 1):
         return "mfma", 2.0 * N * Fd * 2 * H

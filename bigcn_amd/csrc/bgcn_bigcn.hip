@@ -24,28 +24,7 @@ constexpr int H = 64;  // hid = out = 64 (BiGCN_Twitter.py:144; the fused path i
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-// ---------------------------------------------------------------- batch index
-// tree_ptr[b] = lower_bound(batch, b) for b in [0, B]; node_root[i] = rootindex[batch[i]].
-__global__ void k_tree_ptr(const int64_t* __restrict__ batch, int64_t N, int64_t B,
-                           int32_t* __restrict__ tree_ptr) {
-  int64_t b = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (b > B) return;
-  int64_t lo = 0, hi = N;
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (batch[mid] < b) lo = mid + 1; else hi = mid;
-  }
-  tree_ptr[b] = int32_t(lo);
-}
-
-__global__ void k_node_root(const int64_t* __restrict__ batch, const int64_t* __restrict__ rootindex,
-                            int64_t N, int64_t B, int32_t* __restrict__ node_root) {
-  int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  int64_t b = batch[i];
-  int64_t r = (b >= 0 && b < B) ? rootindex[b] : 0;
-  node_root[i] = int32_t((r >= 0 && r < N) ? r : 0);
-}
+// (tree_ptr / node_root are built by the forward prologue, k_prologue in bgcn_sparse.hip)
 
 // ---------------------------------------------------------------- conv2 forward
 // Z2[:, d*H:(d+1)*H] = A2_d . W2_d^T with A2_d[i][k] generated on the fly:
@@ -242,7 +221,7 @@ __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_
 
 // dW2_d[o][c] = sum_s part[d][s][o][c] (fixed order) for c < ldp; the dense config
 // reduces all 64+F columns, the sparse config the relu(H1) block (the root columns come
-// from sparse_dw_cols).  A block owns 64 consecutive outputs; its 4 waves take splits
+// from k_dw2_rootcols).  A block owns 64 consecutive outputs; its 4 waves take splits
 // s = q (mod 4), four loads in flight each, combined in wave order: deterministic.
 // Grid-stride over output tiles, so a small grid retires cheaply when the gate skips it.
 __global__ __launch_bounds__(256) void k_reduce_dw2(const float* __restrict__ part, int S,
@@ -282,21 +261,25 @@ __global__ __launch_bounds__(256) void k_reduce_dw2(const float* __restrict__ pa
 
 // ---------------------------------------------------------------- readout
 // head_in[b] = [BU: mean(relu(H2_bu)) | H1_bu[root] , TD: mean(relu(H2_td)) | H1_td[root]]
-// One 1024-thread block per (tree, direction): 64 row slices x 16 lanes x float4, eight
+// One 1024-thread block per tree: per direction 32 row slices x 16 lanes x float4, eight
 // independent row loads in flight per slice, then a fixed-order two-level LDS reduction
 // (deterministic).  The root half is the mean of identical copies, i.e. H1[root] itself
 // (the reference's root_extend is a detached copy, BiGCN_Twitter.py:42-47, so it has no
-// backward).
-constexpr int kReadSlices = 64;
+// backward).  With hd.W set (bgcn_train_step) wave 0 then runs the classifier head on
+// the tree's row (head_row): fc, log_softmax, NLL term, dz and dhead.
+constexpr int kReadSlices = 32;
 __global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ H1,
                                                       const float* __restrict__ H2,
                                                       const int32_t* __restrict__ tree_ptr,
                                                       const int64_t* __restrict__ rootindex,
-                                                      int64_t N, float* __restrict__ head) {
-  __shared__ float4 red[kReadSlices][16];
-  __shared__ float4 red2[8][16];
-  const int b = blockIdx.x, d = blockIdx.y;
-  const int lane = threadIdx.x & 15, slice = threadIdx.x >> 4;
+                                                      int64_t N, int64_t B, float* __restrict__ head,
+                                                      HeadArgs hd) {
+  __shared__ float4 red[2][kReadSlices][16];
+  __shared__ float4 red2[2][4][16];
+  __shared__ float4 hrow[4 * H / 4];
+  const int b = blockIdx.x;
+  const int d = threadIdx.x >> 9, t = threadIdx.x & 511;
+  const int lane = t & 15, slice = t >> 4;
   const int64_t beg = tree_ptr[b], end = tree_ptr[b + 1];
   const float* src = H2 + d * H + lane * 4;
   float4 s = f4zero();
@@ -309,30 +292,35 @@ __global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ 
     for (int u = 0; u < 8; ++u) s = f4add(s, f4relu(v[u]));
   }
   for (; i < end; i += kReadSlices) s = f4add(s, f4relu(ld4(src + i * (2 * H))));
-  red[slice][lane] = s;
+  red[d][slice][lane] = s;
   __syncthreads();
-  if (threadIdx.x < 128) {
-    const int g = threadIdx.x >> 4;
-    float4 acc = red[g * 8][lane];
+  if (t < 64) {
+    const int g = t >> 4;
+    float4 acc = red[d][g * 8][lane];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) acc = f4add(acc, red[g * 8 + q][lane]);
-    red2[g][lane] = acc;
+    for (int q = 1; q < 8; ++q) acc = f4add(acc, red[d][g * 8 + q][lane]);
+    red2[d][g][lane] = acc;
   }
   __syncthreads();
   const int base = (d == 1 ? 0 : 2 * H) + lane * 4;  // BU first (:128)
-  if (threadIdx.x < 16) {
-    float4 acc = red2[0][lane];
+  if (t < 16) {
+    float4 acc = red2[d][0][lane];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) acc = f4add(acc, red2[q][lane]);
+    for (int q = 1; q < 4; ++q) acc = f4add(acc, red2[d][q][lane]);
     const float cnt = float(end - beg > 0 ? end - beg : 1);
     acc = make_float4(acc.x / cnt, acc.y / cnt, acc.z / cnt, acc.w / cnt);
     st4(head + int64_t(b) * (4 * H) + base, acc);
-  } else if (threadIdx.x < 32) {
+    hrow[base / 4] = acc;
+  } else if (t < 32) {
     const int64_t root = rootindex[b];
     const float4 hr = (end > beg && root >= 0 && root < N)
                           ? ld4(H1 + root * (2 * H) + d * H + lane * 4) : f4zero();
     st4(head + int64_t(b) * (4 * H) + base + H, hr);
+    hrow[(base + H) / 4] = hr;
   }
+  if (hd.W == nullptr) return;
+  __syncthreads();
+  if (threadIdx.x < 64) head_row(hd, b, B, hrow[threadIdx.x]);
 }
 
 // dH2[i][d*H + f] = dhead[b(i)][r1 block of d][f] / cnt_b * [H2 > 0]; block partial
@@ -406,27 +394,37 @@ __global__ __launch_bounds__(256) void k_dh1(const float* __restrict__ dZ2,
                                              const float* __restrict__ W2bu, int64_t ldw2,
                                              int64_t N, KeepSrc keep,
                                              float* __restrict__ dH1, float* __restrict__ colpart) {
+  // dZ2 tile (64 rows x 64) and W2[:, :64] staged in LDS with coalesced float4 loads
+  // (a direct per-lane operand load touches 64 cache lines per instruction); rows are
+  // padded to 65 floats so the MFMA operand reads are bank-conflict free.
+  __shared__ float Ds[kDh1Rows * (H + 1)];
+  __shared__ float Ws[H * (H + 1)];
   __shared__ float red[2][H];
   const int d = blockIdx.y;
   const float* W2 = d == 0 ? W2td : W2bu;
   const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int rh = wid & 1, ch = wid >> 1;
   const int r = l & 31, h = l >> 5;
-  const int64_t row0 = int64_t(blockIdx.x) * kDh1Rows + rh * 32;
+  const int64_t blk0 = int64_t(blockIdx.x) * kDh1Rows;
+  const int64_t row0 = blk0 + rh * 32;
   const int c = ch * 32 + r;  // output column of this lane (within H)
-
-  // Every load is unconditional from a clamped (in-bounds) row: rows past N compute
-  // values that are never stored, and the loads stay independent (a guarded load
-  // compiles to a branch with its own wait).
-  float a[32], bv[32];
-  const int64_t ia = min<int64_t>(row0 + r, N - 1);
+  {
+    float4 dv[4], wv[4];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const float4 v = ld4(dZ2 + ia * (2 * H) + d * H + 32 * h + 4 * q);
-    a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+    for (int u = 0; u < 4; ++u) {   // element e = tid + 256u of a 64 x 16 float4 grid
+      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
+      dv[u] = ld4(dZ2 + min<int64_t>(blk0 + rr, N - 1) * (2 * H) + d * H + q);
+      wv[u] = ld4(W2 + int64_t(rr) * ldw2 + q);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
+      float* dd = &Ds[rr * (H + 1) + q];
+      dd[0] = dv[u].x; dd[1] = dv[u].y; dd[2] = dv[u].z; dd[3] = dv[u].w;
+      float* ww = &Ws[rr * (H + 1) + q];
+      ww[0] = wv[u].x; ww[1] = wv[u].y; ww[2] = wv[u].z; ww[3] = wv[u].w;
+    }
   }
-#pragma unroll
-  for (int kk = 0; kk < 32; ++kk) bv[kk] = W2[int64_t(32 * h + kk) * ldw2 + c];
   float hv[16];
   uint32_t wd[16];
 #pragma unroll
@@ -435,9 +433,13 @@ __global__ __launch_bounds__(256) void k_dh1(const float* __restrict__ dZ2,
     hv[q] = H1[i * (2 * H) + d * H + c];
     wd[q] = keep.get(uint32_t(d), uint32_t(i), uint32_t(c >> 5));
   }
+  __syncthreads();
+  // lane half h owns k in [32h, 32h + 32) (permuted K, same for A and B)
+  const float* ap = &Ds[(rh * 32 + r) * (H + 1) + 32 * h];
+  const float* bp = &Ws[(32 * h) * (H + 1) + c];
   f32x16 acc = {};
 #pragma unroll
-  for (int kk = 0; kk < 32; ++kk) acc = mfma32x32x2(a[kk], bv[kk], acc);
+  for (int kk = 0; kk < 32; ++kk) acc = mfma32x32x2(ap[kk], bp[kk * (H + 1)], acc);
 
   const float sc = keep.scale();
   float cs = 0.f;
@@ -493,7 +495,8 @@ __global__ void k_keep_words(uint64_t seed, int64_t N, int nw, uint32_t* __restr
 struct FusedWs {
   int32_t* node_root;
   float *z1, *z2, *d2, *dz2, *dh1, *dz1;  // [N, 2H]
-  float* colpart;                         // [nblk, 2H]
+  float* colpart;                         // [nblk, 2H] db1 partials (k_dh1)
+  float* colpart2;                        // [nblk, 2H] db2 partials (k_readout_bwd)
   float* spmm_ws; size_t spmm_bytes;
   float* dw2_part;                        // [2][S2][H][H+F]
   float* tn_ws; size_t tn_bytes;
@@ -524,6 +527,7 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   const int64_t nblk = std::max((N + kDh1Rows - 1) / kDh1Rows,
                                  (N + kReadBwdRows - 1) / kReadBwdRows);
   t.colpart = c.take<float>(size_t(nblk) * 2 * H);
+  t.colpart2 = c.take<float>(size_t(nblk) * 2 * H);
   t.S2 = dw2_splits(N, F);
   int64_t kc = (N + t.S2 - 1) / t.S2;
   kc = (kc + BK - 1) / BK * BK;
@@ -637,9 +641,10 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
 // is built on the auxiliary lane right after conv1's lin, overlapped with the
 // latency-bound second half of the forward, and joined before returning.  graph_lane
 // >= 0: the caller is building the TD/BU graphs on that lane (bgcn_train_step), joined
-// just before their first use.
+// just before their first use.  head (bgcn_train_step): classifier head fused into the
+// readout.
 int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
-                       int graph_lane) {
+                       int graph_lane, const HeadArgs* head) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->head_in && a->td_w1 && a->bu_w1 && a->td_w2 && a->bu_w2, "null pointer");
   const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
@@ -650,28 +655,30 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
   KeepSrc keep = make_keep(a);
   const bool sparse = sp.mode != 1;
 
-  if (sparse) BGCN_CHECK_HIP(hipMemsetAsync(a->x_flags, 0, 8 * sizeof(int32_t), s));
-  hipLaunchKernelGGL(k_tree_ptr, dim3(grid_for(B + 1, 256)), dim3(256), 0, s, a->batch, N, B,
-                     a->tree_ptr);
-  BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_node_root, dim3(grid_for(N, 256)), dim3(256), 0, s, a->batch,
-                     a->rootindex, N, B, w.node_root);
-  BGCN_CHECK_LAUNCH();
+  // one prologue launch: weight transposes, node -> root map, tree pointers, flag reset
+  BGCN_TRY(sparse_prologue(sp, a, w.node_root, s));
+  // tree work items (conv2 / dW2 root partials) on the side lane, beside the pass over X
+  bool side_busy = graph_lane >= 0;
+  if (sparse) {
+    hipStream_t xi;
+    BGCN_TRY(aux_fork(s, kLaneSide, &xi));
+    BGCN_TRY(sparse_items(sp, a->tree_ptr, xi));
+    side_busy = side_busy || xi != s;
+  }
   // conv1 lin, TD and BU in one pass over X: sparse (compaction + gather) or dense MFMA
+  // (the conv1 of feat_mode dense; in auto mode a device-gated fallback)
   bool forked = false;
   if (sparse) {
-    BGCN_TRY(sparse_transpose(sp, a, s));
     timing_begin(0, s);
     BGCN_TRY(sparse_compact_conv1(sp, a->x, a->ldx, w.z1, s));
     timing_end(0, s);
-    BGCN_TRY(sparse_items(sp, a->tree_ptr, s));
   }
   timing_begin(sparse ? 4 : 0, s);
   BGCN_TRY(gemm_xwt_impl(a->x, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F, s, gate));
   timing_end(sparse ? 4 : 0, s);
-  // the graphs (built on graph_lane by bgcn_train_step) are needed from here on; the
-  // join comes before the CSC fork so that it never waits for the CSC
-  if (graph_lane >= 0) BGCN_TRY(aux_join(s, graph_lane));
+  // the graphs (built on graph_lane by bgcn_train_step) and the items are needed from
+  // here on; the join comes before the CSC fork so that it never waits for the CSC
+  if (side_busy) BGCN_TRY(aux_join(s, kLaneSide));
   if (sparse && a->save_for_backward) {
     hipStream_t x;
     BGCN_TRY(aux_fork(s, kLaneSide, &x));
@@ -688,16 +695,17 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
   BGCN_CHECK_LAUNCH();
   timing_end(2, s);
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z2, a->h2, a->td_b2, a->bu_b2, BGCN_EPI_NONE, w, s));
-  hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B), 2), dim3(1024), 0, s, a->h1, a->h2,
-                     a->tree_ptr, a->rootindex, N, a->head_in);
+  const HeadArgs no_head{};
+  hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B)), dim3(1024), 0, s, a->h1, a->h2,
+                     a->tree_ptr, a->rootindex, N, B, a->head_in, head ? *head : no_head);
   BGCN_CHECK_LAUNCH();
   if (forked) BGCN_TRY(aux_join(s, kLaneSide));
   return BGCN_OK;
 }
 
-// Backward, given the forward's workspace.  After dZ2 the step splits into two
-// independent chains: dW2 (auxiliary stream) and dH1 -> dZ1 (main stream); they join
-// before the pass over the CSC of X that writes dW1 and the dW2 root columns.
+// Backward, given the forward's workspace.  Main stream: readout' -> dZ2 -> dH1 -> dZ1
+// -> dW1.  Side lane, forked as soon as its inputs exist: db2, the dW2 chain (relu(H1)
+// block, root partials, root columns), db1 and the gated dense dW1; joined at the end.
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->dhead_in && a->td_dw1 && a->bu_dw1 && a->td_dw2 && a->bu_dw2 && a->td_db1 &&
@@ -710,22 +718,22 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate));
   KeepSrc keep = make_keep(a);
   const bool sparse = sp.mode != 1;
+  hipStream_t x;
 
-  // readout + relu' -> dH2, db2
+  // readout + relu' -> dH2; db2 on the side lane
   const int64_t nblk_r = (N + kReadBwdRows - 1) / kReadBwdRows;
   hipLaunchKernelGGL(k_readout_bwd, dim3(unsigned(nblk_r)), dim3(256), 0, s, a->dhead_in, a->h2,
-                     a->batch, a->tree_ptr, N, B, w.d2, w.colpart);
+                     a->batch, a->tree_ptr, N, B, w.d2, w.colpart2);
   BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, s, w.colpart, int(nblk_r), a->td_db2,
-                     a->bu_db2);
+  BGCN_TRY(aux_fork(s, kLaneSide, &x));
+  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, x, w.colpart2, int(nblk_r),
+                     a->td_db2, a->bu_db2);
   BGCN_CHECK_LAUNCH();
   // dZ2 = A^T dH2
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.d2, w.dz2, nullptr, nullptr, BGCN_EPI_NONE, w, s));
 
-  // ---- auxiliary chain: dW2 (both directions, generated A2 operand).  The relu(H1)
-  // columns always by MFMA; the X[root] columns by MFMA (dense) or from the root
-  // non-zeros (sparse, finished in sparse_dw_cols below).
-  hipStream_t x;
+  // ---- side: dW2 (both directions, generated A2 operand).  The relu(H1) columns by
+  // MFMA; the X[root] columns by MFMA (dense) or from the root non-zeros (sparse)
   BGCN_TRY(aux_fork(s, kLaneSide, &x));
   timing_begin(3, x);
   hipLaunchKernelGGL(k_dw2, dim3(grid_for(H + F, 64), w.S2, 2), dim3(256), 0, x, a->x, a->ldx, F,
@@ -746,27 +754,31 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     BGCN_CHECK_LAUNCH();
     BGCN_TRY(sparse_dw2_root_part(sp, a->tree_ptr, w.dz2, x));
     if (!a->save_for_backward) BGCN_TRY(sparse_csc(sp, x));
+    BGCN_TRY(sparse_dw2_rootcols(sp, a, w.node_root, keep, x));
   }
 
-  // ---- main chain: dH1 through dropout and relu, db1, dZ1 = A^T dH1
+  // ---- main: dH1 through dropout and relu (db1 partials), dZ1 = A^T dH1
   const int64_t nblk_h = (N + kDh1Rows - 1) / kDh1Rows;
   hipLaunchKernelGGL(k_dh1, dim3(unsigned(nblk_h), 2), dim3(256), 0, s, w.dz2, a->h1, a->td_w2,
                      a->bu_w2, H + F, N, keep, w.dh1, w.colpart);
   BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, s, w.colpart, int(nblk_h), a->td_db1,
+  BGCN_TRY(aux_fork(s, kLaneSide, &x));
+  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, x, w.colpart, int(nblk_h), a->td_db1,
                      a->bu_db1);
   BGCN_CHECK_LAUNCH();
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.dh1, w.dz1, nullptr, nullptr, BGCN_EPI_NONE, w, s));
-  BGCN_TRY(aux_join(s, kLaneSide));
-  // dW1 = [dZ1_td | dZ1_bu]^T X  (one pass over X for both directions) - dense MFMA, or
-  // over the column-sorted non-zeros of X together with the dW2 root columns
+  // dW1 = [dZ1_td | dZ1_bu]^T X (one pass over X for both directions): over the CSC of X
+  // (sparse, main) or the dense MFMA GEMM (dense mode on main; gated fallback on the side)
   if (sparse) {
+    BGCN_TRY(aux_fork(s, kLaneSide, &x));
+    if (!a->save_for_backward) BGCN_TRY(aux_join(s, kLaneSide));   // CSC built on the side
     timing_begin(5, s);
-    BGCN_TRY(sparse_dw_cols(sp, a, w.dz1, w.node_root, keep, s));
+    BGCN_TRY(sparse_dw1(sp, a, w.dz1, s));
     timing_end(5, s);
   }
   BGCN_TRY(gemm_tn_impl(w.dz1, 2 * H, a->x, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F, N,
-                        w.tn_ws, w.tn_bytes, s, sparse ? 6 : 1, gate));
+                        w.tn_ws, w.tn_bytes, sparse ? x : s, sparse ? 6 : 1, gate));
+  BGCN_TRY(aux_join(s, kLaneSide));
   return BGCN_OK;
 }
 

@@ -46,10 +46,76 @@ int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float
 size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K);
 int tn_splits(int64_t Mc, int64_t Nc, int64_t K);
 
+// ---- classifier head fc -> log_softmax -> NLL (BiGCN_Twitter.py:129-130,186) and its
+// row-local backward; evaluated per tree by one wave (shared by k_readout_fwd's fused
+// form and bgcn_step.hip)
+constexpr int kHeadIn = 256;       // cat(BU_x, TD_x)
+constexpr int kMaxClasses = 16;
+struct HeadArgs {
+  const float* W;        // [C, 256] (nullptr: no head)
+  const float* bias;     // [C]
+  const int64_t* y;      // [B]
+  int C;
+  float* logp;           // [B, C] or nullptr
+  float* dz;             // [B, C] dLoss/dlogits
+  float* loss_row;       // [B]
+  float* dhead;          // [B, 256]
+  int32_t* status;       // bit 1: label out of range
+};
+
+// One wave, row b of the head: h = head_in[b][4l .. 4l+3] held by lane l.
+//   z = h W^T + bias ; logp = z - logsumexp(z) ; loss_row = -logp[y] ;
+//   dz = (softmax - onehot(y)) / B ; dhead = dz W.  Dot products butterfly-reduced.
+__device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4 h) {
+  const int l = threadIdx.x & 63;
+  const int C = hd.C;
+  float z[kMaxClasses];
+#pragma unroll
+  for (int c = 0; c < kMaxClasses; ++c) {
+    z[c] = 0.f;
+    if (c < C) {  // C is uniform: the shuffles stay convergent
+      const float4 w = ld4(hd.W + int64_t(c) * kHeadIn + 4 * l);
+      float p = fmaf(h.x, w.x, fmaf(h.y, w.y, fmaf(h.z, w.z, h.w * w.w)));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
+      z[c] = p + hd.bias[c];
+    }
+  }
+  float m = z[0];
+#pragma unroll
+  for (int c = 1; c < kMaxClasses; ++c)
+    if (c < C) m = fmaxf(m, z[c]);
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < kMaxClasses; ++c)
+    if (c < C) se += expf(z[c] - m);
+  const float lse = m + logf(se);
+  const int64_t yb = hd.y[b];
+  const bool yok = yb >= 0 && yb < C;
+  if (!yok && l == 0 && hd.status) atomicOr(hd.status, 2);
+  const float inv_b = 1.0f / float(B);
+  float4 dh = f4zero();
+#pragma unroll
+  for (int c = 0; c < kMaxClasses; ++c) {
+    if (c < C) {
+      const float lp = z[c] - lse;
+      const float g = yok ? (expf(lp) - (c == yb ? 1.f : 0.f)) * inv_b : 0.f;
+      if (l == 0) {
+        if (hd.logp) hd.logp[b * C + c] = lp;
+        hd.dz[b * C + c] = g;
+        if (c == yb) hd.loss_row[b] = -lp;
+      }
+      dh = f4fma(g, ld4(hd.W + int64_t(c) * kHeadIn + 4 * l), dh);
+    }
+  }
+  if (l == 0 && !yok) hd.loss_row[b] = 0.f;
+  st4(hd.dhead + b * kHeadIn + 4 * l, dh);
+}
+
 // ---- fused encoder (bgcn_bigcn.hip); graph_lane: see bigcn_forward_impl
 size_t bigcn_ws_size(int64_t N, int64_t B, int64_t F, int64_t hid);
 int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
-                       int graph_lane);
+                       int graph_lane, const HeadArgs* head = nullptr);
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s);
 
 // ---- one training step (bgcn_step.hip)

@@ -27,20 +27,23 @@ struct SparseState {
   int32_t *col_start, *col_end;  // [F]
   uint32_t* csc_slot;   // [N*kCap] slots (i*kCap + s) grouped by column, rows in order
   uint32_t* rbits;      // [2][N] forward's root keep masks (bit s: root non-zero s kept)
+  float* csc_val;       // [N*kCap] X value of each csc_slot entry
 };
 
 constexpr int kRowBlock = 256;          // rows per block of the CSC counting sort
 constexpr int64_t kSparseMaxF = 16384;  // LDS bound of the CSC kernels (2 x 4 B x F)
 
 size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S);
-int sparse_transpose(SparseState& S, const bgcn_bigcn_args* a, hipStream_t s);
+// forward prologue: weight transposes (sparse path), node_root, tree_ptr, flag reset
+int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root, hipStream_t s);
 int sparse_compact_conv1(SparseState& S, const float* X, int64_t ldx, float* Z1, hipStream_t s);
 int sparse_items(SparseState& S, const int32_t* tree_ptr, hipStream_t s);
 int sparse_conv2(SparseState& S, const float* H1, const int32_t* tree_ptr, const int64_t* rootindex,
                  float* Z2, KeepSrc keep, hipStream_t s);
 int sparse_csc(SparseState& S, hipStream_t s);
 int sparse_dw2_root_part(SparseState& S, const int32_t* tree_ptr, const float* dZ2, hipStream_t s);
-int sparse_dw_cols(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1,
-                   const int32_t* node_root, KeepSrc keep, hipStream_t s);
+int sparse_dw1(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1, hipStream_t s);
+int sparse_dw2_rootcols(SparseState& S, const bgcn_bigcn_args* a, const int32_t* node_root,
+                        KeepSrc keep, hipStream_t s);
 
 }  // namespace bgcn

@@ -31,17 +31,16 @@ __device__ __forceinline__ bool use_sparse(const SparseState& S) { return S.mode
 // ---------------------------------------------------------------- weight transposes
 // W1T[c][d*64 + o] = W1_d[o][c] (c < F) and W2T_d[k][o] = W2_d[o][k] (k < 64+F):
 // 32 x 32 tiles through LDS; blockIdx.z: 0/1 = W1 td/bu, 2/3 = W2 td/bu.
-__global__ __launch_bounds__(256) void k_transpose_weights(SparseState S, const float* __restrict__ w1td,
-                                                           const float* __restrict__ w1bu,
-                                                           const float* __restrict__ w2td,
-                                                           const float* __restrict__ w2bu) {
-  if (!use_sparse(S)) return;
+__device__ __forceinline__ void transpose_tile(const SparseState& S, int bx, int by, int z,
+                                               const float* __restrict__ w1td,
+                                               const float* __restrict__ w1bu,
+                                               const float* __restrict__ w2td,
+                                               const float* __restrict__ w2bu) {
   __shared__ float tile[32][33];
-  const int z = blockIdx.z;
   const int64_t K = z < 2 ? S.F : S.F + H;
   const float* src = z == 0 ? w1td : z == 1 ? w1bu : z == 2 ? w2td : w2bu;
-  const int64_t k0 = int64_t(blockIdx.x) * 32;
-  const int o0 = blockIdx.y * 32;
+  const int64_t k0 = int64_t(bx) * 32;
+  const int o0 = by * 32;
   if (k0 >= K) return;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
   for (int r = ty; r < 32; r += 8) {
@@ -55,6 +54,44 @@ __global__ __launch_bounds__(256) void k_transpose_weights(SparseState S, const 
     if (z < 2) S.w1t[k * (2 * H) + z * H + o0 + tx] = tile[tx][r];
     else S.w2t[(int64_t(z - 2) * K + k) * H + o0 + tx] = tile[tx][r];
   }
+}
+
+// Forward prologue, one launch: the weight transposes (sparse path), node -> root map,
+// tree pointers (binary search in the sorted batch vector) and the overflow-flag reset.
+// Block ranges: [0, nT) transposes, [nT, nT + nR) node_root, then tree_ptr.
+__global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __restrict__ w1td,
+                                                  const float* __restrict__ w1bu,
+                                                  const float* __restrict__ w2td,
+                                                  const float* __restrict__ w2bu,
+                                                  const int64_t* __restrict__ batch,
+                                                  const int64_t* __restrict__ rootindex,
+                                                  int32_t* __restrict__ node_root,
+                                                  int32_t* __restrict__ tree_ptr, int nTx, int nT,
+                                                  int nR) {
+  const int blk = blockIdx.x;
+  if (blk < nT) {
+    if (S.mode == 1) return;
+    if (blk == 0 && threadIdx.x < 8) S.flags[threadIdx.x] = 0;
+    transpose_tile(S, blk % nTx, (blk / nTx) % 2, blk / (2 * nTx), w1td, w1bu, w2td, w2bu);
+    return;
+  }
+  if (blk < nT + nR) {
+    const int64_t i = int64_t(blk - nT) * 256 + threadIdx.x;
+    if (i >= S.N) return;
+    const int64_t b = batch[i];
+    const int64_t bc = b < 0 ? 0 : (b >= S.B ? S.B - 1 : b);
+    const int64_t r = rootindex[bc];
+    node_root[i] = int32_t((b >= 0 && b < S.B && r >= 0 && r < S.N) ? r : 0);
+    return;
+  }
+  const int64_t b = int64_t(blk - nT - nR) * 256 + threadIdx.x;
+  if (b > S.B) return;
+  int64_t lo = 0, hi = S.N;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (batch[mid] < b) lo = mid + 1; else hi = mid;
+  }
+  tree_ptr[b] = int32_t(lo);
 }
 
 // ---------------------------------------------------------------- X compaction + conv1
@@ -142,14 +179,17 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const floa
 // conv2 lin on the sparse path, one work item (<= kChunk nodes of one tree) per block:
 //   Z2_d[i] = [keep * 2 relu(H1_d[i]) | kept_d(i, s)] . [W2_d^T[0:64] ; Wr_b]
 //   Wr_b[s] = 2 relu(x_root,col_s) W2_d^T[64 + col_s]      (s < nnz(root), else 0)
-// i.e. one [nodes x 96] x [96 x 64] product on the fp32 MFMA per item, with the
-// dropout-masked relu(H1) and the per-node root keep bits (0/1) generated in registers
-// and the tree's root block of W2^T staged in LDS.  The root keep masks are stored in
-// S.rbits for the dW2 root columns of the backward.  K order is permuted per lane half
-// (half h owns k in [48h, 48h + 48)), B rows padded to 66 floats so the two halves read
-// disjoint LDS banks.
-constexpr int kC2K = 2 * H / 4 * 3;  // 96 = 64 relu(H1) columns + 32 root slots
-constexpr int kC2Ld = H + 2;
+// i.e. one [nodes x (64 + nnz(root))] x [. x 64] product on the fp32 MFMA per item, with
+// the dropout-masked relu(H1) and the per-node root keep bits (0/1) generated in
+// registers and the tree's root block of W2^T staged in LDS.  The root keep masks are
+// stored in S.rbits for the dW2 root columns of the backward.  Each wave stages its
+// 32-row H1 tile through LDS (coalesced).  K order per lane half h: H1 columns
+// [32h, 32h+32), then root slots 2j + h (so each lane hashes only its own slots and the
+// steps past the root's non-zeros are skipped); B rows 32 apart for the two halves with
+// an odd row stride (bank-conflict free).
+constexpr int kC2Ld = H + 1;         // odd row stride: rows 32 apart hit disjoint banks
+constexpr int kC2Slot0 = H;          // slot rows: even slots at 64 + s/2, odd at 96 + s/2
+constexpr int kC2Rows = H + 2 * (kCap / 2) + 16;   // 112 (rows 80..95 unused padding)
 __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float* __restrict__ H1,
                                                       const int32_t* __restrict__ tree_ptr,
                                                       const int64_t* __restrict__ rootindex,
@@ -157,7 +197,8 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   if (!use_sparse(S)) return;
   const int item = blockIdx.x;
   if (item >= S.tree_item0[S.B]) return;
-  __shared__ float Bs[kC2K * kC2Ld];
+  __shared__ float Bs[kC2Rows * kC2Ld];
+  __shared__ float Hs[4 * 32 * kC2Ld];
   __shared__ uint32_t rk[kCap];
   const int d = blockIdx.y;
   const int b = S.item_tree[item];
@@ -165,6 +206,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   const int64_t end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
   const int64_t r = rootindex[b];
   const int rn = S.nnz[r];
+  const int mh = (rn + 1) / 2;   // root slot steps per lane half
   const float sc = keep.scale();
   const int64_t K2 = S.F + H;
   const float* w2t = S.w2t + int64_t(d) * K2 * H;
@@ -184,50 +226,72 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
     const float val = S.vals[slot];
     const float4 w = ld4(w2t + int64_t(H + col) * H + q);
     const float av = s < rn ? sc * fmaxf(val, 0.f) : 0.f;
-    float* dst = &Bs[(H + s) * kC2Ld + q];
+    float* dst = &Bs[(kC2Slot0 + (s & 1) * 32 + (s >> 1)) * kC2Ld + q];
     dst[0] = av * w.x; dst[1] = av * w.y; dst[2] = av * w.z; dst[3] = av * w.w;
   }
   __syncthreads();
 
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
+  float* hs = &Hs[wv * 32 * kC2Ld];   // this wave's staged 32 x 64 H1 tile
   for (int t = wv; t < kChunk / 32; t += 4) {
     const int64_t i0 = beg + 32 * t;
     if (i0 >= end) break;
     const int64_t i = i0 + r32;
     const bool ok = i < end;
-    const float* hrow = H1 + (ok ? i : beg) * (2 * H) + d * H;
-    const uint32_t w0 = keep.get(uint32_t(d), uint32_t(ok ? i : beg), 0u);
-    const uint32_t w1 = keep.get(uint32_t(d), uint32_t(ok ? i : beg), 1u);
-    // lane half h supplies k = 48h + kk: H1 columns [48h, 64) then (h = 1) the 32 root
-    // slots.  Both halves run the same straight-line code (clamped column, selects).
+    {   // coalesced staging: 8 x 1 KiB per wave instead of 32 scattered rows per load
+      float4 hv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = l + 64 * u, rr = e >> 4, q = (e & 15) * 4;
+        hv[u] = ld4(H1 + min<int64_t>(i0 + rr, end - 1) * (2 * H) + d * H + q);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = l + 64 * u, rr = e >> 4, q = (e & 15) * 4;
+        float* dst = &hs[rr * kC2Ld + q];
+        dst[0] = hv[u].x; dst[1] = hv[u].y; dst[2] = hv[u].z; dst[3] = hv[u].w;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+    }
+    const float* hrow = &hs[r32 * kC2Ld + 32 * h];
+    const uint32_t ni = uint32_t(ok ? i : beg);
+    // K order (lane half h): kk < 32 -> H1 column 32h + kk (keep word h); kk >= 32 ->
+    // root slot 2(kk - 32) + h.  Each lane hashes only its own slots, and the steps past
+    // the root's non-zeros (uniform per block) are skipped.
+    const uint32_t wd = keep.get(uint32_t(d), ni, uint32_t(h));
     float a[48];
 #pragma unroll
-    for (int q = 0; q < 12; ++q) {
-      const int col = min(48 * h + 4 * q, H - 4);
-      const float4 v = ld4(hrow + col);
-      const float ve[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = 48 * h + 4 * q + e;
-        const uint32_t bit = k < 32 ? (w0 >> (k & 31)) & 1u : (w1 >> (k & 31)) & 1u;
-        a[4 * q + e] = bit ? sc * fmaxf(ve[e], 0.f) : 0.f;   // used when k < 64
-      }
-    }
+    for (int kk = 0; kk < 32; ++kk)
+      a[kk] = ((wd >> kk) & 1u) ? sc * fmaxf(hrow[kk], 0.f) : 0.f;
     uint32_t m = 0;
 #pragma unroll
-    for (int s = 0; s < kCap; ++s) {
-      const uint32_t k = rk[s];
-      const uint32_t bit = (s < rn) ? (keep.get(uint32_t(d), uint32_t(ok ? i : beg), k >> 5) >> (k & 31)) & 1u : 0u;
-      m |= bit << s;
-      if (h == 1) a[16 + s] = bit ? 1.f : 0.f;
+    for (int j = 0; j < kCap / 2; ++j) {
+      uint32_t bit = 0;
+      if (j < mh) {
+        const int sl = 2 * j + h;
+        const uint32_t k = rk[sl];
+        bit = sl < rn ? (keep.get(uint32_t(d), ni, k >> 5) >> (k & 31)) & 1u : 0u;
+      }
+      m |= bit << (2 * j + h);
+      a[32 + j] = bit ? 1.f : 0.f;
     }
-    if (h == 1 && ok) S.rbits[int64_t(d) * S.N + i] = m;
+    m |= __shfl_xor(m, 32);
+    if (h == 0 && ok) S.rbits[int64_t(d) * S.N + i] = m;
     f32x16 acc0 = {}, acc1 = {};
-    const float* bp = &Bs[(48 * h) * kC2Ld + r32];
+    const float* bp = &Bs[(32 * h) * kC2Ld + r32];            // rows 32h + kk
+    const float* bq = &Bs[(kC2Slot0 + 32 * h) * kC2Ld + r32];  // slot rows of this half
 #pragma unroll
-    for (int kk = 0; kk < 48; ++kk) {
+    for (int kk = 0; kk < 32; ++kk) {
       acc0 = mfma32x32x2(a[kk], bp[kk * kC2Ld], acc0);
       acc1 = mfma32x32x2(a[kk], bp[kk * kC2Ld + 32], acc1);
+    }
+#pragma unroll
+    for (int j = 0; j < kCap / 2; ++j) {
+      if (j < mh) {
+        acc0 = mfma32x32x2(a[32 + j], bq[j * kC2Ld], acc0);
+        acc1 = mfma32x32x2(a[32 + j], bq[j * kC2Ld + 32], acc1);
+      }
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -504,6 +568,7 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
         rank[k] = __popc(m & ((1u << rr[k]) - 1u));
         const int64_t i = r0 + bt * kBatchRows + rr[k];
         S.csc_slot[cnt[cc] + rank[k]] = uint32_t(i * kCap + s);
+        S.csc_val[cnt[cc] + rank[k]] = S.vals[i * kCap + s];
       }
     }
     __syncthreads();
@@ -519,91 +584,110 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
   }
 }
 
-// ---------------------------------------------------------------- dW1 + dW2 root columns
-// One wave per column c (16 columns per 1024-thread block), the column's non-zeros in
-// row order, 64 at a time (lane l loads entry l), 8 dZ1 rows in flight:
-//   dW1[:, c]       += x_ic * dZ1[i]                      (lane: outputs 2l, 2l+1)
-//   dW2_d[:, 64+c]  += 2 relu(x_ic) * sum_items part_d    (i a root; lane: output l)
-__global__ __launch_bounds__(1024) void k_dw_cols(SparseState S, const float* __restrict__ dZ1,
-                                                  const int32_t* __restrict__ node_root,
-                                                  const int64_t* __restrict__ batch,
-                                                  float* __restrict__ dw1_td, float* __restrict__ dw1_bu,
-                                                  float* __restrict__ dw2_td, float* __restrict__ dw2_bu,
-                                                  float scale) {
+// dW1 = [dZ1_td | dZ1_bu]^T X over the CSC of X: a wave per column (16 per block), each
+// lane owning 2 of the 128 outputs.  The column's (row, value) pairs come 64 at a time
+// (slot and value loaded side by side: k_csc_place stores the value next to the slot),
+// then the dZ1 row gathers are issued kDw1Depth at a time with clamped indices; (row,
+// value) reach the wave by scalar readlane (the index is wave-uniform), not LDS permutes.
+constexpr int kDw1Depth = 16;
+__global__ __launch_bounds__(1024) void k_dw1_cols(SparseState S, const float* __restrict__ dZ1,
+                                                   float* __restrict__ dw1_td,
+                                                   float* __restrict__ dw1_bu) {
   if (!use_sparse(S)) return;
   __shared__ float t1[2 * H][17];
-  __shared__ float t2[2][H][17];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t F = S.F;
   const int64_t c = int64_t(blockIdx.x) * 16 + wave;
   float2 a1 = make_float2(0.f, 0.f);
-  float a2[2] = {0.f, 0.f};
-  if (c < S.F) {
+  if (c < F) {
     const int64_t beg = S.col_start[c], end = S.col_end[c];
     for (int64_t u0 = beg; u0 < end; u0 += 64) {
-      const int64_t u = u0 + lane;
-      const bool ok = u < end;
-      const uint32_t slot = S.csc_slot[ok ? u : beg];   // clamped: loads stay unconditional
-      const float xv_l = S.vals[slot];
-      const float x_l = ok ? xv_l : 0.f;
-      const int32_t i_l = int32_t(slot / kCap);
-      const int32_t s_l = int32_t(slot % kCap);
-      const bool root_l = ok && node_root[i_l] == i_l;
+      const int64_t u = min<int64_t>(u0 + lane, end - 1);   // clamped: duplicates, x masked
+      const uint32_t slot = S.csc_slot[u];
+      const float xv = S.csc_val[u];
       const int n = int(min<int64_t>(64, end - u0));
-      const uint64_t roots = __ballot(root_l);
-      for (int j0 = 0; j0 < n; j0 += 8) {
-        float2 g[8];
-        float x[8];
+      const float x_l = lane < n ? xv : 0.f;
+      const int32_t i_l = int32_t(slot / kCap);
+      for (int j0 = 0; j0 < n; j0 += kDw1Depth) {
+        float2 gv[kDw1Depth];
+        float x[kDw1Depth];
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-          const int j = j0 + v;
-          const int32_t i = __shfl(i_l, j < 64 ? j : 0, 64);
-          x[v] = j < n ? __shfl(x_l, j < 64 ? j : 0, 64) : 0.f;   // x = 0 masks the tail
-          g[v] = *reinterpret_cast<const float2*>(dZ1 + int64_t(i) * (2 * H) + 2 * lane);
+        for (int v = 0; v < kDw1Depth; ++v) {
+          const int j = j0 + v < n ? j0 + v : n - 1;   // wave-uniform: scalar broadcast
+          const int32_t i = __builtin_amdgcn_readlane(i_l, j);
+          x[v] = j0 + v < n ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x_l), j)) : 0.f;
+          gv[v] = *reinterpret_cast<const float2*>(dZ1 + int64_t(i) * (2 * H) + 2 * lane);
         }
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-          a1.x = fmaf(x[v], g[v].x, a1.x);
-          a1.y = fmaf(x[v], g[v].y, a1.y);
-        }
-      }
-      // root rows (rare): dW2 root columns, in row (= tree) order
-      uint64_t m = roots;
-      while (m) {
-        const int j = __builtin_ctzll(m);
-        m &= m - 1;
-        const int32_t i = __shfl(i_l, j, 64);
-        const int32_t s = __shfl(s_l, j, 64);
-        const float xv = __shfl(x_l, j, 64);
-        const int b = int(batch[i]);
-        const float f = scale * fmaxf(xv, 0.f);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          float sum = 0.f;
-          for (int it = S.tree_item0[b]; it < S.tree_item0[b + 1]; ++it)
-            sum += S.root_part[(int64_t(d) * S.max_items + it) * (kCap * H) + s * H + lane];
-          a2[d] = fmaf(f, sum, a2[d]);
+        for (int v = 0; v < kDw1Depth; ++v) {
+          a1.x = fmaf(x[v], gv[v].x, a1.x);
+          a1.y = fmaf(x[v], gv[v].y, a1.y);
         }
       }
     }
   }
   t1[2 * lane][wave] = a1.x;
   t1[2 * lane + 1][wave] = a1.y;
-  t2[0][lane][wave] = a2[0];
-  t2[1][lane][wave] = a2[1];
   __syncthreads();
   // coalesced stores: 16 consecutive columns per output row
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 x 64
   const int64_t cc = int64_t(blockIdx.x) * 16 + tx;
-  if (cc < S.F) {
-    const int64_t K2 = S.F + H;
+  if (cc < F)
     for (int o = ty; o < 2 * H; o += 64) {
-      float* dst = o < H ? dw1_td + int64_t(o) * S.F : dw1_bu + int64_t(o - H) * S.F;
+      float* dst = o < H ? dw1_td + int64_t(o) * F : dw1_bu + int64_t(o - H) * F;
       dst[cc] = t1[o][tx];
     }
-    for (int o = ty; o < H; o += 64) {
-      dw2_td[int64_t(o) * K2 + H + cc] = t2[0][o][tx];
-      dw2_bu[int64_t(o) * K2 + H + cc] = t2[1][o][tx];
+}
+
+// dW2 root columns: dW2_d[:, 64 + c] = sum over the root rows holding column c (tree
+// order = CSC row order) of 2 relu(x) * sum_items root_part[d][item][slot]; every column
+// is written (zero when no root holds it).  A wave per column; only root rows are read.
+__global__ __launch_bounds__(1024) void k_dw2_rootcols(SparseState S, const int32_t* __restrict__ node_root,
+                                                       const int64_t* __restrict__ batch,
+                                                       float* __restrict__ dw2_td,
+                                                       float* __restrict__ dw2_bu, float scale) {
+  if (!use_sparse(S)) return;
+  __shared__ float t2[2][H][17];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t c = int64_t(blockIdx.x) * 16 + wave;
+  float a2[2] = {0.f, 0.f};
+  if (c < S.F) {
+    const int64_t beg = S.col_start[c], end = S.col_end[c];
+    for (int64_t u0 = beg; u0 < end; u0 += 64) {
+      const int64_t u = u0 + lane;
+      const bool ok = u < end;
+      const uint32_t slot = S.csc_slot[ok ? u : beg];
+      const int32_t i_l = int32_t(slot / kCap);
+      const int32_t s_l = int32_t(slot % kCap);
+      const bool root_l = ok && node_root[i_l] == i_l;
+      uint64_t m = __ballot(root_l);
+      while (m) {   // root rows (rare), in row (= tree) order
+        const int j = __builtin_ctzll(m);
+        m &= m - 1;
+        const int32_t i = __builtin_amdgcn_readlane(i_l, j);     // j is wave-uniform
+        const int32_t sl = __builtin_amdgcn_readlane(s_l, j);
+        const float xv = S.vals[int64_t(i) * kCap + sl];
+        const int b = int(batch[i]);
+        const float f = scale * fmaxf(xv, 0.f);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          float sum = 0.f;
+          for (int it = S.tree_item0[b]; it < S.tree_item0[b + 1]; ++it)
+            sum += S.root_part[(int64_t(d) * S.max_items + it) * (kCap * H) + sl * H + lane];
+          a2[d] = fmaf(f, sum, a2[d]);
+        }
+      }
     }
+  }
+  t2[0][lane][wave] = a2[0];
+  t2[1][lane][wave] = a2[1];
+  __syncthreads();
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 x 64
+  const int64_t cc = int64_t(blockIdx.x) * 16 + tx;
+  if (cc < S.F) {
+    const int64_t K2 = S.F + H;
+    dw2_td[int64_t(ty) * K2 + H + cc] = t2[0][ty][tx];
+    dw2_bu[int64_t(ty) * K2 + H + cc] = t2[1][ty][tx];
   }
 }
 
@@ -630,6 +714,7 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   t.col_end = c.take<int32_t>(size_t(F));
   t.csc_slot = c.take<uint32_t>(slots);
   t.rbits = c.take<uint32_t>(size_t(2) * N);
+  t.csc_val = c.take<float>(slots);
   if (S) {
     t.mode = S->mode;
     t.flags = S->flags;
@@ -641,10 +726,13 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   return c.off;
 }
 
-int sparse_transpose(SparseState& S, const bgcn_bigcn_args* a, hipStream_t s) {
-  dim3 grid(unsigned((S.F + H + 31) / 32), 2, 4);
-  hipLaunchKernelGGL(k_transpose_weights, grid, dim3(256), 0, s, S, a->td_w1, a->bu_w1, a->td_w2,
-                     a->bu_w2);
+int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root, hipStream_t s) {
+  const int nTx = int((S.F + H + 31) / 32);
+  const int nT = S.mode == 1 ? 0 : nTx * 2 * 4;
+  const int nR = int((S.N + 255) / 256);
+  const int nP = int((S.B + 1 + 255) / 256);
+  hipLaunchKernelGGL(k_prologue, dim3(unsigned(nT + nR + nP)), dim3(256), 0, s, S, a->td_w1, a->bu_w1,
+                     a->td_w2, a->bu_w2, a->batch, a->rootindex, node_root, a->tree_ptr, nTx, nT, nR);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -689,10 +777,17 @@ int sparse_csc(SparseState& S, hipStream_t s) {
   return BGCN_OK;
 }
 
-int sparse_dw_cols(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1,
-                   const int32_t* node_root, KeepSrc keep, hipStream_t s) {
-  hipLaunchKernelGGL(k_dw_cols, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, dZ1, node_root,
-                     a->batch, a->td_dw1, a->bu_dw1, a->td_dw2, a->bu_dw2, keep.scale());
+int sparse_dw1(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1, hipStream_t s) {
+  hipLaunchKernelGGL(k_dw1_cols, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, dZ1,
+                     a->td_dw1, a->bu_dw1);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int sparse_dw2_rootcols(SparseState& S, const bgcn_bigcn_args* a, const int32_t* node_root,
+                        KeepSrc keep, hipStream_t s) {
+  hipLaunchKernelGGL(k_dw2_rootcols, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, node_root,
+                     a->batch, a->td_dw2, a->bu_dw2, keep.scale());
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }

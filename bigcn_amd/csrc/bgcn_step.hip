@@ -19,81 +19,23 @@ namespace bgcn {
 namespace {
 
 constexpr int H = 64;
-constexpr int kHeadIn = 4 * H;      // cat(BU_x, TD_x) = 256
-constexpr int kMaxClasses = 16;
 
-// Head forward + the row-local backward, one wave per tree b:
-//   z = head[b] W^T + bias ; logp = z - logsumexp(z) ; loss_row[b] = -logp[y_b]
-//   dz[b] = (softmax(z) - onehot(y_b)) / B ; dhead[b] = dz[b] W
-// Lane l holds head[b][4l .. 4l+3]; dot products are butterfly-reduced (deterministic).
-__global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ head,
-                                                  const float* __restrict__ W,
-                                                  const float* __restrict__ bias,
-                                                  const int64_t* __restrict__ y, int64_t B, int C,
-                                                  float* __restrict__ logp_out,
-                                                  float* __restrict__ dz,
-                                                  float* __restrict__ loss_row,
-                                                  float* __restrict__ dhead,
-                                                  int32_t* __restrict__ status) {
-  const int64_t b = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const int l = threadIdx.x & 63;
-  const float4 h = ld4(head + b * kHeadIn + 4 * l);
-  float z[kMaxClasses];
-#pragma unroll
-  for (int c = 0; c < kMaxClasses; ++c) {
-    z[c] = 0.f;
-    if (c < C) {  // C is uniform: the shuffles stay convergent
-      const float4 w = ld4(W + int64_t(c) * kHeadIn + 4 * l);
-      float p = fmaf(h.x, w.x, fmaf(h.y, w.y, fmaf(h.z, w.z, h.w * w.w)));
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
-      z[c] = p + bias[c];
-    }
-  }
-  float m = z[0];
-#pragma unroll
-  for (int c = 1; c < kMaxClasses; ++c)
-    if (c < C) m = fmaxf(m, z[c]);
-  float se = 0.f;
-#pragma unroll
-  for (int c = 0; c < kMaxClasses; ++c)
-    if (c < C) se += expf(z[c] - m);
-  const float lse = m + logf(se);
-  const int64_t yb = y[b];
-  const bool yok = yb >= 0 && yb < C;
-  if (!yok && l == 0 && status) atomicOr(status, 2);
-  const float inv_b = 1.0f / float(B);
-  float4 dh = f4zero();
-#pragma unroll
-  for (int c = 0; c < kMaxClasses; ++c) {
-    if (c < C) {
-      const float lp = z[c] - lse;
-      const float g = yok ? (expf(lp) - (c == yb ? 1.f : 0.f)) * inv_b : 0.f;
-      if (l == 0) {
-        if (logp_out) logp_out[b * C + c] = lp;
-        dz[b * C + c] = g;
-        if (c == yb) loss_row[b] = -lp;
-      }
-      dh = f4fma(g, ld4(W + int64_t(c) * kHeadIn + 4 * l), dh);
-    }
-  }
-  if (l == 0 && !yok) loss_row[b] = 0.f;
-  st4(dhead + b * kHeadIn + 4 * l, dh);
-}
 
-// Weight-side head backward: dW[c][k] = sum_b dz[b][c] head[b][k] (block c < C, thread k),
-// and in block C: db[c] = sum_b dz[b][c] and loss = sum_b loss_row[b] / B.  Fixed orders.
-__global__ __launch_bounds__(256) void k_head_wgrad(const float* __restrict__ head,
-                                                    const float* __restrict__ dz, int64_t B, int C,
-                                                    const float* __restrict__ loss_row,
-                                                    float* __restrict__ dW, float* __restrict__ db,
-                                                    float* __restrict__ loss) {
-  const int c = blockIdx.x, k = threadIdx.x;
+// Weight-side head backward: dW[c][k] = sum_b dz[b][c] head[b][k] (block c < C; 4
+// quarters of the trees x 256 k, combined in quarter order) and in block C:
+// db[c] = sum_b dz[b][c] and loss = sum_b loss_row[b] / B.  Fixed orders.
+__global__ __launch_bounds__(1024) void k_head_wgrad(const float* __restrict__ head,
+                                                     const float* __restrict__ dz, int64_t B, int C,
+                                                     const float* __restrict__ loss_row,
+                                                     float* __restrict__ dW, float* __restrict__ db,
+                                                     float* __restrict__ loss) {
+  __shared__ float red[4][kHeadIn];
+  const int c = blockIdx.x, k = threadIdx.x & 255, q = threadIdx.x >> 8;
+  const int64_t bq = (B + 3) / 4, b0 = q * bq, b1 = min<int64_t>(B, b0 + bq);
   if (c < C) {
     float acc = 0.f;
-    int64_t b = 0;
-    for (; b + 8 <= B; b += 8) {
+    int64_t b = b0;
+    for (; b + 8 <= b1; b += 8) {
       float hv[8], gv[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -103,25 +45,27 @@ __global__ __launch_bounds__(256) void k_head_wgrad(const float* __restrict__ he
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc = fmaf(gv[u], hv[u], acc);
     }
-    for (; b < B; ++b) acc = fmaf(dz[b * C + c], head[b * kHeadIn + k], acc);
-    dW[int64_t(c) * kHeadIn + k] = acc;
+    for (; b < b1; ++b) acc = fmaf(dz[b * C + c], head[b * kHeadIn + k], acc);
+    red[q][k] = acc;
+    __syncthreads();
+    if (q == 0) dW[int64_t(c) * kHeadIn + k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
     return;
   }
-  __shared__ float red[256];
+  float* lr = &red[0][0];   // 1024 partial sums of the loss rows
   float acc = 0.f;
-  for (int64_t b = k; b < B; b += 256) acc += loss_row[b];
-  red[k] = acc;
-  if (k < C) {
+  for (int64_t b = threadIdx.x; b < B; b += 1024) acc += loss_row[b];
+  lr[threadIdx.x] = acc;
+  if (threadIdx.x < C) {
     float s = 0.f;
-    for (int64_t b = 0; b < B; ++b) s += dz[b * C + k];
-    db[k] = s;
+    for (int64_t b = 0; b < B; ++b) s += dz[b * C + threadIdx.x];
+    db[threadIdx.x] = s;
   }
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (k < o) red[k] += red[k + o];
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) lr[threadIdx.x] += lr[threadIdx.x + o];
     __syncthreads();
   }
-  if (k == 0) *loss = red[0] / float(B);
+  if (threadIdx.x == 0) *loss = lr[0] / float(B);
 }
 
 struct StepWs {
@@ -225,15 +169,18 @@ static int train_step_body(const bgcn_step_args* a, StepWs& w, hipStream_t s) {
   e.td_dw1 = a->grads[0]; e.td_db1 = a->grads[1]; e.td_dw2 = a->grads[2]; e.td_db2 = a->grads[3];
   e.bu_dw1 = a->grads[4]; e.bu_db1 = a->grads[5]; e.bu_dw2 = a->grads[6]; e.bu_db2 = a->grads[7];
   e.save_for_backward = 1;
-  BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, g == s ? -1 : kLaneSide));
-
-  hipLaunchKernelGGL(k_head_fwd, dim3(grid_for(B, 4)), dim3(256), 0, s, w.head, a->params[8],
-                     a->params[9], a->y, B, int(C), a->logp, w.dz, w.loss_row, w.dhead, a->status);
-  BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_head_wgrad, dim3(unsigned(C + 1)), dim3(256), 0, s, w.head, w.dz, B, int(C),
+  // forward with the head fused into the readout (fc, log_softmax, NLL row terms, dz,
+  // dhead per tree)
+  const HeadArgs hd{a->params[8], a->params[9], a->y, int(C), a->logp, w.dz, w.loss_row, w.dhead,
+                    a->status};
+  BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, g == s ? -1 : kLaneSide, &hd));
+  // fc weight/bias gradients and the loss mean are off the critical path: side lane
+  hipStream_t x;
+  BGCN_TRY(aux_fork(s, kLaneSide, &x));
+  hipLaunchKernelGGL(k_head_wgrad, dim3(unsigned(C + 1)), dim3(1024), 0, x, w.head, w.dz, B, int(C),
                      w.loss_row, a->grads[8], a->grads[9], a->loss);
   BGCN_CHECK_LAUNCH();
-  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s);
+  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s);   // joins the side lane at its end
 }
 
 }  // namespace bgcn
