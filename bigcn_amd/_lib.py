@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_scatter_mean_workspace_size", "bgcn_scatter_mean_fwd", "bgcn_scatter_mean_bwd",
     "bgcn_bigcn_workspace_size", "bgcn_bigcn_forward", "bgcn_bigcn_backward",
     "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_adam_step",
+    "bgcn_prepare_workspace_size", "bgcn_prepare_batch",
     "bgcn_train_step_workspace_size", "bgcn_train_step",
 )
 
@@ -79,16 +80,25 @@ class BiGCNArgs(Structure):
 BGCN_STEP_PARAMS = 10
 
 
+class BatchDesc(Structure):
+    """bgcn_batch (include/bgcn.h)."""
+    _fields_ = [
+        ("x", c_void_p), ("ldx", c_int64), ("num_nodes", c_int64), ("num_graphs", c_int64),
+        ("batch", c_void_p), ("rootindex", c_void_p),
+        ("td_edge_index", c_void_p), ("td_num_edges", c_int64),
+        ("bu_edge_index", c_void_p), ("bu_num_edges", c_int64),
+    ]
+
+
 class StepArgs(Structure):
     """bgcn_step_args (include/bgcn.h)."""
     _fields_ = [
-        ("x", c_void_p), ("ldx", c_int64), ("num_nodes", c_int64), ("num_graphs", c_int64),
-        ("in_feats", c_int64), ("num_classes", c_int64), ("batch", c_void_p), ("rootindex", c_void_p),
-        ("y", c_void_p), ("td_edge_index", c_void_p), ("td_num_edges", c_int64),
-        ("bu_edge_index", c_void_p), ("bu_num_edges", c_int64), ("degree_on", c_int32),
-        ("training", c_int32), ("seed", c_uint64), ("feat_mode", c_int32),
+        ("cur", BatchDesc), ("in_feats", c_int64), ("num_classes", c_int64), ("y", c_void_p),
+        ("degree_on", c_int32), ("training", c_int32), ("seed", c_uint64), ("feat_mode", c_int32),
         ("params", c_void_p * BGCN_STEP_PARAMS), ("grads", c_void_p * BGCN_STEP_PARAMS),
         ("loss", c_void_p), ("logp", c_void_p), ("status", c_void_p),
+        ("prepared", c_void_p), ("prepared_bytes", c_size_t), ("prepared_ready", c_int32),
+        ("next", POINTER(BatchDesc)), ("next_prepared", c_void_p), ("next_prepared_bytes", c_size_t),
     ]
 
 
@@ -129,6 +139,9 @@ _SIGS = {
     "bgcn_bigcn_backward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
     "bgcn_keep_words": (c_int, [c_uint64, c_int64, c_int32, c_void_p, c_void_p]),
     "bgcn_adam_step": (c_int, [c_void_p, c_void_p]),
+    "bgcn_prepare_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64, c_int64]),
+    "bgcn_prepare_batch": (c_int, [POINTER(BatchDesc), c_int64, c_int32, c_int32, c_void_p, c_size_t,
+                                   c_void_p]),
     "bgcn_train_step_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64, c_int64, c_int64]),
     "bgcn_train_step": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_set_kernel_timing": (c_int, [c_int]),

@@ -614,7 +614,7 @@ static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool 
 // Workspace + sparse state of one call.  The sparse path's per-row lists and its
 // overflow flag live in caller-owned buffers (saved from forward to backward).
 static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w, SparseState& sp,
-                 const int32_t*& gate) {
+                 const int32_t*& gate, const Prepared* prep) {
   const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
   BGCN_CHECK_ARG(ws && ws_bytes >= bigcn_ws_size(N, B, F, H), "workspace too small");
   BGCN_CHECK_ARG(a->feat_mode == BGCN_FEAT_DENSE ||
@@ -631,6 +631,13 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
   w.spmm_bytes = ws_bytes - align_up(c.off, 256) - 256;
   w.spmm_ws = c.take<float>(1);
+  if (prep) {   // the batch's weight-independent state lives in the prepared buffer
+    w.node_root = prep->node_root;
+    sp.item_tree = prep->item_tree; sp.item_chunk = prep->item_chunk; sp.tree_item0 = prep->tree_item0;
+    sp.hist = prep->hist; sp.col_total = prep->col_total;
+    sp.col_start = prep->col_start; sp.col_end = prep->col_end;
+    sp.csc_slot = prep->csc_slot; sp.csc_val = prep->csc_val;
+  }
   // dense kernels run when feat_mode == dense (no gate) or when the sparse path overflowed
   gate = sp.mode == 1 ? nullptr : a->x_flags;
   return BGCN_OK;
@@ -643,17 +650,34 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
 // >= 0: the caller is building the TD/BU graphs on that lane (bgcn_train_step), joined
 // just before their first use.  head (bgcn_train_step): classifier head fused into the
 // readout.
+static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, KeepSrc keep,
+                        const int32_t* gate, hipStream_t s, const HeadArgs* head, bool forked);
+
 int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
-                       int graph_lane, const HeadArgs* head) {
+                       int graph_lane, const HeadArgs* head, const Prepared* prep) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->head_in && a->td_w1 && a->bu_w1 && a->td_w2 && a->bu_w2, "null pointer");
-  const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
+  const int64_t N = a->num_nodes, F = a->in_feats;
   FusedWs w;
   SparseState sp{};
   const int32_t* gate = nullptr;
-  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate));
+  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate, prep));
   KeepSrc keep = make_keep(a);
   const bool sparse = sp.mode != 1;
+
+  if (prep) {
+    // prepared batch (bgcn_train_step): graphs, tree maps, items, ELL and CSC of X exist;
+    // only the weight transposes and conv1's gather from the ELL remain
+    BGCN_TRY(sparse_prologue(sp, a, w.node_root, s, false));
+    if (sparse) {
+      timing_begin(0, s);
+      BGCN_TRY(sparse_conv1_gather(sp, w.z1, s));
+      timing_end(0, s);
+    }
+    BGCN_TRY(gemm_xwt_impl(a->x, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F, s, gate));
+    if (graph_lane >= 0) BGCN_TRY(aux_join(s, graph_lane));   // K1 of a just-prepared batch
+    return forward_tail(a, w, sp, keep, gate, s, head, false);
+  }
 
   // one prologue launch: weight transposes, node -> root map, tree pointers, flag reset
   BGCN_TRY(sparse_prologue(sp, a, w.node_root, s));
@@ -685,6 +709,15 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
     BGCN_TRY(sparse_csc(sp, x));
     forked = true;
   }
+  return forward_tail(a, w, sp, keep, gate, s, head, forked);
+}
+
+// conv1 propagate -> conv2 -> conv2 propagate -> readout (+ head); joins the side lane
+// when `forked`.
+static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, KeepSrc keep,
+                        const int32_t* gate, hipStream_t s, const HeadArgs* head, bool forked) {
+  const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
+  const bool sparse = sp.mode != 1;
   // conv1 propagate + bias (pre-relu h1 is saved: it is also the detached x2)
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z1, a->h1, a->td_b1, a->bu_b1, BGCN_EPI_NONE, w, s));
   // conv2 lin with the root-extended, relu'd, dropped-out A operand generated in-kernel
@@ -706,7 +739,8 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
 // Backward, given the forward's workspace.  Main stream: readout' -> dZ2 -> dH1 -> dZ1
 // -> dW1.  Side lane, forked as soon as its inputs exist: db2, the dW2 chain (relu(H1)
 // block, root partials, root columns), db1 and the gated dense dW1; joined at the end.
-int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s) {
+int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
+                        const Prepared* prep, bool side_busy) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->dhead_in && a->td_dw1 && a->bu_dw1 && a->td_dw2 && a->bu_dw2 && a->td_db1 &&
                      a->bu_db1 && a->td_db2 && a->bu_db2,
@@ -715,9 +749,10 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   FusedWs w;
   SparseState sp{};
   const int32_t* gate = nullptr;
-  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate));
+  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate, prep));
   KeepSrc keep = make_keep(a);
   const bool sparse = sp.mode != 1;
+  const bool have_csc = a->save_for_backward || prep != nullptr;
   hipStream_t x;
 
   // readout + relu' -> dH2; db2 on the side lane
@@ -732,9 +767,11 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   // dZ2 = A^T dH2
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.d2, w.dz2, nullptr, nullptr, BGCN_EPI_NONE, w, s));
 
-  // ---- side: dW2 (both directions, generated A2 operand).  The relu(H1) columns by
-  // MFMA; the X[root] columns by MFMA (dense) or from the root non-zeros (sparse)
-  BGCN_TRY(aux_fork(s, kLaneSide, &x));
+  // ---- side (or main when the side lane is busy): dW2 (both directions, generated A2
+  // operand).  The relu(H1) columns by MFMA; the X[root] columns by MFMA (dense) or from
+  // the root non-zeros (sparse)
+  if (side_busy) x = s;
+  else BGCN_TRY(aux_fork(s, kLaneSide, &x));
   timing_begin(3, x);
   hipLaunchKernelGGL(k_dw2, dim3(grid_for(H + F, 64), w.S2, 2), dim3(256), 0, x, a->x, a->ldx, F,
                      a->h1, w.dz2, w.node_root, w.dw2_part, N, w.kchunk2, w.S2, keep, gate, 1, H + F);
@@ -753,7 +790,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
                        w.Sh, int64_t(H), H + F, a->td_dw2, a->bu_dw2, gate, 0);
     BGCN_CHECK_LAUNCH();
     BGCN_TRY(sparse_dw2_root_part(sp, a->tree_ptr, w.dz2, x));
-    if (!a->save_for_backward) BGCN_TRY(sparse_csc(sp, x));
+    if (!have_csc) BGCN_TRY(sparse_csc(sp, x));
     BGCN_TRY(sparse_dw2_rootcols(sp, a, w.node_root, keep, x));
   }
 
@@ -771,7 +808,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   // (sparse, main) or the dense MFMA GEMM (dense mode on main; gated fallback on the side)
   if (sparse) {
     BGCN_TRY(aux_fork(s, kLaneSide, &x));
-    if (!a->save_for_backward) BGCN_TRY(aux_join(s, kLaneSide));   // CSC built on the side
+    if (!have_csc) BGCN_TRY(aux_join(s, kLaneSide));   // CSC built on the side
     timing_begin(5, s);
     BGCN_TRY(sparse_dw1(sp, a, w.dz1, s));
     timing_end(5, s);
@@ -799,12 +836,12 @@ extern "C" size_t bgcn_bigcn_workspace_size(int64_t num_nodes, int64_t num_graph
 extern "C" int bgcn_bigcn_forward(const bgcn_bigcn_args* args, void* workspace,
                                   size_t workspace_bytes, bgcn_stream_t stream) {
   return bgcn::bigcn_forward_impl(args, workspace, workspace_bytes,
-                                  reinterpret_cast<hipStream_t>(stream), -1);
+                                  reinterpret_cast<hipStream_t>(stream), -1, nullptr, nullptr);
 }
 extern "C" int bgcn_bigcn_backward(const bgcn_bigcn_args* args, void* workspace,
                                    size_t workspace_bytes, bgcn_stream_t stream) {
   return bgcn::bigcn_backward_impl(args, workspace, workspace_bytes,
-                                   reinterpret_cast<hipStream_t>(stream));
+                                   reinterpret_cast<hipStream_t>(stream), nullptr, false);
 }
 extern "C" int bgcn_keep_words(uint64_t seed, int64_t num_nodes, int32_t num_words,
                                uint32_t* words, bgcn_stream_t stream) {

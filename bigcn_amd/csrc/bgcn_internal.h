@@ -61,6 +61,7 @@ struct HeadArgs {
   float* loss_row;       // [B]
   float* dhead;          // [B, 256]
   int32_t* status;       // bit 1: label out of range
+  const int32_t* in_status;  // OR-ed into *status once (prepared batch's K1 flags), or nullptr
 };
 
 // One wave, row b of the head: h = head_in[b][4l .. 4l+3] held by lane l.
@@ -109,14 +110,41 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
     }
   }
   if (l == 0 && !yok) hd.loss_row[b] = 0.f;
+  if (l == 0 && b == 0 && hd.in_status && hd.status && *hd.in_status) atomicOr(hd.status, *hd.in_status);
   st4(hd.dhead + b * kHeadIn + 4 * l, dh);
 }
 
 // ---- fused encoder (bgcn_bigcn.hip); graph_lane: see bigcn_forward_impl
 size_t bigcn_ws_size(int64_t N, int64_t B, int64_t F, int64_t hid);
+struct Prepared;
 int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
-                       int graph_lane, const HeadArgs* head = nullptr);
-int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s);
+                       int graph_lane, const HeadArgs* head = nullptr,
+                       const Prepared* prep = nullptr);
+// side_busy: the side lane carries other long work (a next-batch preparation); the dW2
+// chain then stays on the caller's stream
+int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
+                        const Prepared* prep = nullptr, bool side_busy = false);
+
+// ---- prepared batch (bgcn_step.hip): the weight-independent state of one batch
+// (sizes shared with bgcn_sparse.h: tree work items of kChunkItems nodes, CSC row blocks)
+constexpr int kChunkItems = 256;
+constexpr int kCscRowBlock = 256;
+constexpr int64_t kSparseMaxFeat = 16384;
+struct Prepared {
+  bgcn_csr_out td, bu;
+  int64_t td_cap, bu_cap;                // E + N
+  int32_t *tree_ptr, *node_root, *status;
+  int32_t *item_tree, *item_chunk, *tree_item0;
+  int32_t *x_flags, *x_nnz, *x_cols;
+  float* x_vals;
+  int32_t *hist, *col_total, *col_start, *col_end;
+  uint32_t* csc_slot;
+  float* csc_val;
+  void* gws;
+  size_t gws_bytes;
+};
+size_t carve_prepared(Carve& c, int64_t N, int64_t B, int64_t F, int64_t Etd, int64_t Ebu,
+                      Prepared* p);
 
 // ---- one training step (bgcn_step.hip)
 size_t train_step_ws_size(int64_t N, int64_t B, int64_t F, int64_t C, int64_t Etd, int64_t Ebu);

@@ -1,12 +1,12 @@
 // Sparse-feature path of the fused encoder (see bgcn_sparse.hip).
 #pragma once
 
-#include "bgcn_common.h"
+#include "bgcn_internal.h"
 
 namespace bgcn {
 
 constexpr int kCap = 32;     // max non-zeros per feature row on the sparse path
-constexpr int kChunk = 256;  // nodes per work item of the dW2 root-column pass
+constexpr int kChunk = kChunkItems;  // nodes per tree work item (conv2, dW2 root partials)
 
 struct SparseState {
   int mode;        // 0 auto, 1 dense (sparse kernels idle), 2 sparse preferred (same as auto)
@@ -30,12 +30,20 @@ struct SparseState {
   float* csc_val;       // [N*kCap] X value of each csc_slot entry
 };
 
-constexpr int kRowBlock = 256;          // rows per block of the CSC counting sort
-constexpr int64_t kSparseMaxF = 16384;  // LDS bound of the CSC kernels (2 x 4 B x F)
+constexpr int kRowBlock = kCscRowBlock;   // rows per block of the CSC counting sort
+constexpr int64_t kSparseMaxF = kSparseMaxFeat;  // LDS bound of the CSC kernels (2 x 4 B x F)
 
 size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S);
 // forward prologue: weight transposes (sparse path), node_root, tree_ptr, flag reset
-int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root, hipStream_t s);
+// batch_part = false: weight transposes only (the batch part came from a Prepared)
+int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root, hipStream_t s,
+                    bool batch_part = true);
+struct Prepared;
+// weight-independent preparation of one batch into p (bgcn_prepare_batch)
+int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
+                   const int64_t* batch, const int64_t* rootindex, const float* X, int64_t ldx,
+                   hipStream_t s);
+int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s);
 int sparse_compact_conv1(SparseState& S, const float* X, int64_t ldx, float* Z1, hipStream_t s);
 int sparse_items(SparseState& S, const int32_t* tree_ptr, hipStream_t s);
 int sparse_conv2(SparseState& S, const float* H1, const int32_t* tree_ptr, const int64_t* rootindex,

@@ -15,10 +15,12 @@
 // A row with more than kCap non-zeros sets a device flag that switches the whole batch
 // to the dense MFMA path (identical results); every kernel of both paths checks the flag
 // on the device, so the choice costs no host sync.
+#include <cstdlib>
 #include <cstring>
 
 
 
+#include "bgcn_internal.h"
 #include "bgcn_sparse.h"
 
 namespace bgcn {
@@ -71,10 +73,10 @@ __global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __
   const int blk = blockIdx.x;
   if (blk < nT) {
     if (S.mode == 1) return;
-    if (blk == 0 && threadIdx.x < 8) S.flags[threadIdx.x] = 0;
     transpose_tile(S, blk % nTx, (blk / nTx) % 2, blk / (2 * nTx), w1td, w1bu, w2td, w2bu);
     return;
   }
+  if (blk == nT && nR > 0 && S.mode != 1 && threadIdx.x < 8) S.flags[threadIdx.x] = 0;
   if (blk < nT + nR) {
     const int64_t i = int64_t(blk - nT) * 256 + threadIdx.x;
     if (i >= S.N) return;
@@ -101,14 +103,45 @@ __global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __
 // all zero across the wave (the common case for bag-of-words rows) costs one ballot -
 // and Z1[i] = sum val * W1T[col] with each lane owning 2 of the 128 outputs.
 constexpr int kRowChunks = 20;  // float4 per lane per pass (F <= 5120 in one pass)
+constexpr unsigned kPrepBlocks = 256;   // grid of the side-lane compaction (1 per CU)
+
+// Z1[i] += sum_s val_s * W1T[col_s] for the (col, val) pairs of lane-held lists: lane s
+// (< cnt) holds pair s; the pairs reach the wave by scalar readlane, gathers unconditional
+// (clamped column), 8 in flight.
+__device__ __forceinline__ float2 conv1_row(const SparseState& S, int cnt, int32_t col_l, float val_l) {
+  const int lane = threadIdx.x & 63;
+  float2 acc = make_float2(0.f, 0.f);
+  for (int s0 = 0; s0 < cnt; s0 += 8) {
+    float2 w[8];
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int sl = s0 + u < cnt ? s0 + u : 0;                // wave-uniform
+      const int32_t c = min(max(__builtin_amdgcn_readlane(col_l, sl), 0), int32_t(S.F - 1));
+      x[u] = s0 + u < cnt ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(val_l), sl)) : 0.f;
+      w[u] = *reinterpret_cast<const float2*>(S.w1t + int64_t(c) * (2 * H) + 2 * lane);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      acc.x = fmaf(x[u], w[u].x, acc.x);
+      acc.y = fmaf(x[u], w[u].y, acc.y);
+    }
+  }
+  return acc;
+}
+
+// kConv1 = true: compaction + conv1 in one pass (the encoder's forward); false: the ELL
+// only (weight-independent batch preparation, bgcn_prepare_batch).
+template <bool kConv1>
 __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const float* __restrict__ X,
                                                        int64_t ldx, float* __restrict__ Z1) {
   __shared__ int32_t s_col[4][kCap];
   __shared__ float s_val[4][kCap];
   if (S.mode == 1) return;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t i = int64_t(blockIdx.x) * 4 + wave;
-  if (i >= S.N) return;
+  // grid-stride over rows: the preparation launches a small grid so that it streams X
+  // beside the training chain without taking every CU slot
+  for (int64_t i = int64_t(blockIdx.x) * 4 + wave; i < S.N; i += int64_t(gridDim.x) * 4) {
   const float* row = X + i * ldx;
   const int nq = int(S.F / 4);   // float4 per row (F % 4 == 0)
   int cnt = 0;
@@ -146,32 +179,33 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const floa
   if (lane == 0) S.nnz[i] = cnt;
   if (cnt > kCap) {
     if (lane == 0) atomicOr(&S.flags[0], 1);
-    return;
+    continue;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes have landed
   __builtin_amdgcn_wave_barrier();
+  const int32_t col_l = lane < cnt ? s_col[wave][lane] : 0;
+  const float val_l = lane < cnt ? s_val[wave][lane] : 0.f;
   if (lane < cnt) {
-    S.cols[i * kCap + lane] = s_col[wave][lane];
-    S.vals[i * kCap + lane] = s_val[wave][lane];
+    S.cols[i * kCap + lane] = col_l;
+    S.vals[i * kCap + lane] = val_l;
   }
-  float2 acc = make_float2(0.f, 0.f);
-  for (int s0 = 0; s0 < cnt; s0 += 8) {
-    float2 w[8];
-    float x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int s = s0 + u;
-      const bool ok = s < cnt;
-      x[u] = ok ? s_val[wave][s] : 0.f;
-      w[u] = ok ? *reinterpret_cast<const float2*>(S.w1t + int64_t(s_col[wave][s]) * (2 * H) + 2 * lane)
-                : make_float2(0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      acc.x = fmaf(x[u], w[u].x, acc.x);
-      acc.y = fmaf(x[u], w[u].y, acc.y);
-    }
+  if (kConv1) {
+    const float2 acc = conv1_row(S, cnt, col_l, val_l);
+    *reinterpret_cast<float2*>(Z1 + i * (2 * H) + 2 * lane) = acc;
   }
+  }
+}
+
+// conv1 lin from a prepared ELL of X (bgcn_prepare_batch): wave per row.
+__global__ __launch_bounds__(256) void k_conv1_gather(SparseState S, float* __restrict__ Z1) {
+  if (!use_sparse(S)) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (i >= S.N) return;
+  const int cnt = min(S.nnz[i], kCap);
+  const int32_t col_l = S.cols[i * kCap + (lane & (kCap - 1))];
+  const float val_l = S.vals[i * kCap + (lane & (kCap - 1))];
+  const float2 acc = conv1_row(S, cnt, col_l, val_l);
   *reinterpret_cast<float2*>(Z1 + i * (2 * H) + 2 * lane) = acc;
 }
 
@@ -726,11 +760,13 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   return c.off;
 }
 
-int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root, hipStream_t s) {
+int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root, hipStream_t s,
+                    bool batch_part) {
   const int nTx = int((S.F + H + 31) / 32);
   const int nT = S.mode == 1 ? 0 : nTx * 2 * 4;
-  const int nR = int((S.N + 255) / 256);
-  const int nP = int((S.B + 1 + 255) / 256);
+  const int nR = batch_part ? int((S.N + 255) / 256) : 0;
+  const int nP = batch_part ? int((S.B + 1 + 255) / 256) : 0;
+  if (nT + nR + nP == 0) return BGCN_OK;
   hipLaunchKernelGGL(k_prologue, dim3(unsigned(nT + nR + nP)), dim3(256), 0, s, S, a->td_w1, a->bu_w1,
                      a->td_w2, a->bu_w2, a->batch, a->rootindex, node_root, a->tree_ptr, nTx, nT, nR);
   BGCN_CHECK_LAUNCH();
@@ -738,7 +774,7 @@ int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root
 }
 
 int sparse_compact_conv1(SparseState& S, const float* X, int64_t ldx, float* Z1, hipStream_t s) {
-  hipLaunchKernelGGL(k_compact_conv1, dim3(grid_for(S.N, 4)), dim3(256), 0, s, S, X, ldx, Z1);
+  hipLaunchKernelGGL(k_compact_conv1<true>, dim3(grid_for(S.N, 4)), dim3(256), 0, s, S, X, ldx, Z1);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -773,6 +809,41 @@ int sparse_csc(SparseState& S, hipStream_t s) {
   hipLaunchKernelGGL(k_csc_colscan, dim3(1), dim3(1024), 0, s, S);
   BGCN_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_csc_place, dim3(unsigned(R)), dim3(256), size_t(2 * S.F) * sizeof(int32_t), s, S);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
+                   const int64_t* batch, const int64_t* rootindex, const float* X, int64_t ldx,
+                   hipStream_t s) {
+  SparseState S{};
+  S.mode = mode;
+  S.N = N; S.F = F; S.B = B;
+  S.max_items = int(N / kChunk + B + 1);
+  S.flags = p.x_flags; S.nnz = p.x_nnz; S.cols = p.x_cols; S.vals = p.x_vals;
+  S.item_tree = p.item_tree; S.item_chunk = p.item_chunk; S.tree_item0 = p.tree_item0;
+  S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
+  S.csc_slot = p.csc_slot; S.csc_val = p.csc_val;
+  const int nR = int((N + 255) / 256), nP = int((B + 1 + 255) / 256);
+  hipLaunchKernelGGL(k_prologue, dim3(unsigned(nR + nP)), dim3(256), 0, s, S, nullptr, nullptr,
+                     nullptr, nullptr, batch, rootindex, p.node_root, p.tree_ptr, 1, 0, nR);
+  BGCN_CHECK_LAUNCH();
+  if (mode == 1) return BGCN_OK;
+  BGCN_TRY(sparse_items(S, p.tree_ptr, s));
+  static const unsigned prep_blocks = [] {
+    const char* e = std::getenv("BGCN_PREP_BLOCKS");   // A/B knob for the side-lane grid
+    return e ? unsigned(std::max(1, atoi(e))) : kPrepBlocks;
+  }();
+  timing_begin(7, s);
+  hipLaunchKernelGGL(k_compact_conv1<false>, dim3(std::min<unsigned>(grid_for(N, 4), prep_blocks)),
+                     dim3(256), 0, s, S, X, ldx, nullptr);
+  timing_end(7, s);
+  BGCN_CHECK_LAUNCH();
+  return sparse_csc(S, s);
+}
+
+int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
+  hipLaunchKernelGGL(k_conv1_gather, dim3(grid_for(S.N, 4)), dim3(256), 0, s, S, Z1);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }

@@ -14,6 +14,7 @@
 // bgcn_adam_step follow.  No host sync anywhere: a bad edge index or label sets a bit
 // of *status on the device.
 #include "bgcn_internal.h"
+#include "bgcn_sparse.h"
 
 namespace bgcn {
 namespace {
@@ -55,10 +56,20 @@ __global__ __launch_bounds__(1024) void k_head_wgrad(const float* __restrict__ h
   float acc = 0.f;
   for (int64_t b = threadIdx.x; b < B; b += 1024) acc += loss_row[b];
   lr[threadIdx.x] = acc;
+  __shared__ float dbp[kMaxClasses][64];
+  {   // db[c] = sum_b dz[b][c]: 64 tree slices per class, then a fixed-order sum
+    const int cc = threadIdx.x >> 6, sl = threadIdx.x & 63;
+    if (cc < C) {
+      float sdb = 0.f;
+      for (int64_t b = sl; b < B; b += 64) sdb += dz[b * C + cc];
+      dbp[cc][sl] = sdb;
+    }
+  }
+  __syncthreads();
   if (threadIdx.x < C) {
-    float s = 0.f;
-    for (int64_t b = 0; b < B; ++b) s += dz[b * C + threadIdx.x];
-    db[threadIdx.x] = s;
+    float sdb = 0.f;
+    for (int q = 0; q < 64; ++q) sdb += dbp[threadIdx.x][q];
+    db[threadIdx.x] = sdb;
   }
   __syncthreads();
   for (int o = 512; o > 0; o >>= 1) {
@@ -69,10 +80,6 @@ __global__ __launch_bounds__(1024) void k_head_wgrad(const float* __restrict__ h
 }
 
 struct StepWs {
-  bgcn_csr_out td, bu;
-  void* gws; size_t gws_bytes;
-  int32_t* x_flags; int32_t* x_nnz; int32_t* x_cols; float* x_vals;
-  int32_t* tree_ptr;
   float *h1, *h2, *head, *dhead, *dz, *loss_row;
   void* enc; size_t enc_bytes;
 };
@@ -88,18 +95,8 @@ void carve_csr(Carve& c, int64_t cap, int64_t N, bgcn_csr_out* g) {
   g->s_w = c.take<float>(size_t(cap));
 }
 
-size_t carve_step(Carve& c, int64_t N, int64_t B, int64_t F, int64_t C, int64_t Etd, int64_t Ebu,
-                  StepWs* w) {
+size_t carve_step(Carve& c, int64_t N, int64_t B, int64_t F, int64_t C, StepWs* w) {
   StepWs t{};
-  carve_csr(c, Etd + N, N, &t.td);
-  carve_csr(c, Ebu + N, N, &t.bu);
-  t.gws_bytes = bgcn_graph_pair_workspace_size(Etd, Ebu, N);
-  t.gws = c.take<char>(t.gws_bytes);
-  t.x_flags = c.take<int32_t>(8);
-  t.x_nnz = c.take<int32_t>(size_t(N));
-  t.x_cols = c.take<int32_t>(size_t(N) * BGCN_SPARSE_CAP);
-  t.x_vals = c.take<float>(size_t(N) * BGCN_SPARSE_CAP);
-  t.tree_ptr = c.take<int32_t>(size_t(B + 1));
   t.h1 = c.take<float>(size_t(N) * 2 * H);
   t.h2 = c.take<float>(size_t(N) * 2 * H);
   t.head = c.take<float>(size_t(B) * kHeadIn);
@@ -116,74 +113,178 @@ bgcn_graph_view view_of(const bgcn_csr_out& g, int64_t cap) {
   return bgcn_graph_view{g.t_ptr, g.t_row, g.t_col, g.t_w, g.s_ptr, g.s_row, g.s_col, g.s_w, cap};
 }
 
+int check_batch(const bgcn_batch* b) {
+  BGCN_CHECK_ARG(b, "null batch");
+  BGCN_CHECK_ARG(b->num_nodes > 0 && b->num_graphs > 0, "bad sizes");
+  BGCN_CHECK_ARG(b->td_num_edges >= 0 && b->bu_num_edges >= 0, "bad edge counts");
+  BGCN_CHECK_ARG(b->x && b->batch && b->rootindex, "null pointer");
+  BGCN_CHECK_ARG((b->td_num_edges == 0 || b->td_edge_index) && (b->bu_num_edges == 0 || b->bu_edge_index),
+                 "null edge_index");
+  return BGCN_OK;
+}
+
 }  // namespace
 
-static int train_step_body(const bgcn_step_args* a, StepWs& w, hipStream_t s);
+size_t carve_prepared(Carve& c, int64_t N, int64_t B, int64_t F, int64_t Etd, int64_t Ebu,
+                      Prepared* p) {
+  Prepared t{};
+  t.td_cap = Etd + N;
+  t.bu_cap = Ebu + N;
+  carve_csr(c, t.td_cap, N, &t.td);
+  carve_csr(c, t.bu_cap, N, &t.bu);
+  t.gws_bytes = bgcn_graph_pair_workspace_size(Etd, Ebu, N);
+  t.gws = c.take<char>(t.gws_bytes);
+  t.tree_ptr = c.take<int32_t>(size_t(B + 1));
+  t.node_root = c.take<int32_t>(size_t(N));
+  t.status = c.take<int32_t>(1);
+  const int64_t max_items = N / kChunkItems + B + 1;
+  t.item_tree = c.take<int32_t>(size_t(max_items));
+  t.item_chunk = c.take<int32_t>(size_t(max_items));
+  t.tree_item0 = c.take<int32_t>(size_t(B + 1));
+  t.x_flags = c.take<int32_t>(8);
+  t.x_nnz = c.take<int32_t>(size_t(N));
+  t.x_cols = c.take<int32_t>(size_t(N) * BGCN_SPARSE_CAP);
+  t.x_vals = c.take<float>(size_t(N) * BGCN_SPARSE_CAP);
+  const int64_t R = (N + kCscRowBlock - 1) / kCscRowBlock;
+  t.hist = c.take<int32_t>(size_t(R) * size_t(F));
+  t.col_total = c.take<int32_t>(size_t(F));
+  t.col_start = c.take<int32_t>(size_t(F));
+  t.col_end = c.take<int32_t>(size_t(F));
+  t.csc_slot = c.take<uint32_t>(size_t(N) * BGCN_SPARSE_CAP);
+  t.csc_val = c.take<float>(size_t(N) * BGCN_SPARSE_CAP);
+  if (p) *p = t;
+  return c.off;
+}
+
+static size_t prepared_size(int64_t N, int64_t B, int64_t F, int64_t Etd, int64_t Ebu) {
+  Carve c(nullptr, 0);
+  return carve_prepared(c, N, B, F, Etd, Ebu, nullptr) + 256;
+}
+
+// gs: stream of the graph build (K1); the caller joins it before the graphs are used
+static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_mode, void* buf,
+                        size_t bytes, hipStream_t s, Prepared* out, hipStream_t gs) {
+  BGCN_TRY(check_batch(b));
+  BGCN_CHECK_ARG(F > 0 && F % 4 == 0 && b->ldx >= F && b->ldx % 4 == 0, "bad in_feats / ldx");
+  const int64_t N = b->num_nodes, B = b->num_graphs;
+  BGCN_CHECK_ARG(buf && bytes >= prepared_size(N, B, F, b->td_num_edges, b->bu_num_edges),
+                 "prepared buffer too small");
+  Prepared p;
+  Carve c(buf, bytes);
+  carve_prepared(c, N, B, F, b->td_num_edges, b->bu_num_edges, &p);
+  BGCN_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int32_t), gs));
+  BGCN_TRY(bgcn_build_graph_pair(b->td_edge_index, b->td_num_edges, b->bu_edge_index,
+                                 b->bu_num_edges, N, degree_on, &p.td, &p.bu, p.status, p.gws,
+                                 p.gws_bytes, reinterpret_cast<bgcn_stream_t>(gs)));
+  const int mode = (feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxFeat) ? 1 : 0;
+  BGCN_TRY(sparse_prepare(p, N, B, F, mode, b->batch, b->rootindex, b->x, b->ldx, s));
+  if (out) *out = p;
+  return BGCN_OK;
+}
+
+static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w, hipStream_t s,
+                           int graph_lane);
 
 size_t train_step_ws_size(int64_t N, int64_t B, int64_t F, int64_t C, int64_t Etd, int64_t Ebu) {
+  (void)Etd; (void)Ebu;
   Carve c(nullptr, 0);
-  return carve_step(c, N, B, F, C, Etd, Ebu, nullptr) + 256;
+  return carve_step(c, N, B, F, C, nullptr) + 256;
 }
 
 int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStream_t s) {
   BGCN_CHECK_ARG(a, "null args");
-  const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats, C = a->num_classes;
-  BGCN_CHECK_ARG(N > 0 && B > 0 && F > 0, "bad sizes");
+  BGCN_TRY(check_batch(&a->cur));
+  const int64_t N = a->cur.num_nodes, B = a->cur.num_graphs, F = a->in_feats, C = a->num_classes;
+  BGCN_CHECK_ARG(F > 0, "bad sizes");
   BGCN_CHECK_ARG(C >= 1 && C <= kMaxClasses, "num_classes must be in [1, 16]");
-  BGCN_CHECK_ARG(a->td_num_edges >= 0 && a->bu_num_edges >= 0, "bad edge counts");
   BGCN_CHECK_ARG(a->y && a->loss, "null pointer");
   for (int k = 0; k < BGCN_STEP_PARAMS; ++k)
     BGCN_CHECK_ARG(a->params[k] && a->grads[k], "null parameter / gradient pointer");
-  BGCN_CHECK_ARG(ws && ws_bytes >= train_step_ws_size(N, B, F, C, a->td_num_edges, a->bu_num_edges),
-                 "workspace too small");
+  BGCN_CHECK_ARG(ws && ws_bytes >= train_step_ws_size(N, B, F, C, 0, 0), "workspace too small");
+  BGCN_CHECK_ARG(a->prepared, "a prepared buffer is required (bgcn_prepare_workspace_size)");
+  if (a->next) {
+    BGCN_TRY(check_batch(a->next));
+    BGCN_CHECK_ARG(a->next_prepared && a->next_prepared != a->prepared,
+                   "next_prepared must be a separate buffer");
+  }
   StepWs w;
   Carve c(ws, ws_bytes);
-  carve_step(c, N, B, F, C, a->td_num_edges, a->bu_num_edges, &w);
+  carve_step(c, N, B, F, C, &w);
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
-  return train_step_body(a, w, s);
+  Prepared p;
+  int graph_lane = -1;
+  if (!a->prepared_ready) {
+    // prepare the current batch first; without a next batch to prefetch, its K1 runs on
+    // the side lane beside the pass over X (joined before the first propagate)
+    hipStream_t g = s;
+    if (!a->next) BGCN_TRY(aux_fork(s, kLaneSide, &g));
+    BGCN_TRY(prepare_into(&a->cur, F, a->degree_on, a->feat_mode, a->prepared, a->prepared_bytes, s,
+                          &p, g));
+    if (g != s) graph_lane = kLaneSide;
+  } else {
+    BGCN_CHECK_ARG(a->prepared_bytes >= prepared_size(N, B, F, a->cur.td_num_edges, a->cur.bu_num_edges),
+                   "prepared buffer too small");
+    Carve cp(a->prepared, a->prepared_bytes);
+    carve_prepared(cp, N, B, F, a->cur.td_num_edges, a->cur.bu_num_edges, &p);
+  }
+  if (a->next) {
+    // the next batch's weight-independent preparation (K1, ELL and CSC of X: the HBM-
+    // bound pass) runs on the side lane beside this step's latency-bound chain
+    hipStream_t x;
+    BGCN_TRY(aux_fork(s, kLaneSide, &x));
+    BGCN_TRY(prepare_into(a->next, F, a->degree_on, a->feat_mode, a->next_prepared,
+                          a->next_prepared_bytes, x, nullptr, x));
+  }
+  return train_step_body(a, p, w, s, graph_lane);
 }
 
-static int train_step_body(const bgcn_step_args* a, StepWs& w, hipStream_t s) {
-  const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats, C = a->num_classes;
+static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w, hipStream_t s,
+                           int graph_lane) {
+  const int64_t N = a->cur.num_nodes, B = a->cur.num_graphs, F = a->in_feats, C = a->num_classes;
   if (a->status) BGCN_CHECK_HIP(hipMemsetAsync(a->status, 0, sizeof(int32_t), s));
-
-  // K1 for both directions on the side lane (joined by the encoder right after its pass
-  // over X, before the CSC of X is queued on the same lane), overlapped with that pass
-  hipStream_t g;
-  BGCN_TRY(aux_fork(s, kLaneSide, &g));
-  BGCN_TRY(bgcn_build_graph_pair(a->td_edge_index, a->td_num_edges, a->bu_edge_index,
-                                 a->bu_num_edges, N, a->degree_on, &w.td, &w.bu, a->status, w.gws,
-                                 w.gws_bytes, reinterpret_cast<bgcn_stream_t>(g)));
-
   bgcn_bigcn_args e{};
-  e.x = a->x; e.ldx = a->ldx; e.num_nodes = N; e.num_graphs = B; e.in_feats = F; e.hid = H;
-  e.batch = a->batch; e.rootindex = a->rootindex;
-  e.td = view_of(w.td, a->td_num_edges + N);
-  e.bu = view_of(w.bu, a->bu_num_edges + N);
+  e.x = a->cur.x; e.ldx = a->cur.ldx; e.num_nodes = N; e.num_graphs = B; e.in_feats = F; e.hid = H;
+  e.batch = a->cur.batch; e.rootindex = a->cur.rootindex;
+  e.td = view_of(p.td, p.td_cap);
+  e.bu = view_of(p.bu, p.bu_cap);
   e.td_w1 = a->params[0]; e.td_b1 = a->params[1]; e.td_w2 = a->params[2]; e.td_b2 = a->params[3];
   e.bu_w1 = a->params[4]; e.bu_b1 = a->params[5]; e.bu_w2 = a->params[6]; e.bu_b2 = a->params[7];
   e.training = a->training; e.seed = a->seed; e.keep_words = nullptr;
   e.feat_mode = a->feat_mode;
-  e.x_flags = w.x_flags; e.x_nnz = w.x_nnz; e.x_cols = w.x_cols; e.x_vals = w.x_vals;
-  e.tree_ptr = w.tree_ptr; e.h1 = w.h1; e.h2 = w.h2; e.head_in = w.head; e.dhead_in = w.dhead;
+  e.x_flags = p.x_flags; e.x_nnz = p.x_nnz; e.x_cols = p.x_cols; e.x_vals = p.x_vals;
+  e.tree_ptr = p.tree_ptr; e.h1 = w.h1; e.h2 = w.h2; e.head_in = w.head; e.dhead_in = w.dhead;
   e.td_dw1 = a->grads[0]; e.td_db1 = a->grads[1]; e.td_dw2 = a->grads[2]; e.td_db2 = a->grads[3];
   e.bu_dw1 = a->grads[4]; e.bu_db1 = a->grads[5]; e.bu_dw2 = a->grads[6]; e.bu_db2 = a->grads[7];
   e.save_for_backward = 1;
   // forward with the head fused into the readout (fc, log_softmax, NLL row terms, dz,
-  // dhead per tree)
+  // dhead per tree); the prepared batch's K1 status is folded into *status
   const HeadArgs hd{a->params[8], a->params[9], a->y, int(C), a->logp, w.dz, w.loss_row, w.dhead,
-                    a->status};
-  BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, g == s ? -1 : kLaneSide, &hd));
+                    a->status, p.status};
+  BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, graph_lane, &hd, &p));
   // fc weight/bias gradients and the loss mean are off the critical path: side lane
   hipStream_t x;
   BGCN_TRY(aux_fork(s, kLaneSide, &x));
   hipLaunchKernelGGL(k_head_wgrad, dim3(unsigned(C + 1)), dim3(1024), 0, x, w.head, w.dz, B, int(C),
                      w.loss_row, a->grads[8], a->grads[9], a->loss);
   BGCN_CHECK_LAUNCH();
-  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s);   // joins the side lane at its end
+  // (joins the side lane at its end; with a next-batch preparation on the side lane the
+  // dW2 chain stays on this stream, which balances the two)
+  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr);
 }
 
 }  // namespace bgcn
+
+extern "C" size_t bgcn_prepare_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,
+                                              int64_t td_num_edges, int64_t bu_num_edges) {
+  return bgcn::prepared_size(num_nodes, num_graphs, in_feats, td_num_edges, bu_num_edges);
+}
+
+extern "C" int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree_on,
+                                  int32_t feat_mode, void* prepared, size_t prepared_bytes,
+                                  bgcn_stream_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return bgcn::prepare_into(batch, in_feats, degree_on, feat_mode, prepared, prepared_bytes, s, nullptr, s);
+}
 
 extern "C" size_t bgcn_train_step_workspace_size(int64_t num_nodes, int64_t num_graphs,
                                                  int64_t in_feats, int64_t num_classes,

@@ -22,7 +22,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import StepArgs, check, ptr, stream_handle, workspace
+from ._lib import BatchDesc, StepArgs, check, ptr, stream_handle, workspace
 from .bigcn import BiGCN, _draw_seed, _num_graphs
 from .dp import GradBucket
 from .ops import _FEAT_MODES
@@ -69,43 +69,88 @@ class FusedTrainStep:
         a.degree_on = self.degree_on
         self._args = a
         self.status = torch.zeros(1, dtype=torch.int32, device=model.fc.weight.device)
+        self._pending = None       # (batch, prepared buffer, feat_mode, tensors) from next_data
+        self._next_desc = None
 
     def grads(self):
         """{parameter: gradient view} of the last step (before the DP all-reduce)."""
         return dict(zip(self.step_params, self.step_grads))
 
-    def forward_backward(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None):
-        """bgcn_train_step only (no all-reduce, no optimiser step); returns the loss."""
-        m = self.model
+    def _desc(self, data):
+        """bgcn_batch of a collated batch (+ the tensors it points into, kept alive)."""
         x = _need(data.x, torch.float32, "x")
-        N, F = x.shape
-        B = _num_graphs(data)
         td_ei = _need(data.edge_index, torch.int64, "edge_index")
         bu_ei = _need(data.BU_edge_index, torch.int64, "BU_edge_index")
         batch = _need(data.batch, torch.int64, "batch")
         root = _need(data.rootindex, torch.int64, "rootindex")
+        d = BatchDesc()
+        d.x, d.ldx, d.num_nodes, d.num_graphs = ptr(x), x.stride(0), x.size(0), _num_graphs(data)
+        d.batch, d.rootindex = ptr(batch), ptr(root)
+        d.td_edge_index, d.td_num_edges = ptr(td_ei), td_ei.size(1)
+        d.bu_edge_index, d.bu_num_edges = ptr(bu_ei), bu_ei.size(1)
+        return d, (x, td_ei, bu_ei, batch, root)
+
+    def _prep_buffer(self, d, F):
+        L = _lib.lib()
+        n = L.bgcn_prepare_workspace_size(d.num_nodes, d.num_graphs, F, d.td_num_edges, d.bu_num_edges)
+        return workspace(n, self.status.device)
+
+    def forward_backward(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None,
+                         next_data=None):
+        """bgcn_train_step only (no all-reduce, no optimiser step); returns the loss.
+
+        ``next_data``: the batch the next call will train on.  Its weight-independent
+        preparation (K1, ELL and CSC of X) then runs inside this call on the auxiliary
+        lane, overlapped with this step's latency-bound chain; the next call finds it
+        ready (matched by identity - do not mutate the batch in between).  Every call
+        still does exactly one preparation's worth of work."""
+        m = self.model
+        d, keep = self._desc(data)
+        F = int(data.x.size(1))
         y = _need(data.y, torch.int64, "y")
         if seed is None:
             seed = _draw_seed() if m.training else 0
         a = self._args
-        a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats = ptr(x), x.stride(0), N, B, F
-        a.batch, a.rootindex, a.y = ptr(batch), ptr(root), ptr(y)
-        a.td_edge_index, a.td_num_edges = ptr(td_ei), td_ei.size(1)
-        a.bu_edge_index, a.bu_num_edges = ptr(bu_ei), bu_ei.size(1)
+        a.cur = d
+        a.in_feats = F
+        a.y = ptr(y)
         a.training, a.seed = int(m.training), int(seed) & (2**64 - 1)
         a.feat_mode = _FEAT_MODES[m.feat_mode]
-        loss = torch.empty(1, dtype=torch.float32, device=x.device)
+        pend = self._pending
+        if pend is not None and pend[0] is data and pend[2] == a.feat_mode:
+            prep = pend[1]
+            a.prepared_ready = 1
+        else:
+            prep = self._prep_buffer(d, F)
+            a.prepared_ready = 0
+        a.prepared, a.prepared_bytes = ptr(prep), prep.numel()
+        self._pending = None
+        nxt = None
+        if next_data is not None:
+            nd, nkeep = self._desc(next_data)
+            nbuf = self._prep_buffer(nd, F)
+            self._next_desc = nd                     # the struct must outlive the call
+            a.next = ctypes.pointer(self._next_desc)
+            a.next_prepared, a.next_prepared_bytes = ptr(nbuf), nbuf.numel()
+            nxt = (next_data, nbuf, a.feat_mode, nkeep)
+        else:
+            a.next = None
+            a.next_prepared, a.next_prepared_bytes = 0, 0
+        loss = torch.empty(1, dtype=torch.float32, device=data.x.device)
         a.loss, a.logp, a.status = ptr(loss), ptr(logp), ptr(self.status)
         L = _lib.lib()
-        ws = workspace(L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, a.td_num_edges,
-                                                        a.bu_num_edges), x.device)
+        N, B = d.num_nodes, d.num_graphs
+        ws = workspace(L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
+                                                        d.bu_num_edges), data.x.device)
         # every auxiliary-lane branch joins back into the caller's stream inside the call,
-        # so the workspace and converted inputs can return to the allocator afterwards
+        # so the workspaces and converted inputs can return to the allocator afterwards
         check(L.bgcn_train_step(ctypes.addressof(a), ptr(ws), ws.numel(), stream_handle()))
+        self._pending = nxt
         return loss.view(())
 
-    def __call__(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None):
-        loss = self.forward_backward(data, seed, logp)
+    def __call__(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None,
+                 next_data=None):
+        loss = self.forward_backward(data, seed, logp, next_data)
         world = self.bucket.world(self.group)
         self.bucket.allreduce_sum_(self.group)
         self.opt.step(grads=self.bucket.views(), grad_scale=1.0 / world)

@@ -240,28 +240,51 @@ int bgcn_bigcn_backward(const bgcn_bigcn_args* args, void* workspace, size_t wor
                         bgcn_stream_t stream);
 
 /* --------------------------------------------------------------------------
+ * Batch preparation: everything about a batch that does not depend on the weights -
+ * K1 (gcn_norm + CSR, both orientations) for TD and BU, tree pointers, node -> root map,
+ * tree work items, the ELL compaction of X (BGCN_FEAT_AUTO) and the CSC of X - into a
+ * caller-owned "prepared" buffer (size from bgcn_prepare_workspace_size).
+ * bgcn_train_step can prepare the NEXT batch on its auxiliary lane while it trains on
+ * the current one (the HBM-bound pass over X then overlaps the latency-bound chain).
+ * -------------------------------------------------------------------------- */
+typedef struct bgcn_batch {
+  const float* x; int64_t ldx;   /* [N, F] node features                     */
+  int64_t num_nodes;             /* N                                        */
+  int64_t num_graphs;            /* B                                        */
+  const int64_t* batch;          /* [N] sorted tree id per node              */
+  const int64_t* rootindex;      /* [B] global root node ids                 */
+  const int64_t* td_edge_index; int64_t td_num_edges;   /* [2, E_td]         */
+  const int64_t* bu_edge_index; int64_t bu_num_edges;   /* [2, E_bu]         */
+} bgcn_batch;
+
+size_t bgcn_prepare_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,
+                                   int64_t td_num_edges, int64_t bu_num_edges);
+/* feat_mode: BGCN_FEAT_AUTO builds the ELL/CSC of X, BGCN_FEAT_DENSE skips them.
+ * A bad edge index sets bit 0 of the buffer's status word (reported by the step). */
+int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree_on,
+                       int32_t feat_mode, void* prepared, size_t prepared_bytes,
+                       bgcn_stream_t stream);
+
+/* --------------------------------------------------------------------------
  * One training step up to the optimiser, as ONE call (the loop body of
- * BiGCN_Twitter.py:183-188): K1 for TD and BU (gcn_norm + CSR, auxiliary lane,
- * overlapped with the pass over X), the fused encoder forward, the head
+ * BiGCN_Twitter.py:183-188): the fused encoder forward on a prepared batch, the head
  * fc -> log_softmax (:129-130) and nll_loss mean (:186), and the complete backward.
  * Every gradient is WRITTEN (not accumulated), so grads[] may point into a flat
  * data-parallel bucket; the all-reduce and bgcn_adam_step follow.  Parameter order:
  * td_w1 td_b1 td_w2 td_b2 bu_w1 bu_b1 bu_w2 bu_b2 fc_w [C, 256] fc_b [C] (the
  * reference state_dict layout).  *status (optional, zeroed by the call): bit 0 = an
  * edge index outside [0, N) (skipped), bit 1 = a label outside [0, C) (ignored).
+ *   prepared / prepared_ready: the current batch's prepared buffer; when not ready the
+ *   call prepares it first (on the same stream).
+ *   next / next_prepared (optional): a batch to prepare during this step on the
+ *   auxiliary lane; pass it as the next call's prepared buffer with prepared_ready = 1.
  * -------------------------------------------------------------------------- */
 #define BGCN_STEP_PARAMS 10
 typedef struct bgcn_step_args {
-  const float* x; int64_t ldx;   /* [N, F] node features                     */
-  int64_t num_nodes;             /* N                                        */
-  int64_t num_graphs;            /* B                                        */
+  bgcn_batch cur;                /* the batch trained on                     */
   int64_t in_feats;              /* F                                        */
   int64_t num_classes;           /* C in [1, 16] (Twitter 4, Weibo 2)        */
-  const int64_t* batch;          /* [N] sorted tree id per node              */
-  const int64_t* rootindex;      /* [B] global root node ids                 */
   const int64_t* y;              /* [B] labels                               */
-  const int64_t* td_edge_index; int64_t td_num_edges;   /* [2, E_td]         */
-  const int64_t* bu_edge_index; int64_t bu_num_edges;   /* [2, E_bu]         */
   int32_t degree_on;             /* BGCN_DEGREE_ON_COL / _ROW                */
   int32_t training;              /* dropout on/off                           */
   uint64_t seed;                 /* dropout draw                             */
@@ -271,8 +294,12 @@ typedef struct bgcn_step_args {
   float* loss;                   /* [1] mean NLL                             */
   float* logp;                   /* [B, C] log-probabilities, or NULL        */
   int32_t* status;               /* [1] or NULL                              */
+  void* prepared; size_t prepared_bytes; int32_t prepared_ready;
+  const bgcn_batch* next;        /* or NULL                                  */
+  void* next_prepared; size_t next_prepared_bytes;
 } bgcn_step_args;
 
+/* workspace of the step itself (the prepared buffers are separate) */
 size_t bgcn_train_step_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,
                                       int64_t num_classes, int64_t td_num_edges,
                                       int64_t bu_num_edges);
@@ -310,10 +337,11 @@ int bgcn_keep_words(uint64_t seed, int64_t num_nodes, int32_t num_words, uint32_
  * kernel class of the fused encoder since bgcn_set_kernel_timing(mask) (process-wide;
  * events are recorded on the launch stream; mask bit c enables class c, 0 disables and
  * keeps the recorded events for bgcn_kernel_timing).  Classes:
- *   0 conv1 (dense: X*W1^T MFMA; auto: k_compact_conv1)  1 dW1 dense MFMA
+ *   0 conv1 (dense: X*W1^T MFMA; auto: k_compact_conv1, or the gather from a prepared ELL)
+ *   1 dW1 dense MFMA
  *   2 conv2 (dense MFMA + sparse root gather)            3 dW2 relu(H1) block MFMA
  *   4 gated dense conv1 fallback (auto)                  5 dW1 + dW2 root columns over CSC(X)
- *   6 gated dense dW1 fallback (auto) */
+ *   6 gated dense dW1 fallback (auto)                   7 ELL compaction of X (batch preparation) */
 int bgcn_set_kernel_timing(int enable);
 int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* launches);
 

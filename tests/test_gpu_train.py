@@ -134,3 +134,40 @@ def test_train_step_reports_bad_inputs():
     step.forward_backward(b, seed=1)
     with pytest.raises(IndexError, match="edge_index"):
         step.check_status()
+
+
+@pytest.mark.parametrize("mode", ["auto", "dense"])
+def test_next_batch_prefetch_matches_plain_steps(mode):
+    """Preparing the next batch inside a step (side lane) gives bitwise the same losses and
+    gradients as preparing every batch inside its own step; a prefetched buffer is only
+    used when the next call trains on that very batch."""
+    from bigcn_amd import FusedTrainStep
+    batches = [_synth(40 + k, 24, 150) for k in range(3)]
+    p = O.make_params(5000, 64, 64, 4, seed=17)
+    ref, got = [], []
+    m1 = _model(p, mode)
+    s1 = FusedTrainStep(m1)
+    for k, b in enumerate(batches):
+        loss = s1.forward_backward(b, seed=k)
+        ref.append((loss.clone(), [v.clone() for v in s1.grads().values()]))
+    m2 = _model(p, mode)
+    s2 = FusedTrainStep(m2)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):                       # non-default stream: real side lane
+        for k, b in enumerate(batches):
+            nxt = batches[k + 1] if k + 1 < len(batches) else None
+            loss = s2.forward_backward(b, seed=k, next_data=nxt)
+            got.append((loss.clone(), [v.clone() for v in s2.grads().values()]))
+        # a prefetched batch that is not the next one trained on is ignored
+        s2.forward_backward(batches[0], seed=9, next_data=batches[1])
+        loss = s2.forward_backward(batches[2], seed=2)
+        got_last = [v.clone() for v in s2.grads().values()]
+    torch.cuda.synchronize()
+    for (l1, g1), (l2, g2) in zip(ref, got):
+        assert torch.equal(l1, l2)
+        for a, c in zip(g1, g2):
+            assert torch.equal(a, c)
+    for a, c in zip(ref[2][1], got_last):
+        assert torch.equal(a, c)
+    s2.check_status()
