@@ -124,26 +124,40 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ X, 
 // ---------------------------------------------------------------- dW2
 // part[d][s][o][c] = sum_{i in split s} dZ2[i][d*H+o] * A2_d[i][c]   (A2_d generated)
 // Block tile 64 (o) x 64 (c), waves 2 x 2; grid (ceil((H+F)/64), S, 2).
+// One launch configuration of k_dw2: a grid of gx column tiles x S node splits x 2
+// directions over partial rows of ldp columns.
+struct Dw2Cfg {
+  int64_t kchunk;
+  int S, gx, want_dense;
+  int64_t ldp;
+  float* part;
+};
+
+// Two configurations share one launch (blocks [0, nblk0) run cfg0, the rest cfg1): the
+// dense path's full grid (all 64+F columns, few node splits; want_dense = 1) and the
+// sparse path's relu(H1) block only (column tile 0, many node splits, ldp = 64;
+// want_dense = 0).  Only the configuration of the path selected on the device works.
 __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_t ldx, int64_t F,
                                              const float* __restrict__ H1,
                                              const float* __restrict__ dZ2,
-                                             const int32_t* __restrict__ node_root,
-                                             float* __restrict__ part, int64_t N, int64_t kchunk,
-                                             int S, KeepSrc keep, const int32_t* __restrict__ gate,
-                                             int want_dense, int64_t ldp) {
-  // Two launch configurations share this kernel: the dense path's full grid (all 64+F
-  // columns, few node splits; want_dense = 1) and the sparse path's relu(H1) block only
-  // (column tile 0, many node splits, partial rows of ldp = 64; want_dense = 0).  Only
-  // the configuration of the path selected on the device does any work.
-  if (dense_active(gate) != (want_dense != 0)) return;
+                                             const int32_t* __restrict__ node_root, int64_t N,
+                                             KeepSrc keep, const int32_t* __restrict__ gate,
+                                             Dw2Cfg cfg0, Dw2Cfg cfg1, int nblk0) {
+  const bool second = int(blockIdx.x) >= nblk0;
+  const Dw2Cfg& cfg = second ? cfg1 : cfg0;
+  const int bl = second ? int(blockIdx.x) - nblk0 : int(blockIdx.x);
+  if (dense_active(gate) != (cfg.want_dense != 0)) return;
+  const int64_t kchunk = cfg.kchunk, ldp = cfg.ldp;
+  const int S = cfg.S;
+  float* __restrict__ part = cfg.part;
   constexpr int BN = 64;
   __shared__ float As[2][BK * H];   // [node][o]
   __shared__ float Bs[2][BK * BN];  // [node][c]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int d = blockIdx.z, split = blockIdx.y;
+  const int bx = bl % cfg.gx, split = (bl / cfg.gx) % S, d = bl / (cfg.gx * S);
   const int64_t K2 = H + F;
-  const int64_t c0 = int64_t(blockIdx.x) * BN;
+  const int64_t c0 = int64_t(bx) * BN;
   const int64_t kb = int64_t(split) * kchunk, ke = min<int64_t>(kb + kchunk, N);
   const float sc = keep.scale();
 
@@ -224,18 +238,29 @@ __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_
 // from k_dw2_rootcols).  A block owns 64 consecutive outputs; its 4 waves take splits
 // s = q (mod 4), four loads in flight each, combined in wave order: deterministic.
 // Grid-stride over output tiles, so a small grid retires cheaply when the gate skips it.
-__global__ __launch_bounds__(256) void k_reduce_dw2(const float* __restrict__ part, int S,
-                                                    int64_t ldp, int64_t K2,
+struct RedCfg {
+  int S;
+  int64_t ldp;
+  int want_dense;
+  int blocks;   // blocks of this configuration in the launch
+};
+
+__global__ __launch_bounds__(256) void k_reduce_dw2(const float* __restrict__ part, int64_t K2,
                                                     float* __restrict__ dw_td,
                                                     float* __restrict__ dw_bu,
-                                                    const int32_t* __restrict__ gate,
-                                                    int want_dense) {
-  if (dense_active(gate) != (want_dense != 0)) return;
+                                                    const int32_t* __restrict__ gate, RedCfg c0,
+                                                    RedCfg c1) {
+  const bool second = int(blockIdx.x) >= c0.blocks;
+  const RedCfg& cfg = second ? c1 : c0;
+  const int bl = second ? int(blockIdx.x) - c0.blocks : int(blockIdx.x);
+  if (dense_active(gate) != (cfg.want_dense != 0)) return;
+  const int S = cfg.S;
+  const int64_t ldp = cfg.ldp;
   __shared__ float red[4][64];
   const int64_t per = int64_t(H) * ldp;
   const int64_t ntiles = (2 * per + 63) / 64;
   const int q = threadIdx.x >> 6, t = threadIdx.x & 63;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int64_t tile = bl; tile < ntiles; tile += cfg.blocks) {
     const int64_t idx = tile * 64 + t;
     const bool valid = idx < 2 * per;
     const int d = valid ? int(idx / per) : 0;
@@ -773,22 +798,24 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   if (side_busy) x = s;
   else BGCN_TRY(aux_fork(s, kLaneSide, &x));
   timing_begin(3, x);
-  hipLaunchKernelGGL(k_dw2, dim3(grid_for(H + F, 64), w.S2, 2), dim3(256), 0, x, a->x, a->ldx, F,
-                     a->h1, w.dz2, w.node_root, w.dw2_part, N, w.kchunk2, w.S2, keep, gate, 1, H + F);
-  BGCN_CHECK_LAUNCH();
-  if (sparse) {
-    hipLaunchKernelGGL(k_dw2, dim3(1, w.Sh, 2), dim3(256), 0, x, a->x, a->ldx, F, a->h1, w.dz2,
-                       w.node_root, w.dw2_part, N, w.kchunkh, w.Sh, keep, gate, 0, int64_t(H));
+  {   // dense config (gated) and, in auto mode, the sparse relu(H1)-block config: one launch
+    const int gxd = int(grid_for(H + F, 64));
+    const Dw2Cfg dense{w.kchunk2, w.S2, gxd, 1, H + F, w.dw2_part};
+    const Dw2Cfg sparsec{w.kchunkh, w.Sh, 1, 0, int64_t(H), w.dw2_part};
+    const int n0 = gxd * w.S2 * 2, n1 = sparse ? w.Sh * 2 : 0;
+    hipLaunchKernelGGL(k_dw2, dim3(unsigned(n0 + n1)), dim3(256), 0, x, a->x, a->ldx, F, a->h1, w.dz2,
+                       w.node_root, N, keep, gate, dense, sparsec, n0);
     BGCN_CHECK_LAUNCH();
   }
   timing_end(3, x);
-  hipLaunchKernelGGL(k_reduce_dw2, dim3(std::min<unsigned>(grid_for(2 * H * (H + F), 64), 1024)),
-                     dim3(256), 0, x, w.dw2_part, w.S2, H + F, H + F, a->td_dw2, a->bu_dw2, gate, 1);
-  BGCN_CHECK_LAUNCH();
-  if (sparse) {
-    hipLaunchKernelGGL(k_reduce_dw2, dim3(grid_for(2 * H * H, 64)), dim3(256), 0, x, w.dw2_part,
-                       w.Sh, int64_t(H), H + F, a->td_dw2, a->bu_dw2, gate, 0);
+  {   // the matching split reductions, also one launch
+    const RedCfg dense{w.S2, H + F, 1, int(std::min<unsigned>(grid_for(2 * H * (H + F), 64), 1024))};
+    const RedCfg sparsec{w.Sh, int64_t(H), 0, int(grid_for(2 * H * H, 64))};
+    hipLaunchKernelGGL(k_reduce_dw2, dim3(unsigned(dense.blocks + (sparse ? sparsec.blocks : 0))),
+                       dim3(256), 0, x, w.dw2_part, H + F, a->td_dw2, a->bu_dw2, gate, dense, sparsec);
     BGCN_CHECK_LAUNCH();
+  }
+  if (sparse) {
     BGCN_TRY(sparse_dw2_root_part(sp, a->tree_ptr, w.dz2, x));
     if (!have_csc) BGCN_TRY(sparse_csc(sp, x));
     BGCN_TRY(sparse_dw2_rootcols(sp, a, w.node_root, keep, x));
