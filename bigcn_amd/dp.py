@@ -25,6 +25,11 @@ def init_from_env(backend: str = "nccl"):
         return 0, 1, 0
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    # BGCN_DIST_BACKEND overrides the backend (e.g. gloo to rehearse several ranks on one
+    # GPU; ranks then share devices round-robin)
+    backend = os.environ.get("BGCN_DIST_BACKEND", backend)
+    if backend != "nccl" and torch.cuda.is_available() and torch.cuda.device_count() > 0:
+        local = local % torch.cuda.device_count()
     if not dist.is_initialized():
         if backend == "nccl":
             torch.cuda.set_device(local)
