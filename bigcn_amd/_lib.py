@@ -13,7 +13,8 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
-from ctypes import POINTER, Structure, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+from ctypes import (POINTER, Structure, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_size_t,
+                    c_uint64, c_void_p)
 
 import torch
 
@@ -37,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_gemm_xwt", "bgcn_gemm_xw", "bgcn_gemm_tn_workspace_size", "bgcn_gemm_tn",
     "bgcn_colsum_workspace_size", "bgcn_colsum",
     "bgcn_scatter_mean_workspace_size", "bgcn_scatter_mean_fwd", "bgcn_scatter_mean_bwd",
+    "bgcn_drop_edges_workspace_size", "bgcn_drop_edges",
     "bgcn_bigcn_workspace_size", "bgcn_bigcn_forward", "bgcn_bigcn_backward",
     "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_adam_step",
     "bgcn_prepare_workspace_size", "bgcn_prepare_batch",
@@ -87,6 +89,7 @@ class BatchDesc(Structure):
         ("batch", c_void_p), ("rootindex", c_void_p),
         ("td_edge_index", c_void_p), ("td_num_edges", c_int64),
         ("bu_edge_index", c_void_p), ("bu_num_edges", c_int64),
+        ("td_droprate", c_double), ("bu_droprate", c_double), ("drop_seed", c_uint64),
     ]
 
 
@@ -139,6 +142,10 @@ _SIGS = {
     "bgcn_bigcn_backward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
     "bgcn_keep_words": (c_int, [c_uint64, c_int64, c_int32, c_void_p, c_void_p]),
     "bgcn_adam_step": (c_int, [c_void_p, c_void_p]),
+    "bgcn_drop_edges_workspace_size": (c_size_t, [c_int64]),
+    "bgcn_drop_edges": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_int64, c_void_p, c_int64, c_double,
+                                c_void_p, c_int64, c_void_p, c_int64, c_int64, c_uint64, c_int32, c_void_p,
+                                c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_prepare_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64, c_int64]),
     "bgcn_prepare_batch": (c_int, [POINTER(BatchDesc), c_int64, c_int32, c_int32, c_void_p, c_size_t,
                                    c_void_p]),

@@ -142,9 +142,19 @@ struct Prepared {
   float* csc_val;
   void* gws;
   size_t gws_bytes;
+  int64_t *td_drop, *bu_drop;            // [2, E] masked DropEdge lists (device DropEdge)
+  void* dws;
+  size_t dws_bytes;
 };
 size_t carve_prepared(Carve& c, int64_t N, int64_t B, int64_t F, int64_t Etd, int64_t Ebu,
                       Prepared* p);
+
+// ---- DropEdge (bgcn_drop.hip)
+size_t drop_ws_size(int64_t B);
+int drop_edges_impl(const int64_t* td, int64_t Etd, int64_t* td_out, int64_t ld_td, double td_rate,
+                    const int64_t* bu, int64_t Ebu, int64_t* bu_out, int64_t ld_bu, double bu_rate,
+                    const int64_t* batch, int64_t N, int64_t B, uint64_t seed, int masked,
+                    int64_t* counts, int32_t* status, void* ws, size_t ws_bytes, hipStream_t s);
 
 // ---- one training step (bgcn_step.hip)
 size_t train_step_ws_size(int64_t N, int64_t B, int64_t F, int64_t C, int64_t Etd, int64_t Ebu);

@@ -120,6 +120,7 @@ int check_batch(const bgcn_batch* b) {
   BGCN_CHECK_ARG(b->x && b->batch && b->rootindex, "null pointer");
   BGCN_CHECK_ARG((b->td_num_edges == 0 || b->td_edge_index) && (b->bu_num_edges == 0 || b->bu_edge_index),
                  "null edge_index");
+  BGCN_CHECK_ARG(b->td_droprate < 1.0 && b->bu_droprate < 1.0, "droprate must be < 1");
   return BGCN_OK;
 }
 
@@ -152,6 +153,10 @@ size_t carve_prepared(Carve& c, int64_t N, int64_t B, int64_t F, int64_t Etd, in
   t.col_end = c.take<int32_t>(size_t(F));
   t.csc_slot = c.take<uint32_t>(size_t(N) * BGCN_SPARSE_CAP);
   t.csc_val = c.take<float>(size_t(N) * BGCN_SPARSE_CAP);
+  t.td_drop = c.take<int64_t>(size_t(2 * Etd));
+  t.bu_drop = c.take<int64_t>(size_t(2 * Ebu));
+  t.dws_bytes = drop_ws_size(B);
+  t.dws = c.take<char>(t.dws_bytes);
   if (p) *p = t;
   return c.off;
 }
@@ -173,9 +178,20 @@ static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_
   Carve c(buf, bytes);
   carve_prepared(c, N, B, F, b->td_num_edges, b->bu_num_edges, &p);
   BGCN_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int32_t), gs));
-  BGCN_TRY(bgcn_build_graph_pair(b->td_edge_index, b->td_num_edges, b->bu_edge_index,
-                                 b->bu_num_edges, N, degree_on, &p.td, &p.bu, p.status, p.gws,
-                                 p.gws_bytes, reinterpret_cast<bgcn_stream_t>(gs)));
+  const int64_t* td = b->td_edge_index;
+  const int64_t* bu = b->bu_edge_index;
+  if (b->td_droprate > 0.0 || b->bu_droprate > 0.0) {
+    // DropEdge (dataset.py:68-90) in the masked form: dropped edges become self loops,
+    // which K1 removes - same graphs as the compacted lists, no kept count on the host
+    BGCN_TRY(drop_edges_impl(td, b->td_num_edges, p.td_drop, b->td_num_edges, b->td_droprate, bu,
+                             b->bu_num_edges, p.bu_drop, b->bu_num_edges, b->bu_droprate, b->batch,
+                             N, B, b->drop_seed, 1, nullptr, p.status, p.dws, p.dws_bytes, gs));
+    if (td) td = p.td_drop;
+    if (bu) bu = p.bu_drop;
+  }
+  BGCN_TRY(bgcn_build_graph_pair(td, b->td_num_edges, bu, b->bu_num_edges, N, degree_on, &p.td,
+                                 &p.bu, p.status, p.gws, p.gws_bytes,
+                                 reinterpret_cast<bgcn_stream_t>(gs)));
   const int mode = (feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxFeat) ? 1 : 0;
   BGCN_TRY(sparse_prepare(p, N, B, F, mode, b->batch, b->rootindex, b->x, b->ldx, s));
   if (out) *out = p;

@@ -120,6 +120,51 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, edge_weight: Optional[
     return g
 
 
+def drop_edges(td_edge_index: Optional[torch.Tensor], bu_edge_index: Optional[torch.Tensor],
+               batch: torch.Tensor, num_graphs: int, tddroprate: float = 0.0, budroprate: float = 0.0,
+               seed: int = 0, masked: bool = False):
+    """DropEdge of ``Process/dataset.py:68-90`` on the device, per tree of a collated batch:
+    keep a uniform random subset of exactly ``int(E_t * (1 - rate))`` edges in their
+    original order (``rate <= 0`` keeps all).  TD and BU are drawn independently from
+    ``seed`` (a counter-based draw, not Python's ``random`` stream).
+
+    ``masked=False`` returns the compacted lists (one host sync for the kept counts);
+    ``masked=True`` returns ``[2, E]`` lists in which every dropped edge ``(s, d)`` is the
+    self loop ``(d, d)``, which :func:`build_graph` removes (no sync)."""
+    ref = td_edge_index if td_edge_index is not None else bu_edge_index
+    if ref is None:
+        raise ValueError("drop_edges: no edge list given")
+    _dev_check(td_edge_index, bu_edge_index, batch)
+    td = None if td_edge_index is None else _check_ei(td_edge_index)
+    bu = None if bu_edge_index is None else _check_ei(bu_edge_index)
+    batch = batch.to(torch.int64).contiguous()
+    N, B = int(batch.numel()), int(num_graphs)
+    dev = batch.device
+    td_out = None if td is None else torch.empty_like(td)
+    bu_out = None if bu is None else torch.empty_like(bu)
+    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    L = _lib.lib()
+    ws = workspace(L.bgcn_drop_edges_workspace_size(B), dev)
+    Etd = 0 if td is None else int(td.size(1))
+    Ebu = 0 if bu is None else int(bu.size(1))
+    check(L.bgcn_drop_edges(ptr(td), Etd, float(tddroprate), ptr(td_out), max(Etd, 1),
+                            ptr(bu), Ebu, float(budroprate), ptr(bu_out), max(Ebu, 1), ptr(batch), N, B,
+                            int(seed) & (2**64 - 1), int(masked), ptr(counts), ptr(status), ptr(ws),
+                            ws.numel(), stream_handle()))
+    if masked:
+        return td_out, bu_out
+    kept = counts.cpu()
+    if int(status.item()) & 1:
+        raise IndexError("drop_edges: an edge index is out of range or the edges are not "
+                         "grouped by tree in batch order")
+    if td_out is not None:
+        td_out = td_out[:, :int(kept[0])].contiguous()
+    if bu_out is not None:
+        bu_out = bu_out[:, :int(kept[1])].contiguous()
+    return td_out, bu_out
+
+
 # ----------------------------------------------------------------------------- K3/K4
 def spmm(g: Graph, x: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
          transposed: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -205,6 +250,10 @@ def gcn_conv(x: torch.Tensor, edge_index_or_graph, weight: torch.Tensor,
              bias: Optional[torch.Tensor] = None, edge_weight: Optional[torch.Tensor] = None,
              degree_on: str = "col") -> torch.Tensor:
     _dev_check(x, weight, bias)
+    if edge_weight is not None and edge_weight.requires_grad and torch.is_grad_enabled():
+        # EBGCN (EBGCN.py:84,178) learns edge weights; that gradient is not on this path
+        raise NotImplementedError("gcn_conv: gradients w.r.t. edge_weight are not supported; "
+                                  "pass edge_weight.detach()")
     g = edge_index_or_graph
     if not isinstance(g, Graph):
         g = build_graph(g, x.size(0), edge_weight, degree_on)

@@ -46,8 +46,18 @@ class FusedTrainStep:
     ``self.bucket`` (``grads()`` maps them back to the parameters)."""
 
     def __init__(self, model: BiGCN, optimizer: Optional[FusedAdam] = None, degree_on: str = "col",
-                 group=None):
+                 group=None, tddroprate: float = 0.0, budroprate: float = 0.0,
+                 drop_seed: Optional[int] = None):
         self.model = model
+        # DropEdge on the device (dataset.py:68-90): batches are then passed UNDROPPED
+        # (BiGraphDataset(tddroprate=0, budroprate=0)) and each preparation draws its own
+        # kept subsets; batch k prepared by this object uses drop seed drop_seed + k
+        if not (0.0 <= tddroprate < 1.0 and 0.0 <= budroprate < 1.0):
+            raise ValueError("droprates must be in [0, 1)")
+        self.tddroprate, self.budroprate = float(tddroprate), float(budroprate)
+        self._drop_seed = _draw_seed() if drop_seed is None else int(drop_seed)
+        self._drop_count = 0
+        self.last_drop_seed = None
         self.opt = optimizer if optimizer is not None else bigcn_adam(model)
         self.group = group
         self.bucket = GradBucket(self.opt.params())
@@ -88,6 +98,10 @@ class FusedTrainStep:
         d.batch, d.rootindex = ptr(batch), ptr(root)
         d.td_edge_index, d.td_num_edges = ptr(td_ei), td_ei.size(1)
         d.bu_edge_index, d.bu_num_edges = ptr(bu_ei), bu_ei.size(1)
+        if self.model.training and (self.tddroprate > 0 or self.budroprate > 0):
+            d.td_droprate, d.bu_droprate = self.tddroprate, self.budroprate
+            d.drop_seed = (self._drop_seed + self._drop_count) & (2**64 - 1)
+            self._drop_count += 1
         return d, (x, td_ei, bu_ei, batch, root)
 
     def _prep_buffer(self, d, F):
@@ -105,24 +119,27 @@ class FusedTrainStep:
         ready (matched by identity - do not mutate the batch in between).  Every call
         still does exactly one preparation's worth of work."""
         m = self.model
-        d, keep = self._desc(data)
         F = int(data.x.size(1))
         y = _need(data.y, torch.int64, "y")
         if seed is None:
             seed = _draw_seed() if m.training else 0
+        mode = _FEAT_MODES[m.feat_mode]
+        pend = self._pending
+        if pend is not None and pend[0] is data and pend[2] == (mode, m.training):
+            # prepared by the previous call (its descriptor, drop seed and inputs)
+            prep, keep, d = pend[1], pend[3], pend[4]
+            ready = 1
+        else:
+            d, keep = self._desc(data)
+            prep = self._prep_buffer(d, F)
+            ready = 0
         a = self._args
         a.cur = d
         a.in_feats = F
         a.y = ptr(y)
         a.training, a.seed = int(m.training), int(seed) & (2**64 - 1)
-        a.feat_mode = _FEAT_MODES[m.feat_mode]
-        pend = self._pending
-        if pend is not None and pend[0] is data and pend[2] == a.feat_mode:
-            prep = pend[1]
-            a.prepared_ready = 1
-        else:
-            prep = self._prep_buffer(d, F)
-            a.prepared_ready = 0
+        a.feat_mode = mode
+        a.prepared_ready = ready
         a.prepared, a.prepared_bytes = ptr(prep), prep.numel()
         self._pending = None
         nxt = None
@@ -132,10 +149,11 @@ class FusedTrainStep:
             self._next_desc = nd                     # the struct must outlive the call
             a.next = ctypes.pointer(self._next_desc)
             a.next_prepared, a.next_prepared_bytes = ptr(nbuf), nbuf.numel()
-            nxt = (next_data, nbuf, a.feat_mode, nkeep)
+            nxt = (next_data, nbuf, (mode, m.training), nkeep, nd)
         else:
             a.next = None
             a.next_prepared, a.next_prepared_bytes = 0, 0
+        self.last_drop_seed = int(a.cur.drop_seed) if a.cur.td_droprate > 0 or a.cur.bu_droprate > 0 else None
         loss = torch.empty(1, dtype=torch.float32, device=data.x.device)
         a.loss, a.logp, a.status = ptr(loss), ptr(logp), ptr(self.status)
         L = _lib.lib()

@@ -164,6 +164,31 @@ int bgcn_scatter_mean_bwd(const float* dout, int64_t ld_dout, const int64_t* ind
                           int64_t ld_dsrc, bgcn_stream_t stream);
 
 /* --------------------------------------------------------------------------
+ * DropEdge (Process/dataset.py:68-90): per tree, keep a uniform random subset of
+ * exactly int(E_t * (1 - droprate)) edges (count computed in double as Python does),
+ * in their original order; droprate <= 0 keeps every edge (the reference's
+ * `if droprate > 0`).  TD (list 0) and BU (list 1) are drawn independently; either
+ * list may be NULL.  The draw is a counter-based function of (seed, list, edge
+ * position) instead of Python's `random.sample`; same distribution, different stream.
+ * Lists: int64 [2, E] (row stride E) in PyG collation order - each tree's edges
+ * contiguous, trees ascending; tree of an edge = batch[src].
+ *   masked = 0: the kept edges, compacted in order, into out [2, ld] (ld = row stride);
+ *               counts[0..1] (device, optional) receive the kept totals.  ld below the
+ *               total sets *status bit 0 and the excess is not written.
+ *   masked = 1: out [2, ld >= E] in place order with every dropped edge (s, d) written
+ *               as the self loop (d, d); bgcn_build_graph removes input self loops, so
+ *               the graph equals that of the compacted list (no kept count needed).
+ * An edge out of range, crossing trees or out of tree order sets *status bit 0.
+ * -------------------------------------------------------------------------- */
+size_t bgcn_drop_edges_workspace_size(int64_t num_graphs);
+int bgcn_drop_edges(const int64_t* td_edge_index, int64_t td_num_edges, double td_droprate,
+                    int64_t* td_out, int64_t ld_td_out, const int64_t* bu_edge_index,
+                    int64_t bu_num_edges, double bu_droprate, int64_t* bu_out, int64_t ld_bu_out,
+                    const int64_t* batch, int64_t num_nodes, int64_t num_graphs, uint64_t seed,
+                    int32_t masked, int64_t* counts, int32_t* status, void* workspace,
+                    size_t workspace_bytes, bgcn_stream_t stream);
+
+/* --------------------------------------------------------------------------
  * Fused bidirectional BiGCN encoder: TDrumorGCN + BUrumorGCN forward/backward
  * (BiGCN_Twitter.py:26-67 and :77-114, Weibo :22-44 / :52-74), producing the
  * head input cat(BU_x, TD_x) [B, 256] of BiGCN.forward (:126-128).
@@ -255,6 +280,11 @@ typedef struct bgcn_batch {
   const int64_t* rootindex;      /* [B] global root node ids                 */
   const int64_t* td_edge_index; int64_t td_num_edges;   /* [2, E_td]         */
   const int64_t* bu_edge_index; int64_t bu_num_edges;   /* [2, E_bu]         */
+  /* DropEdge on the device (optional; zero = off): when a rate is > 0 the lists above
+   * are the undropped ones and preparation draws the kept subsets itself
+   * (bgcn_drop_edges, masked form) from drop_seed before building the graphs. */
+  double td_droprate, bu_droprate;
+  uint64_t drop_seed;
 } bgcn_batch;
 
 size_t bgcn_prepare_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,

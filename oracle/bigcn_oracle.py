@@ -254,3 +254,57 @@ def reference_grads(p: Dict[str, torch.Tensor], batch: dict, training: bool = Fa
     loss = bigcn_loss(logp, batch["y"])
     loss.backward()
     return loss.detach(), logp.detach(), {k: v.grad.detach().clone() for k, v in q.items()}
+
+
+# ----------------------------------------------------------------------------
+# DropEdge (Process/dataset.py:68-90), restated for the device draw
+# ----------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def drop_key(seed: int, direction: int, e):
+    """The 32-bit key of edge position ``e`` (numpy array) of list ``direction``
+    (0 = TD, 1 = BU): splitmix64 finaliser with the salt used by bgcn_drop.hip."""
+    import numpy as np
+    e = np.asarray(e, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        base = np.uint64(((int(seed) & _M64) ^ 0xD1B54A32D192ED03) & _M64)
+        z = base + np.uint64(0x9E3779B97F4A7C15) * (((e << np.uint64(1)) | np.uint64(direction))
+                                                    + np.uint64(1))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(32)).astype(np.uint32)
+
+
+def kept_count(length: int, droprate: float) -> int:
+    """``int(length * (1 - droprate))`` exactly as ``dataset.py:72,84`` computes it
+    (only applied when ``droprate > 0``)."""
+    return int(length * (1 - droprate)) if droprate > 0 else int(length)
+
+
+def drop_edges(edge_index, batch, num_graphs: int, droprate: float, seed: int, direction: int,
+               masked: bool = False):
+    """Per tree (edges grouped by tree in collation order, tree = batch[src]): keep the
+    ``kept_count`` edges with the smallest (key, position), in original order - the
+    device's uniform random subset, restated bit for bit.  Returns the kept [2, E']
+    list, or with ``masked`` the [2, E] list whose dropped edges (s, d) read (d, d)."""
+    import numpy as np
+    ei = np.asarray(edge_index, dtype=np.int64)
+    b = np.asarray(batch, dtype=np.int64)
+    E = ei.shape[1]
+    tree = b[ei[0]] if E else np.zeros(0, np.int64)
+    assert np.all(np.diff(tree) >= 0), "edges must be grouped by tree"
+    bounds = np.searchsorted(tree, np.arange(num_graphs + 1), side="left")
+    keep = np.zeros(E, dtype=bool)
+    for t in range(num_graphs):
+        e0, e1 = int(bounds[t]), int(bounds[t + 1])
+        k = kept_count(e1 - e0, droprate)
+        pos = np.arange(e0, e1)
+        order = np.lexsort((pos, drop_key(seed, direction, pos)))   # key, then position
+        keep[pos[order[:k]]] = True
+    if masked:
+        out = ei.copy()
+        out[0, ~keep] = ei[1, ~keep]
+        return out
+    return ei[:, keep]

@@ -62,7 +62,7 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     structs = {
         "bgcn_graph_view": _lib.GraphView, "bgcn_csr_out": _lib.CsrOut,
         "bgcn_bigcn_args": _lib.BiGCNArgs, "bgcn_step_args": _lib.StepArgs,
-        "bgcn_adam_args": AdamArgs,
+        "bgcn_adam_args": AdamArgs, "bgcn_batch": _lib.BatchDesc,
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for cname, py in structs.items():

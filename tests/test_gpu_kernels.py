@@ -251,3 +251,33 @@ def test_gcnconv_module_fwd_bwd():
     close(xd.grad, x.grad, what="dx")
     close(conv.lin.weight.grad, w.grad, what="dW")
     close(conv.bias.grad, b.grad, what="db")
+
+
+@pytest.mark.parametrize("degree_on", ["col", "row"])
+def test_gcnconv_edge_weight_fwd_bwd(degree_on):
+    """GCNConv(x, edge_index, edge_weight) as EBGCN calls it (EBGCN.py:84,178): the
+    per-edge weight enters gcn_norm's degree and every message; grads w.r.t. x, W, b."""
+    from bigcn_amd import GCNConv
+    rng = np.random.default_rng(12)
+    ei, N = rand_forest(rng, [40, 2, 130], star=True)
+    ew = torch.rand(ei.size(1), dtype=torch.float64) * 2.0 + 0.05
+    torch.manual_seed(1)
+    conv = GCNConv(96, 64, degree_on=degree_on).to(DEV)
+    with torch.no_grad():
+        conv.bias.uniform_(-0.1, 0.1)
+    x = torch.randn(N, 96, dtype=torch.float64, requires_grad=True)
+    w = conv.lin.weight.detach().double().cpu().requires_grad_(True)
+    b = conv.bias.detach().double().cpu().requires_grad_(True)
+    ref = O.gcn_conv(x, ei, w, b, edge_weight=ew, degree_on=degree_on)
+    gout = torch.randn_like(ref)
+    ref.backward(gout)
+    xd = x.detach().float().to(DEV).requires_grad_(True)
+    out = conv(xd, ei.to(DEV), ew.float().to(DEV))
+    out.backward(gout.float().to(DEV))
+    close(out, ref, what="out")
+    close(xd.grad, x.grad, what="dx")
+    close(conv.lin.weight.grad, w.grad, what="dW")
+    close(conv.bias.grad, b.grad, what="db")
+    # a learnable edge weight (EBGCN's edge inference) is refused, not silently detached
+    with pytest.raises(NotImplementedError):
+        conv(xd, ei.to(DEV), ew.float().to(DEV).requires_grad_(True))

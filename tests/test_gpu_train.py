@@ -171,3 +171,69 @@ def test_next_batch_prefetch_matches_plain_steps(mode):
     for a, c in zip(ref[2][1], got_last):
         assert torch.equal(a, c)
     s2.check_status()
+
+
+@pytest.mark.parametrize("mode", ["auto", "dense"])
+@pytest.mark.parametrize("training", [False, True])
+def test_pheme_768_dense_features(training, mode):
+    """PHEME version 2 (BiGCN_Twitter.py:139-140,177-182): x = the [CLS] BERT embedding,
+    768 dense signed features per node.  In auto mode every row overflows the sparse
+    (ELL) capacity, so the device flag routes the whole step to the dense kernels; the
+    relu on the root-extended x (:51) is no longer a no-op."""
+    from bigcn_amd import FusedTrainStep
+    from bigcn_amd.ops import keep_words, unpack_keep
+    b = _synth(33, 16, 90, F=768, root_random=True)
+    g = torch.Generator().manual_seed(33)
+    b.x = torch.randn(b.x.shape, generator=g).to(DEV)
+    p = O.make_params(768, 64, 64, 4, seed=13)
+    m = _model(p, mode)
+    m.train(training)
+    step = FusedTrainStep(m)
+    N = b.x.size(0)
+    seed = 99
+    logp = torch.empty(b.num_graphs, 4, device=DEV)
+    loss = step.forward_backward(b, seed=seed, logp=logp)
+    masks = (None, None)
+    if training:
+        mk = unpack_keep(keep_words(seed, N, 768, DEV).cpu(), 64 + 768)
+        masks = (mk[0], mk[1])
+    rlogp, rloss, rgrads, _ = _oracle(b, p, training, *masks)
+    close(logp, rlogp, what="logp")
+    close(loss, rloss, what="loss")
+    gr = step.grads()
+    for k, prm in zip(KEYS, step.step_params):
+        close(gr[prm], rgrads[k], what=k)
+    step.check_status()
+    # the module path (per-op autograd encoder) on the same batch
+    m.zero_grad()
+    out = m(b, seed=seed) if training else m(b)
+    close(out, rlogp, what="module logp")
+
+
+@pytest.mark.parametrize("training", [False, True])
+def test_sparse_signed_features(training):
+    """Sparse rows with negative values (the auto/ELL path): relu(x_root) must be taken
+    per stored value, and negative stored values must not count as dropped columns."""
+    from bigcn_amd import FusedTrainStep
+    from bigcn_amd.ops import keep_words, unpack_keep
+    b = _synth(34, 12, 70, F=2000, root_random=True)
+    sign = torch.where(torch.rand(b.x.shape, device=DEV) < 0.5, -1.0, 1.0)
+    b.x = b.x * sign
+    p = O.make_params(2000, 64, 64, 4, seed=14)
+    m = _model(p, "auto")
+    m.train(training)
+    step = FusedTrainStep(m)
+    N = b.x.size(0)
+    seed = 7
+    logp = torch.empty(b.num_graphs, 4, device=DEV)
+    loss = step.forward_backward(b, seed=seed, logp=logp)
+    masks = (None, None)
+    if training:
+        mk = unpack_keep(keep_words(seed, N, 2000, DEV).cpu(), 64 + 2000)
+        masks = (mk[0], mk[1])
+    rlogp, rloss, rgrads, _ = _oracle(b, p, training, *masks)
+    close(logp, rlogp, what="logp")
+    close(loss, rloss, what="loss")
+    gr = step.grads()
+    for k, prm in zip(KEYS, step.step_params):
+        close(gr[prm], rgrads[k], what=k)
