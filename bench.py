@@ -102,13 +102,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_pool(wl, rank, pool, device):
+def make_pool(wl, rank, pool, device, drop=None):
+    """drop: (td, bu) rates applied on the host at synthesis (the reference's DataLoader
+    does it per sample); (0, 0) when the step drops edges on the device."""
     from bigcn_amd.data import synth_batch, synth_tree_sizes
+    drop = wl["drop"] if drop is None else drop
     out = []
     for i in range(pool):
         rng = np.random.default_rng(20250205 + 1 + 1000 * rank + i)
         sizes = synth_tree_sizes(rng, wl["trees"], wl["mean"], wl["sigma"])
-        out.append(synth_batch(rng, sizes, wl["feats"], wl["classes"], *wl["drop"], device=device))
+        out.append(synth_batch(rng, sizes, wl["feats"], wl["classes"], *drop, device=device))
     return out
 
 
@@ -198,6 +201,9 @@ def main():
                     help="at N=1 also time the standalone 5000-wide aggregation A_hat . X")
     ap.add_argument("--compare-dense", type=int, default=1,
                     help="at N=1 also time the dense MFMA path and report it beside the main line")
+    ap.add_argument("--dropedge", default="device", choices=["device", "host"],
+                    help="fused path: DropEdge (dataset.py:68-90) inside the step's batch "
+                         "preparation on the device, or pre-applied at synthesis on the host")
     args = ap.parse_args()
 
     from bigcn_amd import BiGCN, FusedTrainStep
@@ -212,7 +218,8 @@ def main():
     torch.cuda.set_device(dev)
     wl = WORKLOADS[args.workload]
     torch.manual_seed(1234 + rank)
-    pool = make_pool(wl, rank, args.pool, dev)
+    device_drop = args.path == "fused" and args.dropedge == "device"
+    pool = make_pool(wl, rank, args.pool, dev, (0.0, 0.0) if device_drop else None)
     nodes = [b.x.size(0) for b in pool]
     model = BiGCN(wl["feats"], 64, 64, dev).to(dev)
     if world > 1:   # identical initial parameters on every rank
@@ -226,7 +233,9 @@ def main():
     opt = bigcn_adam(model)                             # reference groups, one fused launch
     bucket = GradBucket(opt.params())                   # same parameter order as opt
 
-    fused = FusedTrainStep(model, opt)                  # bgcn_train_step + all-reduce + Adam
+    drops = wl["drop"] if device_drop else (0.0, 0.0)
+    fused = FusedTrainStep(model, opt, tddroprate=drops[0], budroprate=drops[1],
+                           drop_seed=4242 + rank)       # bgcn_train_step + all-reduce + Adam
 
     def step(i):
         b = pool[i % len(pool)]
@@ -355,6 +364,7 @@ def main():
                        "in_feats": wl["feats"], "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "final_loss": round(final_loss, 5),
             "feat_mode": args.feat_mode, "step_path": args.path, "prefetch_next_batch": bool(args.prefetch),
+            "dropedge": ("device" if device_drop else "host"),
         }
         if agg is not None:
             out["aggregation_5000"] = agg

@@ -116,6 +116,12 @@ __device__ __forceinline__ float4 ld4_nt(const float* p) {
   const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
   return make_float4(v.x, v.y, v.z, v.w);
 }
+// streaming (non-temporal) 16-byte store: output never re-read by the writer's kernel
+__device__ __forceinline__ void st4_nt(float* p, float4 v) {
+  f32x4 t;
+  t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+  __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
+}
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 __device__ __forceinline__ float4 f4fma(float a, float4 x, float4 acc) {
   acc.x = fmaf(a, x.x, acc.x);

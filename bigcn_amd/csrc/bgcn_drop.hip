@@ -15,26 +15,28 @@
 // bit for bit by the oracle (oracle/bigcn_oracle.py drop_edges).
 //
 // Layout: the list is [2, E] int64 in collation order, every tree's edges contiguous
-// and trees ascending (PyG Batch concatenation).  One launch plans the batch (tree edge
-// ranges by binary search over batch[src], kept counts, output offsets); one block per
+// and trees ascending (PyG Batch concatenation).  k_drop_bounds finds every tree's edge
+// range from the tree boundaries of the list (edge-parallel, no search); one block per
 // (tree, list) then finds its tree's k-th smallest key by a 4-pass 8-bit radix select
 // over keys recomputed from the hash (no key storage: 4 passes cost 4 hashes per edge,
-// not HBM traffic) and writes the kept edges with a block-wide ordered scan.
+// not HBM traffic) and writes the kept edges (compact form: block-wide ordered scan
+// after the kept counts of the preceding trees).
 //
 // Two output forms:
 //   compact: the kept edges, in order, into [2, ld] (ld >= kept count);
-//   masked : [2, E] in place order, each dropped edge (s, d) written as the self loop
-//            (d, d).  gcn_norm's add_remaining_self_loops removes input self loops, so
-//            the K1 graph of the masked list equals that of the compacted one and the
-//            prepared-batch path never needs the kept count on the host.
+//   masked : [2, E]; within each tree's range its kept edges first (in order), then
+//            every dropped edge (s, d) as the self loop (d, d).  gcn_norm's
+//            add_remaining_self_loops removes input self loops, so the K1 graph of the
+//            masked list equals that of the compacted one (unweighted), the prepared-batch
+//            path never needs the kept count on the host, and K1's run-based placement
+//            stays valid (no loop inside a node's run of edges).
 #include "bgcn_common.h"
 #include "bgcn_internal.h"
 
 namespace bgcn {
 namespace {
 
-constexpr int kDropThreads = 256;
-constexpr int kPlanThreads = 1024;
+constexpr int kDropThreads = 1024;   // one block per tree: big trees bound the launch
 
 // splitmix64 finaliser of (seed, dir, e) with a salt that separates it from the
 // dropout keep words (keep_word) drawn from the same step seed
@@ -62,67 +64,32 @@ struct DropList {
   uint32_t dir;
 };
 
-// tree id of edge e (batch[src], clamped so a bad index cannot read out of bounds)
+// tree id of edge e (batch[src], clamped to [0, B] so a bad index cannot read or
+// write out of bounds; edges of a bad tree id are flagged by k_drop_select)
 __device__ __forceinline__ int64_t edge_tree(const int64_t* ei, const int64_t* batch, int64_t N,
-                                             int64_t e) {
+                                             int64_t B, int64_t e) {
   int64_t s = ei[e];
   s = s < 0 ? 0 : (s >= N ? N - 1 : s);
-  return batch[s];
+  const int64_t t = batch[s];
+  return t < 0 ? 0 : (t > B ? B : t);
 }
 
-// eptr[d][t] = first edge of tree t in list d (eptr[d][0] = 0, eptr[d][B] = E);
-// koff[d][t] = exclusive prefix of the kept counts; counts[d] = total kept.
-__global__ __launch_bounds__(kPlanThreads) void k_drop_plan(DropList l0, DropList l1,
-                                                            const int64_t* __restrict__ batch,
-                                                            int64_t N, int64_t B,
-                                                            int64_t* __restrict__ eptr,
-                                                            int64_t* __restrict__ koff,
-                                                            int64_t* __restrict__ counts) {
-  const DropList& L = blockIdx.x == 0 ? l0 : l1;
-  int64_t* ep = eptr + int64_t(blockIdx.x) * (B + 1);
-  int64_t* ko = koff + int64_t(blockIdx.x) * (B + 1);
-  __shared__ int64_t wsum[kPlanThreads / kWave];
-  __shared__ int64_t carry;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
-  if (tid == 0) carry = 0;
-  // edge ranges first (every block thread binary-searches its trees)
-  for (int64_t t = tid; t <= B; t += kPlanThreads) {
-    int64_t lo = 0, hi = L.E;
-    if (t == 0) hi = 0;
-    else if (t == B) lo = L.E;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (edge_tree(L.ei, batch, N, mid) < t) lo = mid + 1; else hi = mid;
-    }
-    ep[t] = lo;
-  }
-  __syncthreads();
-  // kept counts and their exclusive scan, 1024 trees per round
-  for (int64_t base = 0; base < B; base += kPlanThreads) {
-    const int64_t t = base + tid;
-    int64_t k = 0;
-    if (t < B) {
-      const int64_t et = ep[t + 1] - ep[t];
-      k = kept_count(et > 0 ? et : 0, L.rate);
-    }
-    int64_t incl = k;
-    for (int o = 1; o < kWave; o <<= 1) {
-      const int64_t v = __shfl_up(incl, o, kWave);
-      if (lane >= o) incl += v;
-    }
-    if (lane == kWave - 1) wsum[wv] = incl;
-    __syncthreads();
-    int64_t before = carry;
-    for (int w = 0; w < wv; ++w) before += wsum[w];
-    if (t < B) ko[t] = before + incl - k;
-    __syncthreads();
-    if (tid == kPlanThreads - 1) carry = before + incl;
-    __syncthreads();
-  }
-  if (tid == 0) {
-    ko[B] = carry;
-    if (counts) counts[blockIdx.x] = carry;
-  }
+// eptr[d][t] = first edge of tree t in list d (eptr[d][0] = 0, eptr[d][B] = E), from
+// the tree boundaries of the list: edge-parallel, one dependent load (no search).
+// grid (ceil((E+1)/256), lists)
+__global__ __launch_bounds__(kDropThreads) void k_drop_bounds(DropList l0, DropList l1,
+                                                              const int64_t* __restrict__ batch,
+                                                              int64_t N, int64_t B,
+                                                              int64_t* __restrict__ eptr,
+                                                              int32_t* __restrict__ status) {
+  const DropList& L = blockIdx.y == 0 ? l0 : l1;
+  const int64_t e = int64_t(blockIdx.x) * kDropThreads + threadIdx.x;
+  if (e > L.E) return;
+  int64_t* ep = eptr + int64_t(blockIdx.y) * (B + 1);
+  const int64_t tp = e > 0 ? edge_tree(L.ei, batch, N, B, e - 1) : -1;
+  const int64_t tc = e < L.E ? edge_tree(L.ei, batch, N, B, e) : B;
+  for (int64_t t = tp + 1; t <= tc; ++t) ep[t] = e;   // trees (tp, tc] start at e
+  if (tc < tp && status) atomicOr(status, 1);          // trees out of order
 }
 
 // block-wide exclusive scan of 0/1 flags (4 waves); returns the prefix, *total the sum
@@ -148,32 +115,61 @@ __global__ __launch_bounds__(kDropThreads) void k_drop_select(DropList l0, DropL
                                                               const int64_t* __restrict__ batch,
                                                               int64_t N, int64_t B, uint64_t seed,
                                                               const int64_t* __restrict__ eptr,
-                                                              const int64_t* __restrict__ koff,
                                                               int32_t masked,
+                                                              int64_t* __restrict__ counts,
                                                               int32_t* __restrict__ status) {
   const DropList& L = blockIdx.y == 0 ? l0 : l1;
   const int64_t t = blockIdx.x;
   const int64_t* ep = eptr + int64_t(blockIdx.y) * (B + 1);
-  const int64_t* ko = koff + int64_t(blockIdx.y) * (B + 1);
-  const int64_t e0 = ep[t], e1 = ep[t + 1];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const auto clampE = [&](int64_t v) { return v < 0 ? int64_t(0) : (v > L.E ? L.E : v); };
+  const int64_t e0 = clampE(ep[t]), e1 = clampE(ep[t + 1]);
   const int64_t et = e1 > e0 ? e1 - e0 : 0;
   const int64_t k = kept_count(et, L.rate);
-  const int tid = threadIdx.x, lane = tid & (kWave - 1);
 
   __shared__ int32_t hist[256];
-  __shared__ uint32_t sel[2];  // threshold key, rank among ties
+  __shared__ int64_t sel[3];  // digit, rank among ties, number of ties
   __shared__ int wtot[kDropThreads / kWave];
+  __shared__ int64_t red[kDropThreads / kWave];
   __shared__ int64_t run;
 
-  // radix select of the (k-1)-th smallest key (0 < k < et only)
+  // compact output offset: kept counts of the trees before t (all trees for the total)
+  int64_t off = 0;
+  if (!masked) {
+    int64_t part = 0, all = 0;
+    for (int64_t u = tid; u < B; u += kDropThreads) {
+      const int64_t a = clampE(ep[u]), b = clampE(ep[u + 1]);
+      const int64_t ku = kept_count(b > a ? b - a : 0, L.rate);
+      if (u < t) part += ku;
+      all += ku;
+    }
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      part += __shfl_xor(part, o, kWave);
+      all += __shfl_xor(all, o, kWave);
+    }
+    if (lane == 0) red[tid / kWave] = part;
+    __syncthreads();
+    for (int w = 0; w < kDropThreads / kWave; ++w) off += red[w];
+    __syncthreads();
+    if (lane == 0) red[tid / kWave] = all;
+    __syncthreads();
+    if (tid == 0 && t == B - 1 && counts) {
+      int64_t tot = 0;
+      for (int w = 0; w < kDropThreads / kWave; ++w) tot += red[w];
+      counts[blockIdx.y] = tot;
+    }
+  }
+
+  // radix select of the (k-1)-th smallest key (0 < k < et only); afterwards the kept
+  // set is {h < T} plus the first r+1 (in edge order) of the `ties` edges with h == T
   uint32_t T = 0xffffffffu;
-  int64_t r = 0;
+  int64_t r = 0, ties = 1;
   const bool select = k > 0 && k < et;
   if (select) {
     uint32_t prefix = 0, mask = 0;
     r = k - 1;
     for (int shift = 24; shift >= 0; shift -= 8) {
-      hist[tid] = 0;
+      if (tid < 256) hist[tid] = 0;
       __syncthreads();
       for (int64_t e = e0 + tid; e < e1; e += kDropThreads) {
         const uint32_t h = drop_key(seed, L.dir, uint64_t(e));
@@ -181,28 +177,30 @@ __global__ __launch_bounds__(kDropThreads) void k_drop_select(DropList l0, DropL
       }
       __syncthreads();
       if (tid < kWave) {   // wave 0: lane l owns bins 4l..4l+3
-        int c[4], s = 0;
+        int c[4], sum = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { c[j] = hist[4 * lane + j]; s += c[j]; }
-        int incl = s;
+        for (int j = 0; j < 4; ++j) { c[j] = hist[4 * lane + j]; sum += c[j]; }
+        int incl = sum;
         for (int o = 1; o < kWave; o <<= 1) {
           const int v = __shfl_up(incl, o, kWave);
           if (lane >= o) incl += v;
         }
         const uint64_t over = __ballot(int64_t(incl) > r);
-        const int hit = __builtin_ctzll(over);   // r < total, so some lane crosses
+        const int hit = __builtin_ctzll(over);   // r < candidates, so some lane crosses
         if (lane == hit) {
-          int64_t rr = r - (incl - s);   // < s: the crossing bin is one of this lane's
+          int64_t rr = r - (incl - sum);   // < sum: the crossing bin is one of this lane's
           int j = 0;
           while (j < 3 && rr >= c[j]) { rr -= c[j]; ++j; }
-          sel[0] = uint32_t(4 * lane + j);
-          sel[1] = uint32_t(rr);
+          sel[0] = 4 * lane + j;
+          sel[1] = rr;
+          sel[2] = c[j];
         }
       }
       __syncthreads();
-      prefix |= sel[0] << shift;
+      prefix |= uint32_t(sel[0]) << shift;
       mask |= 255u << shift;
       r = sel[1];
+      ties = sel[2];
       __syncthreads();
     }
     T = prefix;
@@ -214,46 +212,46 @@ __global__ __launch_bounds__(kDropThreads) void k_drop_select(DropList l0, DropL
   const int64_t* dst = L.ei + L.E;
   int64_t* o0 = L.out;
   int64_t* o1 = L.out + L.ld;
-  bool bad = e1 < e0;   // trees out of order: some edges are in no tree's range
+  bool bad = false;
+  int64_t tie_run = 0;   // ties seen in earlier chunks (uniform)
   for (int64_t base = e0; base < e1; base += kDropThreads) {
     const int64_t e = base + tid;
     const bool valid = e < e1;
-    bool keep = false;
-    int64_t s = 0, d = 0;
+    int64_t sv = 0, dv = 0;
+    uint32_t h = 0xffffffffu;
     if (valid) {
-      s = src[e];
-      d = dst[e];
-      const bool inb = s >= 0 && s < N && d >= 0 && d < N;
-      bad |= !inb || batch[inb ? s : 0] != t || batch[inb ? d : 0] != t;
-      if (k == et) {
-        keep = true;
-      } else if (select) {
-        const uint32_t h = drop_key(seed, L.dir, uint64_t(e));
-        if (h < T) {
-          keep = true;
-        } else if (h == T) {   // ties in edge order (rare): rank among equal keys
-          int64_t eq = 0;
-          for (int64_t j = e0; j < e; ++j) eq += drop_key(seed, L.dir, uint64_t(j)) == T;
-          keep = eq <= r;
-        }
-      }
+      sv = src[e];
+      dv = dst[e];
+      const bool inb = sv >= 0 && sv < N && dv >= 0 && dv < N;
+      bad |= !inb || batch[inb ? sv : 0] != t || batch[inb ? dv : 0] != t;
+      if (select) h = drop_key(seed, L.dir, uint64_t(e));
     }
-    if (masked) {
+    const bool eq = valid && select && h == T;
+    int64_t tie_rank = 0;
+    if (ties > 1) {   // rare: rank among equal keys by a block scan (uniform branch)
+      int tot;
+      tie_rank = tie_run + block_scan01(eq, wtot, &tot);
+      tie_run += tot;
+    }
+    const bool keep = valid && (k == et || (select && (h < T || (eq && tie_rank <= r))));
+    int total;
+    const int pos = block_scan01(keep, wtot, &total);
+    if (masked) {   // the tree's kept edges first, in order; then its dropped ones as loops
       if (valid) {
-        o0[e] = keep ? s : d;
-        o1[e] = d;
+        const int64_t kept_before = run + pos;
+        const int64_t q = keep ? e0 + kept_before : e0 + k + ((e - e0) - kept_before);
+        o0[q] = keep ? sv : dv;
+        o1[q] = dv;
       }
     } else {
-      int total;
-      const int pos = block_scan01(keep, wtot, &total);
-      const int64_t q = ko[t] + run + pos;
+      const int64_t q = off + run + pos;
       if (keep) {
-        if (q < L.ld) { o0[q] = s; o1[q] = d; } else bad = true;
+        if (q < L.ld) { o0[q] = sv; o1[q] = dv; } else bad = true;
       }
-      __syncthreads();
-      if (tid == 0) run += total;
-      __syncthreads();
     }
+    __syncthreads();
+    if (tid == 0) run += total;
+    __syncthreads();
   }
   if (__ballot(bad) && lane == 0 && status) atomicOr(status, 1);
 }
@@ -262,7 +260,6 @@ __global__ __launch_bounds__(kDropThreads) void k_drop_select(DropList l0, DropL
 
 size_t drop_ws_size(int64_t B) {
   Carve c(nullptr, 0);
-  c.take<int64_t>(size_t(2 * (B + 1)));
   c.take<int64_t>(size_t(2 * (B + 1)));
   return c.off + 256;
 }
@@ -279,26 +276,26 @@ int drop_edges_impl(const int64_t* td, int64_t Etd, int64_t* td_out, int64_t ld_
                  "masked output needs ld >= E");
   BGCN_CHECK_ARG(td_rate < 1.0 && bu_rate < 1.0, "droprate must be < 1");
   BGCN_CHECK_ARG(ws && ws_bytes >= drop_ws_size(B), "workspace too small");
+  if (counts) BGCN_CHECK_HIP(hipMemsetAsync(counts, 0, 2 * sizeof(int64_t), s));
+  if (!td && !bu) return BGCN_OK;
   Carve c(ws, ws_bytes);
   int64_t* eptr = c.take<int64_t>(size_t(2 * (B + 1)));
-  int64_t* koff = c.take<int64_t>(size_t(2 * (B + 1)));
-  // an absent list is planned as an empty one (its counts come out 0)
-  DropList l0{td, td ? Etd : 0, td_out, ld_td, td_rate, 0u};
-  DropList l1{bu, bu ? Ebu : 0, bu_out, ld_bu, bu_rate, 1u};
-  if (!td) l0.ei = bu ? bu : td;
-  if (!bu) l1.ei = l0.ei;
-  if (!l0.ei) return BGCN_OK;  // nothing to do
-  hipLaunchKernelGGL(k_drop_plan, dim3(2), dim3(kPlanThreads), 0, s, l0, l1, batch, N, B, eptr,
-                     koff, counts);
+  // the lists actually present, packed first; their counts land in counts[0] / [1]
+  DropList l[2];
+  int lists = 0;
+  int64_t* cnt[2] = {counts, counts ? counts + 1 : nullptr};
+  int slot[2];
+  if (td) { l[lists] = DropList{td, Etd, td_out, ld_td, td_rate, 0u}; slot[lists++] = 0; }
+  if (bu) { l[lists] = DropList{bu, Ebu, bu_out, ld_bu, bu_rate, 1u}; slot[lists++] = 1; }
+  if (lists == 1) l[1] = l[0];
+  const int64_t Emax = std::max(l[0].E, l[1].E);
+  hipLaunchKernelGGL(k_drop_bounds, dim3(unsigned((Emax + kDropThreads) / kDropThreads), unsigned(lists)),
+                     dim3(kDropThreads), 0, s, l[0], l[1], batch, N, B, eptr, status);
   BGCN_CHECK_LAUNCH();
-  const int lists = bu ? 2 : 1;
-  if (!td) {  // BU only: run it as list 0 of the launch
-    hipLaunchKernelGGL(k_drop_select, dim3(unsigned(B), 1), dim3(kDropThreads), 0, s, l1, l1, batch,
-                       N, B, seed, eptr + (B + 1), koff + (B + 1), masked, status);
-  } else {
-    hipLaunchKernelGGL(k_drop_select, dim3(unsigned(B), unsigned(lists)), dim3(kDropThreads), 0, s,
-                       l0, l1, batch, N, B, seed, eptr, koff, masked, status);
-  }
+  // counts are written per list index; map a lone BU list onto counts[1]
+  int64_t* cbase = (lists == 1 && slot[0] == 1) ? cnt[1] : cnt[0];
+  hipLaunchKernelGGL(k_drop_select, dim3(unsigned(B), unsigned(lists)), dim3(kDropThreads), 0, s,
+                     l[0], l[1], batch, N, B, seed, eptr, masked, cbase, status);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }

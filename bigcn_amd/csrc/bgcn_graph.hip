@@ -77,8 +77,16 @@ __global__ __launch_bounds__(256) void k_count(GraphBatch gb) {
       if (G.status) atomicOr(G.status, 1);
       atomicOr(&G.flags[2], 1);
     } else if (!keep) {  // an input self loop: removed, its weight becomes the loop weight
-      atomicMax(&G.loop_eid[src], int32_t(e + 1));  // (last wins)
-      atomicOr(&G.flags[2], 1);
+      if (G.ew) atomicMax(&G.loop_eid[src], int32_t(e + 1));  // (last wins; unweighted: 1)
+      // run-based ranks (e - run start) hold unless the loop sits inside a run of its
+      // own node, i.e. the next edge is a kept edge at that node; a loop between runs of
+      // other nodes shows up as a surplus run start (k_scan_top's check)
+      if (e + 1 < G.E) {
+        int64_t ns, nd;
+        bool nv;
+        if (edge_kept(G.ei, G.E, N, e + 1, ns, nd, nv) && (ns == src || nd == src))
+          atomicOr(&G.flags[2], 1);
+      }
     } else {
       atomicAdd(&G.cnt_t[dst], 1);
       atomicAdd(&G.cnt_s[src], 1);

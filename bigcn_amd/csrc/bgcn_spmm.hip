@@ -15,8 +15,8 @@
 // Narrow kernel (F = 64 / 128): a group = F/4 lanes, one float4 per lane; the
 // chunk's (row, col, w) triples are loaded once (one entry per lane) and broadcast
 // with cross-lane shuffles; 8 neighbour rows are in flight per group.
-// Wide kernel (any F, e.g. the 5000-dim standalone aggregation): a group = one
-// 256-thread block, blockIdx.y tiles F in 1024-float slices.
+// Wide kernel (F > 128 up to 5120, e.g. the 5000-dim standalone aggregation): a group
+// = one 256-thread block over the full row width.
 // Up to two problems (the fused step's TD and BU graphs) share one launch
 // (blockIdx.y / blockIdx.z = problem).
 #include "bgcn_internal.h"
@@ -150,72 +150,121 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
   }
 }
 
-// Wide kernel (F > 128, e.g. the 5000-dim A_hat . X): a block = one chunk of NPGW
-// entries x one 1024-float slice of F (blockIdx.y); 256 threads x float4 read every
-// neighbour row slice fully coalesced, kWideDepth rows in flight.  Large chunks keep the partial
-// rows (each F floats) few: a 1500-child BU star root crosses ~6 chunk boundaries.
-constexpr int NPGW = 256;
-constexpr int kWideSlice = 1024;
-constexpr int kWideDepth = 16;  // neighbour rows in flight per thread
+// Wide kernel (F > 128, e.g. the 5000-dim A_hat . X).  HBM-bound: every X row is
+// needed by its own output row and by its neighbours' (parent / children), so the
+// design goal is to fetch each row from HBM about once and stream the output out:
+//   * a block processes chunks over the FULL row width (thread t owns float4 columns
+//     t, t+256, ...: F <= 5120 in kWideCols passes) - whole 20 KB rows, page friendly;
+//   * one resident block per CU (kWideBlocks) sweeps a contiguous range of chunks
+//     per XCD (the hardware deals blocks to the 8 XCDs round robin), so the rows in
+//     flight form a narrow moving window (~4k entries, tens of MB): a parent / child row
+//     needed again a few chunks later is still in the XCD's L2 or the Infinity Cache;
+//   * output rows are written non-temporally (never re-read here), keeping the caches
+//     for X;
+//   * chunk boundaries are row-aligned for rows of <= NPGW entries (the nominal boundary
+//     g * NPGW moves back to the start of the row it falls in), so only long rows (BU
+//     star roots) leave partial rows for the fixup pass.
+// kWideDepth entries are in flight per thread (kWideDepth * kWideCols float4 loads).
+constexpr int NPGW = 16;
+constexpr int kWideCols = 5;     // float4 per thread per row: F <= 256 * 4 * 5 = 5120
+constexpr int kWideSlice = 1024; // fixup slice (floats)
+constexpr int kWideDepth = 4;
+constexpr int kWideBlocks = 256; // one per CU
+constexpr int kXcds = 8;
+
+// first entry of chunk g: g*NPGW, or the start of the row containing it when that row
+// is short (<= NPGW entries, never split)
+__device__ __forceinline__ int64_t wide_chunk_start(const SpmmProb& P, int64_t g, int64_t nnz) {
+  const int64_t p = g * NPGW;
+  if (p >= nnz) return nnz;
+  const int32_t r = P.row[p];
+  const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
+  return re - rs <= NPGW ? rs : p;
+}
+
 __global__ __launch_bounds__(256) void k_spmm_wide(SpmmBatch sb) {
-  const SpmmProb& P = sb.p[blockIdx.z];
-  __shared__ int32_t s_r[NPGW], s_c[NPGW];
-  __shared__ float s_w[NPGW];
-  const int64_t g = blockIdx.x;
-  if (g >= P.ngroups) return;
+  const SpmmProb& P = sb.p[blockIdx.y];
+  __shared__ int32_t s_r[2 * NPGW], s_c[2 * NPGW];
+  __shared__ float s_w[2 * NPGW];
+  // XCD x sweeps chunks [x*R, (x+1)*R) with its gridDim.x / 8 blocks
+  const int64_t R = (P.ngroups + kXcds - 1) / kXcds;
+  const int64_t x = blockIdx.x % kXcds, per = gridDim.x / kXcds;   // grid: multiple of kXcds
+  const int64_t gend = min<int64_t>((x + 1) * R, P.ngroups);
   const int64_t nnz = P.ptr[sb.rows];
-  const int64_t p0 = g * NPGW;
-  if (p0 >= nnz) return;
-  const int64_t p1 = min<int64_t>(p0 + NPGW, nnz);
-  const int n = int(p1 - p0);
-  {
-    const int64_t p = min<int64_t>(p0 + threadIdx.x, nnz - 1);   // clamped, unconditional
-    const int32_t r = P.row[p], c = P.col[p];
-    const float w = P.w[p];
-    const bool v = threadIdx.x < n;
-    s_r[threadIdx.x] = v ? r : -1;
-    s_c[threadIdx.x] = v ? c : 0;
-    s_w[threadIdx.x] = v ? w : 0.f;
-  }
-  const int32_t prev_row = p0 > 0 ? P.row[p0 - 1] : -1;
-  const int32_t next_row = p1 < nnz ? P.row[p1] : -1;
-  __syncthreads();
   const int F = sb.F;
-  const int fo = blockIdx.y * kWideSlice + threadIdx.x * 4;
-  const bool act = fo < F;
-  const int foc = act ? fo : 0;
-  const float4 bv = (P.bias && act) ? ld4(P.bias + fo) : f4zero();
-  float4 acc = f4zero();
-  int32_t cur = -1;
-  bool cur_head = false;
-  for (int k0 = 0; k0 < n; k0 += kWideDepth) {
-    float4 v[kWideDepth];
+  int fo[kWideCols];
+  bool act[kWideCols];
+  float4 bv[kWideCols], acc[kWideCols];
 #pragma unroll
-    for (int u = 0; u < kWideDepth; ++u)   // k0 + u < NPGW: padding entries read row 0
-      v[u] = ld4(P.in + int64_t(s_c[k0 + u]) * P.ld_in + foc);
+  for (int j = 0; j < kWideCols; ++j) {
+    fo[j] = (threadIdx.x + 256 * j) * 4;
+    act[j] = fo[j] < F;
+    bv[j] = (P.bias && act[j]) ? ld4(P.bias + fo[j]) : f4zero();
+    if (!act[j]) fo[j] = 0;    // clamped: inactive columns load column 0, never store
+  }
+  const auto store = [&](float* dst, bool fin) {
 #pragma unroll
-    for (int u = 0; u < kWideDepth; ++u) {
-      const int k = k0 + u;
-      const int32_t r = s_r[k];          // -1 past n: padding, skipped
-      if (r >= 0) {
-        if (r != cur) {
-          if (cur >= 0 && act) {
-            if (!cur_head) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
-            else st4(P.part + (g * 2 + 0) * int64_t(F) + fo, acc);
+    for (int j = 0; j < kWideCols; ++j)
+      if (act[j]) {
+        if (fin) st4_nt(dst + fo[j], epilogue(acc[j], bv[j], sb.epi));   // final rows: streamed out
+        else st4(dst + fo[j], acc[j]);                                   // partials: read by the fixup
+      }
+  };
+  for (int64_t g = x * R + blockIdx.x / kXcds; g < gend; g += per) {
+    const int64_t p0 = wide_chunk_start(P, g, nnz), p1 = wide_chunk_start(P, g + 1, nnz);
+    const int n = int(p1 - p0);    // <= 2 * NPGW
+    __syncthreads();               // the previous chunk's entries are consumed
+    if (threadIdx.x < 2 * NPGW) {
+      const int64_t p = min<int64_t>(p0 + threadIdx.x, nnz - 1);   // clamped, unconditional
+      const int32_t r = P.row[p], c = P.col[p];
+      const float w = P.w[p];
+      const bool v = threadIdx.x < n;
+      s_r[threadIdx.x] = v ? r : -1;
+      s_c[threadIdx.x] = v ? c : 0;
+      s_w[threadIdx.x] = v ? w : 0.f;
+    }
+    const int32_t prev_row = p0 > 0 ? P.row[p0 - 1] : -1;
+    const int32_t next_row = p1 < nnz ? P.row[p1] : -1;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kWideCols; ++j) acc[j] = f4zero();
+    int32_t cur = -1;
+    bool cur_head = false;
+    for (int k0 = 0; k0 < n; k0 += kWideDepth) {
+      float4 v[kWideDepth][kWideCols];
+#pragma unroll
+      for (int u = 0; u < kWideDepth; ++u) {   // k0 + u < 2*NPGW: padding entries read row 0
+        const float* src = P.in + int64_t(s_c[k0 + u]) * P.ld_in;
+#pragma unroll
+        for (int j = 0; j < kWideCols; ++j) v[u][j] = ld4(src + fo[j]);
+      }
+#pragma unroll
+      for (int u = 0; u < kWideDepth; ++u) {
+        const int k = k0 + u;
+        const int32_t r = s_r[k];          // -1 past n: padding, skipped
+        if (r >= 0) {
+          if (r != cur) {
+            if (cur >= 0) {
+              if (!cur_head) store(P.out + int64_t(cur) * P.ld_out, true);
+              else store(P.part + (g * 2 + 0) * int64_t(F), false);
+            }
+            cur_head = cur < 0 && r == prev_row;
+            cur = r;
+#pragma unroll
+            for (int j = 0; j < kWideCols; ++j) acc[j] = f4zero();
           }
-          cur_head = cur < 0 && r == prev_row;
-          cur = r;
-          acc = f4zero();
+          const float w = s_w[k];
+#pragma unroll
+          for (int j = 0; j < kWideCols; ++j) acc[j] = f4fma(w, v[u][j], acc[j]);
         }
-        acc = f4fma(s_w[k], v[u], acc);
       }
     }
-  }
-  if (cur >= 0 && act) {
-    const bool ends = next_row != cur;
-    if (!cur_head && ends) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
-    else if (cur_head) st4(P.part + (g * 2 + 0) * int64_t(F) + fo, acc);
-    else st4(P.part + (g * 2 + 1) * int64_t(F) + fo, acc);
+    if (cur >= 0) {
+      const bool ends = next_row != cur;
+      if (!cur_head && ends) store(P.out + int64_t(cur) * P.ld_out, true);
+      else if (cur_head) store(P.part + (g * 2 + 0) * int64_t(F), false);
+      else store(P.part + (g * 2 + 1) * int64_t(F), false);
+    }
   }
 }
 
@@ -232,6 +281,7 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_wide(SpmmBatch sb) {
   const int32_t r = P.row[pb];
   if (P.row[pb - 1] != r) return;
   const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
+  if (re - rs <= NPGW) return;               // short rows are never split (wide_chunk_start)
   const int64_t g0 = rs / NPGW, g1 = (re - 1) / NPGW;
   if (g1 != g) return;
   const int F = sb.F;
@@ -293,8 +343,10 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
     if (gmax > 1)
       hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(unsigned(gmax - 1), gy), dim3(256), 0, stream, sb);
   } else {
+    BGCN_CHECK_ARG(F <= 256 * 4 * kWideCols, "F > 5120 is not supported by the wide aggregation");
     const unsigned slices = unsigned((F + kWideSlice - 1) / kWideSlice);
-    hipLaunchKernelGGL(k_spmm_wide, dim3(unsigned(gmax), slices, gy), dim3(256), 0, stream, sb);
+    const unsigned gx = unsigned((std::min<int64_t>(kWideBlocks, gmax) + kXcds - 1) / kXcds * kXcds);
+    hipLaunchKernelGGL(k_spmm_wide, dim3(gx, gy), dim3(256), 0, stream, sb);
     BGCN_CHECK_LAUNCH();
     if (gmax > 1)
       hipLaunchKernelGGL(k_spmm_fixup_wide, dim3(unsigned(gmax - 1), slices, gy), dim3(256), 0, stream, sb);

@@ -129,8 +129,9 @@ def drop_edges(td_edge_index: Optional[torch.Tensor], bu_edge_index: Optional[to
     ``seed`` (a counter-based draw, not Python's ``random`` stream).
 
     ``masked=False`` returns the compacted lists (one host sync for the kept counts);
-    ``masked=True`` returns ``[2, E]`` lists in which every dropped edge ``(s, d)`` is the
-    self loop ``(d, d)``, which :func:`build_graph` removes (no sync)."""
+    ``masked=True`` returns ``[2, E]`` lists holding, per tree, the kept edges in order
+    and then every dropped edge ``(s, d)`` as the self loop ``(d, d)``, which
+    :func:`build_graph` removes (no sync)."""
     ref = td_edge_index if td_edge_index is not None else bu_edge_index
     if ref is None:
         raise ValueError("drop_edges: no edge list given")

@@ -108,6 +108,7 @@ int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_num_edges,
  * Atomic-free and deterministic: the nnz range is split evenly over lane groups
  * (merge path) and rows that cross a split are combined in a fixed order.
  * `capacity` = allocated entries (E + N); the valid count is read from ptr[rows].
+ * F: a multiple of 4, at most 5120 (64 and 128 take the narrow kernels).
  * -------------------------------------------------------------------------- */
 size_t bgcn_spmm_workspace_size(int64_t capacity, int32_t F);
 int bgcn_spmm(const int32_t* ptr, const int32_t* row, const int32_t* col, const float* w,
@@ -175,9 +176,10 @@ int bgcn_scatter_mean_bwd(const float* dout, int64_t ld_dout, const int64_t* ind
  *   masked = 0: the kept edges, compacted in order, into out [2, ld] (ld = row stride);
  *               counts[0..1] (device, optional) receive the kept totals.  ld below the
  *               total sets *status bit 0 and the excess is not written.
- *   masked = 1: out [2, ld >= E] in place order with every dropped edge (s, d) written
- *               as the self loop (d, d); bgcn_build_graph removes input self loops, so
- *               the graph equals that of the compacted list (no kept count needed).
+ *   masked = 1: out [2, ld >= E]; within each tree's range its kept edges first (in
+ *               order), then every dropped edge (s, d) as the self loop (d, d).
+ *               bgcn_build_graph removes input self loops, so the (unweighted) graph
+ *               equals that of the compacted list and no kept count is needed.
  * An edge out of range, crossing trees or out of tree order sets *status bit 0.
  * -------------------------------------------------------------------------- */
 size_t bgcn_drop_edges_workspace_size(int64_t num_graphs);

@@ -288,7 +288,8 @@ def drop_edges(edge_index, batch, num_graphs: int, droprate: float, seed: int, d
     """Per tree (edges grouped by tree in collation order, tree = batch[src]): keep the
     ``kept_count`` edges with the smallest (key, position), in original order - the
     device's uniform random subset, restated bit for bit.  Returns the kept [2, E']
-    list, or with ``masked`` the [2, E] list whose dropped edges (s, d) read (d, d)."""
+    list, or with ``masked`` the [2, E] list holding, per tree, the kept edges in order
+    followed by the dropped ones as self loops (d, d)."""
     import numpy as np
     ei = np.asarray(edge_index, dtype=np.int64)
     b = np.asarray(batch, dtype=np.int64)
@@ -303,8 +304,15 @@ def drop_edges(edge_index, batch, num_graphs: int, droprate: float, seed: int, d
         pos = np.arange(e0, e1)
         order = np.lexsort((pos, drop_key(seed, direction, pos)))   # key, then position
         keep[pos[order[:k]]] = True
-    if masked:
-        out = ei.copy()
-        out[0, ~keep] = ei[1, ~keep]
+    if masked:   # per tree: kept edges in order, then the dropped ones as loops (d, d)
+        out = np.empty_like(ei)
+        for t in range(num_graphs):
+            e0, e1 = int(bounds[t]), int(bounds[t + 1])
+            kt, dr = keep[e0:e1], ~keep[e0:e1]
+            seg = ei[:, e0:e1]
+            nk = int(kt.sum())
+            out[:, e0:e0 + nk] = seg[:, kt]
+            out[0, e0 + nk:e1] = seg[1, dr]
+            out[1, e0 + nk:e1] = seg[1, dr]
         return out
     return ei[:, keep]

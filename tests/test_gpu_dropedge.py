@@ -60,11 +60,18 @@ def test_drop_edges_uniform_inclusion():
     rng = np.random.default_rng(42)
     sizes = [11] * 3000
     ei, batch = _forest_edges(rng, sizes)
+    td, _ = drop_edges(_dev(ei), None, _dev(batch), len(sizes), 0.2, seed=31337)
+    td = td.cpu().numpy()
+    assert np.all(np.bincount(batch[td[0]], minlength=len(sizes)) == 8)
+    posmap = np.full(len(batch), -1)
+    posmap[ei[1]] = np.arange(ei.shape[1])            # every child has one parent edge
+    kept = np.zeros(ei.shape[1], bool)
+    kept[posmap[td[1]]] = True
+    freq = kept.reshape(len(sizes), 10).mean(axis=0)
+    assert np.all(np.abs(freq - 0.8) < 0.03), freq
     td_m, _ = drop_edges(_dev(ei), None, _dev(batch), len(sizes), 0.2, seed=31337, masked=True)
-    kept = (td_m[0] != td_m[1]).view(len(sizes), 10).float().cpu()
-    assert torch.all(kept.sum(1) == 8)
-    freq = kept.mean(0)
-    assert torch.all((freq - 0.8).abs() < 0.03), freq
+    loops = (td_m[0] == td_m[1]).view(len(sizes), 10).cpu()
+    assert torch.all(loops[:, :8] == 0) and torch.all(loops[:, 8:] == 1)   # kept first, then loops
 
 
 def test_drop_edges_rejects_ungrouped_edges():

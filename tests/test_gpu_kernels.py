@@ -107,6 +107,33 @@ def test_build_graph_drops_input_self_loops_and_flags_bad_index():
         build_graph(bad.to(DEV), 3, validate=True)
 
 
+@pytest.mark.parametrize("case", ["inside_src_run", "inside_dst_run", "between_runs", "tail"])
+def test_build_graph_self_loops_inside_runs(case):
+    """Input self loops placed inside a node's run of edges (which would shift run-based
+    ranks), between runs, and at a tree's tail (the masked DropEdge layout)."""
+    from bigcn_amd.ops import build_graph
+    ei = {"inside_src_run": [[0, 0, 0, 1, 1], [1, 0, 2, 3, 4]],
+          "inside_dst_run": [[1, 2, 2, 3, 0], [2, 2, 2, 2, 1]],
+          "between_runs": [[0, 0, 3, 1, 1], [1, 2, 3, 3, 4]],
+          "tail": [[0, 0, 1, 2, 4], [1, 2, 3, 2, 4]]}[case]
+    ei = torch.tensor(ei)
+    for degree_on in ("col", "row"):
+        g = build_graph(ei.to(DEV), 5, degree_on=degree_on)
+        e, w = O.gcn_norm(ei, None, 5, degree_on, dtype=torch.float64)
+        ref = torch.zeros(5, 5, dtype=torch.float64)
+        ref.index_put_((e[1], e[0]), w, accumulate=True)
+        close(dense_adj(*[x.cpu() for x in (g.t_ptr, g.t_row, g.t_col, g.t_w)], 5), ref, 1e-6)
+        # the transposed orientation holds the same entries
+        refT = ref.t().contiguous()
+        close(dense_adj(*[x.cpu() for x in (g.s_ptr, g.s_row, g.s_col, g.s_w)], 5), refT, 1e-6)
+        # and every row keeps edge order, its self loop last (the reference's summation order)
+        kept = [(int(a), int(b)) for a, b in ei.t() if a != b]
+        for ptr_, col_, key, other in ((g.t_ptr.cpu(), g.t_col.cpu(), 1, 0), (g.s_ptr.cpu(), g.s_col.cpu(), 0, 1)):
+            for i in range(5):
+                want = [ed[other] for ed in kept if ed[key] == i] + [i]
+                assert col_[int(ptr_[i]):int(ptr_[i + 1])].tolist() == want, (case, i)
+
+
 def test_build_graph_edge_weight():
     from bigcn_amd.ops import build_graph
     rng = np.random.default_rng(3)
@@ -138,6 +165,37 @@ def test_spmm_forward_and_transpose(F, star):
     close(outr, torch.relu(A @ x + bias), what="relu")
     outt = spmm(g, x.float().to(DEV), transposed=True)
     close(outt, A.t() @ x, what="A^T x")
+
+
+@pytest.mark.parametrize("F", [12, 300, 5120])
+def test_spmm_wide_row_lengths_around_chunk_size(F):
+    """Wide kernel chunking: rows of 14..18 and 31..34 entries (around the 16-entry
+    chunk, where boundaries are moved to row starts or rows are split) at every offset."""
+    from bigcn_amd.ops import build_graph, spmm
+    rows, cols, off = [], [], 0
+    for deg in [15, 16, 17, 1, 31, 32, 33, 2, 14, 18, 34, 0, 16, 16, 1, 17]:
+        for c in range(deg):        # a star: parent `off`, children off+1..off+deg
+            rows.append(off)
+            cols.append(off + 1 + c)
+        off += deg + 1
+    N = off
+    ei = torch.tensor([rows, cols], dtype=torch.int64)
+    g = build_graph(ei.to(DEV), N)
+    e, w = O.gcn_norm(ei, None, N, "col", dtype=torch.float64)
+    A = torch.zeros(N, N, dtype=torch.float64)
+    A.index_put_((e[1], e[0]), w, accumulate=True)
+    x = torch.randn(N, F, dtype=torch.float64)
+    close(spmm(g, x.float().to(DEV)), A @ x, what="A x")
+    close(spmm(g, x.float().to(DEV), transposed=True), A.t() @ x, what="A^T x")
+
+
+def test_spmm_rejects_too_wide():
+    from bigcn_amd._lib import BGCNError
+    from bigcn_amd.ops import build_graph, spmm
+    ei = torch.tensor([[0], [1]])
+    g = build_graph(ei.to(DEV), 2)
+    with pytest.raises(BGCNError):
+        spmm(g, torch.zeros(2, 5124, device=DEV))
 
 
 def test_spmm_deterministic():

@@ -194,6 +194,10 @@ def test_drop_edges_oracle_uniform():
     rng = np.random.default_rng(6)
     sizes = [11] * 3000
     ei, batch = _forest_edges(rng, sizes)
-    out = O.drop_edges(ei, batch, len(sizes), 0.2, seed=123, direction=1, masked=True)
-    kept = (out[0] != out[1]).reshape(len(sizes), 10).mean(axis=0)
-    assert np.all(np.abs(kept - 0.8) < 0.03), kept
+    out = O.drop_edges(ei, batch, len(sizes), 0.2, seed=123, direction=1)
+    posmap = np.full(len(batch), -1)
+    posmap[ei[1]] = np.arange(ei.shape[1])            # every child has one parent edge
+    kept = np.zeros(ei.shape[1], bool)
+    kept[posmap[out[1]]] = True
+    freq = kept.reshape(len(sizes), 10).mean(axis=0)
+    assert np.all(np.abs(freq - 0.8) < 0.03), freq
