@@ -15,8 +15,8 @@
 // Narrow kernel (F = 64 / 128): a group = F/4 lanes, one float4 per lane; the
 // chunk's (row, col, w) triples are loaded once (one entry per lane) and broadcast
 // with cross-lane shuffles; 8 neighbour rows are in flight per group.
-// Wide kernel (F > 128 up to 5120, e.g. the 5000-dim standalone aggregation): a group
-// = one 256-thread block over the full row width.
+// Wide kernel (F > 128 up to 6144, e.g. the 5000-dim standalone aggregation): a group
+// = one 512-thread block over the full row width.
 // Up to two problems (the fused step's TD and BU graphs) share one launch
 // (blockIdx.y / blockIdx.z = problem).
 #include "bgcn_internal.h"
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
 // needed by its own output row and by its neighbours' (parent / children), so the
 // design goal is to fetch each row from HBM about once and stream the output out:
 //   * a block processes chunks over the FULL row width (thread t owns float4 columns
-//     t, t+256, ...: F <= 5120 in kWideCols passes) - whole 20 KB rows, page friendly;
+//     t, t+512, ...: F <= 6144 in kWideCols passes) - whole 20 KB rows, page friendly;
 //   * one resident block per CU (kWideBlocks) sweeps a contiguous range of chunks
 //     per XCD (the hardware deals blocks to the 8 XCDs round robin), so the rows in
 //     flight form a narrow moving window (~4k entries, tens of MB): a parent / child row
@@ -166,9 +166,10 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
 //     star roots) leave partial rows for the fixup pass.
 // kWideDepth entries are in flight per thread (kWideDepth * kWideCols float4 loads).
 constexpr int NPGW = 16;
-constexpr int kWideCols = 5;     // float4 per thread per row: F <= 256 * 4 * 5 = 5120
+constexpr int kWideThreads = 512;
+constexpr int kWideCols = 3;     // float4 per thread per row: F <= 512 * 4 * 3 = 6144
 constexpr int kWideSlice = 1024; // fixup slice (floats)
-constexpr int kWideDepth = 4;
+constexpr int kWideDepth = 8;
 constexpr int kWideBlocks = 256; // one per CU
 constexpr int kXcds = 8;
 
@@ -182,7 +183,7 @@ __device__ __forceinline__ int64_t wide_chunk_start(const SpmmProb& P, int64_t g
   return re - rs <= NPGW ? rs : p;
 }
 
-__global__ __launch_bounds__(256) void k_spmm_wide(SpmmBatch sb) {
+__global__ __launch_bounds__(kWideThreads) void k_spmm_wide(SpmmBatch sb) {
   const SpmmProb& P = sb.p[blockIdx.y];
   __shared__ int32_t s_r[2 * NPGW], s_c[2 * NPGW];
   __shared__ float s_w[2 * NPGW];
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(256) void k_spmm_wide(SpmmBatch sb) {
   float4 bv[kWideCols], acc[kWideCols];
 #pragma unroll
   for (int j = 0; j < kWideCols; ++j) {
-    fo[j] = (threadIdx.x + 256 * j) * 4;
+    fo[j] = (threadIdx.x + kWideThreads * j) * 4;
     act[j] = fo[j] < F;
     bv[j] = (P.bias && act[j]) ? ld4(P.bias + fo[j]) : f4zero();
     if (!act[j]) fo[j] = 0;    // clamped: inactive columns load column 0, never store
@@ -343,10 +344,10 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
     if (gmax > 1)
       hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(unsigned(gmax - 1), gy), dim3(256), 0, stream, sb);
   } else {
-    BGCN_CHECK_ARG(F <= 256 * 4 * kWideCols, "F > 5120 is not supported by the wide aggregation");
+    BGCN_CHECK_ARG(F <= kWideThreads * 4 * kWideCols, "F > 6144 is not supported by the wide aggregation");
     const unsigned slices = unsigned((F + kWideSlice - 1) / kWideSlice);
     const unsigned gx = unsigned((std::min<int64_t>(kWideBlocks, gmax) + kXcds - 1) / kXcds * kXcds);
-    hipLaunchKernelGGL(k_spmm_wide, dim3(gx, gy), dim3(256), 0, stream, sb);
+    hipLaunchKernelGGL(k_spmm_wide, dim3(gx, gy), dim3(kWideThreads), 0, stream, sb);
     BGCN_CHECK_LAUNCH();
     if (gmax > 1)
       hipLaunchKernelGGL(k_spmm_fixup_wide, dim3(unsigned(gmax - 1), slices, gy), dim3(256), 0, stream, sb);

@@ -108,7 +108,7 @@ int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_num_edges,
  * Atomic-free and deterministic: the nnz range is split evenly over lane groups
  * (merge path) and rows that cross a split are combined in a fixed order.
  * `capacity` = allocated entries (E + N); the valid count is read from ptr[rows].
- * F: a multiple of 4, at most 5120 (64 and 128 take the narrow kernels).
+ * F: a multiple of 4, at most 6144 (64 and 128 take the narrow kernels).
  * -------------------------------------------------------------------------- */
 size_t bgcn_spmm_workspace_size(int64_t capacity, int32_t F);
 int bgcn_spmm(const int32_t* ptr, const int32_t* row, const int32_t* col, const float* w,

@@ -167,7 +167,7 @@ def test_spmm_forward_and_transpose(F, star):
     close(outt, A.t() @ x, what="A^T x")
 
 
-@pytest.mark.parametrize("F", [12, 300, 5120])
+@pytest.mark.parametrize("F", [12, 300, 6144])
 def test_spmm_wide_row_lengths_around_chunk_size(F):
     """Wide kernel chunking: rows of 14..18 and 31..34 entries (around the 16-entry
     chunk, where boundaries are moved to row starts or rows are split) at every offset."""
@@ -195,7 +195,7 @@ def test_spmm_rejects_too_wide():
     ei = torch.tensor([[0], [1]])
     g = build_graph(ei.to(DEV), 2)
     with pytest.raises(BGCNError):
-        spmm(g, torch.zeros(2, 5124, device=DEV))
+        spmm(g, torch.zeros(2, 6148, device=DEV))
 
 
 def test_spmm_deterministic():
