@@ -201,9 +201,12 @@ def main():
                     help="at N=1 also time the standalone 5000-wide aggregation A_hat . X")
     ap.add_argument("--compare-dense", type=int, default=1,
                     help="at N=1 also time the dense MFMA path and report it beside the main line")
-    ap.add_argument("--dropedge", default="device", choices=["device", "host"],
-                    help="fused path: DropEdge (dataset.py:68-90) inside the step's batch "
-                         "preparation on the device, or pre-applied at synthesis on the host")
+    ap.add_argument("--dropedge", default="host", choices=["device", "host"],
+                    help="fused path: DropEdge (dataset.py:68-90) pre-applied at synthesis on the "
+                         "host (the reference's DataLoader does it per sample), or inside the "
+                         "step's batch preparation on the device")
+    ap.add_argument("--compare-dropedge", type=int, default=1,
+                    help="at N=1 also time the other DropEdge placement and report it beside the main line")
     args = ap.parse_args()
 
     from bigcn_amd import BiGCN, FusedTrainStep
@@ -237,7 +240,10 @@ def main():
     fused = FusedTrainStep(model, opt, tddroprate=drops[0], budroprate=drops[1],
                            drop_seed=4242 + rank)       # bgcn_train_step + all-reduce + Adam
 
+    ctx = {"pool": pool, "fused": fused}                # swapped for the DropEdge comparison run
+
     def step(i):
+        pool, fused = ctx["pool"], ctx["fused"]
         b = pool[i % len(pool)]
         if args.path == "fused":                        # K1 + fwd + head + loss + bwd in one call;
             nxt = pool[(i + 1) % len(pool)] if args.prefetch else None   # the next batch's
@@ -344,6 +350,15 @@ def main():
     dense_res = None
     if world == 1 and args.feat_mode != "dense" and args.compare_dense:
         dense_res = run("dense", max(3, args.steps // 2), 2)
+    drop_res = None
+    if world == 1 and args.path == "fused" and args.compare_dropedge:
+        other = not device_drop                         # the other DropEdge placement
+        ctx["pool"] = make_pool(wl, rank, args.pool, dev, (0.0, 0.0) if other else None)
+        d2 = wl["drop"] if other else (0.0, 0.0)
+        ctx["fused"] = FusedTrainStep(model, opt, tddroprate=d2[0], budroprate=d2[1], drop_seed=4242)
+        drop_res = run(args.feat_mode, max(3, args.steps // 2), 2)
+        drop_res["where"] = "device" if other else "host"
+        ctx["pool"], ctx["fused"] = pool, fused
     agg = None
     if world == 1 and args.aggregation:
         agg = aggregation_bench(pool[0])
@@ -368,6 +383,10 @@ def main():
         }
         if agg is not None:
             out["aggregation_5000"] = agg
+        if drop_res is not None:
+            out["dropedge_" + drop_res["where"]] = {
+                "value": round(drop_res["value"], 2), "unit": "trees/s",
+                "ms_per_step": round(drop_res["dt"] / max(3, args.steps // 2) * 1e3, 4)}
         if dense_res is not None:
             out["dense_path"] = {"value": round(dense_res["value"], 2), "unit": "trees/s",
                                  "ms_per_step": round(dense_res["dt"] / max(3, args.steps // 2) * 1e3, 4),
