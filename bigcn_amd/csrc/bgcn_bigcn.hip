@@ -842,6 +842,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   }
   BGCN_TRY(gemm_tn_impl(w.dz1, 2 * H, a->x, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F, N,
                         w.tn_ws, w.tn_bytes, sparse ? x : s, sparse ? 6 : 1, gate));
+  timing_end(9, s);   // the main stream's own chain (span class, bgcn_train_step)
   BGCN_TRY(aux_join(s, kLaneSide));
   return BGCN_OK;
 }

@@ -14,7 +14,7 @@
 namespace bgcn {
 
 namespace {
-constexpr int kTimingClasses = 8;
+constexpr int kTimingClasses = 12;
 thread_local std::string g_err;
 
 struct TimingState {

@@ -229,6 +229,8 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
   Prepared p;
   int graph_lane = -1;
+  timing_begin(10, s);   // span classes: 8 next-batch preparation, 9 main chain, 10 step
+  timing_begin(9, s);
   if (!a->prepared_ready) {
     // prepare the current batch first; without a next batch to prefetch, its K1 runs on
     // the side lane beside the pass over X (joined before the first propagate)
@@ -248,10 +250,14 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
     // bound pass) runs on the side lane beside this step's latency-bound chain
     hipStream_t x;
     BGCN_TRY(aux_fork(s, kLaneSide, &x));
+    timing_begin(8, x);
     BGCN_TRY(prepare_into(a->next, F, a->degree_on, a->feat_mode, a->next_prepared,
                           a->next_prepared_bytes, x, nullptr, x));
+    timing_end(8, x);
   }
-  return train_step_body(a, p, w, s, graph_lane);
+  BGCN_TRY(train_step_body(a, p, w, s, graph_lane));
+  timing_end(10, s);
+  return BGCN_OK;
 }
 
 static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w, hipStream_t s,

@@ -373,7 +373,9 @@ int bgcn_keep_words(uint64_t seed, int64_t num_nodes, int32_t num_words, uint32_
  *   1 dW1 dense MFMA
  *   2 conv2 (dense MFMA + sparse root gather)            3 dW2 relu(H1) block MFMA
  *   4 gated dense conv1 fallback (auto)                  5 dW1 + dW2 root columns over CSC(X)
- *   6 gated dense dW1 fallback (auto)                   7 ELL compaction of X (batch preparation) */
+ *   6 gated dense dW1 fallback (auto)                   7 ELL compaction of X (batch preparation)
+ * Span classes of bgcn_train_step (diagnostics): 8 the next batch's preparation on the
+ * auxiliary lane, 9 the caller stream's own chain up to the final join, 10 the whole call. */
 int bgcn_set_kernel_timing(int enable);
 int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* launches);
 

@@ -1,0 +1,52 @@
+"""Diagnostic: durations of the bgcn_train_step spans (timing classes 8-10): the next
+batch's preparation on the auxiliary lane, the caller stream's own chain, the whole
+call - averaged over K bench steps.  A preparation span close to the step span means the
+side lane bounds the step.
+
+    python tools/span_probe.py [--steps 200] [--dropedge host|device]"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--dropedge", default="host", choices=["device", "host"])
+    args = ap.parse_args()
+    import bench
+    from bigcn_amd import BiGCN, FusedTrainStep, ops
+    from bigcn_amd.optim import bigcn_adam
+    dev = torch.device("cuda", 0)
+    wl = bench.WORKLOADS["twitter15"]
+    dd = args.dropedge == "device"
+    pool = bench.make_pool(wl, 0, 4, dev, (0.0, 0.0) if dd else None)
+    model = BiGCN(wl["feats"], 64, 64, dev).to(dev)
+    model.train()
+    opt = bigcn_adam(model)
+    drops = wl["drop"] if dd else (0.0, 0.0)
+    fused = FusedTrainStep(model, opt, tddroprate=drops[0], budroprate=drops[1], drop_seed=1)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        for i in range(5):
+            fused(pool[i % 4], next_data=pool[(i + 1) % 4])
+        torch.cuda.synchronize()
+        classes = {7: "compaction", 8: "prep span (side lane)", 9: "main chain span", 10: "whole call"}
+        ops.set_kernel_timing(True, classes)
+        for i in range(args.steps):
+            fused(pool[i % 4], next_data=pool[(i + 1) % 4])
+        torch.cuda.synchronize()
+        ops.set_kernel_timing(False)
+        for c, name in classes.items():
+            ms, n = ops.kernel_timing(c)
+            print(f"{name:24s} {ms / max(n, 1) * 1e3:8.1f} us  ({n} spans)")
+
+
+if __name__ == "__main__":
+    main()
