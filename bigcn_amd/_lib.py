@@ -28,6 +28,8 @@ BGCN_EPI_RELU = 1
 BGCN_FEAT_AUTO = 0
 BGCN_FEAT_DENSE = 1
 BGCN_SPARSE_CAP = 32
+BGCN_DTYPE_F32 = 0
+BGCN_DTYPE_BF16 = 1
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
@@ -75,7 +77,7 @@ class BiGCNArgs(Structure):
         ("dhead_in", c_void_p),
         ("td_dw1", c_void_p), ("td_db1", c_void_p), ("td_dw2", c_void_p), ("td_db2", c_void_p),
         ("bu_dw1", c_void_p), ("bu_db1", c_void_p), ("bu_dw2", c_void_p), ("bu_db2", c_void_p),
-        ("save_for_backward", c_int32),
+        ("save_for_backward", c_int32), ("x_dtype", c_int32),
     ]
 
 
@@ -90,6 +92,7 @@ class BatchDesc(Structure):
         ("td_edge_index", c_void_p), ("td_num_edges", c_int64),
         ("bu_edge_index", c_void_p), ("bu_num_edges", c_int64),
         ("td_droprate", c_double), ("bu_droprate", c_double), ("drop_seed", c_uint64),
+        ("x_dtype", c_int32),
     ]
 
 

@@ -31,7 +31,8 @@ __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (
 //   k <  H : keep * s * relu(H1[i][d*H + k])
 //   k >= H : keep * s * relu(X[root(i)][k - H])
 // Block tile 64 nodes x 64 outputs, waves 2 x 2 (32 x 32 each), blockIdx.y = d.
-__global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ X, int64_t ldx,
+template <class TX>
+__global__ __launch_bounds__(256) void k_conv2_fwd(const TX* __restrict__ X, int64_t ldx,
                                                    int64_t F, const float* __restrict__ H1,
                                                    const int32_t* __restrict__ node_root,
                                                    const float* __restrict__ W2td,
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ X, 
   const int gm = tid >> 2, gk = (tid & 3) * 8;
   const int64_t gi = m0 + gm;
   const bool gok = gi < N;
-  const float* xroot = X + int64_t(gok ? node_root[gi] : 0) * ldx;
+  const TX* xroot = X + int64_t(gok ? node_root[gi] : 0) * ldx;
   const float* h1row = H1 + (gok ? gi : 0) * (2 * H) + d * H;
   // B staging map: W2 row o = tid/8 + 32 i, k quad (tid%8)*4
   const int so = tid >> 3, sq = (tid & 7) * 4;
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ X, 
       float4 v = f4zero();
       if (gok) {
         if (kk < H) v = ld4(h1row + kk);
-        else if (kk - H < F) v = ld4(xroot + (kk - H));
+        else if (kk - H < F) v = xq(xroot + (kk - H));
       }
       ga[j] = v;
     }
@@ -137,7 +138,8 @@ struct Dw2Cfg {
 // dense path's full grid (all 64+F columns, few node splits; want_dense = 1) and the
 // sparse path's relu(H1) block only (column tile 0, many node splits, ldp = 64;
 // want_dense = 0).  Only the configuration of the path selected on the device works.
-__global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_t ldx, int64_t F,
+template <class TX>
+__global__ __launch_bounds__(256) void k_dw2(const TX* __restrict__ X, int64_t ldx, int64_t F,
                                              const float* __restrict__ H1,
                                              const float* __restrict__ dZ2,
                                              const int32_t* __restrict__ node_root, int64_t N,
@@ -182,12 +184,14 @@ __global__ __launch_bounds__(256) void k_dw2(const float* __restrict__ X, int64_
     gw = keep.get(uint32_t(d), uint32_t(nc), uint32_t(c / 32));
     gw = ok ? gw : 0u;
     const int32_t root = node_root[nc];
-    const float* xr = X + int64_t(root < 0 ? 0 : root) * ldx;
+    const TX* xr = X + int64_t(root < 0 ? 0 : root) * ldx;
     const float* h1 = H1 + nc * (2 * H) + d * H;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int64_t cc = min<int64_t>(c + 4 * j, K2 - 4);
-      const float4 v = ld4(cc < H ? h1 + cc : xr + (cc - H));
+      float4 v;
+      if constexpr (sizeof(TX) == sizeof(float)) v = ld4(cc < H ? h1 + cc : xr + (cc - H));
+      else v = cc < H ? ld4(h1 + cc) : xq(xr + (cc - H));
       gb[j] = (ok && c + 4 * j < K2) ? v : f4zero();
     }
   };
@@ -588,6 +592,7 @@ int check_args(const bgcn_bigcn_args* a) {
                  "in_feats and ldx must be multiples of 4");
   BGCN_CHECK_ARG(a->x && a->batch && a->rootindex && a->tree_ptr && a->h1 && a->h2,
                  "null pointer");
+  BGCN_CHECK_ARG(a->x_dtype == BGCN_DTYPE_F32 || a->x_dtype == BGCN_DTYPE_BF16, "bad x_dtype");
   BGCN_CHECK_ARG((reinterpret_cast<uintptr_t>(a->x) & 15) == 0, "x must be 16-byte aligned");
   BGCN_CHECK_ARG(a->td.t_ptr && a->bu.t_ptr && a->td.s_ptr && a->bu.s_ptr, "null graph");
   return BGCN_OK;
@@ -699,7 +704,8 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
       BGCN_TRY(sparse_conv1_gather(sp, w.z1, s));
       timing_end(0, s);
     }
-    BGCN_TRY(gemm_xwt_impl(a->x, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F, s, gate));
+    BGCN_TRY(gemm_xwt_x(a->x, a->x_dtype, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H,
+                        F, s, gate));
     if (graph_lane >= 0) BGCN_TRY(aux_join(s, graph_lane));   // K1 of a just-prepared batch
     return forward_tail(a, w, sp, keep, gate, s, head, false);
   }
@@ -719,11 +725,12 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
   bool forked = false;
   if (sparse) {
     timing_begin(0, s);
-    BGCN_TRY(sparse_compact_conv1(sp, a->x, a->ldx, w.z1, s));
+    BGCN_TRY(sparse_compact_conv1(sp, a->x, a->x_dtype, a->ldx, w.z1, s));
     timing_end(0, s);
   }
   timing_begin(sparse ? 4 : 0, s);
-  BGCN_TRY(gemm_xwt_impl(a->x, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F, s, gate));
+  BGCN_TRY(gemm_xwt_x(a->x, a->x_dtype, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F,
+                      s, gate));
   timing_end(sparse ? 4 : 0, s);
   // the graphs (built on graph_lane by bgcn_train_step) and the items are needed from
   // here on; the join comes before the CSC fork so that it never waits for the CSC
@@ -748,8 +755,14 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
   // conv2 lin with the root-extended, relu'd, dropped-out A operand generated in-kernel
   timing_begin(2, s);
   if (sparse) BGCN_TRY(sparse_conv2(sp, a->h1, a->tree_ptr, a->rootindex, w.z2, keep, s));
-  hipLaunchKernelGGL(k_conv2_fwd, dim3(grid_for(N, 64), 2), dim3(256), 0, s, a->x, a->ldx, F,
-                     a->h1, w.node_root, a->td_w2, a->bu_w2, w.z2, N, keep, gate);
+  if (a->x_dtype == BGCN_DTYPE_BF16)
+    hipLaunchKernelGGL(k_conv2_fwd<bf16_t>, dim3(grid_for(N, 64), 2), dim3(256), 0, s,
+                       static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
+                       a->bu_w2, w.z2, N, keep, gate);
+  else
+    hipLaunchKernelGGL(k_conv2_fwd<float>, dim3(grid_for(N, 64), 2), dim3(256), 0, s,
+                       static_cast<const float*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
+                       a->bu_w2, w.z2, N, keep, gate);
   BGCN_CHECK_LAUNCH();
   timing_end(2, s);
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z2, a->h2, a->td_b2, a->bu_b2, BGCN_EPI_NONE, w, s));
@@ -803,8 +816,14 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     const Dw2Cfg dense{w.kchunk2, w.S2, gxd, 1, H + F, w.dw2_part};
     const Dw2Cfg sparsec{w.kchunkh, w.Sh, 1, 0, int64_t(H), w.dw2_part};
     const int n0 = gxd * w.S2 * 2, n1 = sparse ? w.Sh * 2 : 0;
-    hipLaunchKernelGGL(k_dw2, dim3(unsigned(n0 + n1)), dim3(256), 0, x, a->x, a->ldx, F, a->h1, w.dz2,
-                       w.node_root, N, keep, gate, dense, sparsec, n0);
+    if (a->x_dtype == BGCN_DTYPE_BF16)
+      hipLaunchKernelGGL(k_dw2<bf16_t>, dim3(unsigned(n0 + n1)), dim3(256), 0, x,
+                         static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.dz2, w.node_root, N,
+                         keep, gate, dense, sparsec, n0);
+    else
+      hipLaunchKernelGGL(k_dw2<float>, dim3(unsigned(n0 + n1)), dim3(256), 0, x,
+                         static_cast<const float*>(a->x), a->ldx, F, a->h1, w.dz2, w.node_root, N,
+                         keep, gate, dense, sparsec, n0);
     BGCN_CHECK_LAUNCH();
   }
   timing_end(3, x);
@@ -840,8 +859,8 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     BGCN_TRY(sparse_dw1(sp, a, w.dz1, s));
     timing_end(5, s);
   }
-  BGCN_TRY(gemm_tn_impl(w.dz1, 2 * H, a->x, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F, N,
-                        w.tn_ws, w.tn_bytes, sparse ? x : s, sparse ? 6 : 1, gate));
+  BGCN_TRY(gemm_tn_x(w.dz1, 2 * H, a->x, a->x_dtype, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F,
+                     N, w.tn_ws, w.tn_bytes, sparse ? x : s, sparse ? 6 : 1, gate));
   timing_end(9, s);   // the main stream's own chain (span class, bgcn_train_step)
   BGCN_TRY(aux_join(s, kLaneSide));
   return BGCN_OK;

@@ -142,6 +142,30 @@ inline unsigned grid_for(int64_t n, int block) { return unsigned((n + block - 1)
 // Dense-path gate: the fused encoder runs the dense MFMA kernels only when the sparse
 // feature path is off (gate == nullptr: always run) or has flagged an overflow row
 // (*gate != 0).  Decided on the device, so no host sync.
+// ---------------------------------------------------------------- node-feature loads
+// X is fp32 or raw bfloat16 (uint16_t storage; bag-of-words counts are exact in bf16).
+// xq: 4 consecutive features (ldx and the column are multiples of 4), xs: one feature;
+// _nt: streaming.  Kernels reading X are templated on the element type.
+typedef uint16_t bf16_t;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+__device__ __forceinline__ float4 bf4(uint32_t lo, uint32_t hi) {
+  return make_float4(__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                     __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u));
+}
+__device__ __forceinline__ float4 xq(const float* p) { return ld4(p); }
+__device__ __forceinline__ float4 xq(const bf16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return bf4(u.x, u.y);
+}
+__device__ __forceinline__ float4 xq_nt(const float* p) { return ld4_nt(p); }
+__device__ __forceinline__ float4 xq_nt(const bf16_t* p) {
+  const u32x2 u = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+  return bf4(u.x, u.y);
+}
+__device__ __forceinline__ float xs(const float* p) { return *p; }
+__device__ __forceinline__ float xs(const bf16_t* p) { return bf2f(*p); }
+
 __device__ __forceinline__ bool gate_closed(const int32_t* gate) { return gate && *gate == 0; }
 __device__ __forceinline__ bool dense_active(const int32_t* gate) { return !gate_closed(gate); }
 

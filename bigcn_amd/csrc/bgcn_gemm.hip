@@ -30,8 +30,8 @@ __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (
 // BKM = false: W is [Nc, K] (Y = X W^T, GCNConv.lin forward);
 // BKM = true : W is [K, Nc] (Y = X W, the input gradient dX = dZ W of GCNConv.lin),
 //              staged k-major in LDS.  W1/split are ignored for BKM.
-template <bool VEC, bool BKM>
-__global__ __launch_bounds__(256) void k_gemm_xwt(const float* __restrict__ X, int64_t ldx,
+template <bool VEC, bool BKM, class TX = float>
+__global__ __launch_bounds__(256) void k_gemm_xwt(const TX* __restrict__ X, int64_t ldx,
                                                   const float* __restrict__ W0,
                                                   const float* __restrict__ W1, int64_t ldw,
                                                   int64_t split, float* __restrict__ Y,
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void k_gemm_xwt(const float* __restrict__ X, i
   const int64_t m0 = int64_t(blockIdx.x) * BM, n0 = int64_t(blockIdx.y) * BN;
   const int srow = tid >> 3, skq = (tid & 7) * 4;  // staging: row, k offset (float4)
 
-  const float* arow[2];
+  const TX* arow[2];
   bool aok[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -72,11 +72,11 @@ __global__ __launch_bounds__(256) void k_gemm_xwt(const float* __restrict__ X, i
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (VEC) {
-        ra[i] = (aok[i] && k < K) ? ld4(arow[i] + k) : f4zero();
+        ra[i] = (aok[i] && k < K) ? xq(arow[i] + k) : f4zero();
       } else {
         float t[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) t[j] = (aok[i] && k + j < K) ? arow[i][k + j] : 0.f;
+        for (int j = 0; j < 4; ++j) t[j] = (aok[i] && k + j < K) ? xs(arow[i] + k + j) : 0.f;
         ra[i] = make_float4(t[0], t[1], t[2], t[3]);
       }
     }
@@ -172,9 +172,9 @@ __global__ __launch_bounds__(256) void k_gemm_xwt(const float* __restrict__ X, i
 // are k-major in memory (rows = nodes) and staged k-major in LDS (no padding: the
 // MFMA read is 32 consecutive floats per half-wave).
 // ============================================================================
-template <bool VEC>
+template <bool VEC, class TX = float>
 __global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ G, int64_t ldg,
-                                                 const float* __restrict__ X, int64_t ldx,
+                                                 const TX* __restrict__ X, int64_t ldx,
                                                  float* __restrict__ part, int64_t Mc, int64_t Nc,
                                                  int64_t K, int64_t kchunk,
                                                  const int32_t* __restrict__ gate) {
@@ -212,11 +212,11 @@ __global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ G, in
       int64_t k = k0 + x_node + 16 * i;
       int64_t n = n0 + x_q;
       if (VEC) {
-        rx[i] = (k < ke && n < Nc) ? ld4(X + k * ldx + n) : f4zero();
+        rx[i] = (k < ke && n < Nc) ? xq(X + k * ldx + n) : f4zero();
       } else {
         float t[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) t[j] = (k < ke && n + j < Nc) ? X[k * ldx + n + j] : 0.f;
+        for (int j = 0; j < 4; ++j) t[j] = (k < ke && n + j < Nc) ? xs(X + k * ldx + n + j) : 0.f;
         rx[i] = make_float4(t[0], t[1], t[2], t[3]);
       }
     }
@@ -293,25 +293,44 @@ size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K) {
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-int gemm_xwt_impl(const float* X, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
-                  int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
-                  hipStream_t stream, const int32_t* gate) {
+template <class TX>
+static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
+                      int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
+                      hipStream_t stream, const int32_t* gate) {
   BGCN_CHECK_ARG(X && W0 && Y, "null pointer");
   BGCN_CHECK_ARG(M >= 0 && Nc > 0 && K > 0, "bad shape");
   BGCN_CHECK_ARG(ldx >= K && ldw >= K && ldy >= Nc, "bad leading dimension");
   BGCN_CHECK_ARG(split >= Nc || W1, "W1 required when split < Nc");
   if (M == 0) return BGCN_OK;
-  bool vec = K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0 && aligned16(X) && aligned16(W0) &&
+  // the vector path loads 4 features at once (16 B fp32, 8 B bf16)
+  const bool xal = (reinterpret_cast<uintptr_t>(X) & (4 * sizeof(TX) - 1)) == 0;
+  bool vec = K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0 && xal && aligned16(W0) &&
              (!W1 || aligned16(W1));
   dim3 grid(grid_for(M, 64), grid_for(Nc, 128));
   if (vec)
-    hipLaunchKernelGGL((k_gemm_xwt<true, false>), grid, dim3(256), 0, stream, X, ldx, W0, W1, ldw,
-                       split, Y, ldy, M, Nc, K, gate);
+    hipLaunchKernelGGL((k_gemm_xwt<true, false, TX>), grid, dim3(256), 0, stream, X, ldx, W0, W1,
+                       ldw, split, Y, ldy, M, Nc, K, gate);
   else
-    hipLaunchKernelGGL((k_gemm_xwt<false, false>), grid, dim3(256), 0, stream, X, ldx, W0, W1,
+    hipLaunchKernelGGL((k_gemm_xwt<false, false, TX>), grid, dim3(256), 0, stream, X, ldx, W0, W1,
                        ldw, split, Y, ldy, M, Nc, K, gate);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
+}
+
+int gemm_xwt_impl(const float* X, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
+                  int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
+                  hipStream_t stream, const int32_t* gate) {
+  return gemm_xwt_t(X, ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K, stream, gate);
+}
+
+int gemm_xwt_x(const void* X, int xdt, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
+               int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
+               hipStream_t stream, const int32_t* gate) {
+  if (xdt == BGCN_DTYPE_BF16)
+    return gemm_xwt_t(static_cast<const bf16_t*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K,
+                      stream, gate);
+  return gemm_xwt_t(static_cast<const float*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K,
+                    stream, gate);
 }
 
 int gemm_xw_impl(const float* X, int64_t ldx, const float* W, int64_t ldw, float* Y, int64_t ldy,
@@ -381,9 +400,10 @@ int colsum_impl(const float* A, int64_t lda, int64_t rows, int32_t C, float* out
   return BGCN_OK;
 }
 
-int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float* C0, float* C1,
-                 int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
-                 size_t ws_bytes, hipStream_t stream, int timing_cls, const int32_t* gate) {
+template <class TX>
+static int gemm_tn_t(const float* G, int64_t ldg, const TX* X, int64_t ldx, float* C0, float* C1,
+                     int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
+                     size_t ws_bytes, hipStream_t stream, int timing_cls, const int32_t* gate) {
   BGCN_CHECK_ARG(G && X && C0, "null pointer");
   BGCN_CHECK_ARG(Mc > 0 && Nc > 0 && K >= 0, "bad shape");
   BGCN_CHECK_ARG(ldg >= Mc && ldx >= Nc && ldc >= Nc, "bad leading dimension");
@@ -396,22 +416,39 @@ int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float
   S = int((K + kchunk - 1) / kchunk);
   if (S < 1) S = 1;
   float* part = static_cast<float*>(ws);
-  bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) &&
-             aligned16(X);
+  const bool xal = (reinterpret_cast<uintptr_t>(X) & (4 * sizeof(TX) - 1)) == 0;
+  bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) && xal;
   dim3 grid(grid_for(Nc, 64), grid_for(Mc, 128), S);
   timing_begin(timing_cls, stream);
   if (vec)
-    hipLaunchKernelGGL(k_gemm_tn<true>, grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc, Nc,
-                       K, kchunk, gate);
+    hipLaunchKernelGGL((k_gemm_tn<true, TX>), grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc,
+                       Nc, K, kchunk, gate);
   else
-    hipLaunchKernelGGL(k_gemm_tn<false>, grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc, Nc,
-                       K, kchunk, gate);
+    hipLaunchKernelGGL((k_gemm_tn<false, TX>), grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc,
+                       Nc, K, kchunk, gate);
   BGCN_CHECK_LAUNCH();
   timing_end(timing_cls, stream);
   hipLaunchKernelGGL(k_reduce_splits, dim3(std::min<unsigned>(grid_for(Mc * Nc, 256), 1024)), dim3(256), 0, stream, part, S,
                      Mc, Nc, C0, C1, ldc, split, gate);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
+}
+
+int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float* C0, float* C1,
+                 int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
+                 size_t ws_bytes, hipStream_t stream, int timing_cls, const int32_t* gate) {
+  return gemm_tn_t(G, ldg, X, ldx, C0, C1, ldc, split, Mc, Nc, K, ws, ws_bytes, stream, timing_cls,
+                   gate);
+}
+
+int gemm_tn_x(const float* G, int64_t ldg, const void* X, int xdt, int64_t ldx, float* C0,
+              float* C1, int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
+              size_t ws_bytes, hipStream_t stream, int timing_cls, const int32_t* gate) {
+  if (xdt == BGCN_DTYPE_BF16)
+    return gemm_tn_t(G, ldg, static_cast<const bf16_t*>(X), ldx, C0, C1, ldc, split, Mc, Nc, K, ws,
+                     ws_bytes, stream, timing_cls, gate);
+  return gemm_tn_t(G, ldg, static_cast<const float*>(X), ldx, C0, C1, ldc, split, Mc, Nc, K, ws,
+                   ws_bytes, stream, timing_cls, gate);
 }
 
 }  // namespace bgcn

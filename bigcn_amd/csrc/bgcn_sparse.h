@@ -41,10 +41,11 @@ int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root
 struct Prepared;
 // weight-independent preparation of one batch into p (bgcn_prepare_batch)
 int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
-                   const int64_t* batch, const int64_t* rootindex, const float* X, int64_t ldx,
+                   const int64_t* batch, const int64_t* rootindex, const void* X, int xdt, int64_t ldx,
                    hipStream_t s);
 int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s);
-int sparse_compact_conv1(SparseState& S, const float* X, int64_t ldx, float* Z1, hipStream_t s);
+int sparse_compact_conv1(SparseState& S, const void* X, int xdt, int64_t ldx, float* Z1,
+                         hipStream_t s);
 int sparse_items(SparseState& S, const int32_t* tree_ptr, hipStream_t s);
 int sparse_conv2(SparseState& S, const float* H1, const int32_t* tree_ptr, const int64_t* rootindex,
                  float* Z2, KeepSrc keep, hipStream_t s);

@@ -132,8 +132,8 @@ __device__ __forceinline__ float2 conv1_row(const SparseState& S, int cnt, int32
 
 // kConv1 = true: compaction + conv1 in one pass (the encoder's forward); false: the ELL
 // only (weight-independent batch preparation, bgcn_prepare_batch).
-template <bool kConv1>
-__global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const float* __restrict__ X,
+template <bool kConv1, class TX>
+__global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* __restrict__ X,
                                                        int64_t ldx, float* __restrict__ Z1) {
   __shared__ int32_t s_col[4][kCap];
   __shared__ float s_val[4][kCap];
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const floa
   // grid-stride over rows: the preparation launches a small grid so that it streams X
   // beside the training chain without taking every CU slot
   for (int64_t i = int64_t(blockIdx.x) * 4 + wave; i < S.N; i += int64_t(gridDim.x) * 4) {
-  const float* row = X + i * ldx;
+  const TX* row = X + i * ldx;
   const int nq = int(S.F / 4);   // float4 per row (F % 4 == 0)
   int cnt = 0;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const floa
 #pragma unroll
     for (int u = 0; u < kRowChunks; ++u) {
       const int q = q0 + u * 64 + lane;
-      v[u] = q < nq ? ld4_nt(row + int64_t(q) * 4) : f4zero();
+      v[u] = q < nq ? xq_nt(row + int64_t(q) * 4) : f4zero();
     }
 #pragma unroll
     for (int u = 0; u < kRowChunks; ++u) {
@@ -773,8 +773,14 @@ int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root
   return BGCN_OK;
 }
 
-int sparse_compact_conv1(SparseState& S, const float* X, int64_t ldx, float* Z1, hipStream_t s) {
-  hipLaunchKernelGGL(k_compact_conv1<true>, dim3(grid_for(S.N, 4)), dim3(256), 0, s, S, X, ldx, Z1);
+int sparse_compact_conv1(SparseState& S, const void* X, int xdt, int64_t ldx, float* Z1,
+                         hipStream_t s) {
+  if (xdt == BGCN_DTYPE_BF16)
+    hipLaunchKernelGGL((k_compact_conv1<true, bf16_t>), dim3(grid_for(S.N, 4)), dim3(256), 0, s, S,
+                       static_cast<const bf16_t*>(X), ldx, Z1);
+  else
+    hipLaunchKernelGGL((k_compact_conv1<true, float>), dim3(grid_for(S.N, 4)), dim3(256), 0, s, S,
+                       static_cast<const float*>(X), ldx, Z1);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -814,7 +820,7 @@ int sparse_csc(SparseState& S, hipStream_t s) {
 }
 
 int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
-                   const int64_t* batch, const int64_t* rootindex, const float* X, int64_t ldx,
+                   const int64_t* batch, const int64_t* rootindex, const void* X, int xdt, int64_t ldx,
                    hipStream_t s) {
   SparseState S{};
   S.mode = mode;
@@ -835,8 +841,13 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
     return e ? unsigned(std::max(1, atoi(e))) : kPrepBlocks;
   }();
   timing_begin(7, s);
-  hipLaunchKernelGGL(k_compact_conv1<false>, dim3(std::min<unsigned>(grid_for(N, 4), prep_blocks)),
-                     dim3(256), 0, s, S, X, ldx, nullptr);
+  const dim3 grid(std::min<unsigned>(grid_for(N, 4), prep_blocks));
+  if (xdt == BGCN_DTYPE_BF16)
+    hipLaunchKernelGGL((k_compact_conv1<false, bf16_t>), grid, dim3(256), 0, s, S,
+                       static_cast<const bf16_t*>(X), ldx, nullptr);
+  else
+    hipLaunchKernelGGL((k_compact_conv1<false, float>), grid, dim3(256), 0, s, S,
+                       static_cast<const float*>(X), ldx, nullptr);
   timing_end(7, s);
   BGCN_CHECK_LAUNCH();
   return sparse_csc(S, s);

@@ -121,6 +121,8 @@ int check_batch(const bgcn_batch* b) {
   BGCN_CHECK_ARG((b->td_num_edges == 0 || b->td_edge_index) && (b->bu_num_edges == 0 || b->bu_edge_index),
                  "null edge_index");
   BGCN_CHECK_ARG(b->td_droprate < 1.0 && b->bu_droprate < 1.0, "droprate must be < 1");
+  BGCN_CHECK_ARG(b->x_dtype == BGCN_DTYPE_F32 || b->x_dtype == BGCN_DTYPE_BF16, "bad x_dtype");
+  BGCN_CHECK_ARG((reinterpret_cast<uintptr_t>(b->x) & 15) == 0, "x must be 16-byte aligned");
   return BGCN_OK;
 }
 
@@ -193,7 +195,7 @@ static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_
                                  &p.bu, p.status, p.gws, p.gws_bytes,
                                  reinterpret_cast<bgcn_stream_t>(gs)));
   const int mode = (feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxFeat) ? 1 : 0;
-  BGCN_TRY(sparse_prepare(p, N, B, F, mode, b->batch, b->rootindex, b->x, b->ldx, s));
+  BGCN_TRY(sparse_prepare(p, N, B, F, mode, b->batch, b->rootindex, b->x, b->x_dtype, b->ldx, s));
   if (out) *out = p;
   return BGCN_OK;
 }
@@ -265,7 +267,8 @@ static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w
   const int64_t N = a->cur.num_nodes, B = a->cur.num_graphs, F = a->in_feats, C = a->num_classes;
   if (a->status) BGCN_CHECK_HIP(hipMemsetAsync(a->status, 0, sizeof(int32_t), s));
   bgcn_bigcn_args e{};
-  e.x = a->cur.x; e.ldx = a->cur.ldx; e.num_nodes = N; e.num_graphs = B; e.in_feats = F; e.hid = H;
+  e.x = a->cur.x; e.x_dtype = a->cur.x_dtype;
+  e.ldx = a->cur.ldx; e.num_nodes = N; e.num_graphs = B; e.in_feats = F; e.hid = H;
   e.batch = a->cur.batch; e.rootindex = a->cur.rootindex;
   e.td = view_of(p.td, p.td_cap);
   e.bu = view_of(p.bu, p.bu_cap);

@@ -317,9 +317,23 @@ _PARAM_ORDER = ("td_w1", "td_b1", "td_w2", "td_b2", "bu_w1", "bu_b1", "bu_w2", "
 _FEAT_MODES = {"auto": _lib.BGCN_FEAT_AUTO, "sparse": _lib.BGCN_FEAT_AUTO, "dense": _lib.BGCN_FEAT_DENSE}
 
 
+def features(x: torch.Tensor) -> torch.Tensor:
+    """Node features as the fused path reads them: bf16 stays bf16 (the bf16
+    configuration: bag-of-words counts are exact), anything else becomes fp32;
+    contiguous rows."""
+    if x.dtype != torch.bfloat16 and x.dtype != torch.float32:
+        x = x.float()
+    return x.contiguous()
+
+
+def x_dtype_code(x: torch.Tensor) -> int:
+    return _lib.BGCN_DTYPE_BF16 if x.dtype == torch.bfloat16 else _lib.BGCN_DTYPE_F32
+
+
 def _fill_args(a: BiGCNArgs, x, batch, rootindex, td, bu, B, training, seed, keep, feat_mode, xs, params):
     N, F = x.shape
     a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats, a.hid = ptr(x), x.stride(0), N, B, F, HID
+    a.x_dtype = x_dtype_code(x)
     a.batch, a.rootindex = ptr(batch), ptr(rootindex)
     a.td, a.bu = td.view(), bu.view()
     for name, p in zip(_PARAM_ORDER, params):
@@ -335,7 +349,7 @@ class _BiGCNEncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training, seed, keep_words,
                 feat_mode, *params):
-        x = x.contiguous().float()
+        x = features(x)
         N, F = x.shape
         dev = x.device
         L = _lib.lib()

@@ -25,7 +25,7 @@ from . import _lib
 from ._lib import BatchDesc, StepArgs, check, ptr, stream_handle, workspace
 from .bigcn import BiGCN, _draw_seed, _num_graphs
 from .dp import GradBucket
-from .ops import _FEAT_MODES
+from .ops import _FEAT_MODES, features, x_dtype_code
 from .optim import FusedAdam, bigcn_adam
 
 
@@ -88,13 +88,14 @@ class FusedTrainStep:
 
     def _desc(self, data):
         """bgcn_batch of a collated batch (+ the tensors it points into, kept alive)."""
-        x = _need(data.x, torch.float32, "x")
+        x = features(data.x)                         # fp32, or bf16 kept as is
         td_ei = _need(data.edge_index, torch.int64, "edge_index")
         bu_ei = _need(data.BU_edge_index, torch.int64, "BU_edge_index")
         batch = _need(data.batch, torch.int64, "batch")
         root = _need(data.rootindex, torch.int64, "rootindex")
         d = BatchDesc()
         d.x, d.ldx, d.num_nodes, d.num_graphs = ptr(x), x.stride(0), x.size(0), _num_graphs(data)
+        d.x_dtype = x_dtype_code(x)
         d.batch, d.rootindex = ptr(batch), ptr(root)
         d.td_edge_index, d.td_num_edges = ptr(td_ei), td_ei.size(1)
         d.bu_edge_index, d.bu_num_edges = ptr(bu_ei), bu_ei.size(1)

@@ -215,11 +215,16 @@ typedef struct bgcn_graph_view {
  * DENSE: always the dense MFMA kernels. */
 #define BGCN_FEAT_AUTO 0
 #define BGCN_FEAT_DENSE 1
+/* element type of the node features x (x_dtype): fp32, or bfloat16 (the bf16
+ * configuration; bag-of-words counts are exact in bf16, every product accumulates in
+ * fp32, so results equal the fp32 path's on the same values) */
+#define BGCN_DTYPE_F32 0
+#define BGCN_DTYPE_BF16 1
 #define BGCN_SPARSE_CAP 32
 
 typedef struct bgcn_bigcn_args {
   /* batch */
-  const float* x; int64_t ldx;   /* [N, F] node features (data.x)          */
+  const void* x; int64_t ldx;    /* [N, F] node features (data.x), x_dtype  */
   int64_t num_nodes;             /* N                                       */
   int64_t num_graphs;            /* B                                       */
   int64_t in_feats;              /* F (5000 Twitter/Weibo BoW)              */
@@ -251,6 +256,7 @@ typedef struct bgcn_bigcn_args {
   /* 1: a backward will follow - the forward also builds backward-only state (the CSC
    * of X for dW1) on the library's auxiliary stream, overlapped with the forward */
   int32_t save_for_backward;
+  int32_t x_dtype;               /* BGCN_DTYPE_F32 (0) / BGCN_DTYPE_BF16    */
 } bgcn_bigcn_args;
 
 /* The workspace carries state from the forward to the backward (node -> root map,
@@ -275,7 +281,7 @@ int bgcn_bigcn_backward(const bgcn_bigcn_args* args, void* workspace, size_t wor
  * the current one (the HBM-bound pass over X then overlaps the latency-bound chain).
  * -------------------------------------------------------------------------- */
 typedef struct bgcn_batch {
-  const float* x; int64_t ldx;   /* [N, F] node features                     */
+  const void* x; int64_t ldx;    /* [N, F] node features (x_dtype below)     */
   int64_t num_nodes;             /* N                                        */
   int64_t num_graphs;            /* B                                        */
   const int64_t* batch;          /* [N] sorted tree id per node              */
@@ -287,6 +293,7 @@ typedef struct bgcn_batch {
    * (bgcn_drop_edges, masked form) from drop_seed before building the graphs. */
   double td_droprate, bu_droprate;
   uint64_t drop_seed;
+  int32_t x_dtype;               /* BGCN_DTYPE_F32 (0) / BGCN_DTYPE_BF16      */
 } bgcn_batch;
 
 size_t bgcn_prepare_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,

@@ -84,3 +84,15 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
         assert got[(cname, "sizeof")] == ctypes.sizeof(py), cname
         for fname, _ in py._fields_:
             assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
+
+
+def test_constants_match_header():
+    import re
+    from bigcn_amd import _lib
+    text = open(HEADER).read()
+    for name in ("BGCN_DEGREE_ON_COL", "BGCN_DEGREE_ON_ROW", "BGCN_EPI_NONE", "BGCN_EPI_RELU",
+                 "BGCN_FEAT_AUTO", "BGCN_FEAT_DENSE", "BGCN_SPARSE_CAP", "BGCN_DTYPE_F32",
+                 "BGCN_DTYPE_BF16"):
+        m = re.search(rf"#define {name} (\d+)", text)
+        assert m, name
+        assert int(m.group(1)) == getattr(_lib, name), name

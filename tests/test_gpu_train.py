@@ -237,3 +237,53 @@ def test_sparse_signed_features(training):
     gr = step.grads()
     for k, prm in zip(KEYS, step.step_params):
         close(gr[prm], rgrads[k], what=k)
+
+
+@pytest.mark.parametrize("mode", ["auto", "dense"])
+def test_weibo_bf16_features_match_fp32(mode):
+    """The Weibo configuration (BASELINE configs[2]: 2-class Net, bf16): node features
+    stored as bf16 (bag-of-words counts are exact in bf16), every product accumulated in
+    fp32 - the step is bitwise the fp32 step on the same values, on the sparse path and
+    on the dense MFMA path, and matches the oracle."""
+    from bigcn_amd import FusedTrainStep
+    from bigcn_amd.ops import keep_words, unpack_keep
+    b = _synth(35, 16, 110, root_random=True)
+    b.y = b.y % 2                                         # Weibo: 2 classes
+    xb = b.x.to(torch.bfloat16)
+    assert torch.equal(xb.float(), b.x)                  # counts: exact
+    p = O.make_params(5000, 64, 64, 2, seed=16)
+    seed = 2024
+    outs = []
+    for x in (b.x, xb):
+        b.x = x
+        m = _model(p, mode, classes=2)
+        m.train(True)
+        step = FusedTrainStep(m)
+        logp = torch.empty(b.num_graphs, 2, device=DEV)
+        loss = step.forward_backward(b, seed=seed, logp=logp)
+        step.check_status()
+        outs.append((loss.clone(), logp.clone(), [g.clone() for g in step.grads().values()]))
+    (l0, p0, g0), (l1, p1, g1) = outs
+    assert torch.equal(l0, l1) and torch.equal(p0, p1)
+    for a, c in zip(g0, g1):
+        assert torch.equal(a, c)
+    b.x = xb.float()
+    N = b.x.size(0)
+    mk = unpack_keep(keep_words(seed, N, 5000, DEV).cpu(), 64 + 5000)
+    rlogp, rloss, rgrads, _ = _oracle(b, p, True, mk[0], mk[1])
+    close(p1, rlogp, what="logp")
+    close(l1, rloss, what="loss")
+    for k, g in zip(KEYS, g1):
+        close(g, rgrads[k], what=k)
+
+
+def test_bf16_features_module_path():
+    """BiGCN.forward (the per-op autograd encoder) takes bf16 features as well."""
+    b = _synth(36, 8, 60)
+    p = O.make_params(5000, 64, 64, 4, seed=17)
+    m = _model(p)
+    m.eval()
+    out32 = m(b)
+    b.x = b.x.to(torch.bfloat16)
+    out16 = m(b)
+    assert torch.equal(out32, out16)
