@@ -41,6 +41,17 @@ WORKLOADS = {
     "twitter15": dict(trees=128, mean=256, sigma=0.8, feats=5000, classes=4, drop=(0.2, 0.2),
                       desc="Twitter15-shaped synthetic: 128 trees/GPU, LogNormal(0.8) sizes mean 256 "
                            "clamped [2,8192], 5000-dim BoW x, DropEdge 0.2/0.2, dropout 0.5, fp32"),
+    # BASELINE.json configs[2]: Weibo, 5000-dim BoW, batch 128, bf16.  Weibo trees average
+    # ~816 nodes; the reference's Weibo script drops no edges
+    # (BiGCN_Weibo.py:199-200) and has the 2-class head (Net, :76-89).  x is stored bf16
+    # (the counts are exact); accumulation is fp32.
+    "weibo_fp32": dict(trees=128, mean=816, sigma=0.8, feats=5000, classes=2, drop=(0.0, 0.0),
+                       desc="Weibo-shaped synthetic as weibo_bf16 with x stored fp32"),
+    "weibo_bf16": dict(trees=128, mean=816, sigma=0.8, feats=5000, classes=2, drop=(0.0, 0.0),
+                       xdtype="bf16",
+                       desc="Weibo-shaped synthetic: 128 trees/GPU, LogNormal(0.8) sizes mean 816 "
+                            "clamped [2,8192], 5000-dim BoW x stored bf16 (exact counts), no "
+                            "DropEdge, dropout 0.5, fp32 accumulation"),
 }
 
 # kernel classes timed by libbgcn's HIP-event hook (bgcn_set_kernel_timing)
@@ -53,17 +64,18 @@ KERNEL_CLASSES = {
 }
 SPARSE_CAP = 32
 # rocprofv3 kernel symbol of each timed class (for the PMC traffic lookup)
-ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true>", ("auto", 2): "bgcn::k_conv2_sparse",
-                 ("auto", 3): "bgcn::k_dw2", ("auto", 5): "bgcn::k_dw1_cols", ("auto", 7): "bgcn::k_compact_conv1<false>",
-                 ("dense", 0): "bgcn::k_gemm_xwt<true, false>", ("dense", 1): "bgcn::k_gemm_tn<true>",
-                 ("dense", 2): "bgcn::k_conv2_fwd", ("dense", 3): "bgcn::k_dw2"}
+ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2): "bgcn::k_conv2_sparse",
+                 ("auto", 3): "bgcn::k_dw2<float>", ("auto", 5): "bgcn::k_dw1_cols",
+                 ("auto", 7): "bgcn::k_compact_conv1<false, float>",
+                 ("dense", 0): "bgcn::k_gemm_xwt<true, false, float>", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
+                 ("dense", 2): "bgcn::k_conv2_fwd<float>", ("dense", 3): "bgcn::k_dw2<float>"}
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 
 
-def pmc_traffic(mode: str, cls: int):
+def pmc_traffic(mode: str, cls: int, workload: str = "twitter15"):
     """HBM bytes per launch of a kernel class from the committed PMC passes
     (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, same bench workload), or None."""
-    if mode != "auto":   # the committed PMC passes ran the default (auto) bench
+    if mode != "auto" or workload != "twitter15":   # the committed passes ran the default bench
         return None
     name = ROCPROF_NAMES.get((mode, cls))
     try:
@@ -74,16 +86,17 @@ def pmc_traffic(mode: str, cls: int):
     return None if k is None else round(float(k["hbm_bytes"]), 0)
 
 
-def kernel_work(mode: str, cls: int, N: float, Fd: int, prefetch: bool = False):
-    """(bound, algorithmic units per launch): FLOPs for MFMA kernels, bytes for HBM ones."""
+def kernel_work(mode: str, cls: int, N: float, Fd: int, prefetch: bool = False, xbytes: int = 4):
+    """(bound, algorithmic units per launch): FLOPs for MFMA kernels, bytes for HBM ones.
+    xbytes: bytes per stored feature (4 fp32, 2 bf16)."""
     H = 64
     if mode == "auto":
         if cls == 0:   # dense X read once + Z1 [N,128] + the compacted lists written
             if prefetch:   # conv1 from the prepared ELL: lists read, Z1 written
                 return "hbm", N * 2 * H * 4.0 + N * (SPARSE_CAP * 8.0 + 4.0)
-            return "hbm", N * Fd * 4.0 + N * 2 * H * 4.0 + N * (SPARSE_CAP * 8.0 + 4.0)
+            return "hbm", N * Fd * xbytes + N * 2 * H * 4.0 + N * (SPARSE_CAP * 8.0 + 4.0)
         if cls == 7:   # dense X read once + the compacted lists written
-            return "hbm", N * Fd * 4.0 + N * (SPARSE_CAP * 8.0 + 4.0)
+            return "hbm", N * Fd * xbytes + N * (SPARSE_CAP * 8.0 + 4.0)
         if cls == 2:   # H1 [N,128] read + Z2 [N,128] written (gathers of W2^T rows hit L2)
             return "hbm", N * 2 * H * 4.0 * 2
         if cls == 3:   # the relu(H1) block of dW2, both directions, reduction over N
@@ -111,7 +124,8 @@ def make_pool(wl, rank, pool, device, drop=None):
     for i in range(pool):
         rng = np.random.default_rng(20250205 + 1 + 1000 * rank + i)
         sizes = synth_tree_sizes(rng, wl["trees"], wl["mean"], wl["sigma"])
-        out.append(synth_batch(rng, sizes, wl["feats"], wl["classes"], *drop, device=device))
+        xdt = torch.bfloat16 if wl.get("xdtype") == "bf16" else torch.float32
+        out.append(synth_batch(rng, sizes, wl["feats"], wl["classes"], *drop, device=device, dtype=xdt))
     return out
 
 
@@ -157,17 +171,18 @@ def aggregation_bench(b, iters: int = 10):
     2*N*F*4 + 4*(N+1) + 8*(E+N)  (inputs read once, outputs written once, CSR)."""
     from bigcn_amd import ops
     N, Fd = b.x.shape
+    x = b.x.float()          # the aggregation runs in fp32 (a bf16 workload's x is converted)
     res = {}
     for name, ei in (("td", b.edge_index), ("bu", b.BU_edge_index)):
         g = ops.build_graph(ei, N)
         out = torch.empty(N, Fd, dtype=torch.float32, device=b.x.device)
         for _ in range(2):
-            ops.spmm(g, b.x, out=out)
+            ops.spmm(g, x, out=out)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record()
         for _ in range(iters):
-            ops.spmm(g, b.x, out=out)
+            ops.spmm(g, x, out=out)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / iters
@@ -209,7 +224,7 @@ def main():
                     help="at N=1 also time the other DropEdge placement and report it beside the main line")
     args = ap.parse_args()
 
-    from bigcn_amd import BiGCN, FusedTrainStep
+    from bigcn_amd import BiGCN, FusedTrainStep, Net
     from bigcn_amd import ops
     from bigcn_amd.dp import GradBucket, init_from_env
     from bigcn_amd.optim import bigcn_adam
@@ -224,7 +239,7 @@ def main():
     device_drop = args.path == "fused" and args.dropedge == "device"
     pool = make_pool(wl, rank, args.pool, dev, (0.0, 0.0) if device_drop else None)
     nodes = [b.x.size(0) for b in pool]
-    model = BiGCN(wl["feats"], 64, 64, dev).to(dev)
+    model = (BiGCN if wl["classes"] == 4 else Net)(wl["feats"], 64, 64, dev).to(dev)
     if world > 1:   # identical initial parameters on every rank
         for p in model.parameters():
             dist.broadcast(p.data, 0)
@@ -319,7 +334,8 @@ def main():
                 continue
             avg_ms = ms / n
             n_nodes = N_avg if where == "timed loop" else N_warm
-            bound, work = kernel_work(mode, c, n_nodes, wl["feats"], args.prefetch and args.path == "fused")
+            bound, work = kernel_work(mode, c, n_nodes, wl["feats"], args.prefetch and args.path == "fused",
+                                      2 if wl.get("xdtype") == "bf16" else 4)
             ent = {"avg_ms": round(avg_ms, 4), "launches": n, "measured": where}
             if bound == "mfma":
                 ent["tflops"] = round(work / (avg_ms * 1e-3) / 1e12, 2)
@@ -334,12 +350,12 @@ def main():
                 ach = work / (avg_ms * 1e-3) / 1e12
                 roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
-                        "traffic": pmc_traffic(mode, c), "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
+                        "traffic": pmc_traffic(mode, c, args.workload), "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
             else:
                 ach = work / (avg_ms * 1e-3) / 1e9
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(mode, c),
+                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(mode, c, args.workload),
                         "kernel": KERNEL_CLASSES[mode][c], "bytes_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
         value = wl["trees"] * world * steps / dt
@@ -372,7 +388,8 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "trees/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 x, f32 accumulate" if wl.get("xdtype") == "bf16" else "f32",
             "data": "synthetic (reference npz/Batch layout; real Twitter15 trees absent)",
             "config": {"workload": wl["desc"], "trees_per_gpu": wl["trees"], "feat_path": args.feat_mode,
                        "global_batch": wl["trees"] * world, "avg_nodes_per_batch": round(N_avg, 1),

@@ -163,6 +163,38 @@ __device__ __forceinline__ float4 xq_nt(const bf16_t* p) {
   const u32x2 u = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
   return bf4(u.x, u.y);
 }
+// raw streaming loads of 4 features, converted later: a conversion right after its load
+// would make the compiler wait for each load in turn instead of keeping all in flight
+// Row loads go through a buffer descriptor of the row (wave-uniform base, 32-bit lane
+// offsets + immediates, hardware range check: bytes past the row read as 0 - no clamped
+// addresses held in registers), non-temporal.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, uint32_t bytes) {
+  const uint64_t pa = reinterpret_cast<uint64_t>(row);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(pa));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(pa >> 32));
+  void* base = reinterpret_cast<void*>(uint64_t(lo) | (uint64_t(hi) << 32));
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr int kAuxNT = 2;   // buffer-load cache policy: non-temporal
+template <class TX> struct XRaw;
+template <> struct XRaw<float> {
+  typedef u32x4 raw;
+  __device__ static raw ld(__amdgpu_buffer_rsrc_t rs, int quad) {
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, quad * 16, 0, kAuxNT);
+  }
+  __device__ static float4 cvt(raw r) {
+    return make_float4(__uint_as_float(r.x), __uint_as_float(r.y), __uint_as_float(r.z),
+                       __uint_as_float(r.w));
+  }
+};
+template <> struct XRaw<bf16_t> {
+  typedef u32x2 raw;
+  __device__ static raw ld(__amdgpu_buffer_rsrc_t rs, int quad) {
+    return __builtin_amdgcn_raw_buffer_load_b64(rs, quad * 8, 0, kAuxNT);
+  }
+  __device__ static float4 cvt(raw r) { return bf4(r.x, r.y); }
+};
 __device__ __forceinline__ float xs(const float* p) { return *p; }
 __device__ __forceinline__ float xs(const bf16_t* p) { return bf2f(*p); }
 

@@ -136,7 +136,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
 // (sizes shared with bgcn_sparse.h: tree work items of kChunkItems nodes, CSC row blocks)
 constexpr int kChunkItems = 256;
 constexpr int kCscRowBlock = 256;
-constexpr int64_t kSparseMaxFeat = 16384;
+constexpr int64_t kSparseMaxFeat = 5120;   // widest X of the sparse path (one pass per row)
 struct Prepared {
   bgcn_csr_out td, bu;
   int64_t td_cap, bu_cap;                // E + N

@@ -130,61 +130,48 @@ __device__ __forceinline__ float2 conv1_row(const SparseState& S, int cnt, int32
   return acc;
 }
 
-// kConv1 = true: compaction + conv1 in one pass (the encoder's forward); false: the ELL
-// only (weight-independent batch preparation, bgcn_prepare_batch).
+// Row i of X -> its ELL list (+ conv1).  r: the row's quads (kRowChunks per lane: the
+// whole row, F <= kSparseMaxF), already in flight.
+static_assert(kRowChunks * 64 * 4 >= kSparseMaxF, "one pass per row");
 template <bool kConv1, class TX>
-__global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* __restrict__ X,
-                                                       int64_t ldx, float* __restrict__ Z1) {
-  __shared__ int32_t s_col[4][kCap];
-  __shared__ float s_val[4][kCap];
-  if (S.mode == 1) return;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // grid-stride over rows: the preparation launches a small grid so that it streams X
-  // beside the training chain without taking every CU slot
-  for (int64_t i = int64_t(blockIdx.x) * 4 + wave; i < S.N; i += int64_t(gridDim.x) * 4) {
-  const TX* row = X + i * ldx;
-  const int nq = int(S.F / 4);   // float4 per row (F % 4 == 0)
-  int cnt = 0;
+__device__ __forceinline__ void compact_row(const SparseState& S, int64_t i,
+                                            const typename XRaw<TX>::raw* r, int32_t* s_col,
+                                            float* s_val, float* __restrict__ Z1) {
+  const int lane = threadIdx.x & 63;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int q0 = 0; q0 < nq; q0 += kRowChunks * 64) {
-    float4 v[kRowChunks];
+  int cnt = 0;
 #pragma unroll
-    for (int u = 0; u < kRowChunks; ++u) {
-      const int q = q0 + u * 64 + lane;
-      v[u] = q < nq ? xq_nt(row + int64_t(q) * 4) : f4zero();
-    }
+  for (int u = 0; u < kRowChunks; ++u) {
+    const float4 vu = XRaw<TX>::cvt(r[u]);   // past the row: 0 (range-checked load)
+    const bool n0 = vu.x != 0.f, n1 = vu.y != 0.f, n2 = vu.z != 0.f, n3 = vu.w != 0.f;
+    if (__ballot(n0 || n1 || n2 || n3) == 0ull) continue;   // wave-uniform skip
+    const uint64_t m0 = __ballot(n0), m1 = __ballot(n1), m2 = __ballot(n2), m3 = __ballot(n3);
+    // ascending column order: lanes below me contribute all their non-zeros first
+    int pos = cnt + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+    const int col0 = (u * 64 + lane) * 4;
+    const float e[4] = {vu.x, vu.y, vu.z, vu.w};
+    const bool nz[4] = {n0, n1, n2, n3};
 #pragma unroll
-    for (int u = 0; u < kRowChunks; ++u) {
-      const bool n0 = v[u].x != 0.f, n1 = v[u].y != 0.f, n2 = v[u].z != 0.f, n3 = v[u].w != 0.f;
-      if (__ballot(n0 || n1 || n2 || n3) == 0ull) continue;   // wave-uniform skip
-      const uint64_t m0 = __ballot(n0), m1 = __ballot(n1), m2 = __ballot(n2), m3 = __ballot(n3);
-      // ascending column order: lanes below me contribute all their non-zeros first
-      int pos = cnt + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
-      const int col0 = (q0 + u * 64 + lane) * 4;
-      const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-      const bool nz[4] = {n0, n1, n2, n3};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (nz[c]) {
-          if (pos < kCap) {
-            s_col[wave][pos] = col0 + c;
-            s_val[wave][pos] = e[c];
-          }
-          ++pos;
+    for (int c = 0; c < 4; ++c) {
+      if (nz[c]) {
+        if (pos < kCap) {
+          s_col[pos] = col0 + c;
+          s_val[pos] = e[c];
         }
+        ++pos;
       }
-      cnt += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
     }
+    cnt += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
   }
   if (lane == 0) S.nnz[i] = cnt;
   if (cnt > kCap) {
     if (lane == 0) atomicOr(&S.flags[0], 1);
-    continue;
+    return;
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes have landed
   __builtin_amdgcn_wave_barrier();
-  const int32_t col_l = lane < cnt ? s_col[wave][lane] : 0;
-  const float val_l = lane < cnt ? s_val[wave][lane] : 0.f;
+  const int32_t col_l = lane < cnt ? s_col[lane] : 0;
+  const float val_l = lane < cnt ? s_val[lane] : 0.f;
   if (lane < cnt) {
     S.cols[i * kCap + lane] = col_l;
     S.vals[i * kCap + lane] = val_l;
@@ -193,6 +180,37 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* 
     const float2 acc = conv1_row(S, cnt, col_l, val_l);
     *reinterpret_cast<float2*>(Z1 + i * (2 * H) + 2 * lane) = acc;
   }
+}
+
+// kConv1 = true: compaction + conv1 in one pass (the encoder's forward); false: the ELL
+// only (weight-independent batch preparation, bgcn_prepare_batch).  A wave keeps ~20 KB
+// of X in flight: one fp32 row, or two bf16 rows (their loads issued together).
+template <bool kConv1, class TX>
+__global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* __restrict__ X,
+                                                       int64_t ldx, float* __restrict__ Z1) {
+  constexpr int kRows = sizeof(TX) == 2 ? 2 : 1;
+  __shared__ int32_t s_col[4][kCap];
+  __shared__ float s_val[4][kCap];
+  if (S.mode == 1) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // grid-stride over rows: the preparation launches a small grid so that it streams X
+  // beside the training chain without taking every CU slot
+  const int64_t stride = int64_t(gridDim.x) * 4;
+  for (int64_t i0 = int64_t(blockIdx.x) * 4 + wave; i0 < S.N; i0 += stride * kRows) {
+    typename XRaw<TX>::raw r[kRows][kRowChunks];
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {   // all loads in flight; a row past N reads nothing
+      const int64_t ik = i0 + k * stride;
+      const __amdgpu_buffer_rsrc_t rs =
+          row_rsrc(X + min<int64_t>(ik, S.N - 1) * ldx, ik < S.N ? uint32_t(S.F * sizeof(TX)) : 0u);
+#pragma unroll
+      for (int u = 0; u < kRowChunks; ++u) r[k][u] = XRaw<TX>::ld(rs, u * 64 + lane);
+    }
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const int64_t i = i0 + k * stride;
+      if (i < S.N) compact_row<kConv1, TX>(S, i, r[k], s_col[wave], s_val[wave], Z1);
+    }
   }
 }
 

@@ -169,13 +169,24 @@ def drop_edges(td_edge_index: Optional[torch.Tensor], bu_edge_index: Optional[to
 # ----------------------------------------------------------------------------- K3/K4
 def spmm(g: Graph, x: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: bool = False,
          transposed: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``out = A_hat x (+bias)`` (or ``A_hat^T x``); x [N, F] fp32 with F % 4 == 0."""
+    """``out = A_hat x (+bias)`` (or ``A_hat^T x``); x [N, F] with F % 4 == 0 (computed in
+    fp32: other dtypes are converted)."""
     _dev_check(x, bias)
+    if x.dim() != 2 or x.size(0) != g.num_nodes:
+        raise ValueError(f"x must be [num_nodes={g.num_nodes}, F]")
     N, F = x.shape
+    if x.dtype != torch.float32:
+        x = x.float()
     if x.stride(1) != 1:
         x = x.contiguous()
+    if bias is not None:
+        bias = bias.to(torch.float32).contiguous()
+        if bias.numel() != F:
+            raise ValueError("bias must have F elements")
     if out is None:
         out = torch.empty(N, F, dtype=torch.float32, device=x.device)
+    elif out.dtype != torch.float32 or out.shape != (N, F) or out.stride(1) != 1:
+        raise ValueError("out must be a row-major fp32 [N, F] tensor")
     L = _lib.lib()
     ws = workspace(L.bgcn_spmm_workspace_size(g.capacity, F), x.device)
     p = (g.s_ptr, g.s_row, g.s_col, g.s_w) if transposed else (g.t_ptr, g.t_row, g.t_col, g.t_w)
@@ -317,6 +328,21 @@ _PARAM_ORDER = ("td_w1", "td_b1", "td_w2", "td_b2", "bu_w1", "bu_b1", "bu_w2", "
 _FEAT_MODES = {"auto": _lib.BGCN_FEAT_AUTO, "sparse": _lib.BGCN_FEAT_AUTO, "dense": _lib.BGCN_FEAT_DENSE}
 
 
+def check_encoder_shapes(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, params) -> None:
+    """Host-side shape contract of the fused encoder (the kernels trust it)."""
+    if x.dim() != 2:
+        raise ValueError("x must be [N, F]")
+    N, F = x.shape
+    want = [(HID, F), (HID,), (HID, HID + F), (HID,)] * 2
+    for p, shp in zip(params, want):
+        if tuple(p.shape) != shp:
+            raise ValueError(f"parameter of shape {tuple(p.shape)}, expected {shp} for in_feats={F}")
+    if batch.numel() != N:
+        raise ValueError("batch must have one entry per node")
+    if rootindex.dim() != 1:
+        raise ValueError("rootindex must be 1-D")
+
+
 def features(x: torch.Tensor) -> torch.Tensor:
     """Node features as the fused path reads them: bf16 stays bf16 (the bf16
     configuration: bag-of-words counts are exact), anything else becomes fp32;
@@ -419,6 +445,7 @@ def bigcn_encoder(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor,
     for p in params:
         if p.dtype != torch.float32 or not p.is_contiguous():
             raise ValueError("parameters must be contiguous fp32")
+    check_encoder_shapes(x, batch, rootindex, params)
     if keep_words is not None:
         keep_words = keep_words.contiguous()
     return _BiGCNEncoderFn.apply(x, batch.to(torch.int64).contiguous(), rootindex.to(torch.int64).contiguous(),

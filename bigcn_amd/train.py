@@ -25,7 +25,7 @@ from . import _lib
 from ._lib import BatchDesc, StepArgs, check, ptr, stream_handle, workspace
 from .bigcn import BiGCN, _draw_seed, _num_graphs
 from .dp import GradBucket
-from .ops import _FEAT_MODES, features, x_dtype_code
+from .ops import _FEAT_MODES, check_encoder_shapes, features, x_dtype_code
 from .optim import FusedAdam, bigcn_adam
 
 
@@ -89,6 +89,9 @@ class FusedTrainStep:
     def _desc(self, data):
         """bgcn_batch of a collated batch (+ the tensors it points into, kept alive)."""
         x = features(data.x)                         # fp32, or bf16 kept as is
+        check_encoder_shapes(x, data.batch, data.rootindex, self.step_params[:8])
+        if data.rootindex.numel() != _num_graphs(data) or data.y.numel() != _num_graphs(data):
+            raise ValueError("rootindex and y must have one entry per tree")
         td_ei = _need(data.edge_index, torch.int64, "edge_index")
         bu_ei = _need(data.BU_edge_index, torch.int64, "BU_edge_index")
         batch = _need(data.batch, torch.int64, "batch")

@@ -16,16 +16,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=100)
+    ap.add_argument("--workload", default="twitter15")
     args = ap.parse_args()
     import bench
-    from bigcn_amd import BiGCN, FusedTrainStep, _lib
+    from bigcn_amd import BiGCN, FusedTrainStep, Net, _lib
     from bigcn_amd._lib import check, ptr, stream_handle
     from bigcn_amd.ops import _FEAT_MODES
     from bigcn_amd.optim import bigcn_adam
     dev = torch.device("cuda", 0)
-    wl = bench.WORKLOADS["twitter15"]
+    wl = bench.WORKLOADS[args.workload]
     pool = bench.make_pool(wl, 0, 4, dev)
-    model = BiGCN(wl["feats"], 64, 64, dev).to(dev)
+    model = (BiGCN if wl["classes"] == 4 else Net)(wl["feats"], 64, 64, dev).to(dev)
     model.train()
     fused = FusedTrainStep(model, bigcn_adam(model))
     L = _lib.lib()
