@@ -636,7 +636,7 @@ static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool 
                        transposed ? v.s_col : v.t_col, transposed ? v.s_w : v.t_w,
                        in + d * H, 2 * H, out + d * H, 2 * H, d == 0 ? bias_td : bias_bu,
                        reinterpret_cast<float*>(reinterpret_cast<char*>(w.spmm_ws) + d * half),
-                       spmm_groups(v.capacity, H)};
+                       spmm_groups(v.capacity, H), v.capacity};
   }
   return spmm_batch_impl(sb, 2, s);
 }
@@ -697,7 +697,9 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
 
   if (prep) {
     // prepared batch (bgcn_train_step): graphs, tree maps, items, ELL and CSC of X exist;
-    // only the weight transposes and conv1's gather from the ELL remain
+    // only the weight transposes and conv1's gather from the ELL remain (the prologue
+    // also clears the step's status word, which the head ORs into)
+    sp.zero_word = head ? head->status : nullptr;
     BGCN_TRY(sparse_prologue(sp, a, w.node_root, s, false));
     if (sparse) {
       timing_begin(0, s);

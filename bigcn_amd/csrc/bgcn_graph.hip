@@ -285,7 +285,15 @@ __global__ void k_nodes(GraphBatch gb) {
 __global__ void k_normalize(GraphBatch gb) {
   GraphIO& G = gb.g[blockIdx.y];
   const int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p >= int64_t(G.t_ptr[gb.N])) return;
+  if (p >= int64_t(G.t_ptr[gb.N])) {
+    // the unused tail of the capacity (dropped self loops, invalid edges): row -1 marks
+    // it for the aggregation kernels, which then need not read the entry count first
+    if (p < G.E + gb.N) {
+      G.t_row[p] = -1; G.t_col[p] = 0; G.t_w[p] = 0.f;
+      G.s_row[p] = -1; G.s_col[p] = 0; G.s_w[p] = 0.f;
+    }
+    return;
+  }
   // dinv[row] * w * dinv[col] with row = source, col = target (PyG order)
   G.t_w[p] = (G.dinv[G.t_col[p]] * G.t_w[p]) * G.dinv[G.t_row[p]];
   G.s_w[p] = (G.dinv[G.s_row[p]] * G.s_w[p]) * G.dinv[G.s_col[p]];

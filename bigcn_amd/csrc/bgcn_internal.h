@@ -18,6 +18,7 @@ struct SpmmProb {
   const float* bias;
   float* part;  // [ngroups][2][F] partial rows of chunk-crossing rows
   int64_t ngroups;
+  int64_t capacity;  // allocated entries; [ptr[rows], capacity) hold row = -1 (K1 writes them)
 };
 
 struct SpmmBatch {

@@ -28,6 +28,7 @@ struct SparseState {
   uint32_t* csc_slot;   // [N*kCap] slots (i*kCap + s) grouped by column, rows in order
   uint32_t* rbits;      // [2][N] forward's root keep masks (bit s: root non-zero s kept)
   float* csc_val;       // [N*kCap] X value of each csc_slot entry
+  int32_t* zero_word = nullptr;   // zeroed by the prologue (the train step's status word)
 };
 
 constexpr int kRowBlock = kCscRowBlock;   // rows per block of the CSC counting sort

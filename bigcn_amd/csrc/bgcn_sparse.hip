@@ -71,6 +71,7 @@ __global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __
                                                   int32_t* __restrict__ tree_ptr, int nTx, int nT,
                                                   int nR) {
   const int blk = blockIdx.x;
+  if (blk == 0 && threadIdx.x == 0 && S.zero_word) *S.zero_word = 0;
   if (blk < nT) {
     if (S.mode == 1) return;
     transpose_tile(S, blk % nTx, (blk / nTx) % 2, blk / (2 * nTx), w1td, w1bu, w2td, w2bu);
@@ -784,8 +785,9 @@ int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root
   const int nT = S.mode == 1 ? 0 : nTx * 2 * 4;
   const int nR = batch_part ? int((S.N + 255) / 256) : 0;
   const int nP = batch_part ? int((S.B + 1 + 255) / 256) : 0;
-  if (nT + nR + nP == 0) return BGCN_OK;
-  hipLaunchKernelGGL(k_prologue, dim3(unsigned(nT + nR + nP)), dim3(256), 0, s, S, a->td_w1, a->bu_w1,
+  const int nZ = (nT + nR + nP == 0 && S.zero_word) ? 1 : 0;
+  if (nT + nR + nP + nZ == 0) return BGCN_OK;
+  hipLaunchKernelGGL(k_prologue, dim3(unsigned(nT + nR + nP + nZ)), dim3(256), 0, s, S, a->td_w1, a->bu_w1,
                      a->td_w2, a->bu_w2, a->batch, a->rootindex, node_root, a->tree_ptr, nTx, nT, nR);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;

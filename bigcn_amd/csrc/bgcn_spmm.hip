@@ -42,23 +42,27 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
   const int lane = threadIdx.x % LANES;
   const int64_t g = int64_t(blockIdx.x) * GPB + threadIdx.x / LANES;
   if (g >= P.ngroups) return;
-  const int64_t nnz = P.ptr[sb.rows];
+  const int64_t cap = P.capacity;
   const int64_t p0 = g * NPG;
-  if (p0 >= nnz) return;
-  const int64_t p1 = min<int64_t>(p0 + NPG, nnz);
-  const int n = int(p1 - p0);
+  const int64_t p1 = min<int64_t>(p0 + NPG, cap);
   const int fo = lane * 4;
   const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
 
   // entry k of the chunk lives in lane k of the group.  Whether the first row started
   // before the chunk / the last row runs past it is read off the neighbouring entries
-  // (row[p0-1], row[p1]) - loaded alongside the chunk, so no dependent ptr[] loads.
-  const bool mine = lane < n;
-  const int32_t r_l = mine ? P.row[p0 + lane] : -1;
-  const int32_t c_l = mine ? P.col[p0 + lane] : 0;
-  const float w_l = mine ? P.w[p0 + lane] : 0.f;
-  const int32_t prev_row = p0 > 0 ? P.row[p0 - 1] : -1;
-  const int32_t next_row = p1 < nnz ? P.row[p1] : -1;
+  // (row[p0-1], row[p1]) - loaded alongside the chunk, so no dependent loads: entries
+  // past the valid count carry row -1 (K1), so the count itself is never read.
+  const bool mine = lane < NPG && p0 + lane < cap;
+  const int64_t pl = min<int64_t>(p0 + lane, cap - 1);   // clamped, unconditional
+  const int32_t r_ld = P.row[pl], c_ld = P.col[pl];
+  const float w_ld = P.w[pl];
+  const int32_t r_l = mine ? r_ld : -1;
+  const int32_t c_l = mine ? c_ld : 0;
+  const float w_l = mine ? w_ld : 0.f;
+  const int32_t prev_ld = P.row[p0 > 0 ? p0 - 1 : 0], next_ld = P.row[min<int64_t>(p1, cap - 1)];
+  const int32_t prev_row = p0 > 0 ? prev_ld : -1;
+  const int32_t next_row = p1 < cap ? next_ld : -1;
+  const int n = int(p1 - p0);
   const int base_lane = ((threadIdx.x & 63) / LANES) * LANES;  // group's first lane in the wave
 
   float4 acc = f4zero();
@@ -117,11 +121,9 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
   const SpmmProb& P = sb.p[blockIdx.y];
   const int64_t g = int64_t(blockIdx.x) + 1;
   if (g >= P.ngroups) return;
-  const int64_t nnz = P.ptr[sb.rows];
-  const int64_t pb = g * NPG;
-  if (pb >= nnz) return;
-  const int32_t r = P.row[pb];
-  if (P.row[pb - 1] != r) return;            // row starts at the boundary: no crossing
+  const int64_t pb = g * NPG;                // < capacity (g < ngroups)
+  const int32_t r = P.row[pb], rp = P.row[pb - 1];
+  if (r < 0 || rp != r) return;              // padding, or the row starts at the boundary
   const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
   const int64_t g0 = rs / NPG, g1 = (re - 1) / NPG;
   if (g1 != g) return;                       // only the row's last chunk does the fixup
@@ -367,7 +369,7 @@ int spmm_impl(const int32_t* ptr, const int32_t* row, const int32_t* col, const 
   sb.F = F;
   sb.epi = epi;
   sb.p[0] = SpmmProb{ptr, row, col, w, in, ld_in, out, ld_out, bias, static_cast<float*>(ws),
-                     (capacity + npg_for(F) - 1) / npg_for(F)};
+                     (capacity + npg_for(F) - 1) / npg_for(F), capacity};
   return spmm_batch_impl(sb, 1, stream);
 }
 

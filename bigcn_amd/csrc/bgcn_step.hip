@@ -265,7 +265,7 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
 static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w, hipStream_t s,
                            int graph_lane) {
   const int64_t N = a->cur.num_nodes, B = a->cur.num_graphs, F = a->in_feats, C = a->num_classes;
-  if (a->status) BGCN_CHECK_HIP(hipMemsetAsync(a->status, 0, sizeof(int32_t), s));
+  // (*status is cleared by the forward's prologue)
   bgcn_bigcn_args e{};
   e.x = a->cur.x; e.x_dtype = a->cur.x_dtype;
   e.ldx = a->cur.ldx; e.num_nodes = N; e.num_graphs = B; e.in_feats = F; e.hid = H;

@@ -107,7 +107,8 @@ int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_num_edges,
  * out[r, :F] = epi( sum_{p in row r} w[p] * in[col[p], :F]  (+ bias) )
  * Atomic-free and deterministic: the nnz range is split evenly over lane groups
  * (merge path) and rows that cross a split are combined in a fixed order.
- * `capacity` = allocated entries (E + N); the valid count is read from ptr[rows].
+ * `capacity` = allocated entries (E + N); entries [ptr[rows], capacity) must carry
+ * row = -1 (bgcn_build_graph writes them), so the kernels never wait on the count.
  * F: a multiple of 4, at most 6144 (64 and 128 take the narrow kernels).
  * -------------------------------------------------------------------------- */
 size_t bgcn_spmm_workspace_size(int64_t capacity, int32_t F);
