@@ -109,46 +109,80 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
   }
 }
 
-// Fixup, one block per chunk boundary g*NPG (g >= 1), F <= 128: if the row containing
-// entry g*NPG started before it and this is the row's last chunk, sum its partials
-// tail[g0], head[g0+1..g1] and write the row.  A BU star root spans hundreds of chunks,
-// so the partial list is split over 256/LANES sub-groups (sub-group s takes items
-// s, s+SG, ...) and combined in a fixed order: deterministic.
+// Fixup, F <= 128: one block per SG = 256/LANES chunk boundaries, sub-group s checking
+// boundary blockIdx.x*SG + s + 1.  A row that crosses it and ends in that chunk gets its
+// partials tail[g0], head[g0+1..g1] summed in chunk order and is written: by the
+// sub-group itself when it has <= kSmall pieces (TD rows, most BU rows), by the whole
+// block otherwise (a BU star root spans hundreds of chunks: sub-group q takes items
+// q, q+SG, ..., combined in a fixed order).  Deterministic; one row's sum is the same
+// either way.
 template <int LANES>
 __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
   constexpr int SG = 256 / LANES;
+  constexpr int kSmall = 8;                  // pieces a sub-group sums on its own
   __shared__ float4 red[SG][LANES];
+  __shared__ int32_t big[SG];                // rows of > kSmall pieces found by sub-group s
   const SpmmProb& P = sb.p[blockIdx.y];
-  const int64_t g = int64_t(blockIdx.x) + 1;
-  if (g >= P.ngroups) return;
-  const int64_t pb = g * NPG;                // < capacity (g < ngroups)
-  const int32_t r = P.row[pb], rp = P.row[pb - 1];
-  if (r < 0 || rp != r) return;              // padding, or the row starts at the boundary
-  const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
-  const int64_t g0 = rs / NPG, g1 = (re - 1) / NPG;
-  if (g1 != g) return;                       // only the row's last chunk does the fixup
   const int s = threadIdx.x / LANES, fo = (threadIdx.x % LANES) * 4;
-  const int64_t m = g1 - g0 + 1;             // item 0 = tail[g0], item j = head[g0 + j]
-  float4 acc = f4zero();
-  int64_t j = s;
-  for (; j + 3 * SG < m; j += 4 * SG) {
-    float4 v[4];
+  const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
+  auto item = [&](int64_t g0, int64_t j) {   // item 0 = tail[g0], item j = head[g0 + j]
+    return ld4(P.part + ((g0 + j) * 2 + (j == 0 ? 1 : 0)) * (LANES * 4) + fo);
+  };
+  // sub-group s checks boundary g = blockIdx.x * SG + s + 1
+  const int64_t g = int64_t(blockIdx.x) * SG + s + 1;
+  int32_t mine = -1;
+  if (g < P.ngroups) {
+    const int64_t pb = g * NPG;              // < capacity (g < ngroups)
+    const int32_t r = P.row[pb], rp = P.row[pb - 1];
+    if (r >= 0 && rp == r) {                 // a row crossing the boundary ...
+      const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
+      const int64_t g0 = rs / NPG, g1 = (re - 1) / NPG;
+      if (g1 == g) {                         // ... whose last piece is chunk g
+        const int64_t m = g1 - g0 + 1;
+        if (m <= kSmall) {                   // sequential sum, all loads in flight
+          float4 v[kSmall];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t jj = j + u * SG;
-      v[u] = ld4(P.part + ((g0 + jj) * 2 + (jj == 0 ? 1 : 0)) * (LANES * 4) + fo);
+          for (int j = 0; j < kSmall; ++j) v[j] = item(g0, j < m ? j : 0);
+          float4 acc = v[0];
+#pragma unroll
+          for (int j = 1; j < kSmall; ++j)
+            if (j < m) acc = f4add(acc, v[j]);
+          st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+        } else {
+          mine = r;
+        }
+      }
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc = f4add(acc, v[u]);
   }
-  for (; j < m; j += SG) acc = f4add(acc, ld4(P.part + ((g0 + j) * 2 + (j == 0 ? 1 : 0)) * (LANES * 4) + fo));
-  red[s][threadIdx.x % LANES] = acc;
+  if (fo == 0) big[s] = mine;
   __syncthreads();
-  if (s == 0) {
-    float4 t = red[0][threadIdx.x];
+  // rows of many pieces (BU star roots): the whole block, sub-group q takes items
+  // q, q+SG, ..., combined in a fixed order (deterministic)
+  for (int t = 0; t < SG; ++t) {
+    const int32_t r = big[t];
+    if (r < 0) continue;                     // uniform
+    const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
+    const int64_t g0 = rs / NPG, g1 = (re - 1) / NPG;
+    const int64_t m = g1 - g0 + 1;
+    float4 acc = f4zero();
+    int64_t j = s;
+    for (; j + 3 * SG < m; j += 4 * SG) {
+      float4 v[4];
 #pragma unroll
-    for (int q = 1; q < SG; ++q) t = f4add(t, red[q][threadIdx.x]);
-    st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(t, P.bias ? ld4(P.bias + fo) : f4zero(), sb.epi));
+      for (int u = 0; u < 4; ++u) v[u] = item(g0, j + u * SG);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = f4add(acc, v[u]);
+    }
+    for (; j < m; j += SG) acc = f4add(acc, item(g0, j));
+    red[s][threadIdx.x % LANES] = acc;
+    __syncthreads();
+    if (s == 0) {
+      float4 sum = red[0][threadIdx.x];
+#pragma unroll
+      for (int q = 1; q < SG; ++q) sum = f4add(sum, red[q][threadIdx.x]);
+      st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(sum, bv, sb.epi));
+    }
+    __syncthreads();
   }
 }
 
@@ -338,13 +372,15 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
     hipLaunchKernelGGL(k_spmm_narrow<L>, dim3(grid_for(gmax, 256 / L), gy), dim3(256), 0, stream, sb);
     BGCN_CHECK_LAUNCH();
     if (gmax > 1)
-      hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(unsigned(gmax - 1), gy), dim3(256), 0, stream, sb);
+      hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(grid_for(gmax - 1, 256 / L), gy), dim3(256), 0,
+                         stream, sb);
   } else if (F == 128) {
     constexpr int L = 32;
     hipLaunchKernelGGL(k_spmm_narrow<L>, dim3(grid_for(gmax, 256 / L), gy), dim3(256), 0, stream, sb);
     BGCN_CHECK_LAUNCH();
     if (gmax > 1)
-      hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(unsigned(gmax - 1), gy), dim3(256), 0, stream, sb);
+      hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(grid_for(gmax - 1, 256 / L), gy), dim3(256), 0,
+                         stream, sb);
   } else {
     BGCN_CHECK_ARG(F <= kWideThreads * 4 * kWideCols, "F > 6144 is not supported by the wide aggregation");
     const unsigned slices = unsigned((F + kWideSlice - 1) / kWideSlice);
