@@ -565,7 +565,7 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   t.S2 = int((N + kc - 1) / kc);
   if (t.S2 < 1) t.S2 = 1;
   // sparse path: relu(H1) block of dW2 over 256-node splits (partial rows of 64)
-  t.kchunkh = 256;
+  t.kchunkh = 128;
   t.Sh = int((N + t.kchunkh - 1) / t.kchunkh);
   if (t.Sh < 1) t.Sh = 1;
   const size_t dense_part = size_t(2) * t.S2 * H * (H + F), sparse_part = size_t(2) * t.Sh * H * H;
