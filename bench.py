@@ -52,6 +52,15 @@ WORKLOADS = {
                        desc="Weibo-shaped synthetic: 128 trees/GPU, LogNormal(0.8) sizes mean 816 "
                             "clamped [2,8192], 5000-dim BoW x stored bf16 (exact counts), no "
                             "DropEdge, dropout 0.5, fp32 accumulation"),
+    # BASELINE.json configs[4]: synthetic trees of mean 1024 nodes, 5000-dim, bf16 (the
+    # HBM-roofline stress shape); per GPU one step = 128 such trees (weak scaling), the
+    # training-run defaults of the Twitter script (DropEdge 0.2/0.2, 4 classes).
+    # configs[3] (100k trees of mean 256) has the per-GPU step shape of "twitter15".
+    "synth1024_bf16": dict(trees=128, mean=1024, sigma=0.8, feats=5000, classes=4, drop=(0.2, 0.2),
+                           xdtype="bf16",
+                           desc="synthetic stress: 128 trees/GPU, LogNormal(0.8) sizes mean 1024 "
+                                "clamped [2,8192], 5000-dim BoW x stored bf16, DropEdge 0.2/0.2, "
+                                "dropout 0.5, fp32 accumulation"),
 }
 
 # kernel classes timed by libbgcn's HIP-event hook (bgcn_set_kernel_timing)

@@ -15,8 +15,8 @@
 // Narrow kernel (F = 64 / 128): a group = F/4 lanes, one float4 per lane; the
 // chunk's (row, col, w) triples are loaded once (one entry per lane) and broadcast
 // with cross-lane shuffles; 8 neighbour rows are in flight per group.
-// Wide kernel (F > 128 up to 6144, e.g. the 5000-dim standalone aggregation): a group
-// = one 512-thread block over the full row width.
+// Wide kernel (F > 128, e.g. the 5000-dim standalone aggregation): a group = one wave
+// per (chunk, 256-float column slice).
 // Up to two problems (the fused step's TD and BU graphs) share one launch
 // (blockIdx.y / blockIdx.z = problem).
 #include "bgcn_internal.h"
@@ -186,28 +186,14 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
   }
 }
 
-// Wide kernel (F > 128, e.g. the 5000-dim A_hat . X).  HBM-bound: every X row is
-// needed by its own output row and by its neighbours' (parent / children), so the
-// design goal is to fetch each row from HBM about once and stream the output out:
-//   * a block processes chunks over the FULL row width (thread t owns float4 columns
-//     t, t+512, ...: F <= 6144 in kWideCols passes) - whole 20 KB rows, page friendly;
-//   * one resident block per CU (kWideBlocks) sweeps a contiguous range of chunks
-//     per XCD (the hardware deals blocks to the 8 XCDs round robin), so the rows in
-//     flight form a narrow moving window (~4k entries, tens of MB): a parent / child row
-//     needed again a few chunks later is still in the XCD's L2 or the Infinity Cache;
-//   * output rows are written non-temporally (never re-read here), keeping the caches
-//     for X;
-//   * chunk boundaries are row-aligned for rows of <= NPGW entries (the nominal boundary
-//     g * NPGW moves back to the start of the row it falls in), so only long rows (BU
-//     star roots) leave partial rows for the fixup pass.
-// kWideDepth entries are in flight per thread (kWideDepth * kWideCols float4 loads).
+// Wide aggregation (F > 128, e.g. the 5000-dim A_hat . X).  HBM-bound: every X row is
+// needed by its own output row and by its neighbours' (parent / children); the output is
+// written once.  Chunks of NPGW entries (merge path as above) are row-aligned for rows of
+// <= NPGW entries (the nominal boundary g * NPGW moves back to the start of the row it
+// falls in), so only long rows (BU star roots) leave partial rows for the fixup pass.
 constexpr int NPGW = 16;
-constexpr int kWideThreads = 512;
-constexpr int kWideCols = 3;     // float4 per thread per row: F <= 512 * 4 * 3 = 6144
-constexpr int kWideSlice = 1024; // fixup slice (floats)
-constexpr int kWideDepth = 8;
-constexpr int kWideBlocks = 256; // one per CU
-constexpr int kXcds = 8;
+constexpr int kWideSlice = 1024;   // fixup slice (floats)
+constexpr int kWaveBlock = 256;    // 4 waves per block
 
 // first entry of chunk g: g*NPGW, or the start of the row containing it when that row
 // is short (<= NPGW entries, never split)
@@ -219,89 +205,113 @@ __device__ __forceinline__ int64_t wide_chunk_start(const SpmmProb& P, int64_t g
   return re - rs <= NPGW ? rs : p;
 }
 
-__global__ __launch_bounds__(kWideThreads) void k_spmm_wide(SpmmBatch sb) {
+
+// Slice kernel: one short-lived wave per (chunk, 256-float column slice), one float4 per
+// lane.  Measured on MI355X (tools/copy_probe.hip, profiles/r01_agg_variants.txt):
+// HBM streams fastest when the work is cut into small units that the dispatcher hands
+// out in address order, so the bytes in flight form ONE compact moving window (a copy of
+// 1 KB per wave: 6.3-6.5 TB/s) - not when each wave or block sweeps its own run of rows
+// (8 rows per wave: 4.8-4.9 TB/s; a block-per-CU sweep and a wave-per-row-slice sweep of
+// this aggregation ran at 4.6-4.9 TB/s, this kernel at 5.0-5.4).  Waves
+// u = g*S + s, so the S slices of chunk g run side by side and read its rows whole.
+//   * the chunk's entries sit one per lane (plus the entries just before / after it) and
+//     are broadcast with readlane, so row changes, source rows and weights are
+//     wave-uniform; every X / output row is addressed through a buffer descriptor
+//     (scalar base, hardware range check at F);
+//   * 16 source slices in flight per wave: entries are loaded in groups of 8, two
+//     groups ahead; loads of padding entries go through a zero-size buffer descriptor
+//     (no memory traffic), so every load is unconditional and the waits stay exact;
+//   * default-policy X loads (parent / child re-reads hit L2 / the Infinity Cache: the
+//     non-temporal variant measured 13-29 % slower), non-temporal output stores.
+constexpr int kSliceGroup = 8;
+
+__global__ __launch_bounds__(kWaveBlock) void k_spmm_slice(SpmmBatch sb, int slices) {
   const SpmmProb& P = sb.p[blockIdx.y];
-  __shared__ int32_t s_r[2 * NPGW], s_c[2 * NPGW];
-  __shared__ float s_w[2 * NPGW];
-  // XCD x sweeps chunks [x*R, (x+1)*R) with its gridDim.x / 8 blocks
-  const int64_t R = (P.ngroups + kXcds - 1) / kXcds;
-  const int64_t x = blockIdx.x % kXcds, per = gridDim.x / kXcds;   // grid: multiple of kXcds
-  const int64_t gend = min<int64_t>((x + 1) * R, P.ngroups);
-  const int64_t nnz = P.ptr[sb.rows];
   const int F = sb.F;
-  int fo[kWideCols];
-  bool act[kWideCols];
-  float4 bv[kWideCols], acc[kWideCols];
+  const int lane = threadIdx.x & 63;
+  const int64_t wv = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int64_t g = wv / slices;
+  if (g >= P.ngroups) return;
+  const int s = int(wv % slices);
+  const int64_t nnz = P.ptr[sb.rows];
+  const int64_t p0 = wide_chunk_start(P, g, nnz), p1 = wide_chunk_start(P, g + 1, nnz);
+  const int n = __builtin_amdgcn_readfirstlane(int(p1 - p0));   // <= 2 * NPGW, wave-uniform
+  int64_t pm = lane < 2 * NPGW ? p0 + lane : (lane == 2 * NPGW ? p0 - 1 : p1);
+  pm = min<int64_t>(max<int64_t>(pm, 0), nnz - 1);
+  const int32_t r_l = P.row[pm], c_l = P.col[pm];
+  const float w_l = P.w[pm];
+  const int32_t prev_row = p0 > 0 ? __builtin_amdgcn_readlane(r_l, 2 * NPGW) : -1;
+  const int32_t next_row = p1 < nnz ? __builtin_amdgcn_readlane(r_l, 2 * NPGW + 1) : -1;
+  const uint32_t voff = uint32_t(s * 256 + lane * 4) * 4u;
+  const uint32_t rowbytes = uint32_t(F) * 4u;
+  typedef u32x4 raw4;
+  raw4 A[kSliceGroup], Bq[kSliceGroup];
+  float4 acc = f4zero();
+  const auto load8 = [&](raw4* dst, int k0) {   // entries k0..k0+7; past n: no traffic
 #pragma unroll
-  for (int j = 0; j < kWideCols; ++j) {
-    fo[j] = (threadIdx.x + kWideThreads * j) * 4;
-    act[j] = fo[j] < F;
-    bv[j] = (P.bias && act[j]) ? ld4(P.bias + fo[j]) : f4zero();
-    if (!act[j]) fo[j] = 0;    // clamped: inactive columns load column 0, never store
-  }
-  const auto store = [&](float* dst, bool fin) {
-#pragma unroll
-    for (int j = 0; j < kWideCols; ++j)
-      if (act[j]) {
-        if (fin) st4_nt(dst + fo[j], epilogue(acc[j], bv[j], sb.epi));   // final rows: streamed out
-        else st4(dst + fo[j], acc[j]);                                   // partials: read by the fixup
-      }
+    for (int u = 0; u < kSliceGroup; ++u) {
+      const int k = k0 + u;
+      const int32_t c = __builtin_amdgcn_readlane(c_l, k < 2 * NPGW ? k : 0);
+      const __amdgpu_buffer_rsrc_t rs = row_rsrc(P.in + int64_t(c) * P.ld_in, k < n ? rowbytes : 0u);
+      dst[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0);
+    }
   };
-  for (int64_t g = x * R + blockIdx.x / kXcds; g < gend; g += per) {
-    const int64_t p0 = wide_chunk_start(P, g, nnz), p1 = wide_chunk_start(P, g + 1, nnz);
-    const int n = int(p1 - p0);    // <= 2 * NPGW
-    __syncthreads();               // the previous chunk's entries are consumed
-    if (threadIdx.x < 2 * NPGW) {
-      const int64_t p = min<int64_t>(p0 + threadIdx.x, nnz - 1);   // clamped, unconditional
-      const int32_t r = P.row[p], c = P.col[p];
-      const float w = P.w[p];
-      const bool v = threadIdx.x < n;
-      s_r[threadIdx.x] = v ? r : -1;
-      s_c[threadIdx.x] = v ? c : 0;
-      s_w[threadIdx.x] = v ? w : 0.f;
-    }
-    const int32_t prev_row = p0 > 0 ? P.row[p0 - 1] : -1;
-    const int32_t next_row = p1 < nnz ? P.row[p1] : -1;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kWideCols; ++j) acc[j] = f4zero();
-    int32_t cur = -1;
-    bool cur_head = false;
-    for (int k0 = 0; k0 < n; k0 += kWideDepth) {
-      float4 v[kWideDepth][kWideCols];
-#pragma unroll
-      for (int u = 0; u < kWideDepth; ++u) {   // k0 + u < 2*NPGW: padding entries read row 0
-        const float* src = P.in + int64_t(s_c[k0 + u]) * P.ld_in;
-#pragma unroll
-        for (int j = 0; j < kWideCols; ++j) v[u][j] = ld4(src + fo[j]);
+  const auto store = [&](float* row, bool fin) {
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(row, rowbytes);
+    float4 o = acc;
+    if (fin) {
+      if (P.bias) {
+        const raw4 b = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(P.bias, rowbytes), voff, 0, 0);
+        o = f4add(o, make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z),
+                                 __uint_as_float(b.w)));
       }
+      if (sb.epi & BGCN_EPI_RELU) o = f4relu(o);
+    }
+    const raw4 v = {__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(o.w)};
+    if (fin) __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, kAuxNT);
+    else __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, 0);
+  };
+  int32_t cur = -1;
+  bool cur_head = false;
+  const auto consume8 = [&](const raw4* src, int k0) {
 #pragma unroll
-      for (int u = 0; u < kWideDepth; ++u) {
-        const int k = k0 + u;
-        const int32_t r = s_r[k];          // -1 past n: padding, skipped
-        if (r >= 0) {
-          if (r != cur) {
-            if (cur >= 0) {
-              if (!cur_head) store(P.out + int64_t(cur) * P.ld_out, true);
-              else store(P.part + (g * 2 + 0) * int64_t(F), false);
-            }
-            cur_head = cur < 0 && r == prev_row;
-            cur = r;
-#pragma unroll
-            for (int j = 0; j < kWideCols; ++j) acc[j] = f4zero();
-          }
-          const float w = s_w[k];
-#pragma unroll
-          for (int j = 0; j < kWideCols; ++j) acc[j] = f4fma(w, v[u][j], acc[j]);
+    for (int u = 0; u < kSliceGroup; ++u) {
+      const int k = k0 + u;
+      if (k >= n) break;                       // uniform
+      const int32_t r = __builtin_amdgcn_readlane(r_l, k);
+      const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w_l), k));
+      if (r != cur) {
+        if (cur >= 0) {
+          if (!cur_head) store(P.out + int64_t(cur) * P.ld_out, true);
+          else store(P.part + (g * 2 + 0) * int64_t(F), false);
         }
+        cur_head = cur < 0 && r == prev_row;
+        cur = r;
+        acc = f4zero();
       }
+      const float4 x = make_float4(__uint_as_float(src[u].x), __uint_as_float(src[u].y),
+                                   __uint_as_float(src[u].z), __uint_as_float(src[u].w));
+      acc = f4fma(w, x, acc);
     }
-    if (cur >= 0) {
-      const bool ends = next_row != cur;
-      if (!cur_head && ends) store(P.out + int64_t(cur) * P.ld_out, true);
-      else if (cur_head) store(P.part + (g * 2 + 0) * int64_t(F), false);
-      else store(P.part + (g * 2 + 1) * int64_t(F), false);
-    }
+  };
+  static_assert(2 * NPGW <= 4 * kSliceGroup, "four groups cover a chunk");
+  load8(A, 0);
+  load8(Bq, 8);
+  consume8(A, 0);
+  if (n > 16) {                                // uniform; typical chunks stop here
+    load8(A, 16);
+    consume8(Bq, 8);
+    load8(Bq, 24);
+    consume8(A, 16);
+    consume8(Bq, 24);
+  } else {
+    consume8(Bq, 8);
+  }
+  if (cur >= 0) {
+    const bool ends = next_row != cur;
+    if (!cur_head && ends) store(P.out + int64_t(cur) * P.ld_out, true);
+    else if (cur_head) store(P.part + (g * 2 + 0) * int64_t(F), false);
+    else store(P.part + (g * 2 + 1) * int64_t(F), false);
   }
 }
 
@@ -349,6 +359,7 @@ size_t spmm_ws_size(int64_t capacity, int32_t F) {
 
 static bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+
 // count problems (1 or 2) described by sb.p[0..count), each with its own part buffer
 int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   const int F = sb.F;
@@ -382,11 +393,12 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
       hipLaunchKernelGGL(k_spmm_fixup_narrow<L>, dim3(grid_for(gmax - 1, 256 / L), gy), dim3(256), 0,
                          stream, sb);
   } else {
-    BGCN_CHECK_ARG(F <= kWideThreads * 4 * kWideCols, "F > 6144 is not supported by the wide aggregation");
-    const unsigned slices = unsigned((F + kWideSlice - 1) / kWideSlice);
-    const unsigned gx = unsigned((std::min<int64_t>(kWideBlocks, gmax) + kXcds - 1) / kXcds * kXcds);
-    hipLaunchKernelGGL(k_spmm_wide, dim3(gx, gy), dim3(kWideThreads), 0, stream, sb);
+    const int ws = (F + 255) / 256;                 // 256-float slices per chunk
+    const int64_t nblk = (gmax * ws + 3) / 4;
+    BGCN_CHECK_ARG(nblk < (int64_t(1) << 31), "aggregation too large for one launch");
+    hipLaunchKernelGGL(k_spmm_slice, dim3(unsigned(nblk), gy), dim3(kWaveBlock), 0, stream, sb, ws);
     BGCN_CHECK_LAUNCH();
+    const unsigned slices = unsigned((F + kWideSlice - 1) / kWideSlice);
     if (gmax > 1)
       hipLaunchKernelGGL(k_spmm_fixup_wide, dim3(unsigned(gmax - 1), slices, gy), dim3(256), 0, stream, sb);
   }

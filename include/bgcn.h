@@ -109,7 +109,7 @@ int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_num_edges,
  * (merge path) and rows that cross a split are combined in a fixed order.
  * `capacity` = allocated entries (E + N); entries [ptr[rows], capacity) must carry
  * row = -1 (bgcn_build_graph writes them), so the kernels never wait on the count.
- * F: a multiple of 4, at most 6144 (64 and 128 take the narrow kernels).
+ * F: a positive multiple of 4 (64 and 128 take the narrow kernels).
  * -------------------------------------------------------------------------- */
 size_t bgcn_spmm_workspace_size(int64_t capacity, int32_t F);
 int bgcn_spmm(const int32_t* ptr, const int32_t* row, const int32_t* col, const float* w,

@@ -167,7 +167,7 @@ def test_spmm_forward_and_transpose(F, star):
     close(outt, A.t() @ x, what="A^T x")
 
 
-@pytest.mark.parametrize("F", [12, 300, 6144])
+@pytest.mark.parametrize("F", [12, 300, 5000, 6144])
 def test_spmm_wide_row_lengths_around_chunk_size(F):
     """Wide kernel chunking: rows of 14..18 and 31..34 entries (around the 16-entry
     chunk, where boundaries are moved to row starts or rows are split) at every offset."""
@@ -189,13 +189,49 @@ def test_spmm_wide_row_lengths_around_chunk_size(F):
     close(spmm(g, x.float().to(DEV), transposed=True), A.t() @ x, what="A^T x")
 
 
-def test_spmm_rejects_too_wide():
+def test_spmm_wide_many_chunks_per_block():
+    """Wide kernel with > 512 chunks per block (chunk boundaries computed in several
+    windows, next-chunk entries prefetched across window edges): 1.2M nodes of random
+    trees and stars, F = 12, against an index_add restatement in fp64."""
+    from bigcn_amd.ops import build_graph, spmm
+    rng = np.random.default_rng(11)
+    sizes = rng.integers(2, 400, size=6000)
+    sizes[::50] = 3000                      # star roots split over many chunks
+    n = int(sizes.sum())
+    par = []
+    off = 0
+    for s in sizes:                         # vectorised rand_forest: parent 0 or uniform earlier
+        k = np.arange(1, s)
+        p = np.where(rng.random(s - 1) < 0.5, 0, (rng.random(s - 1) * np.maximum(k - 1, 1)).astype(np.int64) + 1)
+        p = np.where(k == 1, 0, np.minimum(p, k - 1))
+        if s == 3000:
+            p[:] = 0
+        par.append(np.stack([off + p, off + k]))
+        off += s
+    ei = torch.from_numpy(np.concatenate(par, 1))
+    g = build_graph(ei.to(DEV), n)
+    e, w = O.gcn_norm(ei, None, n, "col", dtype=torch.float64)
+    x = torch.randn(n, 12, dtype=torch.float64)
+    for transposed in (False, True):
+        src, dst = (e[1], e[0]) if transposed else (e[0], e[1])
+        ref = torch.zeros(n, 12, dtype=torch.float64).index_add_(0, dst, w[:, None] * x[src])
+        close(spmm(g, x.float().to(DEV), transposed=transposed), ref, what=f"A x (T={transposed})")
+
+
+def test_spmm_any_width_and_rejects_bad_width():
+    """The wide aggregation has no width limit (256-float slices); F must stay a
+    multiple of 4 (float4 rows), else the C ABI refuses the call."""
     from bigcn_amd._lib import BGCNError
     from bigcn_amd.ops import build_graph, spmm
-    ei = torch.tensor([[0], [1]])
-    g = build_graph(ei.to(DEV), 2)
+    ei = torch.tensor([[0, 0, 1], [1, 2, 3]])
+    g = build_graph(ei.to(DEV), 4)
+    e, w = O.gcn_norm(ei, None, 4, "col", dtype=torch.float64)
+    A = torch.zeros(4, 4, dtype=torch.float64)
+    A.index_put_((e[1], e[0]), w, accumulate=True)
+    x = torch.randn(4, 9000, dtype=torch.float64)
+    close(spmm(g, x.float().to(DEV)), A @ x, what="A x at F=9000")
     with pytest.raises(BGCNError):
-        spmm(g, torch.zeros(2, 6148, device=DEV))
+        spmm(g, torch.zeros(4, 6146, device=DEV))
 
 
 def test_spmm_deterministic():

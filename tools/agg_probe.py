@@ -47,7 +47,13 @@ def main():
     print(f"colsum    {ms * 1e3:8.1f} us  {nb / ms / 1e6:7.0f} GB/s (read)")
     ms = timed(lambda: y.fill_(1.0), args.iters)
     print(f"fill      {ms * 1e3:8.1f} us  {nb / ms / 1e6:7.0f} GB/s (write)")
-    for name, ei in (("td", b.edge_index), ("bu", b.BU_edge_index)):
+    # structure probes on the same X: self loops only (a copy through the kernel) and
+    # chains (every parent re-read by the very next row: ideal reuse distance)
+    ptr = b.ptr.tolist()
+    ch_r = torch.cat([torch.arange(ptr[i], ptr[i + 1] - 1) for i in range(len(ptr) - 1)])
+    probes = [("self", torch.zeros(2, 0, dtype=torch.int64, device=dev)),
+              ("chain", torch.stack([ch_r, ch_r + 1]).to(dev))]
+    for name, ei in probes + [("td", b.edge_index), ("bu", b.BU_edge_index)]:
         g = ops.build_graph(ei, N)
         ms = timed(lambda: ops.spmm(g, x, out=y), args.iters)
         alg = 2.0 * nb
