@@ -27,6 +27,8 @@ BGCN_EPI_NONE = 0
 BGCN_EPI_RELU = 1
 BGCN_FEAT_AUTO = 0
 BGCN_FEAT_DENSE = 1
+BGCN_FEAT_SPARSE = 2
+BGCN_SPARSE_CAP = 32
 BGCN_SPARSE_CAP = 32
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1

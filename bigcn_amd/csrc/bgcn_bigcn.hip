@@ -595,6 +595,10 @@ int check_args(const bgcn_bigcn_args* a) {
   BGCN_CHECK_ARG(a->x_dtype == BGCN_DTYPE_F32 || a->x_dtype == BGCN_DTYPE_BF16, "bad x_dtype");
   BGCN_CHECK_ARG((reinterpret_cast<uintptr_t>(a->x) & 15) == 0, "x must be 16-byte aligned");
   BGCN_CHECK_ARG(a->td.t_ptr && a->bu.t_ptr && a->td.s_ptr && a->bu.s_ptr, "null graph");
+  BGCN_CHECK_ARG(a->feat_mode == BGCN_FEAT_AUTO || a->feat_mode == BGCN_FEAT_DENSE ||
+                     a->feat_mode == BGCN_FEAT_SPARSE, "bad feat_mode");
+  BGCN_CHECK_ARG(a->feat_mode != BGCN_FEAT_SPARSE || a->in_feats <= kSparseMaxF,
+                 "BGCN_FEAT_SPARSE needs in_feats <= 5120");
   return BGCN_OK;
 }
 
@@ -669,8 +673,14 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
     sp.csc_slot = prep->csc_slot; sp.csc_val = prep->csc_val;
   }
   // dense kernels run when feat_mode == dense (no gate) or when the sparse path overflowed
+  // (auto); under BGCN_FEAT_SPARSE they are not launched (dense_launched)
   gate = sp.mode == 1 ? nullptr : a->x_flags;
   return BGCN_OK;
+}
+
+// whether the (gated) dense kernels are launched at all
+static bool dense_launched(const bgcn_bigcn_args* a, const SparseState& sp) {
+  return sp.mode == 1 || a->feat_mode != BGCN_FEAT_SPARSE;
 }
 
 // Forward.  Main stream: node maps, conv1 (sparse compaction + gather, or dense MFMA),
@@ -706,8 +716,9 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
       BGCN_TRY(sparse_conv1_gather(sp, w.z1, s));
       timing_end(0, s);
     }
-    BGCN_TRY(gemm_xwt_x(a->x, a->x_dtype, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H,
-                        F, s, gate));
+    if (dense_launched(a, sp))
+      BGCN_TRY(gemm_xwt_x(a->x, a->x_dtype, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H,
+                          F, s, gate));
     if (graph_lane >= 0) BGCN_TRY(aux_join(s, graph_lane));   // K1 of a just-prepared batch
     return forward_tail(a, w, sp, keep, gate, s, head, false);
   }
@@ -730,10 +741,12 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
     BGCN_TRY(sparse_compact_conv1(sp, a->x, a->x_dtype, a->ldx, w.z1, s));
     timing_end(0, s);
   }
-  timing_begin(sparse ? 4 : 0, s);
-  BGCN_TRY(gemm_xwt_x(a->x, a->x_dtype, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F,
-                      s, gate));
-  timing_end(sparse ? 4 : 0, s);
+  if (dense_launched(a, sp)) {
+    timing_begin(sparse ? 4 : 0, s);
+    BGCN_TRY(gemm_xwt_x(a->x, a->x_dtype, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F,
+                        s, gate));
+    timing_end(sparse ? 4 : 0, s);
+  }
   // the graphs (built on graph_lane by bgcn_train_step) and the items are needed from
   // here on; the join comes before the CSC fork so that it never waits for the CSC
   if (side_busy) BGCN_TRY(aux_join(s, kLaneSide));
@@ -757,15 +770,17 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
   // conv2 lin with the root-extended, relu'd, dropped-out A operand generated in-kernel
   timing_begin(2, s);
   if (sparse) BGCN_TRY(sparse_conv2(sp, a->h1, a->tree_ptr, a->rootindex, w.z2, keep, s));
-  if (a->x_dtype == BGCN_DTYPE_BF16)
-    hipLaunchKernelGGL(k_conv2_fwd<bf16_t>, dim3(grid_for(N, 64), 2), dim3(256), 0, s,
-                       static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
-                       a->bu_w2, w.z2, N, keep, gate);
-  else
-    hipLaunchKernelGGL(k_conv2_fwd<float>, dim3(grid_for(N, 64), 2), dim3(256), 0, s,
-                       static_cast<const float*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
-                       a->bu_w2, w.z2, N, keep, gate);
-  BGCN_CHECK_LAUNCH();
+  if (dense_launched(a, sp)) {
+    if (a->x_dtype == BGCN_DTYPE_BF16)
+      hipLaunchKernelGGL(k_conv2_fwd<bf16_t>, dim3(grid_for(N, 64), 2), dim3(256), 0, s,
+                         static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
+                         a->bu_w2, w.z2, N, keep, gate);
+    else
+      hipLaunchKernelGGL(k_conv2_fwd<float>, dim3(grid_for(N, 64), 2), dim3(256), 0, s,
+                         static_cast<const float*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
+                         a->bu_w2, w.z2, N, keep, gate);
+    BGCN_CHECK_LAUNCH();
+  }
   timing_end(2, s);
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z2, a->h2, a->td_b2, a->bu_b2, BGCN_EPI_NONE, w, s));
   const HeadArgs no_head{};
@@ -817,7 +832,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     const int gxd = int(grid_for(H + F, 64));
     const Dw2Cfg dense{w.kchunk2, w.S2, gxd, 1, H + F, w.dw2_part};
     const Dw2Cfg sparsec{w.kchunkh, w.Sh, 1, 0, int64_t(H), w.dw2_part};
-    const int n0 = gxd * w.S2 * 2, n1 = sparse ? w.Sh * 2 : 0;
+    const int n0 = dense_launched(a, sp) ? gxd * w.S2 * 2 : 0, n1 = sparse ? w.Sh * 2 : 0;
     if (a->x_dtype == BGCN_DTYPE_BF16)
       hipLaunchKernelGGL(k_dw2<bf16_t>, dim3(unsigned(n0 + n1)), dim3(256), 0, x,
                          static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.dz2, w.node_root, N,
@@ -830,7 +845,8 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   }
   timing_end(3, x);
   {   // the matching split reductions, also one launch
-    const RedCfg dense{w.S2, H + F, 1, int(std::min<unsigned>(grid_for(2 * H * (H + F), 64), 1024))};
+    const RedCfg dense{w.S2, H + F, 1,
+                       dense_launched(a, sp) ? int(std::min<unsigned>(grid_for(2 * H * (H + F), 64), 1024)) : 0};
     const RedCfg sparsec{w.Sh, int64_t(H), 0, int(grid_for(2 * H * H, 64))};
     hipLaunchKernelGGL(k_reduce_dw2, dim3(unsigned(dense.blocks + (sparse ? sparsec.blocks : 0))),
                        dim3(256), 0, x, w.dw2_part, H + F, a->td_dw2, a->bu_dw2, gate, dense, sparsec);
@@ -861,8 +877,9 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     BGCN_TRY(sparse_dw1(sp, a, w.dz1, s));
     timing_end(5, s);
   }
-  BGCN_TRY(gemm_tn_x(w.dz1, 2 * H, a->x, a->x_dtype, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F,
-                     N, w.tn_ws, w.tn_bytes, sparse ? x : s, sparse ? 6 : 1, gate));
+  if (dense_launched(a, sp))
+    BGCN_TRY(gemm_tn_x(w.dz1, 2 * H, a->x, a->x_dtype, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F,
+                       N, w.tn_ws, w.tn_bytes, sparse ? x : s, sparse ? 6 : 1, gate));
   timing_end(9, s);   // the main stream's own chain (span class, bgcn_train_step)
   BGCN_TRY(aux_join(s, kLaneSide));
   return BGCN_OK;

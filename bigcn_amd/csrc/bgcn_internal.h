@@ -70,6 +70,7 @@ struct HeadArgs {
   float* dhead;          // [B, 256]
   int32_t* status;       // bit 1: label out of range
   const int32_t* in_status;  // OR-ed into *status once (prepared batch's K1 flags), or nullptr
+  const int32_t* in_xflags;  // BGCN_FEAT_SPARSE: the compaction's overflow flag (-> bit 2)
 };
 
 // One wave, row b of the head: h = head_in[b][4l .. 4l+3] held by lane l.
@@ -119,6 +120,7 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
   }
   if (l == 0 && !yok) hd.loss_row[b] = 0.f;
   if (l == 0 && b == 0 && hd.in_status && hd.status && *hd.in_status) atomicOr(hd.status, *hd.in_status);
+  if (l == 0 && b == 0 && hd.in_xflags && hd.status && *hd.in_xflags) atomicOr(hd.status, 4);
   st4(hd.dhead + b * kHeadIn + 4 * l, dh);
 }
 

@@ -284,7 +284,7 @@ static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w
   // forward with the head fused into the readout (fc, log_softmax, NLL row terms, dz,
   // dhead per tree); the prepared batch's K1 status is folded into *status
   const HeadArgs hd{a->params[8], a->params[9], a->y, int(C), a->logp, w.dz, w.loss_row, w.dhead,
-                    a->status, p.status};
+                    a->status, p.status, a->feat_mode == BGCN_FEAT_SPARSE ? p.x_flags : nullptr};
   BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, graph_lane, &hd, &p));
   // fc weight/bias gradients and the loss mean are off the critical path: side lane
   hipStream_t x;

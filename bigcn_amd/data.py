@@ -138,6 +138,7 @@ class Sample:
     rootindex: torch.Tensor
     cls: Optional[torch.Tensor] = None
     tweetids: Optional[torch.Tensor] = None
+    x_nnz_max: Optional[int] = None     # most non-zeros in one row of x (feature-path hint)
 
 
 def _drop(row: np.ndarray, col: np.ndarray, rate: float, rnd: random.Random):
@@ -161,8 +162,10 @@ def make_sample(d: dict, tddroprate: float = 0.0, budroprate: float = 0.0,
     tweetids = None
     if "tweetids" in d:
         tweetids = torch.tensor([int(v) for v in d["tweetids"]], dtype=torch.int64)
+    x = torch.tensor(d["x"], dtype=torch.float32)
     return Sample(
-        x=torch.tensor(d["x"], dtype=torch.float32),
+        x=x,
+        x_nnz_max=int((x != 0).sum(1).max()) if x.numel() else 0,
         edge_index=torch.as_tensor(np.stack([row, col]), dtype=torch.int64),
         BU_edge_index=torch.as_tensor(np.stack([burow, bucol]), dtype=torch.int64),
         y=torch.tensor([int(d["y"])], dtype=torch.int64),
@@ -206,11 +209,23 @@ class Batch:
         return int(self.x.size(0))
 
     def to(self, device, non_blocking: bool = False):
+        hinted = self.__dict__.get("_x_nnz_of") is self.__dict__.get("x")
         for k, v in list(self.__dict__.items()):
-            if isinstance(v, torch.Tensor):
+            if isinstance(v, torch.Tensor) and not k.startswith("_"):
                 self.__dict__[k] = v.to(device, non_blocking=non_blocking)
         self.__dict__.pop("_bgcn_graphs", None)
+        if hinted:
+            self._x_nnz_of = self.x
         return self
+
+    # Host-side feature-path hint: the most non-zeros in one row of x.  It is bound to the
+    # x tensor it was computed for and ignored once x is replaced.
+    def set_x_nnz_max(self, n: int) -> None:
+        self.x_nnz_max = int(n)
+        self._x_nnz_of = self.x
+
+    def x_nnz_hint(self):
+        return self.__dict__.get("x_nnz_max") if self.__dict__.get("_x_nnz_of") is self.x else None
 
     def keys(self):
         return [k for k in self.__dict__ if not k.startswith("_")]
@@ -238,7 +253,12 @@ def collate(samples: Sequence[Sample]) -> Batch:
         kw["cls"] = torch.cat([s.cls for s in samples], 0)
     if all(s.tweetids is not None for s in samples):
         kw["tweetids"] = torch.cat([s.tweetids for s in samples], 0)
-    return Batch(**kw)
+    out = Batch(**kw)
+    if all(s.x_nnz_max is not None for s in samples):
+        # host-side hint: FusedTrainStep skips the dense fallback when every row fits the
+        # sparse feature path (BGCN_FEAT_SPARSE)
+        out.set_x_nnz_max(max(s.x_nnz_max for s in samples))
+    return out
 
 
 # ----------------------------------------------------------------------------- bulk synthetic batches
@@ -284,4 +304,6 @@ def synth_batch(rng: np.random.Generator, sizes: Sequence[int], vocab: int = VOC
     # on the BiGCN path; it is omitted here.
     out = Batch(x=x, edge_index=ei, BU_edge_index=bei, y=y, rootindex=rootindex, batch=batch,
                 ptr=torch.as_tensor(offs, dtype=torch.int64), num_graphs=B)
-    return out.to(device)
+    out = out.to(device)
+    out.set_x_nnz_max(int(nnz.max()) if N else 0)   # upper bound (duplicate ids collapse)
+    return out

@@ -29,6 +29,19 @@ from .ops import _FEAT_MODES, check_encoder_shapes, features, x_dtype_code
 from .optim import FusedAdam, bigcn_adam
 
 
+def _step_feat_mode(feat_mode: str, data) -> int:
+    """C-ABI feature path of a step: "auto" becomes BGCN_FEAT_SPARSE (no dense fallback
+    launched) when the batch carries a host-side ``x_nnz_max`` within the sparse cap
+    (collate / synth_batch set it); "sparse" forces it (overflow -> check_status raises)."""
+    if feat_mode == "sparse":
+        return _lib.BGCN_FEAT_SPARSE
+    if feat_mode == "auto":
+        hint = data.x_nnz_hint() if hasattr(data, "x_nnz_hint") else None
+        if hint is not None and int(hint) <= _lib.BGCN_SPARSE_CAP and int(data.x.size(1)) <= 5120:
+            return _lib.BGCN_FEAT_SPARSE
+    return _FEAT_MODES[feat_mode]
+
+
 def _need(t: torch.Tensor, dtype, name: str) -> torch.Tensor:
     if t.dtype != dtype:
         t = t.to(dtype)
@@ -127,9 +140,9 @@ class FusedTrainStep:
         y = _need(data.y, torch.int64, "y")
         if seed is None:
             seed = _draw_seed() if m.training else 0
-        mode = _FEAT_MODES[m.feat_mode]
+        mode = _step_feat_mode(m.feat_mode, data)
         pend = self._pending
-        if pend is not None and pend[0] is data and pend[2] == (mode, m.training):
+        if pend is not None and pend[0] is data and pend[2] == (mode == _lib.BGCN_FEAT_DENSE, m.training):
             # prepared by the previous call (its descriptor, drop seed and inputs)
             prep, keep, d = pend[1], pend[3], pend[4]
             ready = 1
@@ -153,7 +166,7 @@ class FusedTrainStep:
             self._next_desc = nd                     # the struct must outlive the call
             a.next = ctypes.pointer(self._next_desc)
             a.next_prepared, a.next_prepared_bytes = ptr(nbuf), nbuf.numel()
-            nxt = (next_data, nbuf, (mode, m.training), nkeep, nd)
+            nxt = (next_data, nbuf, (mode == _lib.BGCN_FEAT_DENSE, m.training), nkeep, nd)
         else:
             a.next = None
             a.next_prepared, a.next_prepared_bytes = 0, 0
@@ -179,9 +192,14 @@ class FusedTrainStep:
         return loss
 
     def check_status(self) -> None:
-        """Host sync: raise on a bad edge index / label seen by the last step."""
+        """Host sync: raise on a bad edge index / label / (feat_mode "sparse") an
+        over-full feature row seen by the last step."""
         s = int(self.status.item())
         if s & 1:
             raise IndexError("edge_index contains an index out of range [0, num_nodes)")
         if s & 2:
             raise IndexError("label out of range [0, num_classes)")
+        if s & 4:
+            raise ValueError(f"feat_mode 'sparse': a feature row holds more than "
+                             f"{_lib.BGCN_SPARSE_CAP} non-zeros (the step's results are invalid); "
+                             f"use 'auto' or 'dense'")

@@ -213,9 +213,14 @@ typedef struct bgcn_graph_view {
  * at most BGCN_SPARSE_CAP (col, val) pairs; products with X / X[root] then skip the zero
  * entries (exact: bag-of-words rows hold ~10-20 non-zeros of 5000).  If any row holds
  * more, the batch falls back to the dense MFMA kernels on the device (no host sync).
- * DENSE: always the dense MFMA kernels. */
+ * DENSE: always the dense MFMA kernels.
+ * SPARSE: the AUTO path without the dense fallback - the caller guarantees rows of at
+ * most BGCN_SPARSE_CAP non-zeros (e.g. known from the sparse source features); the
+ * gated dense kernels are then not launched at all (shorter step).  A row with more
+ * non-zeros makes the results invalid and sets bit 2 of the step's *status. */
 #define BGCN_FEAT_AUTO 0
 #define BGCN_FEAT_DENSE 1
+#define BGCN_FEAT_SPARSE 2
 /* element type of the node features x (x_dtype): fp32, or bfloat16 (the bf16
  * configuration; bag-of-words counts are exact in bf16, every product accumulates in
  * fp32, so results equal the fp32 path's on the same values) */
@@ -299,7 +304,7 @@ typedef struct bgcn_batch {
 
 size_t bgcn_prepare_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,
                                    int64_t td_num_edges, int64_t bu_num_edges);
-/* feat_mode: BGCN_FEAT_AUTO builds the ELL/CSC of X, BGCN_FEAT_DENSE skips them.
+/* feat_mode: BGCN_FEAT_AUTO / _SPARSE build the ELL/CSC of X, BGCN_FEAT_DENSE skips them.
  * A bad edge index sets bit 0 of the buffer's status word (reported by the step). */
 int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree_on,
                        int32_t feat_mode, void* prepared, size_t prepared_bytes,
@@ -313,7 +318,8 @@ int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree
  * data-parallel bucket; the all-reduce and bgcn_adam_step follow.  Parameter order:
  * td_w1 td_b1 td_w2 td_b2 bu_w1 bu_b1 bu_w2 bu_b2 fc_w [C, 256] fc_b [C] (the
  * reference state_dict layout).  *status (optional, zeroed by the call): bit 0 = an
- * edge index outside [0, N) (skipped), bit 1 = a label outside [0, C) (ignored).
+ * edge index outside [0, N) (skipped), bit 1 = a label outside [0, C) (ignored),
+ * bit 2 = a feature row with more than BGCN_SPARSE_CAP non-zeros under BGCN_FEAT_SPARSE.
  *   prepared / prepared_ready: the current batch's prepared buffer; when not ready the
  *   call prepares it first (on the same stream).
  *   next / next_prepared (optional): a batch to prepare during this step on the
@@ -328,7 +334,7 @@ typedef struct bgcn_step_args {
   int32_t degree_on;             /* BGCN_DEGREE_ON_COL / _ROW                */
   int32_t training;              /* dropout on/off                           */
   uint64_t seed;                 /* dropout draw                             */
-  int32_t feat_mode;             /* BGCN_FEAT_AUTO / _DENSE                  */
+  int32_t feat_mode;             /* BGCN_FEAT_AUTO / _DENSE / _SPARSE        */
   const float* params[BGCN_STEP_PARAMS];
   float* grads[BGCN_STEP_PARAMS];
   float* loss;                   /* [1] mean NLL                             */

@@ -18,6 +18,13 @@ KEYS = ["TDrumorGCN.conv1.lin.weight", "TDrumorGCN.conv1.bias", "TDrumorGCN.conv
         "BUrumorGCN.conv2.lin.weight", "BUrumorGCN.conv2.bias", "fc.weight", "fc.bias"]
 
 
+def _unhinted(b):
+    """Drop the batch's host-side nnz hint: "auto" then runs the device-gated fallback
+    path instead of BGCN_FEAT_SPARSE."""
+    b._x_nnz_of = None
+    return b
+
+
 def _model(p, mode="auto", classes=4):
     from bigcn_amd import BiGCN, Net
     m = (BiGCN if classes == 4 else Net)(p["TDrumorGCN.conv1.lin.weight"].shape[1], 64, 64).to(DEV)
@@ -26,12 +33,17 @@ def _model(p, mode="auto", classes=4):
     return m
 
 
-@pytest.mark.parametrize("mode", ["auto", "dense"])
+@pytest.mark.parametrize("mode", ["auto", "auto-hinted", "sparse", "dense"])
 @pytest.mark.parametrize("training", [False, True])
 def test_train_step_matches_oracle(training, mode):
+    """auto: sparse path + device-gated dense fallback; auto-hinted: the batch's host nnz
+    hint selects BGCN_FEAT_SPARSE (no fallback launched); sparse: forced; dense."""
     from bigcn_amd import FusedTrainStep
     from bigcn_amd.ops import keep_words, unpack_keep
     b = _synth(31, 16, 150, root_random=True)
+    if mode == "auto":
+        _unhinted(b)
+    mode = "auto" if mode == "auto-hinted" else mode
     p = O.make_params(5000, 64, 64, 4, seed=12)
     m = _model(p, mode)
     m.train(training)
@@ -136,7 +148,7 @@ def test_train_step_reports_bad_inputs():
         step.check_status()
 
 
-@pytest.mark.parametrize("mode", ["auto", "dense"])
+@pytest.mark.parametrize("mode", ["auto", "sparse", "dense"])
 def test_next_batch_prefetch_matches_plain_steps(mode):
     """Preparing the next batch inside a step (side lane) gives bitwise the same losses and
     gradients as preparing every batch inside its own step; a prefetched buffer is only
@@ -287,3 +299,40 @@ def test_bf16_features_module_path():
     b.x = b.x.to(torch.bfloat16)
     out16 = m(b)
     assert torch.equal(out32, out16)
+
+
+def test_sparse_hint_matches_gated_fallback_path():
+    """BGCN_FEAT_SPARSE (chosen by the hint) and AUTO (gate on the device) launch
+    different kernel sets but compute the same step, bit for bit."""
+    from bigcn_amd import FusedTrainStep
+    b = _synth(45, 32, 200)
+    p = O.make_params(5000, 64, 64, 4, seed=19)
+    res = []
+    for hinted in (True, False):
+        if not hinted:
+            _unhinted(b)
+        step = FusedTrainStep(_model(p))
+        loss = step.forward_backward(b, seed=5)
+        res.append((loss.clone(), [v.clone() for v in step.grads().values()]))
+        step.check_status()
+    assert torch.equal(res[0][0], res[1][0])
+    for a, c in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, c)
+
+
+def test_sparse_mode_flags_overfull_rows():
+    """feat_mode "sparse" with a row of more than 32 non-zeros: status bit 2, check_status
+    raises; a replaced x invalidates the batch's hint (auto then falls back correctly)."""
+    from bigcn_amd import FusedTrainStep
+    b = _synth(46, 8, 60, F=768)
+    g = torch.Generator().manual_seed(46)
+    b.x = torch.randn(b.x.shape, generator=g).to(DEV)   # dense rows: every row overflows
+    assert b.x_nnz_hint() is None                       # hint bound to the old x
+    p = O.make_params(768, 64, 64, 4, seed=21)
+    step = FusedTrainStep(_model(p, "sparse"))
+    step.forward_backward(b, seed=1)
+    with pytest.raises(ValueError):
+        step.check_status()
+    step = FusedTrainStep(_model(p, "auto"))
+    step.forward_backward(b, seed=1)
+    step.check_status()

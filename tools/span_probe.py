@@ -46,6 +46,37 @@ def main():
         for c, name in classes.items():
             ms, n = ops.kernel_timing(c)
             print(f"{name:24s} {ms / max(n, 1) * 1e3:8.1f} us  ({n} spans)")
+        # host side: time spent inside the enqueueing call vs wall time per step (no
+        # timing hook): a call time close to the step time means the step is host-bound
+        import time
+        torch.cuda.synchronize()
+        host = 0.0
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            h0 = time.perf_counter()
+            fused(pool[i % 4], next_data=pool[(i + 1) % 4])
+            host += time.perf_counter() - h0
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        print(f"{'host call (enqueue)':24s} {host / args.steps * 1e6:8.1f} us")
+        print(f"{'wall per step':24s} {wall / args.steps * 1e6:8.1f} us")
+        # the chain alone: batch 0 prepared once, every step reuses its prepared buffer
+        # (no preparation on the side lane, so no HBM contention from the pass over X)
+        fused(pool[3], next_data=pool[0])
+        pend = fused._pending
+        torch.cuda.synchronize()
+        ops.set_kernel_timing(True, {9: "main", 10: "whole"})
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            fused._pending = pend
+            fused(pool[0])
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ops.set_kernel_timing(False)
+        for c, name in ((9, "chain alone: main span"), (10, "chain alone: whole call")):
+            ms, n = ops.kernel_timing(c)
+            print(f"{name:24s} {ms / max(n, 1) * 1e3:8.1f} us  ({n} spans)")
+        print(f"{'chain alone: wall/step':24s} {wall / args.steps * 1e6:8.1f} us")
 
 
 if __name__ == "__main__":
