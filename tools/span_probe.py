@@ -19,12 +19,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--dropedge", default="host", choices=["device", "host"])
+    ap.add_argument("--workload", default="twitter15")
     args = ap.parse_args()
     import bench
     from bigcn_amd import BiGCN, FusedTrainStep, ops
     from bigcn_amd.optim import bigcn_adam
     dev = torch.device("cuda", 0)
-    wl = bench.WORKLOADS["twitter15"]
+    wl = bench.WORKLOADS[args.workload]
     dd = args.dropedge == "device"
     pool = bench.make_pool(wl, 0, 4, dev, (0.0, 0.0) if dd else None)
     model = BiGCN(wl["feats"], 64, 64, dev).to(dev)
@@ -77,6 +78,34 @@ def main():
             ms, n = ops.kernel_timing(c)
             print(f"{name:24s} {ms / max(n, 1) * 1e3:8.1f} us  ({n} spans)")
         print(f"{'chain alone: wall/step':24s} {wall / args.steps * 1e6:8.1f} us")
+        # interference probes: the chain beside (a) a spin kernel (queue only, no memory),
+        # (b) one big device copy of X (HBM only, one kernel) on another stream
+        side = torch.cuda.Stream(dev)
+        xs = pool[1].x
+        ys = torch.empty_like(xs)
+        small_x, small_y = xs[:1600].clone(), torch.empty_like(xs[:1600])    # 32 MB
+        colsum = torch.empty(xs.size(1), device=dev)
+
+        def small_copies():
+            for _ in range(18):
+                small_y.copy_(small_x)
+
+        for name, job in (("spin", lambda: torch.cuda._sleep(600000)), ("copy X", lambda: ys.copy_(xs)),
+                          ("read X", lambda: torch.sum(xs, 0, out=colsum)), ("fill Y", lambda: ys.fill_(1.0)),
+                          ("32MB copy x18", small_copies)):
+            torch.cuda.synchronize()
+            ops.set_kernel_timing(True, {9: "main"})
+            for i in range(args.steps):
+                side.wait_stream(stream)
+                with torch.cuda.stream(side):
+                    job()
+                fused._pending = pend
+                fused(pool[0])
+                stream.wait_stream(side)
+            torch.cuda.synchronize()
+            ops.set_kernel_timing(False)
+            ms, n = ops.kernel_timing(9)
+            print(f"{'chain beside ' + name:24s} {ms / max(n, 1) * 1e3:8.1f} us  ({n} spans)")
 
 
 if __name__ == "__main__":
