@@ -29,6 +29,8 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--graphs", default="self,chain,td,bu", help="comma list of self,chain,td,bu")
+    ap.add_argument("--no-streams", action="store_true", help="skip the copy / colsum / fill lines")
     args = ap.parse_args()
     import bench
     from bigcn_amd import ops
@@ -39,21 +41,25 @@ def main():
     N, F = x.shape
     nb = N * F * 4
     y = torch.empty_like(x)
-    ms = timed(lambda: y.copy_(x), args.iters)
     print(f"N={N} F={F} X={nb / 1e6:.0f} MB")
-    print(f"copy      {ms * 1e3:8.1f} us  {2 * nb / ms / 1e6:7.0f} GB/s (read+write)")
-    s = torch.empty(F, device=dev)
-    ms = timed(lambda: torch.sum(x, 0, out=s), args.iters)
-    print(f"colsum    {ms * 1e3:8.1f} us  {nb / ms / 1e6:7.0f} GB/s (read)")
-    ms = timed(lambda: y.fill_(1.0), args.iters)
-    print(f"fill      {ms * 1e3:8.1f} us  {nb / ms / 1e6:7.0f} GB/s (write)")
+    if not args.no_streams:
+        ms = timed(lambda: y.copy_(x), args.iters)
+        print(f"copy      {ms * 1e3:8.1f} us  {2 * nb / ms / 1e6:7.0f} GB/s (read+write)")
+        s = torch.empty(F, device=dev)
+        ms = timed(lambda: torch.sum(x, 0, out=s), args.iters)
+        print(f"colsum    {ms * 1e3:8.1f} us  {nb / ms / 1e6:7.0f} GB/s (read)")
+        ms = timed(lambda: y.fill_(1.0), args.iters)
+        print(f"fill      {ms * 1e3:8.1f} us  {nb / ms / 1e6:7.0f} GB/s (write)")
     # structure probes on the same X: self loops only (a copy through the kernel) and
     # chains (every parent re-read by the very next row: ideal reuse distance)
     ptr = b.ptr.tolist()
     ch_r = torch.cat([torch.arange(ptr[i], ptr[i + 1] - 1) for i in range(len(ptr) - 1)])
     probes = [("self", torch.zeros(2, 0, dtype=torch.int64, device=dev)),
               ("chain", torch.stack([ch_r, ch_r + 1]).to(dev))]
+    want = set(args.graphs.split(","))
     for name, ei in probes + [("td", b.edge_index), ("bu", b.BU_edge_index)]:
+        if name not in want:
+            continue
         g = ops.build_graph(ei, N)
         ms = timed(lambda: ops.spmm(g, x, out=y), args.iters)
         alg = 2.0 * nb

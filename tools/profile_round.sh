@@ -19,4 +19,13 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write"
 python tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" --out "$OUT/pmc_traffic.json" > "$OUT/pmc_traffic.txt"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/agg" -o run -- \
   python tools/agg_probe.py > "$OUT/agg_probe.txt" 2> "$OUT/agg.log"
+# HBM traffic of the 5000-wide aggregation (k_spmm_slice + fixup), TD and BU graphs apart
+for g in td bu; do
+  timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/agg_fetch_$g" -- \
+    python tools/agg_probe.py --graphs $g --no-streams --iters 5 > /dev/null 2>> "$OUT/agg.log"
+  timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/agg_write_$g" -- \
+    python tools/agg_probe.py --graphs $g --no-streams --iters 5 > /dev/null 2>> "$OUT/agg.log"
+  python tools/pmc_traffic.py "$OUT/agg_fetch_$g" "$OUT/agg_write_$g" --out "$OUT/agg_pmc_$g.json" \
+    > "$OUT/agg_pmc_$g.txt"
+done
 echo done
