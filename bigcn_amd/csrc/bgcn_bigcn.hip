@@ -531,6 +531,7 @@ struct FusedWs {
   float* tn_ws; size_t tn_bytes;
   int S2; int64_t kchunk2;
   int Sh; int64_t kchunkh;
+  SpmmPlan plan[2][2];                    // [td, bu][forward, backward] (prepared batch) or null
 };
 
 int dw2_splits(int64_t N, int64_t F) {
@@ -640,7 +641,7 @@ static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool 
                        transposed ? v.s_col : v.t_col, transposed ? v.s_w : v.t_w,
                        in + d * H, 2 * H, out + d * H, 2 * H, d == 0 ? bias_td : bias_bu,
                        reinterpret_cast<float*>(reinterpret_cast<char*>(w.spmm_ws) + d * half),
-                       spmm_groups(v.capacity, H), v.capacity};
+                       spmm_groups(v.capacity, H), v.capacity, w.plan[d][transposed ? 1 : 0]};
   }
   return spmm_batch_impl(sb, 2, s);
 }
@@ -665,6 +666,8 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
   w.spmm_bytes = ws_bytes - align_up(c.off, 256) - 256;
   w.spmm_ws = c.take<float>(1);
+  for (int d = 0; d < 2; ++d)
+    for (int o = 0; o < 2; ++o) w.plan[d][o] = prep ? prep->plan[d][o] : SpmmPlan{nullptr, nullptr, nullptr};
   if (prep) {   // the batch's weight-independent state lives in the prepared buffer
     w.node_root = prep->node_root;
     sp.item_tree = prep->item_tree; sp.item_chunk = prep->item_chunk; sp.tree_item0 = prep->tree_item0;

@@ -198,6 +198,19 @@ template <> struct XRaw<bf16_t> {
 __device__ __forceinline__ float xs(const float* p) { return *p; }
 __device__ __forceinline__ float xs(const bf16_t* p) { return bf2f(*p); }
 
+// Aggregation plan of one CSR orientation (built by K1 for the fused step, weight-
+// independent): chunk g of the nominal kPlanChunk-entry grid covers the entries
+// [bnd[g].x, bnd[g].y) - complete rows of <= kPlanChunk entries only (the boundary moves
+// back to the row start; an empty or negative range means no work); the rows of more
+// entries ("long rows", BU star roots) are listed in longs[0 .. *nlong) and aggregated by
+// one block each.  No row is split, so no fixup pass follows.
+constexpr int kPlanChunk = 16;
+struct SpmmPlan {
+  const int2* bnd;
+  const int32_t* longs;
+  const int32_t* nlong;
+};
+
 __device__ __forceinline__ bool gate_closed(const int32_t* gate) { return gate && *gate == 0; }
 __device__ __forceinline__ bool dense_active(const int32_t* gate) { return !gate_closed(gate); }
 

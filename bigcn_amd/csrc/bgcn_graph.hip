@@ -45,6 +45,9 @@ struct GraphIO {
   int32_t *tmp_t, *tmp_s;                                // general path: eid per slot
   int32_t* bsum;                                         // [nb][4]: sum_t, sum_s, distinct_t, distinct_s
   float* dinv;
+  int32_t* nlong;                                        // [2] long rows t / s (zeroed block)
+  int2 *bnd_t, *bnd_s;                                   // aggregation plans (SpmmPlan)
+  int32_t *long_t, *long_s;
 };
 
 struct GraphBatch {
@@ -264,6 +267,9 @@ __global__ void k_nodes(GraphBatch gb) {
   const int le = G.loop_eid[i];
   const float lw = (le > 0 && G.ew) ? G.ew[le - 1] : 1.f;
   const int64_t pt = G.t_ptr[i + 1] - 1, ps = G.s_ptr[i + 1] - 1;
+  // rows of more than kPlanChunk entries: aggregated by a block each (SpmmPlan)
+  if (pt + 1 - G.t_ptr[i] > kPlanChunk) G.long_t[atomicAdd(&G.nlong[0], 1)] = int32_t(i);
+  if (ps + 1 - G.s_ptr[i] > kPlanChunk) G.long_s[atomicAdd(&G.nlong[1], 1)] = int32_t(i);
   G.t_row[pt] = int32_t(i); G.t_col[pt] = int32_t(i); G.t_w[pt] = lw;
   G.s_row[ps] = int32_t(i); G.s_col[ps] = int32_t(i); G.s_w[ps] = lw;
   // scatter_add over the final edge list in order (real edges, then the loop)
@@ -282,9 +288,29 @@ __global__ void k_nodes(GraphBatch gb) {
   G.dinv[i] = d;
 }
 
+// chunk bounds of a plan: lo = the entry where chunk g starts (a long row at the boundary
+// is skipped), hi = where it ends (a long row is excluded)
+__device__ __forceinline__ int2 plan_bounds(const int32_t* ptr, const int32_t* row, int64_t nnz, int64_t g) {
+  const int64_t p0 = g * kPlanChunk, p1 = p0 + kPlanChunk;
+  int lo = int(nnz), hi = int(nnz);
+  if (p0 < nnz) {
+    const int32_t r = row[p0];
+    const int32_t rs = ptr[r], re = ptr[r + 1];
+    lo = re - rs > kPlanChunk ? re : rs;
+  }
+  if (p1 < nnz) hi = ptr[row[p1]];
+  return make_int2(lo, hi);
+}
+
 __global__ void k_normalize(GraphBatch gb) {
   GraphIO& G = gb.g[blockIdx.y];
   const int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  // the plans' chunk bounds, chunk g = thread p (the first ngroups threads; rows are
+  // final here, k_nodes wrote the self loops)
+  if (G.bnd_t && p < (G.E + gb.N + kPlanChunk - 1) / kPlanChunk) {
+    G.bnd_t[p] = plan_bounds(G.t_ptr, G.t_row, G.t_ptr[gb.N], p);
+    G.bnd_s[p] = plan_bounds(G.s_ptr, G.s_row, G.s_ptr[gb.N], p);
+  }
   if (p >= int64_t(G.t_ptr[gb.N])) {
     // the unused tail of the capacity (dropped self loops, invalid edges): row -1 marks
     // it for the aggregation kernels, which then need not read the entry count first
@@ -314,12 +340,18 @@ size_t carve(Carve& c, int64_t E, int64_t N, GraphIO* G) {
   t.cur_s = c.take<int32_t>(n);
   t.loop_eid = c.take<int32_t>(n);
   t.flags = c.take<int32_t>(8);
+  t.nlong = c.take<int32_t>(2);
   t.run_t = c.take<int32_t>(n);
   t.run_s = c.take<int32_t>(n);
   t.tmp_t = c.take<int32_t>(cap);
   t.tmp_s = c.take<int32_t>(cap);
   t.bsum = c.take<int32_t>(size_t(nb) * 4);
   t.dinv = c.take<float>(n);
+  const size_t ng = (cap + kPlanChunk - 1) / kPlanChunk;
+  t.bnd_t = c.take<int2>(ng);
+  t.bnd_s = c.take<int2>(ng);
+  t.long_t = c.take<int32_t>(n);
+  t.long_s = c.take<int32_t>(n);
   if (G) *G = t;
   return c.off;
 }
@@ -390,6 +422,20 @@ int build_graphs_impl(const GraphArgs* ga, int count, int64_t N, int degree_on, 
   hipLaunchKernelGGL(k_normalize, dim3(grid_for(Emax + N, blk), gy), dim3(blk), 0, s, gb);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
+}
+
+void graph_pair_plans(void* ws, size_t ws_bytes, int64_t Etd, int64_t Ebu, int64_t N, SpmmPlan td[2],
+                      SpmmPlan bu[2]) {
+  const size_t half = ws_bytes / 2 / 256 * 256;
+  char* base = static_cast<char*>(ws);
+  for (int k = 0; k < 2; ++k) {
+    Carve c(base + k * half, half);
+    GraphIO G{};
+    carve(c, k == 0 ? Etd : Ebu, N, &G);
+    SpmmPlan* o = k == 0 ? td : bu;
+    o[0] = SpmmPlan{G.bnd_t, G.long_t, G.nlong};
+    o[1] = SpmmPlan{G.bnd_s, G.long_s, G.nlong + 1};
+  }
 }
 
 }  // namespace bgcn

@@ -19,6 +19,7 @@ struct SpmmProb {
   float* part;  // [ngroups][2][F] partial rows of chunk-crossing rows
   int64_t ngroups;
   int64_t capacity;  // allocated entries; [ptr[rows], capacity) hold row = -1 (K1 writes them)
+  SpmmPlan plan;     // F = 64 only; plan.bnd == nullptr -> merge-path chunks + fixup
 };
 
 struct SpmmBatch {
@@ -29,6 +30,9 @@ struct SpmmBatch {
 };
 
 int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream);
+// the plans K1 left in a graph-pair workspace (bgcn_build_graph_pair layout)
+void graph_pair_plans(void* ws, size_t ws_bytes, int64_t Etd, int64_t Ebu, int64_t N, SpmmPlan td[2],
+                      SpmmPlan bu[2]);
 int64_t spmm_groups(int64_t capacity, int32_t F);
 size_t spmm_ws_size(int64_t capacity, int32_t F);
 int spmm_impl(const int32_t* ptr, const int32_t* row, const int32_t* col, const float* w,
@@ -142,6 +146,7 @@ constexpr int kCscRowBlock = 256;
 constexpr int64_t kSparseMaxFeat = 5120;   // widest X of the sparse path (one pass per row)
 struct Prepared {
   bgcn_csr_out td, bu;
+  SpmmPlan plan[2][2];                   // [td, bu][t (forward), s (backward)]
   int64_t td_cap, bu_cap;                // E + N
   int32_t *tree_ptr, *node_root, *status;
   int32_t *item_tree, *item_chunk, *tree_item0;

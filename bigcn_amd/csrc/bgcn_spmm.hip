@@ -26,6 +26,7 @@ namespace bgcn {
 namespace {
 
 constexpr int NPG = 16;  // CSR entries per lane group
+static_assert(NPG == kPlanChunk, "K1's plans use the narrow kernel's chunk grid");
 
 __device__ __forceinline__ float4 epilogue(float4 acc, float4 bias, int epi) {
   float4 o = f4add(acc, bias);
@@ -106,6 +107,100 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
     if (!cur_head && ends) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
     else if (cur_head) st4(P.part + (g * 2 + 0) * (LANES * 4) + fo, acc);  // head (may also extend past p1)
     else st4(P.part + (g * 2 + 1) * (LANES * 4) + fo, acc);               // tail
+  }
+}
+
+// Planned narrow aggregation (F = 64, the fused step): with K1's SpmmPlan no row is split,
+// so no fixup launch follows.  Blocks [0, nchunk) hold 64 groups of 16 lanes; group g
+// aggregates chunk g's complete short rows [bnd.x, bnd.y) (<= 31 entries, two per lane,
+// broadcast by shuffles, 8 gathers in flight).  Blocks [nchunk, nchunk + nlongblk) take
+// the long rows longs[j], j = block, block + nlongblk, ...: the 64 groups sum entries
+// q, q + 64, ... of the row (8 in flight) and combine their partials in LDS in group
+// order (deterministic; a row's sum does not depend on which block takes it).
+constexpr int kRowsThreads = 1024;
+constexpr int kRowsGroups = kRowsThreads / 16;
+
+__global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
+  constexpr int LANES = 16;
+  const SpmmProb& P = sb.p[blockIdx.y];
+  const int lane = threadIdx.x % LANES, grp = threadIdx.x / LANES;
+  const int fo = lane * 4;
+  const int base_lane = ((threadIdx.x & 63) / LANES) * LANES;
+  __shared__ float4 red[kRowsGroups][LANES];
+  if (int64_t(blockIdx.x) < nchunk) {
+    const int64_t g = int64_t(blockIdx.x) * kRowsGroups + grp;
+    if (g >= P.ngroups) return;
+    const int2 bd = P.plan.bnd[g];
+    const int n = bd.y - bd.x;                       // <= 2 * LANES - 1; <= 0: no rows
+    if (n <= 0) return;
+    const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
+    // entries bd.x + lane and bd.x + 16 + lane (clamped, unconditional; masked by n)
+    const int64_t e0 = min<int64_t>(bd.x + lane, P.capacity - 1);
+    const int64_t e1 = min<int64_t>(bd.x + LANES + lane, P.capacity - 1);
+    const int32_t r0 = P.row[e0], c0 = P.col[e0], r1 = P.row[e1], c1 = P.col[e1];
+    const float w0 = P.w[e0], w1 = P.w[e1];
+    float4 acc = f4zero();
+    int32_t cur = -1;
+    for (int k0 = 0; k0 < n; k0 += 8) {
+      float4 v[8];
+      int32_t rr[8];
+      float ww[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u;                        // < 32
+        const int src = base_lane + (k & (LANES - 1));
+        const bool hi = k >= LANES;                  // uniform
+        const int32_t rk = __shfl(hi ? r1 : r0, src, 64);
+        const int32_t ck = __shfl(hi ? c1 : c0, src, 64);
+        ww[u] = __shfl(hi ? w1 : w0, src, 64);
+        rr[u] = k < n ? rk : -1;
+        v[u] = ld4(P.in + int64_t(ck) * P.ld_in + fo);   // unconditional (ck is a real row)
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int32_t r = rr[u];
+        if (r < 0) break;
+        if (r != cur) {
+          if (cur >= 0) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+          cur = r;
+          acc = f4zero();
+        }
+        acc = f4fma(ww[u], v[u], acc);
+      }
+    }
+    if (cur >= 0) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+    return;
+  }
+  // long rows: one block per row
+  const int nl = *P.plan.nlong;
+  for (int j = int(blockIdx.x - nchunk); j < nl; j += nlongblk) {
+    const int32_t r = P.plan.longs[j];
+    const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
+    float4 acc = f4zero();
+    int64_t e = rs + grp;
+    for (; e + 7 * kRowsGroups < re; e += 8 * kRowsGroups) {
+      float4 v[8];
+      float ww[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t eu = e + u * kRowsGroups;
+        ww[u] = P.w[eu];
+        v[u] = ld4(P.in + int64_t(P.col[eu]) * P.ld_in + fo);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = f4fma(ww[u], v[u], acc);
+    }
+    for (; e < re; e += kRowsGroups) acc = f4fma(P.w[e], ld4(P.in + int64_t(P.col[e]) * P.ld_in + fo), acc);
+    red[grp][lane] = acc;
+    __syncthreads();
+    if (grp == 0) {
+      float4 t = red[0][lane];
+#pragma unroll 8
+      for (int q = 1; q < kRowsGroups; ++q) t = f4add(t, red[q][lane]);
+      const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
+      st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(t, bv, sb.epi));
+    }
+    __syncthreads();
   }
 }
 
@@ -378,7 +473,18 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   }
   if (gmax == 0) return BGCN_OK;
   const unsigned gy = unsigned(count);
-  if (F == 64) {
+  bool planned = F == 64;
+  int64_t capmax = 0;
+  for (int k = 0; k < count; ++k) {
+    planned = planned && sb.p[k].plan.bnd && sb.p[k].plan.longs && sb.p[k].plan.nlong;
+    capmax = sb.p[k].capacity > capmax ? sb.p[k].capacity : capmax;
+  }
+  if (planned) {   // K1's plans: complete rows per chunk, long rows per block, no fixup
+    const int64_t nchunk = (gmax + kRowsGroups - 1) / kRowsGroups;
+    const int nlongblk = int(std::min<int64_t>(256, std::max<int64_t>(1, capmax / (kPlanChunk + 1))));
+    hipLaunchKernelGGL(k_spmm_rows, dim3(unsigned(nchunk + nlongblk), gy), dim3(kRowsThreads), 0, stream,
+                       sb, nchunk, nlongblk);
+  } else if (F == 64) {
     constexpr int L = 16;
     hipLaunchKernelGGL(k_spmm_narrow<L>, dim3(grid_for(gmax, 256 / L), gy), dim3(256), 0, stream, sb);
     BGCN_CHECK_LAUNCH();

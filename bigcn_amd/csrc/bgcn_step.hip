@@ -137,6 +137,8 @@ size_t carve_prepared(Carve& c, int64_t N, int64_t B, int64_t F, int64_t Etd, in
   carve_csr(c, t.bu_cap, N, &t.bu);
   t.gws_bytes = bgcn_graph_pair_workspace_size(Etd, Ebu, N);
   t.gws = c.take<char>(t.gws_bytes);
+  // K1 leaves each orientation's aggregation plan in its graph workspace
+  if (p && c.base) graph_pair_plans(t.gws, t.gws_bytes, Etd, Ebu, N, t.plan[0], t.plan[1]);
   t.tree_ptr = c.take<int32_t>(size_t(B + 1));
   t.node_root = c.take<int32_t>(size_t(N));
   t.status = c.take<int32_t>(1);
