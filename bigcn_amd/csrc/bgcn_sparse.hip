@@ -104,7 +104,10 @@ __global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __
 // all zero across the wave (the common case for bag-of-words rows) costs one ballot -
 // and Z1[i] = sum val * W1T[col] with each lane owning 2 of the 128 outputs.
 constexpr int kRowChunks = 20;  // float4 per lane per pass (F <= 5120 in one pass)
-constexpr unsigned kPrepBlocks = 256;   // grid of the side-lane compaction (1 per CU)
+// side-lane compaction grid: one block per 4 rows (8 bf16 rows), i.e. short-lived waves
+// handed out in address order - measured 111 vs 128 us beside the training chain for a
+// persistent 256-block grid, same step time (BGCN_PREP_BLOCKS caps it for A/B runs)
+constexpr unsigned kPrepBlocks = 0xffffffffu;
 
 // Z1[i] += sum_s val_s * W1T[col_s] for the (col, val) pairs of lane-held lists: lane s
 // (< cnt) holds pair s; the pairs reach the wave by scalar readlane, gathers unconditional
@@ -194,8 +197,8 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* 
   __shared__ float s_val[4][kCap];
   if (S.mode == 1) return;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // grid-stride over rows: the preparation launches a small grid so that it streams X
-  // beside the training chain without taking every CU slot
+  // grid-stride over rows (the preparation's grid covers every row once: one fp32 row or
+  // two bf16 rows per wave; a capped grid strides)
   const int64_t stride = int64_t(gridDim.x) * 4;
   for (int64_t i0 = int64_t(blockIdx.x) * 4 + wave; i0 < S.N; i0 += stride * kRows) {
     typename XRaw<TX>::raw r[kRows][kRowChunks];
@@ -861,7 +864,7 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
     return e ? unsigned(std::max(1, atoi(e))) : kPrepBlocks;
   }();
   timing_begin(7, s);
-  const dim3 grid(std::min<unsigned>(grid_for(N, 4), prep_blocks));
+  const dim3 grid(std::min<unsigned>(grid_for(N, xdt == BGCN_DTYPE_BF16 ? 8 : 4), prep_blocks));
   if (xdt == BGCN_DTYPE_BF16)
     hipLaunchKernelGGL((k_compact_conv1<false, bf16_t>), grid, dim3(256), 0, s, S,
                        static_cast<const bf16_t*>(X), ldx, nullptr);

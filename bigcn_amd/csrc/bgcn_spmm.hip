@@ -118,6 +118,7 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
 // q, q + 64, ... of the row (8 in flight) and combine their partials in LDS in group
 // order (deterministic; a row's sum does not depend on which block takes it).
 constexpr int kRowsThreads = 1024;
+constexpr int64_t kPlanMaxEntries = int64_t(1) << 17;   // capacity (E + N) up to which plans are used
 constexpr int kRowsGroups = kRowsThreads / 16;
 
 __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
@@ -479,6 +480,13 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
     planned = planned && sb.p[k].plan.bnd && sb.p[k].plan.longs && sb.p[k].plan.nlong;
     capmax = sb.p[k].capacity > capmax ? sb.p[k].capacity : capmax;
   }
+  // The plan pays off while long rows are few and short (one block each): measured on the
+  // fused step beside the next batch's preparation, Twitter15-sized batches (E + N = 55k)
+  // 0.356 vs 0.362 ms per step, Weibo-sized ones (188k) 0.85 vs 0.77 ms - there a few
+  // blocks summing thousands of entries each become the tail under memory contention.
+  // BGCN_SPMM_PLAN=0/1 forces either form (A/B runs).
+  static const int plan_env = [] { const char* e = std::getenv("BGCN_SPMM_PLAN"); return e ? atoi(e) : -1; }();
+  planned = planned && (plan_env == 1 || (plan_env != 0 && capmax <= kPlanMaxEntries));
   if (planned) {   // K1's plans: complete rows per chunk, long rows per block, no fixup
     const int64_t nchunk = (gmax + kRowsGroups - 1) / kRowsGroups;
     const int nlongblk = int(std::min<int64_t>(256, std::max<int64_t>(1, capmax / (kPlanChunk + 1))));
