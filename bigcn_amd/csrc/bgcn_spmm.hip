@@ -485,7 +485,8 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   // 0.356 vs 0.362 ms per step, Weibo-sized ones (188k) 0.85 vs 0.77 ms - there a few
   // blocks summing thousands of entries each become the tail under memory contention.
   // BGCN_SPMM_PLAN=0/1 forces either form (A/B runs).
-  static const int plan_env = [] { const char* e = std::getenv("BGCN_SPMM_PLAN"); return e ? atoi(e) : -1; }();
+  const char* pe = std::getenv("BGCN_SPMM_PLAN");   // read per call: tests switch it
+  const int plan_env = pe ? atoi(pe) : -1;
   planned = planned && (plan_env == 1 || (plan_env != 0 && capmax <= kPlanMaxEntries));
   if (planned) {   // K1's plans: complete rows per chunk, long rows per block, no fixup
     const int64_t nchunk = (gmax + kRowsGroups - 1) / kRowsGroups;

@@ -336,3 +336,31 @@ def test_sparse_mode_flags_overfull_rows():
     step = FusedTrainStep(_model(p, "auto"))
     step.forward_backward(b, seed=1)
     step.check_status()
+
+
+@pytest.mark.parametrize("plan", ["0", "1"])
+def test_planned_and_merge_path_aggregation_match_oracle(plan, monkeypatch):
+    """Both aggregation forms of the fused step - K1's plans (complete rows per chunk,
+    long rows per block, no fixup) and merge-path chunks + fixup (chosen above 2^17
+    entries) - against the oracle, on trees with star roots of hundreds of children."""
+    from bigcn_amd import FusedTrainStep
+    from bigcn_amd.data import synth_batch
+    from bigcn_amd.ops import keep_words, unpack_keep
+    monkeypatch.setenv("BGCN_SPMM_PLAN", plan)
+    rng = np.random.default_rng(47)
+    b = synth_batch(rng, [700, 3, 40, 17, 18, 2, 300], 512, 4, 0.2, 0.2, device=DEV)
+    p = O.make_params(512, 64, 64, 4, seed=23)
+    m = _model(p)
+    m.train()
+    step = FusedTrainStep(m)
+    seed = 31
+    logp = torch.empty(b.num_graphs, 4, device=DEV)
+    loss = step.forward_backward(b, seed=seed, logp=logp)
+    mk = unpack_keep(keep_words(seed, b.x.size(0), 512, DEV).cpu(), 64 + 512)
+    rlogp, rloss, rgrads, _ = _oracle(b, p, True, mk[0], mk[1])
+    close(logp, rlogp, what="logp")
+    close(loss, rloss, what="loss")
+    g = step.grads()
+    for k, prm in zip(KEYS, step.step_params):
+        close(g[prm], rgrads[k], what=k)
+    step.check_status()
