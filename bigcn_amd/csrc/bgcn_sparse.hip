@@ -218,17 +218,53 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* 
   }
 }
 
-// conv1 lin from a prepared ELL of X (bgcn_prepare_batch): wave per row.
+// conv1 lin from a prepared ELL of X (bgcn_prepare_batch): four rows per wave, one per
+// 16-lane quarter, lane l of a quarter owning outputs [8l, 8l + 8) of the 128 (both
+// directions).  The kernel is latency-bound (ELL load -> W1^T row gathers from L2 ->
+// store per row), so a wave keeps four rows' gathers in flight instead of one
+// (measured at Weibo size: 62 us for one row per wave, beside nothing).  Entry s of a
+// row reaches its quarter by shuffle (entries s and s + 16 per lane); past a row's count
+// the value is 0 and the (clamped) column still loads, so every load is unconditional.
+constexpr int kC1Rows = 4;
 __global__ __launch_bounds__(256) void k_conv1_gather(SparseState S, float* __restrict__ Z1) {
   if (!use_sparse(S)) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t i = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (i >= S.N) return;
-  const int cnt = min(S.nnz[i], kCap);
-  const int32_t col_l = S.cols[i * kCap + (lane & (kCap - 1))];
-  const float val_l = S.vals[i * kCap + (lane & (kCap - 1))];
-  const float2 acc = conv1_row(S, cnt, col_l, val_l);
-  *reinterpret_cast<float2*>(Z1 + i * (2 * H) + 2 * lane) = acc;
+  const int lane = threadIdx.x & 63, ql = lane & 15, qb = lane & 48;
+  const int64_t i = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * kC1Rows + (lane >> 4);
+  const bool live = i < S.N;
+  const int64_t ic = live ? i : S.N - 1;
+  const int cnt = live ? min(S.nnz[ic], kCap) : 0;
+  const int32_t c0 = S.cols[ic * kCap + ql], c1 = S.cols[ic * kCap + 16 + ql];
+  const float v0 = S.vals[ic * kCap + ql], v1 = S.vals[ic * kCap + 16 + ql];
+  // the wave's longest row bounds the loop (uniform)
+  int cmax = cnt;
+  cmax = max(cmax, __shfl_xor(cmax, 16, 64));
+  cmax = max(cmax, __shfl_xor(cmax, 32, 64));
+  float4 a0 = f4zero(), a1 = f4zero();
+  for (int s0 = 0; s0 < cmax; s0 += 8) {
+    float4 w0[8], w1[8];
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int sl = s0 + u;                          // uniform
+      const int src = qb + (sl & 15);
+      const int32_t c = __shfl(sl < 16 ? c0 : c1, src, 64);
+      const float v = __shfl(sl < 16 ? v0 : v1, src, 64);
+      x[u] = sl < cnt ? v : 0.f;
+      const int32_t cc = min(max(c, 0), int32_t(S.F - 1));
+      const float* wr = S.w1t + int64_t(cc) * (2 * H) + 8 * ql;
+      w0[u] = ld4(wr);
+      w1[u] = ld4(wr + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a0 = f4fma(x[u], w0[u], a0);
+      a1 = f4fma(x[u], w1[u], a1);
+    }
+  }
+  if (live) {
+    st4(Z1 + i * (2 * H) + 8 * ql, a0);
+    st4(Z1 + i * (2 * H) + 8 * ql + 4, a1);
+  }
 }
 
 // ---------------------------------------------------------------- conv2 forward
@@ -640,24 +676,30 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
   }
 }
 
-// dW1 = [dZ1_td | dZ1_bu]^T X over the CSC of X: a wave per column (16 per block), each
-// lane owning 2 of the 128 outputs.  The column's (row, value) pairs come 64 at a time
-// (slot and value loaded side by side: k_csc_place stores the value next to the slot),
-// then the dZ1 row gathers are issued kDw1Depth at a time with clamped indices; (row,
-// value) reach the wave by scalar readlane (the index is wave-uniform), not LDS permutes.
+// dW1 = [dZ1_td | dZ1_bu]^T X over the CSC of X: four waves per column (four columns per
+// block), each lane owning 2 of the 128 outputs; wave k of a column takes the column's
+// 64-entry batches k, k + 4, ... (slot and value loaded side by side: k_csc_place stores
+// the value next to the slot), then issues the dZ1 row gathers kDw1Depth at a time with
+// clamped indices; (row, value) reach the wave by scalar readlane.  The four partials are
+// combined in LDS in wave order (deterministic).  One wave per column leaves the chip with
+// F = 5000 waves, each walking its whole column serially: fine at Twitter size (~70
+// entries per column; the split measured 14 us slower there), slow at Weibo size (~225).
 constexpr int kDw1Depth = 16;
+template <int kDw1Split>                       // waves per column (1 or 4)
 __global__ __launch_bounds__(1024) void k_dw1_cols(SparseState S, const float* __restrict__ dZ1,
                                                    float* __restrict__ dw1_td,
                                                    float* __restrict__ dw1_bu) {
+  constexpr int kDw1Cols = 16 / kDw1Split;   // columns per 1024-thread block
   if (!use_sparse(S)) return;
   __shared__ float t1[2 * H][17];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int part = wave % kDw1Split;
   const int64_t F = S.F;
-  const int64_t c = int64_t(blockIdx.x) * 16 + wave;
+  const int64_t c = int64_t(blockIdx.x) * kDw1Cols + wave / kDw1Split;
   float2 a1 = make_float2(0.f, 0.f);
   if (c < F) {
     const int64_t beg = S.col_start[c], end = S.col_end[c];
-    for (int64_t u0 = beg; u0 < end; u0 += 64) {
+    for (int64_t u0 = beg + 64 * part; u0 < end; u0 += 64 * kDw1Split) {
       const int64_t u = min<int64_t>(u0 + lane, end - 1);   // clamped: duplicates, x masked
       const uint32_t slot = S.csc_slot[u];
       const float xv = S.csc_val[u];
@@ -685,14 +727,17 @@ __global__ __launch_bounds__(1024) void k_dw1_cols(SparseState S, const float* _
   t1[2 * lane][wave] = a1.x;
   t1[2 * lane + 1][wave] = a1.y;
   __syncthreads();
-  // coalesced stores: 16 consecutive columns per output row
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 x 64
-  const int64_t cc = int64_t(blockIdx.x) * 16 + tx;
-  if (cc < F)
-    for (int o = ty; o < 2 * H; o += 64) {
-      float* dst = o < H ? dw1_td + int64_t(o) * F : dw1_bu + int64_t(o - H) * F;
-      dst[cc] = t1[o][tx];
-    }
+  // combine the column's partials in wave order, then store (kDw1Cols consecutive columns
+  // per output row)
+  const int tx = threadIdx.x % kDw1Cols;
+  const int64_t cc = int64_t(blockIdx.x) * kDw1Cols + tx;
+  for (int ty = threadIdx.x / kDw1Cols; ty < 2 * H && cc < F; ty += 1024 / kDw1Cols) {
+    float acc = t1[ty][tx * kDw1Split];
+#pragma unroll
+    for (int k = 1; k < kDw1Split; ++k) acc += t1[ty][tx * kDw1Split + k];
+    float* dst = ty < H ? dw1_td + int64_t(ty) * F : dw1_bu + int64_t(ty - H) * F;
+    dst[cc] = acc;
+  }
 }
 
 // dW2 root columns: dW2_d[:, 64 + c] = sum over the root rows holding column c (tree
@@ -877,13 +922,21 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
 }
 
 int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
-  hipLaunchKernelGGL(k_conv1_gather, dim3(grid_for(S.N, 4)), dim3(256), 0, s, S, Z1);
+  hipLaunchKernelGGL(k_conv1_gather, dim3(grid_for(S.N, 4 * kC1Rows)), dim3(256), 0, s, S, Z1);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
 
 int sparse_dw1(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1, hipStream_t s) {
-  hipLaunchKernelGGL(k_dw1_cols, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, dZ1,
+  // one wave per column at Twitter-sized batches, four from 64k rows (longer columns);
+  // BGCN_DW1_SPLIT=1/4 forces either (read per call: tests compare both)
+  const char* e = std::getenv("BGCN_DW1_SPLIT");
+  const int split = e ? atoi(e) : (S.N >= 65536 ? 4 : 1);
+  if (split == 4)
+    hipLaunchKernelGGL(k_dw1_cols<4>, dim3(unsigned((S.F + 3) / 4)), dim3(1024), 0, s, S, dZ1,
+                     a->td_dw1, a->bu_dw1);
+  else
+    hipLaunchKernelGGL(k_dw1_cols<1>, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, dZ1,
                      a->td_dw1, a->bu_dw1);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
