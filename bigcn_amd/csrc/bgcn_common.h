@@ -177,23 +177,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, uint
   return __builtin_amdgcn_make_buffer_rsrc(base, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 constexpr int kAuxNT = 2;   // buffer-load cache policy: non-temporal
-template <class TX> struct XRaw;
-template <> struct XRaw<float> {
-  typedef u32x4 raw;
-  __device__ static raw ld(__amdgpu_buffer_rsrc_t rs, int quad) {
-    return __builtin_amdgcn_raw_buffer_load_b128(rs, quad * 16, 0, kAuxNT);
-  }
-  __device__ static float4 cvt(raw r) {
-    return make_float4(__uint_as_float(r.x), __uint_as_float(r.y), __uint_as_float(r.z),
-                       __uint_as_float(r.w));
-  }
+// 16 B of an X row as one lane loads it: four fp32 or eight bf16 elements.  The zero
+// tests work on the raw bits (magnitude bits only: -0 is zero, NaN is not, as `!= 0.f`),
+// so a bf16 chunk costs the same instructions as an fp32 one for twice the elements.
+template <class TX> struct XChunk;
+template <> struct XChunk<float> {
+  static constexpr int kElems = 4;
+  __device__ static bool any(u32x4 r) { return ((r.x | r.y | r.z | r.w) & 0x7fffffffu) != 0; }
+  __device__ static bool nz(u32x4 r, int c) { return (r[c] & 0x7fffffffu) != 0; }
+  __device__ static float elem(u32x4 r, int c) { return __uint_as_float(r[c]); }
 };
-template <> struct XRaw<bf16_t> {
-  typedef u32x2 raw;
-  __device__ static raw ld(__amdgpu_buffer_rsrc_t rs, int quad) {
-    return __builtin_amdgcn_raw_buffer_load_b64(rs, quad * 8, 0, kAuxNT);
+template <> struct XChunk<bf16_t> {
+  static constexpr int kElems = 8;
+  __device__ static bool any(u32x4 r) { return ((r.x | r.y | r.z | r.w) & 0x7fff7fffu) != 0; }
+  __device__ static bool nz(u32x4 r, int c) {
+    return (r[c >> 1] & ((c & 1) ? 0x7fff0000u : 0x00007fffu)) != 0;
   }
-  __device__ static float4 cvt(raw r) { return bf4(r.x, r.y); }
+  __device__ static float elem(u32x4 r, int c) {   // element 2w is the low half of word w
+    return __uint_as_float((c & 1) ? (r[c >> 1] & 0xffff0000u) : (r[c >> 1] << 16));
+  }
 };
 __device__ __forceinline__ float xs(const float* p) { return *p; }
 __device__ __forceinline__ float xs(const bf16_t* p) { return bf2f(*p); }

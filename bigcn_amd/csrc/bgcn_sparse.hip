@@ -98,9 +98,9 @@ __global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __
 }
 
 // ---------------------------------------------------------------- X compaction + conv1
-// One wave per row.  The whole row is requested up front (kRowChunks float4 per lane:
+// One wave per row.  The whole row is requested up front (16-byte pieces per lane:
 // 20 KiB of a 5000-wide row in flight per wave) so HBM sees deep, independent streams;
-// then the non-zeros are compacted in ascending column order - a float4 group that is
+// then the non-zeros are compacted in ascending column order - a 16-byte piece that is
 // all zero across the wave (the common case for bag-of-words rows) costs one ballot -
 // and Z1[i] = sum val * W1T[col] with each lane owning 2 of the 128 outputs.
 constexpr int kRowChunks = 20;  // float4 per lane per pass (F <= 5120 in one pass)
@@ -134,38 +134,41 @@ __device__ __forceinline__ float2 conv1_row(const SparseState& S, int cnt, int32
   return acc;
 }
 
-// Row i of X -> its ELL list (+ conv1).  r: the row's quads (kRowChunks per lane: the
-// whole row, F <= kSparseMaxF), already in flight.
+// Row i of X -> its ELL list (+ conv1).  r: the row's 16-byte chunks (row_chunks<TX>()
+// per lane: the whole row, F <= kSparseMaxF), already in flight.
 static_assert(kRowChunks * 64 * 4 >= kSparseMaxF, "one pass per row");
+template <class TX> constexpr int row_chunks() { return kRowChunks * 4 / XChunk<TX>::kElems; }
 template <bool kConv1, class TX>
-__device__ __forceinline__ void compact_row(const SparseState& S, int64_t i,
-                                            const typename XRaw<TX>::raw* r, int32_t* s_col,
-                                            float* s_val, float* __restrict__ Z1) {
+__device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, const u32x4* r,
+                                            int32_t* s_col, float* s_val, float* __restrict__ Z1) {
+  typedef XChunk<TX> XC;
+  constexpr int E = XC::kElems;
   const int lane = threadIdx.x & 63;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   int cnt = 0;
 #pragma unroll
-  for (int u = 0; u < kRowChunks; ++u) {
-    const float4 vu = XRaw<TX>::cvt(r[u]);   // past the row: 0 (range-checked load)
-    const bool n0 = vu.x != 0.f, n1 = vu.y != 0.f, n2 = vu.z != 0.f, n3 = vu.w != 0.f;
-    if (__ballot(n0 || n1 || n2 || n3) == 0ull) continue;   // wave-uniform skip
-    const uint64_t m0 = __ballot(n0), m1 = __ballot(n1), m2 = __ballot(n2), m3 = __ballot(n3);
+  for (int u = 0; u < row_chunks<TX>(); ++u) {
+    const u32x4 ru = r[u];                           // past the row: 0 (range-checked load)
+    if (__ballot(XC::any(ru)) == 0ull) continue;     // wave-uniform skip
     // ascending column order: lanes below me contribute all their non-zeros first
-    int pos = cnt + __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
-    const int col0 = (u * 64 + lane) * 4;
-    const float e[4] = {vu.x, vu.y, vu.z, vu.w};
-    const bool nz[4] = {n0, n1, n2, n3};
+    int pos = cnt;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (nz[c]) {
+    for (int c = 0; c < E; ++c) {
+      const uint64_t m = __ballot(XC::nz(ru, c));
+      pos += __popcll(m & lt);
+      cnt += __popcll(m);
+    }
+    const int col0 = (u * 64 + lane) * E;
+#pragma unroll
+    for (int c = 0; c < E; ++c) {
+      if (XC::nz(ru, c)) {
         if (pos < kCap) {
           s_col[pos] = col0 + c;
-          s_val[pos] = e[c];
+          s_val[pos] = XC::elem(ru, c);
         }
         ++pos;
       }
     }
-    cnt += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
   }
   if (lane == 0) S.nnz[i] = cnt;
   if (cnt > kCap) {
@@ -201,14 +204,15 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* 
   // two bf16 rows per wave; a capped grid strides)
   const int64_t stride = int64_t(gridDim.x) * 4;
   for (int64_t i0 = int64_t(blockIdx.x) * 4 + wave; i0 < S.N; i0 += stride * kRows) {
-    typename XRaw<TX>::raw r[kRows][kRowChunks];
+    u32x4 r[kRows][row_chunks<TX>()];
 #pragma unroll
     for (int k = 0; k < kRows; ++k) {   // all loads in flight; a row past N reads nothing
       const int64_t ik = i0 + k * stride;
       const __amdgpu_buffer_rsrc_t rs =
           row_rsrc(X + min<int64_t>(ik, S.N - 1) * ldx, ik < S.N ? uint32_t(S.F * sizeof(TX)) : 0u);
 #pragma unroll
-      for (int u = 0; u < kRowChunks; ++u) r[k][u] = XRaw<TX>::ld(rs, u * 64 + lane);
+      for (int u = 0; u < row_chunks<TX>(); ++u)
+        r[k][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * 64 + lane) * 16, 0, kAuxNT);
     }
 #pragma unroll
     for (int k = 0; k < kRows; ++k) {

@@ -289,6 +289,44 @@ def test_weibo_bf16_features_match_fp32(mode):
         close(g, rgrads[k], what=k)
 
 
+@pytest.mark.parametrize("F", [5000, 4996, 4100])
+def test_bf16_compaction_any_width_matches_fp32(F):
+    """The compaction reads X in 16-byte pieces per lane (eight bf16 or four fp32
+    elements): widths whose bf16 row does not end on a 16-byte boundary, non-zeros in the
+    last columns and negative zeros (not counted), inside the step and in the next-batch
+    preparation, give bitwise the fp32 result."""
+    from bigcn_amd import FusedTrainStep
+    batches = []
+    for k in range(2):
+        b = _unhinted(_synth(60 + k, 12, 90, F=F))
+        x = b.x.clone()
+        x[::3, F - 1] = 3.0
+        x[1::4, F - 4] = 1.0
+        x[::5, F - 9] = -0.0
+        b.x = x
+        batches.append(b)
+    p = O.make_params(F, 64, 64, 4, seed=18)
+    outs = []
+    for dt in (torch.float32, torch.bfloat16):
+        xs = [b.x for b in batches]
+        for b in batches:
+            b.x = b.x.to(dt)
+        step = FusedTrainStep(_model(p, "auto"))
+        res = []
+        for k, b in enumerate(batches):
+            nxt = batches[k + 1] if k + 1 < len(batches) else None
+            loss = step.forward_backward(b, seed=k, next_data=nxt)
+            res.append((loss.clone(), [g.clone() for g in step.grads().values()]))
+        step.check_status()
+        outs.append(res)
+        for b, x in zip(batches, xs):
+            b.x = x
+    for (l0, g0), (l1, g1) in zip(*outs):
+        assert torch.equal(l0, l1)
+        for a, c in zip(g0, g1):
+            assert torch.equal(a, c)
+
+
 def test_bf16_features_module_path():
     """BiGCN.forward (the per-op autograd encoder) takes bf16 features as well."""
     b = _synth(36, 8, 60)
