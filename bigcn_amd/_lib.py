@@ -107,6 +107,7 @@ class StepArgs(Structure):
         ("loss", c_void_p), ("logp", c_void_p), ("status", c_void_p),
         ("prepared", c_void_p), ("prepared_bytes", c_size_t), ("prepared_ready", c_int32),
         ("next", POINTER(BatchDesc)), ("next_prepared", c_void_p), ("next_prepared_bytes", c_size_t),
+        ("status_flag", c_void_p),
     ]
 
 
@@ -183,7 +184,7 @@ def load_library(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.bgcn_abi_version() != 1:
+        if lib.bgcn_abi_version() != 2:
             raise ImportError("libbgcn.so ABI version mismatch")
         _lib = lib
         return lib

@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from .conv import GCNConv
-from .ops import Graph, bigcn_encoder, build_graph_pair, scatter_mean
+from .ops import Graph, bigcn_encoder, build_graph_pair, degree_code, scatter_mean
 
 
 def _graphs(data, degree_on: str = "col"):
@@ -46,15 +46,17 @@ class _RumorGCN(torch.nn.Module):
 
     edge_key = "edge_index"
 
-    def __init__(self, in_feats, hid_feats, out_feats, device=None):
+    def __init__(self, in_feats, hid_feats, out_feats, device=None, degree_on: str = "col"):
         super().__init__()
-        self.conv1 = GCNConv(in_feats, hid_feats)
-        self.conv2 = GCNConv(hid_feats + in_feats, out_feats)
+        self.conv1 = GCNConv(in_feats, hid_feats, degree_on=degree_on)
+        self.conv2 = GCNConv(hid_feats + in_feats, out_feats, degree_on=degree_on)
         self.device = device
 
     def forward(self, data):
         x = data.x.float()
-        td, bu = _graphs(data)
+        if self.conv1.degree_on != self.conv2.degree_on:
+            raise ValueError("conv1 and conv2 must use the same degree_on convention")
+        td, bu = _graphs(data, self.conv1.degree_on)
         g = td if self.edge_key == "edge_index" else bu
         batch, rootindex = data.batch, data.rootindex
         root_of_node = rootindex[batch]                       # :46-50 as one gather
@@ -84,21 +86,43 @@ def _draw_seed() -> int:
 
 
 class BiGCN(torch.nn.Module):
-    """``BiGCN(in_feats, hid_feats, out_feats, device)`` (``BiGCN_Twitter.py:117-131``)."""
+    """``BiGCN(in_feats, hid_feats, out_feats, device)`` (``BiGCN_Twitter.py:117-131``).
+
+    ``degree_on``: gcn_norm degree convention of every GCNConv of the model - ``'col'``
+    (PyG >= 1.6, target degree; the fork's) or ``'row'`` (PyG 1.3.2, source degree).  It
+    is one model-wide setting (the ``degree_on`` property sets all four convolutions), so
+    the per-op path, the fused encoder and :class:`FusedTrainStep` always agree."""
 
     num_classes = 4
 
-    def __init__(self, in_feats, hid_feats, out_feats, device=None):
+    def __init__(self, in_feats, hid_feats, out_feats, device=None, degree_on: str = "col"):
         super().__init__()
         if hid_feats != 64 or out_feats != 64:
             raise ValueError("the fused MI355X encoder is specialised for hid = out = 64 "
                              "(the reference configuration, BiGCN_Twitter.py:144)")
-        self.TDrumorGCN = TDrumorGCN(in_feats, hid_feats, out_feats, device)
-        self.BUrumorGCN = BUrumorGCN(in_feats, hid_feats, out_feats, device)
+        degree_code(degree_on)
+        self.TDrumorGCN = TDrumorGCN(in_feats, hid_feats, out_feats, device, degree_on)
+        self.BUrumorGCN = BUrumorGCN(in_feats, hid_feats, out_feats, device, degree_on)
         self.fc = torch.nn.Linear((out_feats + hid_feats) * 2, self.num_classes)
         self.device = device
         self.keep_words = None  # optional injected dropout draw (tests)
         self.feat_mode = "auto"  # "auto": sparse feature path with device-side dense fallback
+
+    def _convs(self):
+        return (self.TDrumorGCN.conv1, self.TDrumorGCN.conv2, self.BUrumorGCN.conv1, self.BUrumorGCN.conv2)
+
+    @property
+    def degree_on(self) -> str:
+        conv = {c.degree_on for c in self._convs()}
+        if len(conv) != 1:
+            raise ValueError(f"the model's GCNConvs disagree on degree_on: {sorted(conv)}")
+        return conv.pop()
+
+    @degree_on.setter
+    def degree_on(self, value: str) -> None:
+        degree_code(value)
+        for c in self._convs():
+            c.degree_on = value
 
     def encoder_params(self):
         t, b = self.TDrumorGCN, self.BUrumorGCN
@@ -106,7 +130,7 @@ class BiGCN(torch.nn.Module):
                 b.conv1.lin.weight, b.conv1.bias, b.conv2.lin.weight, b.conv2.bias)
 
     def encode(self, data, seed=None):
-        td, bu = _graphs(data)
+        td, bu = _graphs(data, self.degree_on)
         if seed is None:
             seed = _draw_seed() if self.training else 0
         return bigcn_encoder(data.x, data.batch, data.rootindex, td, bu, _num_graphs(data),
@@ -125,8 +149,8 @@ class Net(BiGCN):
 
     num_classes = 2
 
-    def __init__(self, in_feats, hid_feats, out_feats, device=None):
-        super().__init__(in_feats, hid_feats, out_feats, device)
+    def __init__(self, in_feats, hid_feats, out_feats, device=None, degree_on: str = "col"):
+        super().__init__(in_feats, hid_feats, out_feats, device, degree_on)
 
 
 def make_optimizer(model: BiGCN, lr: float = 5e-4, weight_decay: float = 1e-4, fused: bool = False):

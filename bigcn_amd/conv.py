@@ -13,7 +13,7 @@ from typing import Optional
 
 import torch
 
-from .ops import Graph, gcn_conv
+from .ops import Graph, degree_code, gcn_conv
 
 
 class _Lin(torch.nn.Module):
@@ -38,6 +38,7 @@ class GCNConv(torch.nn.Module):
     def __init__(self, in_channels: int, out_channels: int, bias: bool = True, degree_on: str = "col"):
         super().__init__()
         self.in_channels, self.out_channels = in_channels, out_channels
+        degree_code(degree_on)
         self.degree_on = degree_on
         self.lin = _Lin(in_channels, out_channels)
         if bias:

@@ -30,6 +30,7 @@ __device__ __forceinline__ void adam_elem(float& p, float gr, float& m, float& v
 }
 
 __global__ __launch_bounds__(256) void k_adam(bgcn_adam_args a) {
+  if (a.skip_flag && *a.skip_flag != 0.0f) return;   // invalid step (any rank): no update
   // locate this block's tensor (at most BGCN_ADAM_MAX_TENSORS, uniform scan)
   int k = 0;
   while (k + 1 < a.count && int64_t(blockIdx.x) >= a.block_start[k + 1]) ++k;

@@ -29,7 +29,9 @@ __global__ __launch_bounds__(1024) void k_head_wgrad(const float* __restrict__ h
                                                      const float* __restrict__ dz, int64_t B, int C,
                                                      const float* __restrict__ loss_row,
                                                      float* __restrict__ dW, float* __restrict__ db,
-                                                     float* __restrict__ loss) {
+                                                     float* __restrict__ loss,
+                                                     const int32_t* __restrict__ status,
+                                                     float* __restrict__ status_flag) {
   __shared__ float red[4][kHeadIn];
   const int c = blockIdx.x, k = threadIdx.x & 255, q = threadIdx.x >> 8;
   const int64_t bq = (B + 3) / 4, b0 = q * bq, b1 = min<int64_t>(B, b0 + bq);
@@ -76,7 +78,12 @@ __global__ __launch_bounds__(1024) void k_head_wgrad(const float* __restrict__ h
     if (threadIdx.x < o) lr[threadIdx.x] += lr[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *loss = lr[0] / float(B);
+  if (threadIdx.x == 0) {
+    *loss = lr[0] / float(B);
+    // every status bit is known once the readout/head has run (it folds in the prepared
+    // batch's flags), which precedes this kernel
+    if (status_flag) *status_flag = status ? float(*status & 7) : 0.0f;
+  }
 }
 
 struct StepWs {
@@ -292,7 +299,7 @@ static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w
   hipStream_t x;
   BGCN_TRY(aux_fork(s, kLaneSide, &x));
   hipLaunchKernelGGL(k_head_wgrad, dim3(unsigned(C + 1)), dim3(1024), 0, x, w.head, w.dz, B, int(C),
-                     w.loss_row, a->grads[8], a->grads[9], a->loss);
+                     w.loss_row, a->grads[8], a->grads[9], a->loss, a->status, a->status_flag);
   BGCN_CHECK_LAUNCH();
   // (joins the side lane at its end; with a next-batch preparation on the side lane the
   // dW2 chain stays on this stream, which balances the two)

@@ -40,14 +40,21 @@ def init_from_env(backend: str = "nccl"):
 
 
 class GradBucket:
-    """One flat gradient bucket for all parameters (fixed order)."""
+    """One flat gradient bucket for all parameters (fixed order).
 
-    def __init__(self, params: Iterable[torch.nn.Parameter]):
+    ``status_slot``: one extra fp32 element after the gradients (``self.flag``).  The
+    fused step writes its validity flag there, so the same all-reduce that sums the
+    gradients also tells every rank whether any rank's step was invalid (the fused Adam
+    then skips the update everywhere, keeping the replicas identical)."""
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], status_slot: bool = False):
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
         self.numels = [p.numel() for p in self.params]
         dev = self.params[0].device
-        self.flat = torch.zeros(sum(self.numels), dtype=torch.float32, device=dev)
-        self._views = [v.view_as(p) for v, p in zip(torch.split(self.flat, self.numels), self.params)]
+        n = sum(self.numels)
+        self.flat = torch.zeros(n + (1 if status_slot else 0), dtype=torch.float32, device=dev)
+        self.flag = self.flat[n:] if status_slot else None
+        self._views = [v.view_as(p) for v, p in zip(torch.split(self.flat[:n], self.numels), self.params)]
 
     def views(self) -> List[torch.Tensor]:
         """Persistent per-parameter views of the flat bucket (parameter order): kernels
@@ -67,7 +74,7 @@ class GradBucket:
         views of the reduced bucket in parameter order (the caller divides by world)."""
         grads = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(n, device=self.flat.device)
                  for p, n in zip(self.params, self.numels)]
-        torch.cat(grads, out=self.flat)
+        torch.cat(grads, out=self.flat[:sum(self.numels)])
         self.allreduce_sum_(group)
         return self._views
 

@@ -74,6 +74,16 @@ def _csr_out(g: Graph) -> _lib.CsrOut:
     return c
 
 
+def degree_code(degree_on: str) -> int:
+    """C-ABI code of a gcn_norm degree convention: 'col' (PyG >= 1.6: target degree) -> 0,
+    'row' (PyG 1.3.2: source degree) -> 1; anything else raises."""
+    if degree_on == "col":
+        return 0
+    if degree_on == "row":
+        return 1
+    raise ValueError(f"degree_on must be 'col' or 'row', got {degree_on!r}")
+
+
 def _check_ei(edge_index: torch.Tensor) -> torch.Tensor:
     if edge_index.dim() != 2 or edge_index.size(0) != 2:
         raise ValueError("edge_index must be [2, E]")
@@ -84,6 +94,7 @@ def build_graph_pair(td_edge_index: torch.Tensor, bu_edge_index: torch.Tensor, n
                      degree_on: str = "col", validate: bool = False):
     """TD and BU graphs of one batch in one launch sequence (the fused step's K1)."""
     _dev_check(td_edge_index, bu_edge_index)
+    dcode = degree_code(degree_on)
     td_ei, bu_ei = _check_ei(td_edge_index), _check_ei(bu_edge_index)
     N = int(num_nodes)
     dev = td_ei.device
@@ -94,7 +105,7 @@ def build_graph_pair(td_edge_index: torch.Tensor, bu_edge_index: torch.Tensor, n
     ws = workspace(L.bgcn_graph_pair_workspace_size(td.num_edges, bu.num_edges, N), dev)
     a, b = _csr_out(td), _csr_out(bu)
     check(L.bgcn_build_graph_pair(ptr(td_ei), td.num_edges, ptr(bu_ei), bu.num_edges, N,
-                                  0 if degree_on == "col" else 1, ctypes.byref(a), ctypes.byref(b),
+                                  dcode, ctypes.byref(a), ctypes.byref(b),
                                   ptr(status), ptr(ws), ws.numel(), stream_handle()))
     if validate:
         td.check()
@@ -104,6 +115,7 @@ def build_graph_pair(td_edge_index: torch.Tensor, bu_edge_index: torch.Tensor, n
 def build_graph(edge_index: torch.Tensor, num_nodes: int, edge_weight: Optional[torch.Tensor] = None,
                 degree_on: str = "col", validate: bool = False) -> Graph:
     _dev_check(edge_index, edge_weight)
+    dcode = degree_code(degree_on)
     ei = _check_ei(edge_index)
     ew = None if edge_weight is None else edge_weight.to(torch.float32).contiguous()
     E, N = int(ei.size(1)), int(num_nodes)
@@ -111,7 +123,7 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, edge_weight: Optional[
     g = _alloc_graph(E, N, dev)
     L = _lib.lib()
     ws = workspace(L.bgcn_graph_workspace_size(E, N), dev)
-    check(L.bgcn_build_graph(ptr(ei), ptr(ew), E, N, 0 if degree_on == "col" else 1,
+    check(L.bgcn_build_graph(ptr(ei), ptr(ew), E, N, dcode,
                              ptr(g.t_ptr), ptr(g.t_row), ptr(g.t_col), ptr(g.t_w),
                              ptr(g.s_ptr), ptr(g.s_row), ptr(g.s_col), ptr(g.s_w),
                              ptr(g.status), ptr(ws), ws.numel(), stream_handle()))

@@ -29,7 +29,7 @@ class AdamArgs(ctypes.Structure):
                 ("count", ctypes.c_int), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
                 ("bias_correction1", ctypes.c_float), ("bias_correction2_sqrt", ctypes.c_float),
-                ("grad_scale", ctypes.c_float)]
+                ("grad_scale", ctypes.c_float), ("skip_flag", ctypes.c_void_p)]
 
 
 class FusedAdam:
@@ -64,8 +64,15 @@ class FusedAdam:
                 p.grad.zero_()
 
     @torch.no_grad()
-    def step(self, grads: Optional[Sequence[torch.Tensor]] = None, grad_scale: float = 1.0) -> None:
-        """``grads`` overrides ``p.grad`` (e.g. views of a reduced flat DP bucket)."""
+    def step(self, grads: Optional[Sequence[torch.Tensor]] = None, grad_scale: float = 1.0,
+             skip_flag: Optional[torch.Tensor] = None) -> None:
+        """``grads`` overrides ``p.grad`` (e.g. views of a reduced flat DP bucket).
+        ``skip_flag``: a one-element fp32 device tensor; when it holds a non-zero value at
+        execution time the launch updates nothing (an invalid training step, decided on
+        the device without a host sync; the step counter still advances).
+
+        Learning rates are read from ``param_groups`` on every call, so schedulers that
+        edit ``group['lr']`` (as with torch.optim.Adam) take effect."""
         self.step_count += 1
         t = self.step_count
         b1, b2 = self.betas
@@ -80,6 +87,7 @@ class FusedAdam:
             # persistent, so a training loop builds it once)
             a = AdamArgs()
             keep = []
+            groups = []         # param_groups index of each table entry (lr refreshed per step)
             k = 0
             for gi, p in enumerate(self.params()):
                 gr = gs[gi]
@@ -90,24 +98,31 @@ class FusedAdam:
                 m, v = self.state[p]
                 e = a.t[k]
                 e.param, e.grad, e.exp_avg, e.exp_avg_sq = ptr(p), ptr(gr), ptr(m), ptr(v)
-                e.numel, e.lr = p.numel(), self._lr_of(p)
+                e.numel = p.numel()
+                groups.append(self._group_of(p))
                 k += 1
             a.count = k
             a.beta1, a.beta2, a.eps, a.weight_decay = b1, b2, self.eps, self.weight_decay
-            cached = (key, a, keep)
+            cached = (key, a, keep, groups)
             self._cache = cached if cacheable else None
-        a = cached[1]
+        a, groups = cached[1], cached[3]
         if a.count == 0:
             return
+        for k, gi in enumerate(groups):
+            a.t[k].lr = float(self.param_groups[gi]["lr"])
+        if skip_flag is not None:
+            if skip_flag.dtype != torch.float32 or skip_flag.numel() != 1 or skip_flag.device != self.params()[0].device:
+                raise ValueError("skip_flag must be a one-element fp32 tensor on the parameters' device")
+        a.skip_flag = ptr(skip_flag)
         a.bias_correction1 = 1.0 - b1 ** t
         a.bias_correction2_sqrt = math.sqrt(1.0 - b2 ** t)
         a.grad_scale = grad_scale
         check(_lib.lib().bgcn_adam_step(ctypes.addressof(a), stream_handle()))
 
-    def _lr_of(self, p) -> float:
-        for g in self.param_groups:
+    def _group_of(self, p) -> int:
+        for gi, g in enumerate(self.param_groups):
             if any(q is p for q in g["params"]):
-                return g["lr"]
+                return gi
         raise KeyError("parameter not managed by this optimiser")
 
 

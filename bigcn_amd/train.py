@@ -25,7 +25,7 @@ from . import _lib
 from ._lib import BatchDesc, StepArgs, check, ptr, stream_handle, workspace
 from .bigcn import BiGCN, _draw_seed, _num_graphs
 from .dp import GradBucket
-from .ops import _FEAT_MODES, check_encoder_shapes, features, x_dtype_code
+from .ops import _FEAT_MODES, check_encoder_shapes, degree_code, features, x_dtype_code
 from .optim import FusedAdam, bigcn_adam
 
 
@@ -58,7 +58,7 @@ class FusedTrainStep:
     reference's three groups, :func:`bigcn_amd.optim.bigcn_adam`).  Gradients live in
     ``self.bucket`` (``grads()`` maps them back to the parameters)."""
 
-    def __init__(self, model: BiGCN, optimizer: Optional[FusedAdam] = None, degree_on: str = "col",
+    def __init__(self, model: BiGCN, optimizer: Optional[FusedAdam] = None, degree_on: Optional[str] = None,
                  group=None, tddroprate: float = 0.0, budroprate: float = 0.0,
                  drop_seed: Optional[int] = None):
         self.model = model
@@ -73,7 +73,7 @@ class FusedTrainStep:
         self.last_drop_seed = None
         self.opt = optimizer if optimizer is not None else bigcn_adam(model)
         self.group = group
-        self.bucket = GradBucket(self.opt.params())
+        self.bucket = GradBucket(self.opt.params(), status_slot=True)
         by_id = {id(p): v for p, v in zip(self.bucket.params, self.bucket.views())}
         self.step_params = list(model.encoder_params()) + [model.fc.weight, model.fc.bias]
         missing = [i for i, p in enumerate(self.step_params) if id(p) not in by_id]
@@ -84,7 +84,12 @@ class FusedTrainStep:
             if p.dtype != torch.float32 or not p.is_contiguous():
                 raise ValueError("parameters must be contiguous fp32")
         self.num_classes = model.fc.out_features
-        self.degree_on = 0 if degree_on == "col" else 1
+        # the gcn_norm convention is the model's (BiGCN.degree_on), so the fused step
+        # trains with the normalisation model(data) evaluates with
+        if degree_on is not None and degree_on != model.degree_on:
+            raise ValueError(f"degree_on={degree_on!r} differs from the model's "
+                             f"{model.degree_on!r}; set model.degree_on instead")
+        self.degree_on = degree_code(model.degree_on)
         a = StepArgs()
         for k, (p, g) in enumerate(zip(self.step_params, self.step_grads)):
             a.params[k], a.grads[k] = ptr(p), ptr(g)
@@ -173,6 +178,7 @@ class FusedTrainStep:
         self.last_drop_seed = int(a.cur.drop_seed) if a.cur.td_droprate > 0 or a.cur.bu_droprate > 0 else None
         loss = torch.empty(1, dtype=torch.float32, device=data.x.device)
         a.loss, a.logp, a.status = ptr(loss), ptr(logp), ptr(self.status)
+        a.status_flag = ptr(self.bucket.flag)
         L = _lib.lib()
         N, B = d.num_nodes, d.num_graphs
         ws = workspace(L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
@@ -188,7 +194,9 @@ class FusedTrainStep:
         loss = self.forward_backward(data, seed, logp, next_data)
         world = self.bucket.world(self.group)
         self.bucket.allreduce_sum_(self.group)
-        self.opt.step(grads=self.bucket.views(), grad_scale=1.0 / world)
+        # an invalid step (status bits, any rank: the flag is summed by the all-reduce)
+        # updates nothing; check_status() reports why
+        self.opt.step(grads=self.bucket.views(), grad_scale=1.0 / world, skip_flag=self.bucket.flag)
         return loss
 
     def check_status(self) -> None:

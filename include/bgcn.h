@@ -47,7 +47,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 1
+#define BGCN_ABI_VERSION 2
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -324,6 +324,10 @@ int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree
  *   call prepares it first (on the same stream).
  *   next / next_prepared (optional): a batch to prepare during this step on the
  *   auxiliary lane; pass it as the next call's prepared buffer with prepared_ready = 1.
+ *   status_flag (optional): receives float(status & 7) once the forward has seen every
+ *   flag; placed at the tail of the flat gradient bucket it travels through the DP
+ *   all-reduce, so bgcn_adam_step's skip_flag skips the update on EVERY rank when any
+ *   rank's step was invalid.
  * -------------------------------------------------------------------------- */
 #define BGCN_STEP_PARAMS 10
 typedef struct bgcn_step_args {
@@ -343,6 +347,7 @@ typedef struct bgcn_step_args {
   void* prepared; size_t prepared_bytes; int32_t prepared_ready;
   const bgcn_batch* next;        /* or NULL                                  */
   void* next_prepared; size_t next_prepared_bytes;
+  float* status_flag;            /* [1] or NULL                              */
 } bgcn_step_args;
 
 /* workspace of the step itself (the prepared buffers are separate) */
@@ -358,6 +363,8 @@ int bgcn_train_step(const bgcn_step_args* args, void* workspace, size_t workspac
  * amsgrad = False; weight_decay is L2 added to the gradient (torch Adam semantics).
  * grad_scale multiplies every gradient first (1/world for a summed DP bucket).
  * bias_correction1 = 1 - beta1^t, bias_correction2_sqrt = sqrt(1 - beta2^t).
+ * skip_flag (optional): when *skip_flag != 0 on the device the launch leaves every
+ * parameter and moment untouched (an invalid step, see bgcn_step_args.status_flag).
  * block_start is scratch filled by the library.
  * -------------------------------------------------------------------------- */
 #define BGCN_ADAM_MAX_TENSORS 16
@@ -371,6 +378,7 @@ typedef struct bgcn_adam_args {
   int count;
   float beta1, beta2, eps, weight_decay;
   float bias_correction1, bias_correction2_sqrt, grad_scale;
+  const float* skip_flag;        /* [1] or NULL                              */
 } bgcn_adam_args;
 int bgcn_adam_step(const bgcn_adam_args* args, bgcn_stream_t stream);
 

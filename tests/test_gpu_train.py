@@ -423,3 +423,84 @@ def test_dw1_column_split_matches(monkeypatch):
             close(res["4"][k], res["1"][k], what=k)
         else:
             assert torch.equal(res["1"][k], res["4"][k]), k
+
+
+def test_inplace_x_edit_after_collate_skips_update():
+    """The host nnz hint (collate / synth_batch) is bound to the x tensor object, so an
+    in-place edit that overfills a row goes unseen by the hint.  The step then flags
+    status bit 2 on the device, the fused Adam skips the update (parameters and moments
+    unchanged, no host sync) and check_status() raises."""
+    from bigcn_amd import FusedTrainStep
+    b = _synth(47, 8, 60)
+    assert b.x_nnz_hint() is not None
+    b.x[3, :40] = 1.0                                   # 40 non-zeros > the sparse cap, in place
+    p = O.make_params(5000, 64, 64, 4, seed=22)
+    m = _model(p)
+    m.train()
+    step = FusedTrainStep(m)
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    step(b, seed=3)
+    torch.cuda.synchronize()
+    assert float(step.bucket.flag) != 0.0
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    for mom in step.opt.state.values():
+        assert not mom[0].any() and not mom[1].any()
+    with pytest.raises(ValueError, match="non-zeros"):
+        step.check_status()
+    # a valid batch afterwards trains again (flag rewritten by the step)
+    b2 = _synth(48, 8, 60)
+    step(b2, seed=4)
+    torch.cuda.synchronize()
+    step.check_status()
+    assert float(step.bucket.flag) == 0.0
+    assert any(not torch.equal(v, before[k]) for k, v in m.state_dict().items())
+
+
+def test_fused_adam_follows_lr_changes():
+    """FusedAdam reads param_groups[i]['lr'] every step (an LR scheduler works as with
+    torch.optim.Adam): three steps with a StepLR-like halving match torch Adam."""
+    from bigcn_amd import FusedTrainStep, make_optimizer
+    b = _synth(49, 8, 100)
+    p = O.make_params(5000, 64, 64, 4, seed=23)
+    m = _model(p)
+    m.train()
+    step = FusedTrainStep(m)
+    shadow = _model(p)
+    topt = make_optimizer(shadow)
+    for it in range(3):
+        step.forward_backward(b, seed=2000 + it)
+        for sp, prm in zip(shadow.parameters(), m.parameters()):
+            sp.grad = step.grads()[prm].clone()
+        topt.step()
+        step.opt.step(grads=step.bucket.views(), grad_scale=1.0)
+        for g, tg in zip(step.opt.param_groups, topt.param_groups):
+            g["lr"] *= 0.5
+            tg["lr"] *= 0.5
+    for (k, v), (k2, v2) in zip(m.state_dict().items(), shadow.state_dict().items()):
+        close(v, v2, tol=1e-6, what=k)
+
+
+def test_row_degree_model_trains_and_evaluates_consistently():
+    """degree_on is model-wide: FusedTrainStep and model(data) use the same (PyG 1.3.2
+    source-degree) normalisation, and both match the oracle's row convention."""
+    from bigcn_amd import FusedTrainStep
+    b = _synth(50, 16, 120, root_random=True)
+    p = O.make_params(5000, 64, 64, 4, seed=24)
+    m = _model(p)
+    m.degree_on = "row"
+    m.eval()
+    step = FusedTrainStep(m)
+    loss = step.forward_backward(b)
+    _, rloss, rgrads, _ = _oracle(b, p, False, degree_on="row")
+    close(loss, rloss, what="loss")
+    for k, prm in zip(KEYS, step.step_params):
+        close(step.grads()[prm], rgrads[k], what=k)
+    m.zero_grad()
+    ref = F.nll_loss(m(b), b.y)
+    close(ref, rloss, what="model(data) loss")
+    ref.backward()
+    for k, prm in zip(KEYS, step.step_params):
+        close(prm.grad, rgrads[k], what="autograd " + k)
+    with pytest.raises(ValueError):
+        FusedTrainStep(m, degree_on="col")

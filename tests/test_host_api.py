@@ -1,0 +1,52 @@
+"""Host-side API contracts that need no GPU: argument validation of the drop-in
+modules and the fused step (no kernel is launched)."""
+import pytest
+import torch
+
+from bigcn_amd import BiGCN, GCNConv, Net
+from bigcn_amd.ops import degree_code
+
+
+def test_degree_on_values_are_validated():
+    assert degree_code("col") == 0 and degree_code("row") == 1
+    for bad in ("rows", "COL", "target", ""):
+        with pytest.raises(ValueError):
+            degree_code(bad)
+        with pytest.raises(ValueError):
+            GCNConv(8, 4, degree_on=bad)
+        with pytest.raises(ValueError):
+            BiGCN(8, 64, 64, degree_on=bad)
+
+
+def test_degree_on_is_model_wide():
+    m = Net(16, 64, 64, degree_on="row")
+    assert m.degree_on == "row"
+    convs = (m.TDrumorGCN.conv1, m.TDrumorGCN.conv2, m.BUrumorGCN.conv1, m.BUrumorGCN.conv2)
+    assert all(c.degree_on == "row" for c in convs)
+    m.degree_on = "col"
+    assert all(c.degree_on == "col" for c in convs)
+    with pytest.raises(ValueError):
+        m.degree_on = "source"
+    m.TDrumorGCN.conv2.degree_on = "row"          # edited behind the model's back
+    with pytest.raises(ValueError, match="disagree"):
+        _ = m.degree_on
+
+
+def test_fused_step_takes_the_models_degree_convention():
+    from bigcn_amd import FusedTrainStep
+    m = BiGCN(16, 64, 64, degree_on="row")
+    assert FusedTrainStep(m).degree_on == 1
+    assert FusedTrainStep(m, degree_on="row").degree_on == 1
+    with pytest.raises(ValueError, match="model"):
+        FusedTrainStep(m, degree_on="col")
+
+
+def test_fused_step_bucket_carries_the_status_slot():
+    from bigcn_amd import FusedTrainStep
+    m = BiGCN(16, 64, 64)
+    st = FusedTrainStep(m)
+    n = sum(p.numel() for p in m.parameters())
+    assert st.bucket.flat.numel() == n + 1
+    assert st.bucket.flag.numel() == 1
+    assert st.bucket.flag.data_ptr() == st.bucket.flat.data_ptr() + 4 * n
+    assert sum(v.numel() for v in st.bucket.views()) == n
