@@ -354,7 +354,8 @@ __global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ 
 
 // dH2[i][d*H + f] = dhead[b(i)][r1 block of d][f] / cnt_b * [H2 > 0]; block partial
 // column sums -> colpart[blk][2H].  256 threads = 8 row phases x 32 lanes x float4; a
-// block covers kReadBwdRows rows, every thread's rows are loaded before use.
+// block covers kReadBwdRows rows, every thread's rows are loaded before use.  Blocks
+// from nblk on run the classifier head's weight gradients (hj, bgcn_train_step).
 constexpr int kReadBwdRows = 64;
 __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dhead,
                                                      const float* __restrict__ H2,
@@ -362,7 +363,12 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
                                                      const int32_t* __restrict__ tree_ptr,
                                                      int64_t N, int64_t B,
                                                      float* __restrict__ dH2,
-                                                     float* __restrict__ colpart) {
+                                                     float* __restrict__ colpart,
+                                                     int nblk, HeadGradJob hj) {
+  if (int(blockIdx.x) >= nblk) {
+    head_grad_block(hj, int(blockIdx.x) - nblk);
+    return;
+  }
   constexpr int kPer = kReadBwdRows / 8;
   __shared__ float4 red[8][32];
   const int l = threadIdx.x & 31, ph = threadIdx.x >> 5;
@@ -416,13 +422,20 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
 // fp32 MFMA (32x32x2): four waves as 2 row halves x 2 column halves, K = H = 64 in 32
 // steps.  The K order is permuted (lane half h owns k in [32h, 32h+32)) so each lane's
 // dZ2 operand is one contiguous 128-byte run; W2 rows come straight from L2.
+// Blocks x >= nblk (y = 0) run a column-sum job (db2 from the readout backward's
+// partials).
 constexpr int kDh1Rows = 64;
 __global__ __launch_bounds__(256) void k_dh1(const float* __restrict__ dZ2,
                                              const float* __restrict__ H1,
                                              const float* __restrict__ W2td,
                                              const float* __restrict__ W2bu, int64_t ldw2,
                                              int64_t N, KeepSrc keep,
-                                             float* __restrict__ dH1, float* __restrict__ colpart) {
+                                             float* __restrict__ dH1, float* __restrict__ colpart,
+                                             int nblk, ColsumJob job) {
+  if (int(blockIdx.x) >= nblk) {
+    if (blockIdx.y == 0) colsum_job_block(job, int(blockIdx.x) - nblk);
+    return;
+  }
   // dZ2 tile (64 rows x 64) and W2[:, :64] staged in LDS with coalesced float4 loads
   // (a direct per-lane operand load touches 64 cache lines per instruction); rows are
   // padded to 65 floats so the MFMA operand reads are bank-conflict free.
@@ -798,7 +811,7 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
 // -> dW1.  Side lane, forked as soon as its inputs exist: db2, the dW2 chain (relu(H1)
 // block, root partials, root columns), db1 and the gated dense dW1; joined at the end.
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
-                        const Prepared* prep, bool side_busy) {
+                        const Prepared* prep, bool side_busy, const HeadGradJob* head) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->dhead_in && a->td_dw1 && a->bu_dw1 && a->td_dw2 && a->bu_dw2 && a->td_db1 &&
                      a->bu_db1 && a->td_db2 && a->bu_db2,
@@ -813,14 +826,13 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   const bool have_csc = a->save_for_backward || prep != nullptr;
   hipStream_t x;
 
-  // readout + relu' -> dH2; db2 on the side lane
+  // readout + relu' -> dH2 (+ the head's weight gradients in extra blocks); db2 is
+  // reduced by extra blocks of k_dh1
   const int64_t nblk_r = (N + kReadBwdRows - 1) / kReadBwdRows;
-  hipLaunchKernelGGL(k_readout_bwd, dim3(unsigned(nblk_r)), dim3(256), 0, s, a->dhead_in, a->h2,
-                     a->batch, a->tree_ptr, N, B, w.d2, w.colpart2);
-  BGCN_CHECK_LAUNCH();
-  BGCN_TRY(aux_fork(s, kLaneSide, &x));
-  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, x, w.colpart2, int(nblk_r),
-                     a->td_db2, a->bu_db2);
+  const HeadGradJob no_head{};
+  const int nhead = head ? head->C + 1 : 0;
+  hipLaunchKernelGGL(k_readout_bwd, dim3(unsigned(nblk_r + nhead)), dim3(256), 0, s, a->dhead_in, a->h2,
+                     a->batch, a->tree_ptr, N, B, w.d2, w.colpart2, int(nblk_r), head ? *head : no_head);
   BGCN_CHECK_LAUNCH();
   // dZ2 = A^T dH2
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.d2, w.dz2, nullptr, nullptr, BGCN_EPI_NONE, w, s));
@@ -863,21 +875,26 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
 
   // ---- main: dH1 through dropout and relu (db1 partials), dZ1 = A^T dH1
   const int64_t nblk_h = (N + kDh1Rows - 1) / kDh1Rows;
-  hipLaunchKernelGGL(k_dh1, dim3(unsigned(nblk_h), 2), dim3(256), 0, s, w.dz2, a->h1, a->td_w2,
-                     a->bu_w2, H + F, N, keep, w.dh1, w.colpart);
+  const ColsumJob db2_job{w.colpart2, int(nblk_r), a->td_db2, a->bu_db2};
+  hipLaunchKernelGGL(k_dh1, dim3(unsigned(nblk_h + colsum_job_blocks(256)), 2), dim3(256), 0, s, w.dz2,
+                     a->h1, a->td_w2, a->bu_w2, H + F, N, keep, w.dh1, w.colpart, int(nblk_h), db2_job);
   BGCN_CHECK_LAUNCH();
-  BGCN_TRY(aux_fork(s, kLaneSide, &x));
-  hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, x, w.colpart, int(nblk_h), a->td_db1,
-                     a->bu_db1);
-  BGCN_CHECK_LAUNCH();
+  // db1: extra blocks of the sparse dW1 launch, or (dense mode) a side-lane reduction
+  const ColsumJob db1_job{w.colpart, int(nblk_h), a->td_db1, a->bu_db1};
+  if (!sparse) {
+    BGCN_TRY(aux_fork(s, kLaneSide, &x));
+    hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, x, w.colpart, int(nblk_h), a->td_db1,
+                       a->bu_db1);
+    BGCN_CHECK_LAUNCH();
+  }
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.dh1, w.dz1, nullptr, nullptr, BGCN_EPI_NONE, w, s));
   // dW1 = [dZ1_td | dZ1_bu]^T X (one pass over X for both directions): over the CSC of X
   // (sparse, main) or the dense MFMA GEMM (dense mode on main; gated fallback on the side)
   if (sparse) {
-    BGCN_TRY(aux_fork(s, kLaneSide, &x));
+    if (dense_launched(a, sp)) BGCN_TRY(aux_fork(s, kLaneSide, &x));   // gated dense dW1
     if (!have_csc) BGCN_TRY(aux_join(s, kLaneSide));   // CSC built on the side
     timing_begin(5, s);
-    BGCN_TRY(sparse_dw1(sp, a, w.dz1, s));
+    BGCN_TRY(sparse_dw1(sp, a, w.dz1, s, db1_job));
     timing_end(5, s);
   }
   if (dense_launched(a, sp))

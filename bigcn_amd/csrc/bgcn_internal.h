@@ -128,6 +128,122 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
   st4(hd.dhead + b * kHeadIn + 4 * l, dh);
 }
 
+// ---- small reductions carried by extra blocks of a launch the caller's stream makes
+// anyway.  Forking them onto the side lane instead costs the caller's stream ~6 us per
+// fork (the event record's barrier packet stalls the queue; measured on the step's
+// kernel trace), more than the reductions themselves.
+
+// out_td[c] = sum_p part[p][c], out_bu[c] = sum_p part[p][H + c] (c < 64): 16 threads
+// per column stride the partials (p = g, g + 16, ...), the 16 group sums are then added
+// in group order - a fixed order (deterministic).  Job block jb of kColsumGroups *
+// blockDim.x / 16 ... : each block holds blockDim.x / 16 whole columns.
+struct ColsumJob {
+  const float* part;   // [P][128] or nullptr (no job)
+  int P;
+  float* out_td;
+  float* out_bu;
+};
+constexpr int kColsumGroups = 16;
+__host__ __device__ constexpr int colsum_job_blocks(int threads) {
+  return 128 * kColsumGroups / threads;
+}
+__device__ inline void colsum_job_block(const ColsumJob& j, int jb) {
+  __shared__ float red[kColsumGroups * 64];
+  const int cpb = int(blockDim.x) / kColsumGroups;    // columns per block (<= 64)
+  const int cl = threadIdx.x % cpb, g = threadIdx.x / cpb;
+  const int c = jb * cpb + cl;
+  float acc = 0.f;
+  int p = g;
+  for (; p + 3 * kColsumGroups < j.P; p += 4 * kColsumGroups) {   // 4 loads in flight
+    const float v0 = j.part[int64_t(p) * 128 + c], v1 = j.part[int64_t(p + kColsumGroups) * 128 + c];
+    const float v2 = j.part[int64_t(p + 2 * kColsumGroups) * 128 + c];
+    const float v3 = j.part[int64_t(p + 3 * kColsumGroups) * 128 + c];
+    acc += v0; acc += v1; acc += v2; acc += v3;
+  }
+  for (; p < j.P; p += kColsumGroups) acc += j.part[int64_t(p) * 128 + c];
+  red[g * cpb + cl] = acc;
+  __syncthreads();
+  if (g == 0) {
+    float s = red[cl];
+    for (int q = 1; q < kColsumGroups; ++q) s += red[q * cpb + cl];
+    if (c < 64) j.out_td[c] = s; else j.out_bu[c - 64] = s;
+  }
+}
+
+// Weight side of the classifier head's backward (bgcn_train_step), as C + 1 extra
+// 256-thread blocks: block c < C: dW[c][k] = sum_b dz[b][c] head[b][k] (4 quarters of the
+// trees x 64 float4 column groups, quarters combined in order); block C: db[c] =
+// sum_b dz[b][c] (64 tree slices per class, combined in order), loss = sum_b loss_row[b]
+// / B (fixed tree), and the step's validity flag float(status & 7) (every status bit is
+// known once the readout / head has run).
+struct HeadGradJob {
+  const float* head;     // [B, 256] or nullptr (no job)
+  const float* dz;       // [B, C]
+  int64_t B;
+  int C;
+  const float* loss_row;  // [B]
+  float* dW;             // [C, 256]
+  float* db;             // [C]
+  float* loss;           // [1]
+  const int32_t* status;  // or nullptr
+  float* status_flag;    // or nullptr
+};
+__device__ inline void head_grad_block(const HeadGradJob& j, int hb) {
+  __shared__ float4 r4[4][64];
+  __shared__ float ls[256];
+  __shared__ float dbp[kMaxClasses][64];
+  const int t = threadIdx.x;
+  const int64_t B = j.B;
+  const int C = j.C;
+  if (hb < C) {
+    const int kq = t & 63, q = t >> 6;
+    const int64_t bq = (B + 3) / 4, b0 = q * bq, b1 = min<int64_t>(B, b0 + bq);
+    float4 acc = f4zero();
+    int64_t b = b0;
+    for (; b + 8 <= b1; b += 8) {
+      float4 hv[8];
+      float gv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        hv[u] = ld4(j.head + (b + u) * kHeadIn + 4 * kq);
+        gv[u] = j.dz[(b + u) * C + hb];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = f4fma(gv[u], hv[u], acc);
+    }
+    for (; b < b1; ++b) acc = f4fma(j.dz[b * C + hb], ld4(j.head + b * kHeadIn + 4 * kq), acc);
+    r4[q][kq] = acc;
+    __syncthreads();
+    if (q == 0)
+      st4(j.dW + int64_t(hb) * kHeadIn + 4 * kq,
+          f4add(f4add(f4add(r4[0][kq], r4[1][kq]), r4[2][kq]), r4[3][kq]));
+    return;
+  }
+  float a = 0.f;
+  for (int64_t b = t; b < B; b += 256) a += j.loss_row[b];
+  ls[t] = a;
+  for (int cc = t >> 6; cc < C; cc += 4) {
+    const int sl = t & 63;
+    float s = 0.f;
+    for (int64_t b = sl; b < B; b += 64) s += j.dz[b * C + cc];
+    dbp[cc][sl] = s;
+  }
+  __syncthreads();
+  if (t < C) {
+    float s = 0.f;
+    for (int q = 0; q < 64; ++q) s += dbp[t][q];
+    j.db[t] = s;
+  }
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) ls[t] += ls[t + o];
+    __syncthreads();
+  }
+  if (t == 0) {
+    *j.loss = ls[0] / float(B);
+    if (j.status_flag) *j.status_flag = j.status ? float(*j.status & 7) : 0.0f;
+  }
+}
+
 // ---- fused encoder (bgcn_bigcn.hip); graph_lane: see bigcn_forward_impl
 size_t bigcn_ws_size(int64_t N, int64_t B, int64_t F, int64_t hid);
 struct Prepared;
@@ -136,8 +252,11 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
                        const Prepared* prep = nullptr);
 // side_busy: the side lane carries other long work (a next-batch preparation); the dW2
 // chain then stays on the caller's stream
+// head (bgcn_train_step): the classifier head's weight gradients, run as extra blocks of
+// the readout backward
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
-                        const Prepared* prep = nullptr, bool side_busy = false);
+                        const Prepared* prep = nullptr, bool side_busy = false,
+                        const HeadGradJob* head = nullptr);
 
 // ---- prepared batch (bgcn_step.hip): the weight-independent state of one batch
 // (sizes shared with bgcn_sparse.h: tree work items of kChunkItems nodes, CSC row blocks)

@@ -52,7 +52,8 @@ int sparse_conv2(SparseState& S, const float* H1, const int32_t* tree_ptr, const
                  float* Z2, KeepSrc keep, hipStream_t s);
 int sparse_csc(SparseState& S, hipStream_t s);
 int sparse_dw2_root_part(SparseState& S, const int32_t* tree_ptr, const float* dZ2, hipStream_t s);
-int sparse_dw1(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1, hipStream_t s);
+int sparse_dw1(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1, hipStream_t s,
+               const ColsumJob& job);
 int sparse_dw2_rootcols(SparseState& S, const bgcn_bigcn_args* a, const int32_t* node_root,
                         KeepSrc keep, hipStream_t s);
 

@@ -689,11 +689,17 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
 // F = 5000 waves, each walking its whole column serially: fine at Twitter size (~70
 // entries per column; the split measured 14 us slower there), slow at Weibo size (~225).
 constexpr int kDw1Depth = 16;
+// Blocks from nblk on run a column-sum job (db1 from k_dh1's partials), whether or not
+// the sparse path is live (the gated dense dW1 does not compute db1).
 template <int kDw1Split>                       // waves per column (1 or 4)
 __global__ __launch_bounds__(1024) void k_dw1_cols(SparseState S, const float* __restrict__ dZ1,
                                                    float* __restrict__ dw1_td,
-                                                   float* __restrict__ dw1_bu) {
+                                                   float* __restrict__ dw1_bu, int nblk, ColsumJob job) {
   constexpr int kDw1Cols = 16 / kDw1Split;   // columns per 1024-thread block
+  if (int(blockIdx.x) >= nblk) {
+    colsum_job_block(job, int(blockIdx.x) - nblk);
+    return;
+  }
   if (!use_sparse(S)) return;
   __shared__ float t1[2 * H][17];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -931,17 +937,22 @@ int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
   return BGCN_OK;
 }
 
-int sparse_dw1(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1, hipStream_t s) {
+int sparse_dw1(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1, hipStream_t s,
+               const ColsumJob& job) {
   // one wave per column at Twitter-sized batches, four from 64k rows (longer columns);
   // BGCN_DW1_SPLIT=1/4 forces either (read per call: tests compare both)
   const char* e = std::getenv("BGCN_DW1_SPLIT");
   const int split = e ? atoi(e) : (S.N >= 65536 ? 4 : 1);
-  if (split == 4)
-    hipLaunchKernelGGL(k_dw1_cols<4>, dim3(unsigned((S.F + 3) / 4)), dim3(1024), 0, s, S, dZ1,
-                     a->td_dw1, a->bu_dw1);
-  else
-    hipLaunchKernelGGL(k_dw1_cols<1>, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, dZ1,
-                     a->td_dw1, a->bu_dw1);
+  const int nj = job.part ? colsum_job_blocks(1024) : 0;
+  if (split == 4) {
+    const int nb = int((S.F + 3) / 4);
+    hipLaunchKernelGGL(k_dw1_cols<4>, dim3(unsigned(nb + nj)), dim3(1024), 0, s, S, dZ1,
+                       a->td_dw1, a->bu_dw1, nb, job);
+  } else {
+    const int nb = int((S.F + 15) / 16);
+    hipLaunchKernelGGL(k_dw1_cols<1>, dim3(unsigned(nb + nj)), dim3(1024), 0, s, S, dZ1,
+                       a->td_dw1, a->bu_dw1, nb, job);
+  }
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }

@@ -5,11 +5,13 @@
 //       loss = F.nll_loss(out_labels, Batch_data.y)          :186
 //       optimizer.zero_grad(); loss.backward()               :187-188
 //
-// K1 (gcn_norm + CSR of TD and BU) runs on the auxiliary lane, overlapped with the
-// encoder's pass over X on the caller's stream; then the CSC of X (same lane) overlaps
-// the second half of the forward, and the dW2 chain overlaps dH1 -> dZ1.  The head
-// (fc -> log_softmax -> nll mean, BiGCN_Twitter.py:129-130,186) and its backward are
-// two small kernels.  Every parameter gradient is written (not accumulated), so the
+// The weight-independent preparation (DropEdge, K1 = gcn_norm + CSR of TD and BU, the
+// ELL / CSC of X) of the NEXT batch runs on the auxiliary lane beside this step's chain.
+// The caller's stream forks only once per step: a fork's event record stalls the stream
+// ~6 us, so small side reductions (db1, db2, the head's weight gradients) ride as extra
+// blocks of launches the chain makes anyway.  The head (fc -> log_softmax -> nll mean,
+// BiGCN_Twitter.py:129-130,186) is fused into the readout.  Every parameter gradient is
+// written (not accumulated), so the
 // caller's buffers can be views of a flat data-parallel bucket; the all-reduce and
 // bgcn_adam_step follow.  No host sync anywhere: a bad edge index or label sets a bit
 // of *status on the device.
@@ -21,70 +23,6 @@ namespace {
 
 constexpr int H = 64;
 
-
-// Weight-side head backward: dW[c][k] = sum_b dz[b][c] head[b][k] (block c < C; 4
-// quarters of the trees x 256 k, combined in quarter order) and in block C:
-// db[c] = sum_b dz[b][c] and loss = sum_b loss_row[b] / B.  Fixed orders.
-__global__ __launch_bounds__(1024) void k_head_wgrad(const float* __restrict__ head,
-                                                     const float* __restrict__ dz, int64_t B, int C,
-                                                     const float* __restrict__ loss_row,
-                                                     float* __restrict__ dW, float* __restrict__ db,
-                                                     float* __restrict__ loss,
-                                                     const int32_t* __restrict__ status,
-                                                     float* __restrict__ status_flag) {
-  __shared__ float red[4][kHeadIn];
-  const int c = blockIdx.x, k = threadIdx.x & 255, q = threadIdx.x >> 8;
-  const int64_t bq = (B + 3) / 4, b0 = q * bq, b1 = min<int64_t>(B, b0 + bq);
-  if (c < C) {
-    float acc = 0.f;
-    int64_t b = b0;
-    for (; b + 8 <= b1; b += 8) {
-      float hv[8], gv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        hv[u] = head[(b + u) * kHeadIn + k];
-        gv[u] = dz[(b + u) * C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc = fmaf(gv[u], hv[u], acc);
-    }
-    for (; b < b1; ++b) acc = fmaf(dz[b * C + c], head[b * kHeadIn + k], acc);
-    red[q][k] = acc;
-    __syncthreads();
-    if (q == 0) dW[int64_t(c) * kHeadIn + k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
-    return;
-  }
-  float* lr = &red[0][0];   // 1024 partial sums of the loss rows
-  float acc = 0.f;
-  for (int64_t b = threadIdx.x; b < B; b += 1024) acc += loss_row[b];
-  lr[threadIdx.x] = acc;
-  __shared__ float dbp[kMaxClasses][64];
-  {   // db[c] = sum_b dz[b][c]: 64 tree slices per class, then a fixed-order sum
-    const int cc = threadIdx.x >> 6, sl = threadIdx.x & 63;
-    if (cc < C) {
-      float sdb = 0.f;
-      for (int64_t b = sl; b < B; b += 64) sdb += dz[b * C + cc];
-      dbp[cc][sl] = sdb;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < C) {
-    float sdb = 0.f;
-    for (int q = 0; q < 64; ++q) sdb += dbp[threadIdx.x][q];
-    db[threadIdx.x] = sdb;
-  }
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if (threadIdx.x < o) lr[threadIdx.x] += lr[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    *loss = lr[0] / float(B);
-    // every status bit is known once the readout/head has run (it folds in the prepared
-    // batch's flags), which precedes this kernel
-    if (status_flag) *status_flag = status ? float(*status & 7) : 0.0f;
-  }
-}
 
 struct StepWs {
   float *h1, *h2, *head, *dhead, *dz, *loss_row;
@@ -295,15 +233,12 @@ static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w
   const HeadArgs hd{a->params[8], a->params[9], a->y, int(C), a->logp, w.dz, w.loss_row, w.dhead,
                     a->status, p.status, a->feat_mode == BGCN_FEAT_SPARSE ? p.x_flags : nullptr};
   BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, graph_lane, &hd, &p));
-  // fc weight/bias gradients and the loss mean are off the critical path: side lane
-  hipStream_t x;
-  BGCN_TRY(aux_fork(s, kLaneSide, &x));
-  hipLaunchKernelGGL(k_head_wgrad, dim3(unsigned(C + 1)), dim3(1024), 0, x, w.head, w.dz, B, int(C),
-                     w.loss_row, a->grads[8], a->grads[9], a->loss, a->status, a->status_flag);
-  BGCN_CHECK_LAUNCH();
-  // (joins the side lane at its end; with a next-batch preparation on the side lane the
-  // dW2 chain stays on this stream, which balances the two)
-  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr);
+  // fc weight/bias gradients, the loss mean and the validity flag: extra blocks of the
+  // readout backward (joins the side lane at its end; with a next-batch preparation on
+  // the side lane the dW2 chain stays on this stream, which balances the two)
+  const HeadGradJob hj{w.head, w.dz, B, int(C), w.loss_row, a->grads[8], a->grads[9], a->loss,
+                       a->status, a->status_flag};
+  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr, &hj);
 }
 
 }  // namespace bgcn

@@ -1,0 +1,58 @@
+// Diagnostic side-stream jobs for tools/interfere_probe.py: what kind of concurrent
+// activity slows the latency-bound training chain (CU occupancy / clocks, L2 or
+// Infinity-Cache traffic, HBM streaming, page-translation pressure)?
+//   hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/interfere.hip -o tools/libinterfere.so
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+// ALU only: every lane runs `iters` dependent FMA rounds (no memory traffic)
+__global__ void k_alu(int iters, float* out) {
+  float a = threadIdx.x * 1e-3f, b = 1.0001f, c = 0.9999f;
+  for (int i = 0; i < iters; ++i) {
+    a = fmaf(a, b, c);
+    b = fmaf(b, c, a * 1e-9f);
+  }
+  if (a == 12345.f) out[0] = b;
+}
+
+// reads n16 16-byte words of buf `reps` times, grid-stride (lane-contiguous)
+__global__ void k_read(const uint4* __restrict__ buf, int64_t n16, int reps, uint32_t* out) {
+  uint32_t acc = 0;
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int r = 0; r < reps; ++r)
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += stride) {
+      const uint4 v = buf[i];
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  if (acc == 0x9e3779b9u) out[0] = acc;
+}
+
+// page-hopping reads: each lane reads one 16-byte word per 64 KiB page, walking the
+// buffer; little bandwidth, many distinct pages (translation pressure)
+__global__ void k_pages(const uint4* __restrict__ buf, int64_t n16, int reps, uint32_t* out) {
+  uint32_t acc = 0;
+  const int64_t step = 4096;  // 64 KiB in 16-byte words
+  const int64_t lanes = int64_t(gridDim.x) * blockDim.x;
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (int r = 0; r < reps; ++r)
+    for (int64_t p = t; p * step < n16; p += lanes) {
+      const uint4 v = buf[(p * step + r * 17) % n16];
+      acc ^= v.x;
+    }
+  if (acc == 0x9e3779b9u) out[0] = acc;
+}
+
+extern "C" int ifr_alu(int blocks, int iters, float* out, void* stream) {
+  hipLaunchKernelGGL(k_alu, dim3(blocks), dim3(256), 0, (hipStream_t)stream, iters, out);
+  return hipGetLastError();
+}
+extern "C" int ifr_read(const void* buf, int64_t bytes, int blocks, int reps, uint32_t* out, void* stream) {
+  hipLaunchKernelGGL(k_read, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)buf, bytes / 16, reps, out);
+  return hipGetLastError();
+}
+extern "C" int ifr_pages(const void* buf, int64_t bytes, int blocks, int reps, uint32_t* out, void* stream) {
+  hipLaunchKernelGGL(k_pages, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)buf, bytes / 16, reps, out);
+  return hipGetLastError();
+}

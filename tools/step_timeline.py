@@ -2,7 +2,8 @@
 
     python tools/step_timeline.py <run_kernel_trace.csv> [--step 15]
 
-Steps are delimited by the fused Adam kernel.  Prints every kernel of the chosen step
+Steps are delimited by the fused Adam kernel (or by --after KERNEL, e.g. the spin that
+tools/trace_probe.py puts before every step).  Prints every kernel of the chosen step
 (start / end relative to the previous Adam's end, stream) and per-stream busy time."""
 import argparse
 import collections
@@ -21,10 +22,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--step", type=int, default=15)
+    ap.add_argument("--after", default="k_adam",
+                    help="kernel that delimits steps (tools/trace_probe.py: k_alu, the spin before each step)")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    adam = [i for i, r in enumerate(rows) if "k_adam" in r["Kernel_Name"]]
-    i0, i1 = adam[a.step], adam[a.step + 1]
+    adam = [i for i, r in enumerate(rows) if a.after in r["Kernel_Name"]]
+    i0 = adam[a.step]
+    if a.after == "k_adam":
+        i1 = adam[a.step + 1]
+    else:   # through the step's Adam
+        i1 = next(i for i in range(i0 + 1, len(rows)) if "k_adam" in rows[i]["Kernel_Name"])
     t0 = int(rows[i0]["End_Timestamp"])
     busy = collections.defaultdict(float)
     for r in rows[i0 + 1:i1 + 1]:
