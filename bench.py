@@ -69,13 +69,14 @@ KERNEL_CLASSES = {
     "dense": {0: "conv1 X.W1^T MFMA (TD+BU fused)", 1: "dW1 = dZ1^T X MFMA (TD+BU fused)",
               2: "conv2 A2.W2^T MFMA (generated A2)", 3: "dW2 = dZ2^T A2 MFMA (generated A2)"},
     "auto": {0: "conv1: k_compact_conv1 (X read + compaction + gather) or gather from prepared ELL",
-             2: "conv2 (sparse root gather)", 3: "dW2 relu(H1) block MFMA", 5: "dW1 over CSC(X)",
+             2: "conv2 (sparse root gather)", 3: "k_bwd_mid: dW2 partials + root partials + dH1",
+             5: "k_bwd_tail: dW1 over CSC(X) + dW2 root columns + reductions",
              7: "k_compact_conv1<false>: X read + BoW compaction (next-batch preparation)"},
 }
 SPARSE_CAP = 32
 # rocprofv3 kernel symbol of each timed class (for the PMC traffic lookup)
 ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2): "bgcn::k_conv2_sparse",
-                 ("auto", 3): "bgcn::k_dw2<float>", ("auto", 5): "bgcn::k_dw1_cols",
+                 ("auto", 3): "bgcn::k_bwd_mid<float>", ("auto", 5): "bgcn::k_bwd_tail<1>",
                  ("auto", 7): "bgcn::k_compact_conv1<false, float>",
                  ("dense", 0): "bgcn::k_gemm_xwt<true, false, float>", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
                  ("dense", 2): "bgcn::k_conv2_fwd<float>", ("dense", 3): "bgcn::k_dw2<float>"}
@@ -109,8 +110,8 @@ def kernel_work(mode: str, cls: int, N: float, Fd: int, prefetch: bool = False, 
             return "hbm", N * Fd * xbytes + N * (SPARSE_CAP * 8.0 + 4.0)
         if cls == 2:   # H1 [N,128] read + Z2 [N,128] written (gathers of W2^T rows hit L2)
             return "hbm", N * 2 * H * 4.0 * 2
-        if cls == 3:   # the relu(H1) block of dW2, both directions, reduction over N
-            return "mfma", 2.0 * N * H * H * 2
+        if cls == 3:   # dZ2 read by three roles, H1 by two, dH1 written (the [N, 128] streams)
+            return "hbm", N * 2 * H * 4.0 * 6
         if cls == 5:   # ELL + CSC slots + dZ1 [N,128] read once, dW1 [128, F] written
             return "hbm", N * SPARSE_CAP * 12.0 + N * 2 * H * 4.0 + 4.0 * Fd * 2 * H
         return None, 0.0

@@ -12,17 +12,13 @@
 //   out = mean_tree([relu(H2) | H1[root]])   (:57-65; H1[root] is the detached x2)
 // Backward follows SURVEY.md 8(a) "Gradient dataflow": no gradient reaches conv1
 // through the root-extended x2 (copy.copy makes a new leaf, :44).
+#include "bgcn_bwd.h"
 #include "bgcn_internal.h"
 #include "bgcn_sparse.h"
 
 namespace bgcn {
 
 namespace {
-
-constexpr int BK = 32;
-constexpr int H = 64;  // hid = out = 64 (BiGCN_Twitter.py:144; the fused path is specialised)
-
-__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
 // (tree_ptr / node_root are built by the forward prologue, k_prologue in bgcn_sparse.hip)
 
@@ -119,172 +115,6 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const TX* __restrict__ X, int
   for (int r = 0; r < 16; ++r) {
     int64_t m = m0 + wr * 32 + acc_row(r, lane);
     if (m < N) Z2[m * (2 * H) + d * H + wc * 32 + r32] = acc[r];
-  }
-}
-
-// ---------------------------------------------------------------- dW2
-// part[d][s][o][c] = sum_{i in split s} dZ2[i][d*H+o] * A2_d[i][c]   (A2_d generated)
-// Block tile 64 (o) x 64 (c), waves 2 x 2; grid (ceil((H+F)/64), S, 2).
-// One launch configuration of k_dw2: a grid of gx column tiles x S node splits x 2
-// directions over partial rows of ldp columns.
-struct Dw2Cfg {
-  int64_t kchunk;
-  int S, gx, want_dense;
-  int64_t ldp;
-  float* part;
-};
-
-// Two configurations share one launch (blocks [0, nblk0) run cfg0, the rest cfg1): the
-// dense path's full grid (all 64+F columns, few node splits; want_dense = 1) and the
-// sparse path's relu(H1) block only (column tile 0, many node splits, ldp = 64;
-// want_dense = 0).  Only the configuration of the path selected on the device works.
-template <class TX>
-__global__ __launch_bounds__(256) void k_dw2(const TX* __restrict__ X, int64_t ldx, int64_t F,
-                                             const float* __restrict__ H1,
-                                             const float* __restrict__ dZ2,
-                                             const int32_t* __restrict__ node_root, int64_t N,
-                                             KeepSrc keep, const int32_t* __restrict__ gate,
-                                             Dw2Cfg cfg0, Dw2Cfg cfg1, int nblk0) {
-  const bool second = int(blockIdx.x) >= nblk0;
-  const Dw2Cfg& cfg = second ? cfg1 : cfg0;
-  const int bl = second ? int(blockIdx.x) - nblk0 : int(blockIdx.x);
-  if (dense_active(gate) != (cfg.want_dense != 0)) return;
-  const int64_t kchunk = cfg.kchunk, ldp = cfg.ldp;
-  const int S = cfg.S;
-  float* __restrict__ part = cfg.part;
-  constexpr int BN = 64;
-  __shared__ float As[2][BK * H];   // [node][o]
-  __shared__ float Bs[2][BK * BN];  // [node][c]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int bx = bl % cfg.gx, split = (bl / cfg.gx) % S, d = bl / (cfg.gx * S);
-  const int64_t K2 = H + F;
-  const int64_t c0 = int64_t(bx) * BN;
-  const int64_t kb = int64_t(split) * kchunk, ke = min<int64_t>(kb + kchunk, N);
-  const float sc = keep.scale();
-
-  // A staging: dZ2 tile 32 nodes x 64 -> node = tid/16 + 16 i, o quad (tid%16)*4
-  const int an = tid >> 4, aq = (tid & 15) * 4;
-  // B generation: node = tid/8, 8 columns at (tid%8)*8
-  const int bn = tid >> 3, bc = (tid & 7) * 8;
-  float4 ra[2], gb[2];
-  uint32_t gw = 0;
-  // unconditional loads from clamped nodes / columns, zeroed by select (see k_dh1)
-  auto gload = [&](int64_t k0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t node = k0 + an + 16 * i;
-      const float4 v = ld4(dZ2 + min<int64_t>(node, ke - 1) * (2 * H) + d * H + aq);
-      ra[i] = node < ke ? v : f4zero();
-    }
-    const int64_t node = k0 + bn;
-    const bool ok = node < ke;
-    const int64_t nc = min<int64_t>(node, ke - 1);
-    const int64_t c = c0 + bc;
-    gw = keep.get(uint32_t(d), uint32_t(nc), uint32_t(c / 32));
-    gw = ok ? gw : 0u;
-    const int32_t root = node_root[nc];
-    const TX* xr = X + int64_t(root < 0 ? 0 : root) * ldx;
-    const float* h1 = H1 + nc * (2 * H) + d * H;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t cc = min<int64_t>(c + 4 * j, K2 - 4);
-      float4 v;
-      if constexpr (sizeof(TX) == sizeof(float)) v = ld4(cc < H ? h1 + cc : xr + (cc - H));
-      else v = cc < H ? ld4(h1 + cc) : xq(xr + (cc - H));
-      gb[j] = (ok && c + 4 * j < K2) ? v : f4zero();
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) st4(&As[buf][(an + 16 * i) * H + aq], ra[i]);
-    const int bit0 = int((c0 + bc) & 31);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float v[4] = {gb[j].x, gb[j].y, gb[j].z, gb[j].w};
-      float o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        o[e] = ((gw >> (bit0 + 4 * j + e)) & 1u) ? sc * fmaxf(v[e], 0.f) : 0.f;
-      st4(&Bs[buf][bn * BN + bc + 4 * j], make_float4(o[0], o[1], o[2], o[3]));
-    }
-  };
-
-  f32x16 acc = {0};
-  const int h = lane >> 5, r32 = lane & 31;
-  const int nk = int((ke - kb + BK - 1) / BK);
-  if (nk > 0) {
-    gload(kb);
-    sstore(0);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload(kb + int64_t(kt + 1) * BK);
-    const float* A = &As[buf][h * H + wr * 32 + r32];
-    const float* B = &Bs[buf][h * BN + wc * 32 + r32];
-#pragma unroll
-    for (int s = 0; s < BK / 2; ++s) acc = mfma32x32x2(A[2 * s * H], B[2 * s * BN], acc);
-    if (kt + 1 < nk) sstore(buf ^ 1);
-    __syncthreads();
-  }
-  float* out = part + (int64_t(d) * S + split) * (H * ldp);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    int64_t c = c0 + wc * 32 + r32;
-    int o = wr * 32 + acc_row(r, lane);
-    if (c < ldp) out[int64_t(o) * ldp + c] = acc[r];
-  }
-}
-
-// dW2_d[o][c] = sum_s part[d][s][o][c] (fixed order) for c < ldp; the dense config
-// reduces all 64+F columns, the sparse config the relu(H1) block (the root columns come
-// from k_dw2_rootcols).  A block owns 64 consecutive outputs; its 4 waves take splits
-// s = q (mod 4), four loads in flight each, combined in wave order: deterministic.
-// Grid-stride over output tiles, so a small grid retires cheaply when the gate skips it.
-struct RedCfg {
-  int S;
-  int64_t ldp;
-  int want_dense;
-  int blocks;   // blocks of this configuration in the launch
-};
-
-__global__ __launch_bounds__(256) void k_reduce_dw2(const float* __restrict__ part, int64_t K2,
-                                                    float* __restrict__ dw_td,
-                                                    float* __restrict__ dw_bu,
-                                                    const int32_t* __restrict__ gate, RedCfg c0,
-                                                    RedCfg c1) {
-  const bool second = int(blockIdx.x) >= c0.blocks;
-  const RedCfg& cfg = second ? c1 : c0;
-  const int bl = second ? int(blockIdx.x) - c0.blocks : int(blockIdx.x);
-  if (dense_active(gate) != (cfg.want_dense != 0)) return;
-  const int S = cfg.S;
-  const int64_t ldp = cfg.ldp;
-  __shared__ float red[4][64];
-  const int64_t per = int64_t(H) * ldp;
-  const int64_t ntiles = (2 * per + 63) / 64;
-  const int q = threadIdx.x >> 6, t = threadIdx.x & 63;
-  for (int64_t tile = bl; tile < ntiles; tile += cfg.blocks) {
-    const int64_t idx = tile * 64 + t;
-    const bool valid = idx < 2 * per;
-    const int d = valid ? int(idx / per) : 0;
-    const int64_t e = valid ? idx % per : 0;
-    const float* p = part + int64_t(d) * S * per + e;
-    float acc = 0.f;
-    int s = q;
-    if (valid) {
-      for (; s + 12 < S; s += 16) {
-        const float v0 = p[int64_t(s) * per], v1 = p[int64_t(s + 4) * per];
-        const float v2 = p[int64_t(s + 8) * per], v3 = p[int64_t(s + 12) * per];
-        acc += v0; acc += v1; acc += v2; acc += v3;
-      }
-      for (; s < S; s += 4) acc += p[int64_t(s) * per];
-    }
-    red[q][t] = acc;
-    __syncthreads();
-    if (q == 0 && valid)
-      (d == 0 ? dw_td : dw_bu)[(e / ldp) * K2 + e % ldp] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
-    __syncthreads();
   }
 }
 
@@ -415,91 +245,6 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
     for (int q = 1; q < 8; ++q) acc = f4add(acc, red[q][l]);
     st4(colpart + int64_t(blockIdx.x) * (2 * H) + c, acc);
   }
-}
-
-// dH1[i][d*H + c] = (dZ2_d[i] . W2_d[:, c]) * keep(d,i,c) * s * [H1 > 0], c < H,
-// + block partial column sums.  A 64-row x 64-column tile per (block, direction) on the
-// fp32 MFMA (32x32x2): four waves as 2 row halves x 2 column halves, K = H = 64 in 32
-// steps.  The K order is permuted (lane half h owns k in [32h, 32h+32)) so each lane's
-// dZ2 operand is one contiguous 128-byte run; W2 rows come straight from L2.
-// Blocks x >= nblk (y = 0) run a column-sum job (db2 from the readout backward's
-// partials).
-constexpr int kDh1Rows = 64;
-__global__ __launch_bounds__(256) void k_dh1(const float* __restrict__ dZ2,
-                                             const float* __restrict__ H1,
-                                             const float* __restrict__ W2td,
-                                             const float* __restrict__ W2bu, int64_t ldw2,
-                                             int64_t N, KeepSrc keep,
-                                             float* __restrict__ dH1, float* __restrict__ colpart,
-                                             int nblk, ColsumJob job) {
-  if (int(blockIdx.x) >= nblk) {
-    if (blockIdx.y == 0) colsum_job_block(job, int(blockIdx.x) - nblk);
-    return;
-  }
-  // dZ2 tile (64 rows x 64) and W2[:, :64] staged in LDS with coalesced float4 loads
-  // (a direct per-lane operand load touches 64 cache lines per instruction); rows are
-  // padded to 65 floats so the MFMA operand reads are bank-conflict free.
-  __shared__ float Ds[kDh1Rows * (H + 1)];
-  __shared__ float Ws[H * (H + 1)];
-  __shared__ float red[2][H];
-  const int d = blockIdx.y;
-  const float* W2 = d == 0 ? W2td : W2bu;
-  const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int rh = wid & 1, ch = wid >> 1;
-  const int r = l & 31, h = l >> 5;
-  const int64_t blk0 = int64_t(blockIdx.x) * kDh1Rows;
-  const int64_t row0 = blk0 + rh * 32;
-  const int c = ch * 32 + r;  // output column of this lane (within H)
-  {
-    float4 dv[4], wv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {   // element e = tid + 256u of a 64 x 16 float4 grid
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      dv[u] = ld4(dZ2 + min<int64_t>(blk0 + rr, N - 1) * (2 * H) + d * H + q);
-      wv[u] = ld4(W2 + int64_t(rr) * ldw2 + q);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      float* dd = &Ds[rr * (H + 1) + q];
-      dd[0] = dv[u].x; dd[1] = dv[u].y; dd[2] = dv[u].z; dd[3] = dv[u].w;
-      float* ww = &Ws[rr * (H + 1) + q];
-      ww[0] = wv[u].x; ww[1] = wv[u].y; ww[2] = wv[u].z; ww[3] = wv[u].w;
-    }
-  }
-  float hv[16];
-  uint32_t wd[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int64_t i = min<int64_t>(row0 + (q & 3) + 8 * (q >> 2) + 4 * h, N - 1);
-    hv[q] = H1[i * (2 * H) + d * H + c];
-    wd[q] = keep.get(uint32_t(d), uint32_t(i), uint32_t(c >> 5));
-  }
-  __syncthreads();
-  // lane half h owns k in [32h, 32h + 32) (permuted K, same for A and B)
-  const float* ap = &Ds[(rh * 32 + r) * (H + 1) + 32 * h];
-  const float* bp = &Ws[(32 * h) * (H + 1) + c];
-  f32x16 acc = {};
-#pragma unroll
-  for (int kk = 0; kk < 32; ++kk) acc = mfma32x32x2(ap[kk], bp[kk * (H + 1)], acc);
-
-  const float sc = keep.scale();
-  float cs = 0.f;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-    const float g = (((wd[q] >> (c & 31)) & 1u) && hv[q] > 0.f) ? acc[q] * sc : 0.f;
-    if (i < N) {
-      dH1[i * (2 * H) + d * H + c] = g;
-      cs += g;
-    }
-  }
-  cs += __shfl_xor(cs, 32);
-  if (h == 0) red[rh][c] = cs;
-  __syncthreads();
-  if (threadIdx.x < H)
-    colpart[int64_t(blockIdx.x) * (2 * H) + d * H + threadIdx.x] =
-        red[0][threadIdx.x] + red[1][threadIdx.x];
 }
 
 // out_td[c] = sum_p colpart[p][c], out_bu[c] = sum_p colpart[p][H + c]: one block per
@@ -836,70 +581,64 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   BGCN_CHECK_LAUNCH();
   // dZ2 = A^T dH2
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.d2, w.dz2, nullptr, nullptr, BGCN_EPI_NONE, w, s));
-
-  // ---- side (or main when the side lane is busy): dW2 (both directions, generated A2
-  // operand).  The relu(H1) columns by MFMA; the X[root] columns by MFMA (dense) or from
-  // the root non-zeros (sparse)
-  if (side_busy) x = s;
-  else BGCN_TRY(aux_fork(s, kLaneSide, &x));
-  timing_begin(3, x);
-  {   // dense config (gated) and, in auto mode, the sparse relu(H1)-block config: one launch
-    const int gxd = int(grid_for(H + F, 64));
-    const Dw2Cfg dense{w.kchunk2, w.S2, gxd, 1, H + F, w.dw2_part};
-    const Dw2Cfg sparsec{w.kchunkh, w.Sh, 1, 0, int64_t(H), w.dw2_part};
-    const int n0 = dense_launched(a, sp) ? gxd * w.S2 * 2 : 0, n1 = sparse ? w.Sh * 2 : 0;
-    if (a->x_dtype == BGCN_DTYPE_BF16)
-      hipLaunchKernelGGL(k_dw2<bf16_t>, dim3(unsigned(n0 + n1)), dim3(256), 0, x,
-                         static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.dz2, w.node_root, N,
-                         keep, gate, dense, sparsec, n0);
-    else
-      hipLaunchKernelGGL(k_dw2<float>, dim3(unsigned(n0 + n1)), dim3(256), 0, x,
-                         static_cast<const float*>(a->x), a->ldx, F, a->h1, w.dz2, w.node_root, N,
-                         keep, gate, dense, sparsec, n0);
-    BGCN_CHECK_LAUNCH();
-  }
-  timing_end(3, x);
-  {   // the matching split reductions, also one launch
-    const RedCfg dense{w.S2, H + F, 1,
-                       dense_launched(a, sp) ? int(std::min<unsigned>(grid_for(2 * H * (H + F), 64), 1024)) : 0};
-    const RedCfg sparsec{w.Sh, int64_t(H), 0, int(grid_for(2 * H * H, 64))};
-    hipLaunchKernelGGL(k_reduce_dw2, dim3(unsigned(dense.blocks + (sparse ? sparsec.blocks : 0))),
-                       dim3(256), 0, x, w.dw2_part, H + F, a->td_dw2, a->bu_dw2, gate, dense, sparsec);
-    BGCN_CHECK_LAUNCH();
-  }
-  if (sparse) {
-    BGCN_TRY(sparse_dw2_root_part(sp, a->tree_ptr, w.dz2, x));
-    if (!have_csc) BGCN_TRY(sparse_csc(sp, x));
-    BGCN_TRY(sparse_dw2_rootcols(sp, a, w.node_root, keep, x));
-  }
-
-  // ---- main: dH1 through dropout and relu (db1 partials), dZ1 = A^T dH1
-  const int64_t nblk_h = (N + kDh1Rows - 1) / kDh1Rows;
-  const ColsumJob db2_job{w.colpart2, int(nblk_r), a->td_db2, a->bu_db2};
-  hipLaunchKernelGGL(k_dh1, dim3(unsigned(nblk_h + colsum_job_blocks(256)), 2), dim3(256), 0, s, w.dz2,
-                     a->h1, a->td_w2, a->bu_w2, H + F, N, keep, w.dh1, w.colpart, int(nblk_h), db2_job);
-  BGCN_CHECK_LAUNCH();
-  // db1: extra blocks of the sparse dW1 launch, or (dense mode) a side-lane reduction
-  const ColsumJob db1_job{w.colpart, int(nblk_h), a->td_db1, a->bu_db1};
-  if (!sparse) {
+  // the CSC of X, when the forward did not leave one, is built on the side lane
+  bool forked = false;
+  if (sparse && !have_csc) {
     BGCN_TRY(aux_fork(s, kLaneSide, &x));
-    hipLaunchKernelGGL(k_colsum_reduce, dim3(2 * H), dim3(256), 0, x, w.colpart, int(nblk_h), a->td_db1,
-                       a->bu_db1);
-    BGCN_CHECK_LAUNCH();
+    BGCN_TRY(sparse_csc(sp, x));
+    forked = true;
   }
+
+  // ---- middle launch: dW2 partials (the dense config, gated, and the sparse path's
+  // relu(H1) block), the dW2 root-column partials, dH1 through dropout and relu (+ db1
+  // partials) and the db2 column sums.  One dependent launch instead of four.
+  const int64_t nblk_h = (N + kDh1Rows - 1) / kDh1Rows;
+  const int gxd = int(grid_for(H + F, 64));
+  BwdMidArgs m{};
+  m.S = sp;
+  m.X = a->x; m.ldx = a->ldx; m.H1 = a->h1; m.dZ2 = w.dz2;
+  m.node_root = w.node_root; m.tree_ptr = a->tree_ptr; m.gate = gate; m.keep = keep;
+  m.dw2_dense = Dw2Cfg{w.kchunk2, w.S2, gxd, 1, H + F, w.dw2_part};
+  m.dw2_sparse = Dw2Cfg{w.kchunkh, w.Sh, 1, 0, int64_t(H), w.dw2_part};
+  m.n_dw2_dense = dense_launched(a, sp) ? gxd * w.S2 * 2 : 0;
+  m.n_dw2 = m.n_dw2_dense + (sparse ? w.Sh * 2 : 0);
+  m.W2td = a->td_w2; m.W2bu = a->bu_w2; m.dH1 = w.dh1; m.colpart = w.colpart; m.nblk_h = int(nblk_h);
+  m.db2 = ColsumJob{w.colpart2, int(nblk_r), a->td_db2, a->bu_db2};
+  timing_begin(3, s);
+  BGCN_TRY(bwd_mid_launch(m, a->x_dtype, s));
+  timing_end(3, s);
+
+  // dZ1 = A^T dH1
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.dh1, w.dz1, nullptr, nullptr, BGCN_EPI_NONE, w, s));
-  // dW1 = [dZ1_td | dZ1_bu]^T X (one pass over X for both directions): over the CSC of X
-  // (sparse, main) or the dense MFMA GEMM (dense mode on main; gated fallback on the side)
-  if (sparse) {
-    if (dense_launched(a, sp)) BGCN_TRY(aux_fork(s, kLaneSide, &x));   // gated dense dW1
-    if (!have_csc) BGCN_TRY(aux_join(s, kLaneSide));   // CSC built on the side
-    timing_begin(5, s);
-    BGCN_TRY(sparse_dw1(sp, a, w.dz1, s, db1_job));
-    timing_end(5, s);
-  }
-  if (dense_launched(a, sp))
+  // dW1 by the dense MFMA GEMM: dense mode on main; the gated fallback of auto mode on
+  // the side lane
+  if (dense_launched(a, sp)) {
+    if (sparse) {
+      BGCN_TRY(aux_fork(s, kLaneSide, &x));
+      forked = true;
+    }
     BGCN_TRY(gemm_tn_x(w.dz1, 2 * H, a->x, a->x_dtype, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F,
                        N, w.tn_ws, w.tn_bytes, sparse ? x : s, sparse ? 6 : 1, gate));
+  }
+  if (sparse && !have_csc) BGCN_TRY(aux_join(s, kLaneSide));   // CSC built on the side
+
+  // ---- tail launch: dW1 over the CSC of X (sparse), the dW2 root columns, the dW2
+  // partial reductions and the db1 column sums
+  BwdTailArgs t{};
+  t.S = sp;
+  t.dZ1 = w.dz1; t.dw1_td = a->td_dw1; t.dw1_bu = a->bu_dw1;
+  t.node_root = w.node_root; t.batch = a->batch; t.dw2_td = a->td_dw2; t.dw2_bu = a->bu_dw2;
+  t.keep_scale = keep.scale(); t.dw2_part = w.dw2_part; t.gate = gate;
+  // 1024-thread blocks, 4 output tiles of 64 each
+  t.red_dense = RedCfg{w.S2, H + F, 1,
+                       dense_launched(a, sp) ? int(std::min<unsigned>(grid_for(2 * H * (H + F), 256), 256)) : 0};
+  t.red_sparse = RedCfg{w.Sh, int64_t(H), 0, sparse ? int(grid_for(2 * H * H, 256)) : 0};
+  t.db1 = ColsumJob{w.colpart, int(nblk_h), a->td_db1, a->bu_db1};
+  timing_begin(5, s);
+  BGCN_TRY(bwd_tail_launch(t, s));
+  timing_end(5, s);
+  (void)side_busy;
+  (void)forked;
   timing_end(9, s);   // the main stream's own chain (span class, bgcn_train_step)
   BGCN_TRY(aux_join(s, kLaneSide));
   return BGCN_OK;

@@ -1,0 +1,256 @@
+// Device bodies of the backward's middle and tail launches (bgcn_sparse.hip defines the
+// merged kernels): the dW2 relu(H1)-block / dense partials, their fixed-order reduction
+// and dH1.  Each body takes its block id within its role and a slice of the launch's
+// shared memory, so several roles share one launch (one dependent launch instead of
+// four on the caller's stream).
+#pragma once
+
+#include "bgcn_internal.h"
+#include "bgcn_sparse.h"
+
+namespace bgcn {
+
+constexpr int BK = 32;
+constexpr int H = 64;  // hid = out = 64 (BiGCN_Twitter.py:144; the fused path is specialised)
+
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// ---------------------------------------------------------------- dW2
+// part[d][s][o][c] = sum_{i in split s} dZ2[i][d*H+o] * A2_d[i][c]   (A2_d generated)
+// Block tile 64 (o) x 64 (c), waves 2 x 2; grid (ceil((H+F)/64), S, 2).
+// One launch configuration of k_dw2: a grid of gx column tiles x S node splits x 2
+// directions over partial rows of ldp columns.
+
+// Two configurations share one launch (blocks [0, nblk0) run cfg0, the rest cfg1): the
+// dense path's full grid (all 64+F columns, few node splits; want_dense = 1) and the
+// sparse path's relu(H1) block only (column tile 0, many node splits, ldp = 64;
+// want_dense = 0).  Only the configuration of the path selected on the device works.
+// Device body, 256 threads, block id `bid` of the role; smem: kDw2Smem floats.
+constexpr int kDw2Smem = 4 * BK * H;
+template <class TX>
+__device__ inline void dw2_body(const TX* __restrict__ X, int64_t ldx, int64_t F,
+                                const float* __restrict__ H1, const float* __restrict__ dZ2,
+                                const int32_t* __restrict__ node_root, int64_t N, KeepSrc keep,
+                                const int32_t* __restrict__ gate, const Dw2Cfg& cfg0,
+                                const Dw2Cfg& cfg1, int nblk0, int bid, float* smem) {
+  const bool second = bid >= nblk0;
+  const Dw2Cfg& cfg = second ? cfg1 : cfg0;
+  const int bl = second ? bid - nblk0 : bid;
+  if (dense_active(gate) != (cfg.want_dense != 0)) return;
+  const int64_t kchunk = cfg.kchunk, ldp = cfg.ldp;
+  const int S = cfg.S;
+  float* __restrict__ part = cfg.part;
+  constexpr int BN = 64;
+  float (*As)[BK * H] = reinterpret_cast<float (*)[BK * H]>(smem);              // [node][o]
+  float (*Bs)[BK * BN] = reinterpret_cast<float (*)[BK * BN]>(smem + 2 * BK * H);  // [node][c]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int bx = bl % cfg.gx, split = (bl / cfg.gx) % S, d = bl / (cfg.gx * S);
+  const int64_t K2 = H + F;
+  const int64_t c0 = int64_t(bx) * BN;
+  const int64_t kb = int64_t(split) * kchunk, ke = min<int64_t>(kb + kchunk, N);
+  const float sc = keep.scale();
+
+  // A staging: dZ2 tile 32 nodes x 64 -> node = tid/16 + 16 i, o quad (tid%16)*4
+  const int an = tid >> 4, aq = (tid & 15) * 4;
+  // B generation: node = tid/8, 8 columns at (tid%8)*8
+  const int bn = tid >> 3, bc = (tid & 7) * 8;
+  float4 ra[2], gb[2];
+  uint32_t gw = 0;
+  // unconditional loads from clamped nodes / columns, zeroed by select (see k_dh1)
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t node = k0 + an + 16 * i;
+      const float4 v = ld4(dZ2 + min<int64_t>(node, ke - 1) * (2 * H) + d * H + aq);
+      ra[i] = node < ke ? v : f4zero();
+    }
+    const int64_t node = k0 + bn;
+    const bool ok = node < ke;
+    const int64_t nc = min<int64_t>(node, ke - 1);
+    const int64_t c = c0 + bc;
+    gw = keep.get(uint32_t(d), uint32_t(nc), uint32_t(c / 32));
+    gw = ok ? gw : 0u;
+    const int32_t root = node_root[nc];
+    const TX* xr = X + int64_t(root < 0 ? 0 : root) * ldx;
+    const float* h1 = H1 + nc * (2 * H) + d * H;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t cc = min<int64_t>(c + 4 * j, K2 - 4);
+      float4 v;
+      if constexpr (sizeof(TX) == sizeof(float)) v = ld4(cc < H ? h1 + cc : xr + (cc - H));
+      else v = cc < H ? ld4(h1 + cc) : xq(xr + (cc - H));
+      gb[j] = (ok && c + 4 * j < K2) ? v : f4zero();
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) st4(&As[buf][(an + 16 * i) * H + aq], ra[i]);
+    const int bit0 = int((c0 + bc) & 31);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float v[4] = {gb[j].x, gb[j].y, gb[j].z, gb[j].w};
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = ((gw >> (bit0 + 4 * j + e)) & 1u) ? sc * fmaxf(v[e], 0.f) : 0.f;
+      st4(&Bs[buf][bn * BN + bc + 4 * j], make_float4(o[0], o[1], o[2], o[3]));
+    }
+  };
+
+  f32x16 acc = {0};
+  const int h = lane >> 5, r32 = lane & 31;
+  const int nk = int((ke - kb + BK - 1) / BK);
+  if (nk > 0) {
+    gload(kb);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kb + int64_t(kt + 1) * BK);
+    const float* A = &As[buf][h * H + wr * 32 + r32];
+    const float* B = &Bs[buf][h * BN + wc * 32 + r32];
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) acc = mfma32x32x2(A[2 * s * H], B[2 * s * BN], acc);
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+  float* out = part + (int64_t(d) * S + split) * (H * ldp);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    int64_t c = c0 + wc * 32 + r32;
+    int o = wr * 32 + acc_row(r, lane);
+    if (c < ldp) out[int64_t(o) * ldp + c] = acc[r];
+  }
+}
+
+// dW2_d[o][c] = sum_s part[d][s][o][c] (fixed order) for c < ldp; the dense config
+// reduces all 64+F columns, the sparse config the relu(H1) block (the root columns come
+// from the root-column body).  A 256-thread group owns 64 consecutive outputs (a tile);
+// its 4 waves take splits s = q (mod 4), four loads in flight each, combined in wave
+// order: deterministic.  A 1024-thread block runs 4 groups on 4 consecutive tiles and
+// strides over the tiles in step (every group passes the same barriers); `blocks` of
+// the configuration share the tiles, so a small grid retires cheaply when the gate
+// skips it.
+
+constexpr int kRedSmem = 4 * 4 * 64;
+__device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K2,
+                                       float* __restrict__ dw_td, float* __restrict__ dw_bu,
+                                       const int32_t* __restrict__ gate, const RedCfg& c0,
+                                       const RedCfg& c1, int bid, float* smem) {
+  const bool second = bid >= c0.blocks;
+  const RedCfg& cfg = second ? c1 : c0;
+  const int bl = second ? bid - c0.blocks : bid;
+  if (dense_active(gate) != (cfg.want_dense != 0)) return;
+  const int S = cfg.S;
+  const int64_t ldp = cfg.ldp;
+  const int grp = threadIdx.x >> 8;
+  float (*red)[64] = reinterpret_cast<float (*)[64]>(smem + grp * 4 * 64);
+  const int64_t per = int64_t(H) * ldp;
+  const int64_t ntiles = (2 * per + 63) / 64;
+  const int q = (threadIdx.x >> 6) & 3, t = threadIdx.x & 63;
+  for (int64_t base = int64_t(bl) * 4; base < ntiles; base += int64_t(cfg.blocks) * 4) {
+    const int64_t tile = base + grp;
+    const int64_t idx = tile * 64 + t;
+    const bool valid = tile < ntiles && idx < 2 * per;
+    const int d = valid ? int(idx / per) : 0;
+    const int64_t e = valid ? idx % per : 0;
+    const float* p = part + int64_t(d) * S * per + e;
+    float acc = 0.f;
+    int s = q;
+    if (valid) {
+      for (; s + 12 < S; s += 16) {
+        const float v0 = p[int64_t(s) * per], v1 = p[int64_t(s + 4) * per];
+        const float v2 = p[int64_t(s + 8) * per], v3 = p[int64_t(s + 12) * per];
+        acc += v0; acc += v1; acc += v2; acc += v3;
+      }
+      for (; s < S; s += 4) acc += p[int64_t(s) * per];
+    }
+    red[q][t] = acc;
+    __syncthreads();
+    if (q == 0 && valid)
+      (d == 0 ? dw_td : dw_bu)[(e / ldp) * K2 + e % ldp] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    __syncthreads();
+  }
+}
+
+// dH1[i][d*H + c] = (dZ2_d[i] . W2_d[:, c]) * keep(d,i,c) * s * [H1 > 0], c < H,
+// + block partial column sums.  A 64-row x 64-column tile per (block, direction) on the
+// fp32 MFMA (32x32x2): four waves as 2 row halves x 2 column halves, K = H = 64 in 32
+// steps.  The K order is permuted (lane half h owns k in [32h, 32h+32)) so each lane's
+// dZ2 operand is one contiguous 128-byte run; W2 rows come straight from L2.
+// Device body, 256 threads: row block bx of direction d; smem: kDh1Smem floats.
+constexpr int kDh1Rows = 64;
+constexpr int kDh1Smem = kDh1Rows * (H + 1) + H * (H + 1) + 2 * H;
+__device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __restrict__ H1,
+                                const float* __restrict__ W2td, const float* __restrict__ W2bu,
+                                int64_t ldw2, int64_t N, KeepSrc keep, float* __restrict__ dH1,
+                                float* __restrict__ colpart, int bx, int d, float* smem) {
+  // dZ2 tile (64 rows x 64) and W2[:, :64] staged in LDS with coalesced float4 loads
+  // (a direct per-lane operand load touches 64 cache lines per instruction); rows are
+  // padded to 65 floats so the MFMA operand reads are bank-conflict free.
+  float* Ds = smem;
+  float* Ws = smem + kDh1Rows * (H + 1);
+  float (*red)[H] = reinterpret_cast<float (*)[H]>(smem + kDh1Rows * (H + 1) + H * (H + 1));
+  const float* W2 = d == 0 ? W2td : W2bu;
+  const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int rh = wid & 1, ch = wid >> 1;
+  const int r = l & 31, h = l >> 5;
+  const int64_t blk0 = int64_t(bx) * kDh1Rows;
+  const int64_t row0 = blk0 + rh * 32;
+  const int c = ch * 32 + r;  // output column of this lane (within H)
+  {
+    float4 dv[4], wv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {   // element e = tid + 256u of a 64 x 16 float4 grid
+      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
+      dv[u] = ld4(dZ2 + min<int64_t>(blk0 + rr, N - 1) * (2 * H) + d * H + q);
+      wv[u] = ld4(W2 + int64_t(rr) * ldw2 + q);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
+      float* dd = &Ds[rr * (H + 1) + q];
+      dd[0] = dv[u].x; dd[1] = dv[u].y; dd[2] = dv[u].z; dd[3] = dv[u].w;
+      float* ww = &Ws[rr * (H + 1) + q];
+      ww[0] = wv[u].x; ww[1] = wv[u].y; ww[2] = wv[u].z; ww[3] = wv[u].w;
+    }
+  }
+  float hv[16];
+  uint32_t wd[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t i = min<int64_t>(row0 + (q & 3) + 8 * (q >> 2) + 4 * h, N - 1);
+    hv[q] = H1[i * (2 * H) + d * H + c];
+    wd[q] = keep.get(uint32_t(d), uint32_t(i), uint32_t(c >> 5));
+  }
+  __syncthreads();
+  // lane half h owns k in [32h, 32h + 32) (permuted K, same for A and B)
+  const float* ap = &Ds[(rh * 32 + r) * (H + 1) + 32 * h];
+  const float* bp = &Ws[(32 * h) * (H + 1) + c];
+  f32x16 acc = {};
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) acc = mfma32x32x2(ap[kk], bp[kk * (H + 1)], acc);
+
+  const float sc = keep.scale();
+  float cs = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    const float g = (((wd[q] >> (c & 31)) & 1u) && hv[q] > 0.f) ? acc[q] * sc : 0.f;
+    if (i < N) {
+      dH1[i * (2 * H) + d * H + c] = g;
+      cs += g;
+    }
+  }
+  cs += __shfl_xor(cs, 32);
+  if (h == 0) red[rh][c] = cs;
+  __syncthreads();
+  if (threadIdx.x < H)
+    colpart[int64_t(bx) * (2 * H) + d * H + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x];
+}
+
+
+}  // namespace bgcn

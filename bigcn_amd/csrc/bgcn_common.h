@@ -72,6 +72,9 @@ void timing_begin(int cls, hipStream_t s);
 void timing_end(int cls, hipStream_t s);
 
 constexpr int kWave = 64;
+// status word bits: 1 bad edge index, 2 bad label, 4 over-full feature row (sparse
+// mode), 8 an internal hand-off timed out (kStatusInternal; results invalid)
+constexpr int32_t kStatusInternal = 8;
 
 // ---------------------------------------------------------------- device
 // Dropout keep word for (seed, direction, node, word): 32 keep bits covering

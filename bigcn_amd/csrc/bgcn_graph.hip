@@ -21,96 +21,28 @@
 //
 // Several graphs are built per launch sequence (blockIdx.y = graph): the fused step
 // builds TD and BU together.
-#include "bgcn_common.h"
+#include "bgcn_graph_body.h"
 
 namespace bgcn {
 namespace {
 
-constexpr int kMaxGraphs = 2;
-constexpr int kScanThreads = 256, kScanItems = 4, kScanChunk = kScanThreads * kScanItems;
-
-struct GraphIO {
-  const int64_t* ei;
-  const float* ew;
-  int64_t E;
-  int32_t *t_ptr, *t_row, *t_col;
-  float* t_w;
-  int32_t *s_ptr, *s_row, *s_col;
-  float* s_w;
-  int32_t* status;
-  // scratch
-  int32_t *cnt_t, *cnt_s, *cur_t, *cur_s, *loop_eid;  // zero-initialised block
-  int32_t* flags;                                        // [0] runs_t [1] runs_s [2] excluded [3] grouped_t [4] grouped_s
-  int32_t *run_t, *run_s;                                // run start per key
-  int32_t *tmp_t, *tmp_s;                                // general path: eid per slot
-  int32_t* bsum;                                         // [nb][4]: sum_t, sum_s, distinct_t, distinct_s
-  float* dinv;
-  int32_t* nlong;                                        // [2] long rows t / s (zeroed block)
-  int2 *bnd_t, *bnd_s;                                   // aggregation plans (SpmmPlan)
-  int32_t *long_t, *long_s;
-};
-
-struct GraphBatch {
-  GraphIO g[kMaxGraphs];
-  int64_t N;
-  int degree_on;
-};
-
-__device__ __forceinline__ bool edge_kept(const int64_t* ei, int64_t E, int64_t N, int64_t e,
-                                          int64_t& src, int64_t& dst, bool& valid) {
-  src = ei[e];
-  dst = ei[E + e];
-  valid = src >= 0 && src < N && dst >= 0 && dst < N;
-  return valid && src != dst;
+__global__ __launch_bounds__(kGraphThreads) void k_count(GraphBatch gb) {
+  graph_count_body(gb, gb.g[blockIdx.y], int(blockIdx.x));
 }
 
-// Run-start counters are wave-aggregated (ballot + popcount, one atomic per wave): in a
-// propagation tree nearly every edge starts a run, and per-edge atomics on one address
-// serialise.
-__global__ __launch_bounds__(256) void k_count(GraphBatch gb) {
-  GraphIO& G = gb.g[blockIdx.y];
-  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  const int64_t N = gb.N;
-  bool start_t = false, start_s = false;
-  if (e < G.E) {
-    int64_t src, dst;
-    bool valid;
-    const bool keep = edge_kept(G.ei, G.E, N, e, src, dst, valid);
-    if (!valid) {
-      if (G.status) atomicOr(G.status, 1);
-      atomicOr(&G.flags[2], 1);
-    } else if (!keep) {  // an input self loop: removed, its weight becomes the loop weight
-      if (G.ew) atomicMax(&G.loop_eid[src], int32_t(e + 1));  // (last wins; unweighted: 1)
-      // run-based ranks (e - run start) hold unless the loop sits inside a run of its
-      // own node, i.e. the next edge is a kept edge at that node; a loop between runs of
-      // other nodes shows up as a surplus run start (k_scan_top's check)
-      if (e + 1 < G.E) {
-        int64_t ns, nd;
-        bool nv;
-        if (edge_kept(G.ei, G.E, N, e + 1, ns, nd, nv) && (ns == src || nd == src))
-          atomicOr(&G.flags[2], 1);
-      }
-    } else {
-      atomicAdd(&G.cnt_t[dst], 1);
-      atomicAdd(&G.cnt_s[src], 1);
-      int64_t psrc = -1, pdst = -1;
-      if (e > 0) {
-        bool pv;
-        edge_kept(G.ei, G.E, N, e - 1, psrc, pdst, pv);
-      }
-      start_t = e == 0 || pdst != dst;
-      start_s = e == 0 || psrc != src;
-      if (start_t) G.run_t[dst] = int32_t(e);
-      if (start_s) G.run_s[src] = int32_t(e);
-    }
-  }
-  const int nt = __popcll(__ballot(start_t)), ns = __popcll(__ballot(start_s));
-  if ((threadIdx.x & (kWave - 1)) == 0) {
-    if (nt) atomicAdd(&G.flags[0], nt);
-    if (ns) atomicAdd(&G.flags[1], ns);
-  }
+__global__ __launch_bounds__(kScanThreads) void k_scan_lb(GraphBatch gb) {
+  graph_scan_body(gb, gb.g[blockIdx.y]);
 }
 
+__global__ __launch_bounds__(kGraphThreads) void k_fill_nodes(GraphBatch gb, int nfill) {
+  graph_fill_nodes_body(gb, gb.g[blockIdx.y], int(blockIdx.x), nfill);
+}
+
+__global__ __launch_bounds__(kGraphThreads) void k_rank_norm(GraphBatch gb, int ne, int nn) {
+  graph_rank_norm_body(gb, gb.g[blockIdx.y], int(blockIdx.x), ne, nn);
+}
+
+// ---- the multi-block scan (N > kScanSingleMax) and the edge-weighted steps
 // block partial sums of (cnt + 1) and of (cnt > 0) over [0, N)
 __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(GraphBatch gb) {
   GraphIO& G = gb.g[blockIdx.y];
@@ -325,11 +257,9 @@ __global__ void k_normalize(GraphBatch gb) {
   G.s_w[p] = (G.dinv[G.s_row[p]] * G.s_w[p]) * G.dinv[G.s_col[p]];
 }
 
-struct Scratch {
-  size_t zero_off, zero_bytes;
-};
+}  // namespace
 
-size_t carve(Carve& c, int64_t E, int64_t N, GraphIO* G) {
+size_t graph_carve(Carve& c, int64_t E, int64_t N, GraphIO* G, size_t* zero_bytes) {
   const size_t n = size_t(N > 0 ? N : 1), cap = size_t(E + N > 0 ? E + N : 1);
   const int64_t nb = (N + 1 + kScanChunk - 1) / kScanChunk;
   GraphIO t{};
@@ -341,6 +271,7 @@ size_t carve(Carve& c, int64_t E, int64_t N, GraphIO* G) {
   t.loop_eid = c.take<int32_t>(n);
   t.flags = c.take<int32_t>(8);
   t.nlong = c.take<int32_t>(2);
+  t.lb = c.take<uint64_t>(size_t(graph_scan_tiles(N)));
   t.run_t = c.take<int32_t>(n);
   t.run_s = c.take<int32_t>(n);
   t.tmp_t = c.take<int32_t>(cap);
@@ -353,14 +284,13 @@ size_t carve(Carve& c, int64_t E, int64_t N, GraphIO* G) {
   t.long_t = c.take<int32_t>(n);
   t.long_s = c.take<int32_t>(n);
   if (G) *G = t;
+  if (zero_bytes) *zero_bytes = size_t(reinterpret_cast<char*>(t.run_t) - reinterpret_cast<char*>(t.cnt_t));
   return c.off;
 }
 
-}  // namespace
-
 size_t graph_ws_size(int64_t E, int64_t N) {
   Carve c(nullptr, 0);
-  carve(c, E, N, nullptr);
+  graph_carve(c, E, N, nullptr, nullptr);
   return c.off + 256;
 }
 
@@ -389,21 +319,33 @@ int build_graphs_impl(const GraphArgs* ga, int count, int64_t N, int degree_on, 
     BGCN_CHECK_ARG(a.ws && a.ws_bytes >= graph_ws_size(a.E, N), "workspace too small");
     Carve c(a.ws, a.ws_bytes);
     GraphIO& G = gb.g[k];
-    carve(c, a.E, N, &G);
+    size_t zero_bytes = 0;
+    graph_carve(c, a.E, N, &G, &zero_bytes);
     G.ei = a.ei; G.ew = a.ew; G.E = a.E;
     G.t_ptr = a.t_ptr; G.t_row = a.t_row; G.t_col = a.t_col; G.t_w = a.t_w;
     G.s_ptr = a.s_ptr; G.s_row = a.s_row; G.s_col = a.s_col; G.s_w = a.s_w;
     G.status = a.status;
-    const size_t zero_bytes = reinterpret_cast<char*>(G.run_t) - reinterpret_cast<char*>(G.cnt_t);
     BGCN_CHECK_HIP(hipMemsetAsync(G.cnt_t, 0, zero_bytes, s));
     Emax = a.E > Emax ? a.E : Emax;
   }
   const unsigned gy = unsigned(count);
   const int blk = 256;
   const int64_t nb = (N + 1 + kScanChunk - 1) / kScanChunk;
+  bool weighted = false;
+  for (int k = 0; k < count; ++k) weighted = weighted || ga[k].ew != nullptr;
   if (Emax > 0) {
     hipLaunchKernelGGL(k_count, dim3(grid_for(Emax, blk), gy), dim3(blk), 0, s, gb);
     BGCN_CHECK_LAUNCH();
+  }
+  if (!weighted) {   // count -> scan -> fill_nodes -> rank_norm (bgcn_graph_body.h)
+    hipLaunchKernelGGL(k_scan_lb, dim3(unsigned(graph_scan_tiles(N)), gy), dim3(kScanThreads), 0, s, gb);
+    BGCN_CHECK_LAUNCH();
+    const int ne = graph_edge_blocks(Emax), nn = graph_node_blocks(N), np = graph_pos_blocks(Emax, N);
+    hipLaunchKernelGGL(k_fill_nodes, dim3(unsigned(ne + nn), gy), dim3(kGraphThreads), 0, s, gb, ne);
+    BGCN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_rank_norm, dim3(unsigned(ne + nn + np), gy), dim3(kGraphThreads), 0, s, gb, ne, nn);
+    BGCN_CHECK_LAUNCH();
+    return BGCN_OK;
   }
   hipLaunchKernelGGL(k_scan_blocks, dim3(unsigned(nb), gy), dim3(kScanThreads), 0, s, gb);
   BGCN_CHECK_LAUNCH();
@@ -431,7 +373,7 @@ void graph_pair_plans(void* ws, size_t ws_bytes, int64_t Etd, int64_t Ebu, int64
   for (int k = 0; k < 2; ++k) {
     Carve c(base + k * half, half);
     GraphIO G{};
-    carve(c, k == 0 ? Etd : Ebu, N, &G);
+    graph_carve(c, k == 0 ? Etd : Ebu, N, &G, nullptr);
     SpmmPlan* o = k == 0 ? td : bu;
     o[0] = SpmmPlan{G.bnd_t, G.long_t, G.nlong};
     o[1] = SpmmPlan{G.bnd_s, G.long_s, G.nlong + 1};

@@ -174,7 +174,7 @@ __device__ inline void colsum_job_block(const ColsumJob& j, int jb) {
 // 256-thread blocks: block c < C: dW[c][k] = sum_b dz[b][c] head[b][k] (4 quarters of the
 // trees x 64 float4 column groups, quarters combined in order); block C: db[c] =
 // sum_b dz[b][c] (64 tree slices per class, combined in order), loss = sum_b loss_row[b]
-// / B (fixed tree), and the step's validity flag float(status & 7) (every status bit is
+// / B (fixed tree), and the step's validity flag float(status & 15) (every status bit is
 // known once the readout / head has run).
 struct HeadGradJob {
   const float* head;     // [B, 256] or nullptr (no job)
@@ -240,7 +240,7 @@ __device__ inline void head_grad_block(const HeadGradJob& j, int hb) {
   }
   if (t == 0) {
     *j.loss = ls[0] / float(B);
-    if (j.status_flag) *j.status_flag = j.status ? float(*j.status & 7) : 0.0f;
+    if (j.status_flag) *j.status_flag = j.status ? float(*j.status & 15) : 0.0f;
   }
 }
 

@@ -41,9 +41,10 @@ int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root
                     bool batch_part = true);
 struct Prepared;
 // weight-independent preparation of one batch into p (bgcn_prepare_batch)
+// part 1: node maps, tree items, the ELL of X (the pass over X); part 2: the CSC of X
 int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
                    const int64_t* batch, const int64_t* rootindex, const void* X, int xdt, int64_t ldx,
-                   hipStream_t s);
+                   hipStream_t s, int part = 3);
 int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s);
 int sparse_compact_conv1(SparseState& S, const void* X, int xdt, int64_t ldx, float* Z1,
                          hipStream_t s);
@@ -51,10 +52,49 @@ int sparse_items(SparseState& S, const int32_t* tree_ptr, hipStream_t s);
 int sparse_conv2(SparseState& S, const float* H1, const int32_t* tree_ptr, const int64_t* rootindex,
                  float* Z2, KeepSrc keep, hipStream_t s);
 int sparse_csc(SparseState& S, hipStream_t s);
-int sparse_dw2_root_part(SparseState& S, const int32_t* tree_ptr, const float* dZ2, hipStream_t s);
-int sparse_dw1(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1, hipStream_t s,
-               const ColsumJob& job);
-int sparse_dw2_rootcols(SparseState& S, const bgcn_bigcn_args* a, const int32_t* node_root,
-                        KeepSrc keep, hipStream_t s);
+// The backward's middle and tail launches (bgcn_sparse.hip): role block counts the
+// launchers fill in are marked (set by launcher).
+struct Dw2Cfg {
+  int64_t kchunk;
+  int S, gx, want_dense;
+  int64_t ldp;
+  float* part;
+};
+struct RedCfg {
+  int S;
+  int64_t ldp;
+  int want_dense;
+  int blocks;   // 1024-thread blocks of this configuration in the launch
+};
+struct BwdMidArgs {
+  SparseState S;                 // sizes (N, F, max_items), root partials (sparse)
+  const void* X; int64_t ldx;
+  const float *H1, *dZ2;
+  const int32_t *node_root, *tree_ptr, *gate;
+  KeepSrc keep;
+  Dw2Cfg dw2_dense, dw2_sparse;  // dW2 partials: dense config blocks first
+  int n_dw2_dense, n_dw2;
+  int n_root;                    // (set by launcher)
+  const float *W2td, *W2bu;      // dH1
+  float *dH1, *colpart;
+  int nblk_h;
+  ColsumJob db2;
+};
+struct BwdTailArgs {
+  SparseState S;
+  const float* dZ1;
+  float *dw1_td, *dw1_bu;
+  int n_dw1, n_rootcols;         // (set by launcher)
+  const int32_t* node_root;
+  const int64_t* batch;
+  float *dw2_td, *dw2_bu;
+  float keep_scale;
+  const float* dw2_part;
+  const int32_t* gate;
+  RedCfg red_dense, red_sparse;
+  ColsumJob db1;
+};
+int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s);
+int bwd_tail_launch(BwdTailArgs& a, hipStream_t s);
 
 }  // namespace bgcn

@@ -20,13 +20,12 @@
 
 
 
+#include "bgcn_bwd.h"
 #include "bgcn_internal.h"
 #include "bgcn_sparse.h"
 
 namespace bgcn {
 namespace {
-
-constexpr int H = 64;
 
 __device__ __forceinline__ bool use_sparse(const SparseState& S) { return S.mode != 1 && S.flags[0] == 0; }
 
@@ -444,14 +443,15 @@ __global__ __launch_bounds__(1024) void k_items(SparseState S, const int32_t* __
 // a [32 x nodes] x [nodes x 64] product with the 0/1 keep masks of the forward (S.rbits)
 // as A.  Each wave takes 64 of the item's nodes (lane half h owns 32 of them: permuted
 // K); the four waves' partials are combined in a fixed order.
-__global__ __launch_bounds__(256) void k_dw2_root_part(SparseState S, const float* __restrict__ dZ2,
-                                                       const int32_t* __restrict__ tree_ptr) {
+// Device body, 256 threads: work item `item` of direction d; smem: kRootPartSmem floats.
+constexpr int kRootPartSmem = kChunk + 4 * kCap * H;
+__device__ inline void root_part_body(const SparseState& S, const float* __restrict__ dZ2,
+                                      const int32_t* __restrict__ tree_ptr, int item, int d,
+                                      float* smem) {
   if (!use_sparse(S)) return;
-  const int item = blockIdx.x;
   if (item >= S.tree_item0[S.B]) return;
-  __shared__ uint32_t bits[kChunk];
-  __shared__ float red[4][kCap * H];
-  const int d = blockIdx.y;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
+  float (*red)[kCap * H] = reinterpret_cast<float (*)[kCap * H]>(smem + kChunk);
   const int b = S.item_tree[item];
   const int64_t beg = int64_t(tree_ptr[b]) + int64_t(S.item_chunk[item]) * kChunk;
   const int64_t end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
@@ -689,23 +689,19 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
 // F = 5000 waves, each walking its whole column serially: fine at Twitter size (~70
 // entries per column; the split measured 14 us slower there), slow at Weibo size (~225).
 constexpr int kDw1Depth = 16;
-// Blocks from nblk on run a column-sum job (db1 from k_dh1's partials), whether or not
-// the sparse path is live (the gated dense dW1 does not compute db1).
+// Device body, 1024 threads, column block bid; smem: kDw1Smem floats.
+constexpr int kDw1Smem = 2 * H * 17;
 template <int kDw1Split>                       // waves per column (1 or 4)
-__global__ __launch_bounds__(1024) void k_dw1_cols(SparseState S, const float* __restrict__ dZ1,
-                                                   float* __restrict__ dw1_td,
-                                                   float* __restrict__ dw1_bu, int nblk, ColsumJob job) {
+__device__ inline void dw1_body(const SparseState& S, const float* __restrict__ dZ1,
+                                float* __restrict__ dw1_td, float* __restrict__ dw1_bu, int bid,
+                                float* smem) {
   constexpr int kDw1Cols = 16 / kDw1Split;   // columns per 1024-thread block
-  if (int(blockIdx.x) >= nblk) {
-    colsum_job_block(job, int(blockIdx.x) - nblk);
-    return;
-  }
   if (!use_sparse(S)) return;
-  __shared__ float t1[2 * H][17];
+  float (*t1)[17] = reinterpret_cast<float (*)[17]>(smem);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int part = wave % kDw1Split;
   const int64_t F = S.F;
-  const int64_t c = int64_t(blockIdx.x) * kDw1Cols + wave / kDw1Split;
+  const int64_t c = int64_t(bid) * kDw1Cols + wave / kDw1Split;
   float2 a1 = make_float2(0.f, 0.f);
   if (c < F) {
     const int64_t beg = S.col_start[c], end = S.col_end[c];
@@ -740,7 +736,7 @@ __global__ __launch_bounds__(1024) void k_dw1_cols(SparseState S, const float* _
   // combine the column's partials in wave order, then store (kDw1Cols consecutive columns
   // per output row)
   const int tx = threadIdx.x % kDw1Cols;
-  const int64_t cc = int64_t(blockIdx.x) * kDw1Cols + tx;
+  const int64_t cc = int64_t(bid) * kDw1Cols + tx;
   for (int ty = threadIdx.x / kDw1Cols; ty < 2 * H && cc < F; ty += 1024 / kDw1Cols) {
     float acc = t1[ty][tx * kDw1Split];
 #pragma unroll
@@ -753,14 +749,15 @@ __global__ __launch_bounds__(1024) void k_dw1_cols(SparseState S, const float* _
 // dW2 root columns: dW2_d[:, 64 + c] = sum over the root rows holding column c (tree
 // order = CSC row order) of 2 relu(x) * sum_items root_part[d][item][slot]; every column
 // is written (zero when no root holds it).  A wave per column; only root rows are read.
-__global__ __launch_bounds__(1024) void k_dw2_rootcols(SparseState S, const int32_t* __restrict__ node_root,
-                                                       const int64_t* __restrict__ batch,
-                                                       float* __restrict__ dw2_td,
-                                                       float* __restrict__ dw2_bu, float scale) {
+// Device body, 1024 threads, column block bid; smem: kRootColsSmem floats.
+constexpr int kRootColsSmem = 2 * H * 17;
+__device__ inline void rootcols_body(const SparseState& S, const int32_t* __restrict__ node_root,
+                                     const int64_t* __restrict__ batch, float* __restrict__ dw2_td,
+                                     float* __restrict__ dw2_bu, float scale, int bid, float* smem) {
   if (!use_sparse(S)) return;
-  __shared__ float t2[2][H][17];
+  float (*t2)[H][17] = reinterpret_cast<float (*)[H][17]>(smem);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t c = int64_t(blockIdx.x) * 16 + wave;
+  const int64_t c = int64_t(bid) * 16 + wave;
   float a2[2] = {0.f, 0.f};
   if (c < S.F) {
     const int64_t beg = S.col_start[c], end = S.col_end[c];
@@ -794,7 +791,7 @@ __global__ __launch_bounds__(1024) void k_dw2_rootcols(SparseState S, const int3
   t2[1][lane][wave] = a2[1];
   __syncthreads();
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 x 64
-  const int64_t cc = int64_t(blockIdx.x) * 16 + tx;
+  const int64_t cc = int64_t(bid) * 16 + tx;
   if (cc < S.F) {
     const int64_t K2 = S.F + H;
     dw2_td[int64_t(ty) * K2 + H + cc] = t2[0][ty][tx];
@@ -802,7 +799,87 @@ __global__ __launch_bounds__(1024) void k_dw2_rootcols(SparseState S, const int3
   }
 }
 
+// ---------------------------------------------------------------- merged backward launches
+// middle (256 threads): dW2 partials (dense / relu(H1) block), dW2 root partials, dH1,
+// db2 column sums;  tail (1024 threads): dW1 over the CSC, dW2 root columns, the dW2
+// partial reduction, db1 column sums.  Roles by block range, in that order.
+constexpr int kMidSmem = kDw2Smem > kRootPartSmem ? (kDw2Smem > kDh1Smem ? kDw2Smem : kDh1Smem)
+                                                  : (kRootPartSmem > kDh1Smem ? kRootPartSmem : kDh1Smem);
+template <class TX>
+__global__ __launch_bounds__(256) void k_bwd_mid(BwdMidArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[kMidSmem];
+  int b = int(blockIdx.x);
+  if (b < a.n_dw2) {
+    dw2_body<TX>(static_cast<const TX*>(a.X), a.ldx, a.S.F, a.H1, a.dZ2, a.node_root, a.S.N, a.keep,
+                 a.gate, a.dw2_dense, a.dw2_sparse, a.n_dw2_dense, b, smem);
+    return;
+  }
+  b -= a.n_dw2;
+  if (b < a.n_root) {
+    root_part_body(a.S, a.dZ2, a.tree_ptr, b % a.S.max_items, b / a.S.max_items, smem);
+    return;
+  }
+  b -= a.n_root;
+  if (b < 2 * a.nblk_h) {
+    dh1_body(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, b % a.nblk_h,
+             b / a.nblk_h, smem);
+    return;
+  }
+  colsum_job_block(a.db2, b - 2 * a.nblk_h);
+}
+
+constexpr int kTailSmem = kDw1Smem > kRootColsSmem ? (kDw1Smem > kRedSmem ? kDw1Smem : kRedSmem)
+                                                   : (kRootColsSmem > kRedSmem ? kRootColsSmem : kRedSmem);
+template <int kDw1Split>
+__global__ __launch_bounds__(1024) void k_bwd_tail(BwdTailArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[kTailSmem];
+  int b = int(blockIdx.x);
+  if (b < a.n_dw1) {
+    dw1_body<kDw1Split>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, b, smem);
+    return;
+  }
+  b -= a.n_dw1;
+  if (b < a.n_rootcols) {
+    rootcols_body(a.S, a.node_root, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem);
+    return;
+  }
+  b -= a.n_rootcols;
+  if (b < a.red_dense.blocks + a.red_sparse.blocks) {
+    reduce_dw2_body(a.dw2_part, a.S.F + H, a.dw2_td, a.dw2_bu, a.gate, a.red_dense, a.red_sparse, b, smem);
+    return;
+  }
+  colsum_job_block(a.db1, b - a.red_dense.blocks - a.red_sparse.blocks);
+}
+
 }  // namespace
+
+int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s) {
+  a.n_root = (a.S.mode != 1) ? 2 * a.S.max_items : 0;
+  const int n = a.n_dw2 + a.n_root + 2 * a.nblk_h + colsum_job_blocks(256);
+  if (x_dtype == BGCN_DTYPE_BF16)
+    hipLaunchKernelGGL(k_bwd_mid<bf16_t>, dim3(unsigned(n)), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_bwd_mid<float>, dim3(unsigned(n)), dim3(256), 0, s, a);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int bwd_tail_launch(BwdTailArgs& a, hipStream_t s) {
+  // one wave per column at Twitter-sized batches, four from 64k rows (longer columns);
+  // BGCN_DW1_SPLIT=1/4 forces either (read per call: tests compare both)
+  const char* e = std::getenv("BGCN_DW1_SPLIT");
+  const bool sparse = a.S.mode != 1;
+  const int split = e ? atoi(e) : (a.S.N >= 65536 ? 4 : 1);
+  a.n_dw1 = sparse ? int(split == 4 ? (a.S.F + 3) / 4 : (a.S.F + 15) / 16) : 0;
+  a.n_rootcols = sparse ? int((a.S.F + 15) / 16) : 0;
+  const int n = a.n_dw1 + a.n_rootcols + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(1024);
+  if (split == 4)
+    hipLaunchKernelGGL(k_bwd_tail<4>, dim3(unsigned(n)), dim3(1024), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_bwd_tail<1>, dim3(unsigned(n)), dim3(1024), 0, s, a);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
 
 // ---------------------------------------------------------------- host side
 size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
@@ -877,12 +954,6 @@ int sparse_conv2(SparseState& S, const float* H1, const int32_t* tree_ptr, const
   return BGCN_OK;
 }
 
-int sparse_dw2_root_part(SparseState& S, const int32_t* tree_ptr, const float* dZ2, hipStream_t s) {
-  hipLaunchKernelGGL(k_dw2_root_part, dim3(unsigned(S.max_items), 2), dim3(256), 0, s, S, dZ2,
-                     tree_ptr);
-  BGCN_CHECK_LAUNCH();
-  return BGCN_OK;
-}
 
 int sparse_csc(SparseState& S, hipStream_t s) {
   const int R = int((S.N + kRowBlock - 1) / kRowBlock);
@@ -899,7 +970,7 @@ int sparse_csc(SparseState& S, hipStream_t s) {
 
 int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
                    const int64_t* batch, const int64_t* rootindex, const void* X, int xdt, int64_t ldx,
-                   hipStream_t s) {
+                   hipStream_t s, int part) {
   SparseState S{};
   S.mode = mode;
   S.N = N; S.F = F; S.B = B;
@@ -908,6 +979,7 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
   S.item_tree = p.item_tree; S.item_chunk = p.item_chunk; S.tree_item0 = p.tree_item0;
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
   S.csc_slot = p.csc_slot; S.csc_val = p.csc_val;
+  if (!(part & 1)) return mode == 1 ? BGCN_OK : sparse_csc(S, s);
   const int nR = int((N + 255) / 256), nP = int((B + 1 + 255) / 256);
   hipLaunchKernelGGL(k_prologue, dim3(unsigned(nR + nP)), dim3(256), 0, s, S, nullptr, nullptr,
                      nullptr, nullptr, batch, rootindex, p.node_root, p.tree_ptr, 1, 0, nR);
@@ -928,7 +1000,7 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
                        static_cast<const float*>(X), ldx, nullptr);
   timing_end(7, s);
   BGCN_CHECK_LAUNCH();
-  return sparse_csc(S, s);
+  return (part & 2) ? sparse_csc(S, s) : BGCN_OK;
 }
 
 int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
@@ -937,32 +1009,6 @@ int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
   return BGCN_OK;
 }
 
-int sparse_dw1(SparseState& S, const bgcn_bigcn_args* a, const float* dZ1, hipStream_t s,
-               const ColsumJob& job) {
-  // one wave per column at Twitter-sized batches, four from 64k rows (longer columns);
-  // BGCN_DW1_SPLIT=1/4 forces either (read per call: tests compare both)
-  const char* e = std::getenv("BGCN_DW1_SPLIT");
-  const int split = e ? atoi(e) : (S.N >= 65536 ? 4 : 1);
-  const int nj = job.part ? colsum_job_blocks(1024) : 0;
-  if (split == 4) {
-    const int nb = int((S.F + 3) / 4);
-    hipLaunchKernelGGL(k_dw1_cols<4>, dim3(unsigned(nb + nj)), dim3(1024), 0, s, S, dZ1,
-                       a->td_dw1, a->bu_dw1, nb, job);
-  } else {
-    const int nb = int((S.F + 15) / 16);
-    hipLaunchKernelGGL(k_dw1_cols<1>, dim3(unsigned(nb + nj)), dim3(1024), 0, s, S, dZ1,
-                       a->td_dw1, a->bu_dw1, nb, job);
-  }
-  BGCN_CHECK_LAUNCH();
-  return BGCN_OK;
-}
 
-int sparse_dw2_rootcols(SparseState& S, const bgcn_bigcn_args* a, const int32_t* node_root,
-                        KeepSrc keep, hipStream_t s) {
-  hipLaunchKernelGGL(k_dw2_rootcols, dim3(unsigned((S.F + 15) / 16)), dim3(1024), 0, s, S, node_root,
-                     a->batch, a->td_dw2, a->bu_dw2, keep.scale());
-  BGCN_CHECK_LAUNCH();
-  return BGCN_OK;
-}
 
 }  // namespace bgcn

@@ -288,9 +288,13 @@ def synth_batch(rng: np.random.Generator, sizes: Sequence[int], vocab: int = VOC
         bu_rows.append(c_s[keep_bu] + offs[b]); bu_cols.append(p_s[keep_bu] + offs[b])
     nnz = np.minimum(1 + rng.poisson(11.0, size=N), vocab)
     rows = np.repeat(np.arange(N, dtype=np.int64), nnz)
-    # distinct ids per row: random ids, duplicates within a row collapse (set semantics)
+    # distinct ids per row: random ids, duplicates within a row collapse (set semantics);
+    # the first draw of a duplicated (row, id) is kept, on the host, so x does not depend
+    # on which duplicate a device scatter happens to write last
     cols = rng.integers(0, vocab, size=int(nnz.sum()), dtype=np.int64)
     vals = rng.integers(1, 4, size=int(nnz.sum())).astype(np.float32)
+    _, first = np.unique(rows * vocab + cols, return_index=True)
+    rows, cols, vals = rows[first], cols[first], vals[first]
     x = torch.zeros(N, vocab, dtype=dtype, device=device)
     x.index_put_((torch.as_tensor(rows, device=device), torch.as_tensor(cols, device=device)),
                  torch.as_tensor(vals, device=device).to(dtype))

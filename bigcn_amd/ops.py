@@ -50,7 +50,10 @@ class Graph:
 
     def check(self) -> None:
         """Host sync: raise IndexError if edge_index held an index outside [0, N)."""
-        if int(self.status.item()) != 0:
+        s = int(self.status.item())
+        if s & 8:
+            raise RuntimeError("libbgcn: an internal cross-workgroup hand-off timed out")
+        if s != 0:
             raise IndexError("edge_index contains an index out of range [0, num_nodes)")
 
 

@@ -211,3 +211,6 @@ class FusedTrainStep:
             raise ValueError(f"feat_mode 'sparse': a feature row holds more than "
                              f"{_lib.BGCN_SPARSE_CAP} non-zeros (the step's results are invalid); "
                              f"use 'auto' or 'dense'")
+        if s & 8:
+            raise RuntimeError("libbgcn: an internal cross-workgroup hand-off timed out "
+                               "(the step's results are invalid)")
