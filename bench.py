@@ -71,13 +71,13 @@ KERNEL_CLASSES = {
     "auto": {0: "conv1: k_compact_conv1 (X read + compaction + gather) or gather from prepared ELL",
              2: "conv2 (sparse root gather)", 3: "k_bwd_mid: dW2 partials + root partials + dH1",
              5: "k_bwd_tail: dW1 over CSC(X) + dW2 root columns + reductions",
-             7: "k_compact_conv1<false>: X read + BoW compaction (next-batch preparation)"},
+             7: "k_prep_b: X read + BoW compaction of the next batch (beside its DropEdge select + tree items)"},
 }
 SPARSE_CAP = 32
 # rocprofv3 kernel symbol of each timed class (for the PMC traffic lookup)
 ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2): "bgcn::k_conv2_sparse",
                  ("auto", 3): "bgcn::k_bwd_mid<float>", ("auto", 5): "bgcn::k_bwd_tail<1>",
-                 ("auto", 7): "bgcn::k_compact_conv1<false, float>",
+                 ("auto", 7): "bgcn::k_prep_b<float>",
                  ("dense", 0): "bgcn::k_gemm_xwt<true, false, float>", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
                  ("dense", 2): "bgcn::k_conv2_fwd<float>", ("dense", 3): "bgcn::k_dw2<float>"}
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")

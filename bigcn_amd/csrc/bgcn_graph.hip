@@ -294,12 +294,33 @@ size_t graph_ws_size(int64_t E, int64_t N) {
   return c.off + 256;
 }
 
-struct GraphArgs {
-  const int64_t* ei; const float* ew; int64_t E;
-  int32_t *t_ptr, *t_row, *t_col; float* t_w;
-  int32_t *s_ptr, *s_row, *s_col; float* s_w;
-  int32_t* status; void* ws; size_t ws_bytes;
-};
+int graph_batch_setup(const GraphArgs* ga, int count, int64_t N, int degree_on, GraphBatch* out,
+                      size_t zero_bytes[kMaxGraphs]) {
+  BGCN_CHECK_ARG(count >= 1 && count <= kMaxGraphs, "1 or 2 graphs per call");
+  BGCN_CHECK_ARG(N > 0 && N < (int64_t(1) << 31) - 1, "num_nodes out of range");
+  BGCN_CHECK_ARG(degree_on == BGCN_DEGREE_ON_COL || degree_on == BGCN_DEGREE_ON_ROW,
+                 "degree_on must be 0 (col) or 1 (row)");
+  GraphBatch gb{};
+  gb.N = N;
+  gb.degree_on = degree_on;
+  for (int k = 0; k < count; ++k) {
+    const GraphArgs& a = ga[k];
+    BGCN_CHECK_ARG(a.E >= 0 && a.E + N < (int64_t(1) << 31), "num_edges out of range");
+    BGCN_CHECK_ARG(a.t_ptr && a.t_row && a.t_col && a.t_w && a.s_ptr && a.s_row && a.s_col && a.s_w,
+                   "null output pointer");
+    BGCN_CHECK_ARG(a.E == 0 || a.ei, "null edge_index");
+    BGCN_CHECK_ARG(a.ws && a.ws_bytes >= graph_ws_size(a.E, N), "workspace too small");
+    Carve c(a.ws, a.ws_bytes);
+    GraphIO& G = gb.g[k];
+    graph_carve(c, a.E, N, &G, &zero_bytes[k]);
+    G.ei = a.ei; G.ew = a.ew; G.E = a.E;
+    G.t_ptr = a.t_ptr; G.t_row = a.t_row; G.t_col = a.t_col; G.t_w = a.t_w;
+    G.s_ptr = a.s_ptr; G.s_row = a.s_row; G.s_col = a.s_col; G.s_w = a.s_w;
+    G.status = a.status;
+  }
+  *out = gb;
+  return BGCN_OK;
+}
 
 int build_graphs_impl(const GraphArgs* ga, int count, int64_t N, int degree_on, hipStream_t s) {
   BGCN_CHECK_ARG(count >= 1 && count <= kMaxGraphs, "1 or 2 graphs per call");
@@ -402,6 +423,19 @@ extern "C" size_t bgcn_graph_pair_workspace_size(int64_t td_num_edges, int64_t b
   int64_t e = td_num_edges > bu_num_edges ? td_num_edges : bu_num_edges;
   return 2 * bgcn::align_up(bgcn::graph_ws_size(e, num_nodes), 256);
 }
+
+namespace bgcn {
+void graph_pair_args(const int64_t* td_ei, int64_t Etd, const int64_t* bu_ei, int64_t Ebu,
+                     const bgcn_csr_out* td, const bgcn_csr_out* bu, int32_t* status, void* workspace,
+                     size_t workspace_bytes, GraphArgs a[2]) {
+  const size_t half = workspace_bytes / 2 / 256 * 256;
+  char* ws = static_cast<char*>(workspace);
+  a[0] = GraphArgs{td_ei, nullptr, Etd, td->t_ptr, td->t_row, td->t_col, td->t_w, td->s_ptr,
+                   td->s_row, td->s_col, td->s_w, status, ws, half};
+  a[1] = GraphArgs{bu_ei, nullptr, Ebu, bu->t_ptr, bu->t_row, bu->t_col, bu->t_w, bu->s_ptr,
+                   bu->s_row, bu->s_col, bu->s_w, status, ws ? ws + half : nullptr, half};
+}
+}  // namespace bgcn
 
 extern "C" int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_num_edges,
                                      const int64_t* bu_edge_index, int64_t bu_num_edges,

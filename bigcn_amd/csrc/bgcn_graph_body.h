@@ -385,6 +385,20 @@ __host__ inline int graph_pos_blocks(int64_t E, int64_t N) {
 }
 
 size_t graph_ws_size(int64_t E, int64_t N);
+struct GraphArgs {
+  const int64_t* ei; const float* ew; int64_t E;
+  int32_t *t_ptr, *t_row, *t_col; float* t_w;
+  int32_t *s_ptr, *s_row, *s_col; float* s_w;
+  int32_t* status; void* ws; size_t ws_bytes;
+};
+// the GraphBatch of 1-2 graphs without launching anything; zero_bytes[k]: the prefix of
+// graph k's workspace (at gb.g[k].cnt_t) that must be zero before the count step
+int graph_batch_setup(const GraphArgs* ga, int count, int64_t N, int degree_on, GraphBatch* out,
+                      size_t zero_bytes[kMaxGraphs]);
+// GraphArgs of bgcn_build_graph_pair's layout (two workspace halves)
+void graph_pair_args(const int64_t* td_ei, int64_t Etd, const int64_t* bu_ei, int64_t Ebu,
+                     const bgcn_csr_out* td, const bgcn_csr_out* bu, int32_t* status, void* workspace,
+                     size_t workspace_bytes, GraphArgs a[2]);
 // carve a graph's workspace (bgcn_graph.hip); zero_bytes = the prefix that must be zero
 // before the count step
 size_t graph_carve(Carve& c, int64_t E, int64_t N, GraphIO* G, size_t* zero_bytes);

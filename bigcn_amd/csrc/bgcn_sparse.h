@@ -95,6 +95,10 @@ struct BwdTailArgs {
   ColsumJob db1;
 };
 int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s);
+// the whole weight-independent preparation of one batch on one stream (six launches;
+// mode 1 = dense: no ELL / CSC of X)
+int prep_pipeline(const Prepared& p, const bgcn_batch* b, int64_t F, int degree_on, int mode,
+                  hipStream_t s, bool x_part = true);
 int bwd_tail_launch(BwdTailArgs& a, hipStream_t s);
 
 }  // namespace bgcn

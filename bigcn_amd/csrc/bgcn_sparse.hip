@@ -21,6 +21,8 @@
 
 
 #include "bgcn_bwd.h"
+#include "bgcn_drop_body.h"
+#include "bgcn_graph_body.h"
 #include "bgcn_internal.h"
 #include "bgcn_sparse.h"
 
@@ -57,6 +59,33 @@ __device__ __forceinline__ void transpose_tile(const SparseState& S, int bx, int
   }
 }
 
+// Batch part of the prologue (block bid of blockDim threads): blocks [0, nR) the node ->
+// root map (block 0 also resets the overflow flags), then the tree pointers (binary
+// search in the sorted batch vector).
+__device__ inline void prologue_batch_body(const SparseState& S, const int64_t* __restrict__ batch,
+                                           const int64_t* __restrict__ rootindex,
+                                           int32_t* __restrict__ node_root, int32_t* __restrict__ tree_ptr,
+                                           int bid, int nR) {
+  if (bid == 0 && nR > 0 && S.mode != 1 && threadIdx.x < 8) S.flags[threadIdx.x] = 0;
+  if (bid < nR) {
+    const int64_t i = int64_t(bid) * blockDim.x + threadIdx.x;
+    if (i >= S.N) return;
+    const int64_t b = batch[i];
+    const int64_t bc = b < 0 ? 0 : (b >= S.B ? S.B - 1 : b);
+    const int64_t r = rootindex[bc];
+    node_root[i] = int32_t((b >= 0 && b < S.B && r >= 0 && r < S.N) ? r : 0);
+    return;
+  }
+  const int64_t b = int64_t(bid - nR) * blockDim.x + threadIdx.x;
+  if (b > S.B) return;
+  int64_t lo = 0, hi = S.N;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (batch[mid] < b) lo = mid + 1; else hi = mid;
+  }
+  tree_ptr[b] = int32_t(lo);
+}
+
 // Forward prologue, one launch: the weight transposes (sparse path), node -> root map,
 // tree pointers (binary search in the sorted batch vector) and the overflow-flag reset.
 // Block ranges: [0, nT) transposes, [nT, nT + nR) node_root, then tree_ptr.
@@ -76,24 +105,7 @@ __global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __
     transpose_tile(S, blk % nTx, (blk / nTx) % 2, blk / (2 * nTx), w1td, w1bu, w2td, w2bu);
     return;
   }
-  if (blk == nT && nR > 0 && S.mode != 1 && threadIdx.x < 8) S.flags[threadIdx.x] = 0;
-  if (blk < nT + nR) {
-    const int64_t i = int64_t(blk - nT) * 256 + threadIdx.x;
-    if (i >= S.N) return;
-    const int64_t b = batch[i];
-    const int64_t bc = b < 0 ? 0 : (b >= S.B ? S.B - 1 : b);
-    const int64_t r = rootindex[bc];
-    node_root[i] = int32_t((b >= 0 && b < S.B && r >= 0 && r < S.N) ? r : 0);
-    return;
-  }
-  const int64_t b = int64_t(blk - nT - nR) * 256 + threadIdx.x;
-  if (b > S.B) return;
-  int64_t lo = 0, hi = S.N;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (batch[mid] < b) lo = mid + 1; else hi = mid;
-  }
-  tree_ptr[b] = int32_t(lo);
+  prologue_batch_body(S, batch, rootindex, node_root, tree_ptr, blk - nT, nR);
 }
 
 // ---------------------------------------------------------------- X compaction + conv1
@@ -191,9 +203,10 @@ __device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, con
 // kConv1 = true: compaction + conv1 in one pass (the encoder's forward); false: the ELL
 // only (weight-independent batch preparation, bgcn_prepare_batch).  A wave keeps ~20 KB
 // of X in flight: one fp32 row, or two bf16 rows (their loads issued together).
+// Body: block bid of nblk 256-thread blocks (grid-stride over rows).
 template <bool kConv1, class TX>
-__global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* __restrict__ X,
-                                                       int64_t ldx, float* __restrict__ Z1) {
+__device__ inline void compact_body(const SparseState& S, const TX* __restrict__ X, int64_t ldx,
+                                    float* __restrict__ Z1, int bid, int nblk) {
   constexpr int kRows = sizeof(TX) == 2 ? 2 : 1;
   __shared__ int32_t s_col[4][kCap];
   __shared__ float s_val[4][kCap];
@@ -201,8 +214,8 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // grid-stride over rows (the preparation's grid covers every row once: one fp32 row or
   // two bf16 rows per wave; a capped grid strides)
-  const int64_t stride = int64_t(gridDim.x) * 4;
-  for (int64_t i0 = int64_t(blockIdx.x) * 4 + wave; i0 < S.N; i0 += stride * kRows) {
+  const int64_t stride = int64_t(nblk) * 4;
+  for (int64_t i0 = int64_t(bid) * 4 + wave; i0 < S.N; i0 += stride * kRows) {
     u32x4 r[kRows][row_chunks<TX>()];
 #pragma unroll
     for (int k = 0; k < kRows; ++k) {   // all loads in flight; a row past N reads nothing
@@ -219,6 +232,12 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* 
       if (i < S.N) compact_row<kConv1, TX>(S, i, r[k], s_col[wave], s_val[wave], Z1);
     }
   }
+}
+
+template <bool kConv1, class TX>
+__global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* __restrict__ X,
+                                                       int64_t ldx, float* __restrict__ Z1) {
+  compact_body<kConv1, TX>(S, X, ldx, Z1, int(blockIdx.x), int(gridDim.x));
 }
 
 // conv1 lin from a prepared ELL of X (bgcn_prepare_batch): four rows per wave, one per
@@ -406,18 +425,19 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
 // non-zeros s (the 2 relu(x) factor is applied in k_dw_cols).
 // one block: items per tree = ceil(n_b / kChunk), exclusive scan over trees (1024 at a
 // time with a carry), then every tree writes its item descriptors.
-__global__ __launch_bounds__(1024) void k_items(SparseState S, const int32_t* __restrict__ tree_ptr) {
-  if (!use_sparse(S)) return;
+__device__ inline void items_body(const SparseState& S, const int32_t* __restrict__ tree_ptr) {
+  if (S.mode == 1) return;   // (not the overflow flag: the pass over X may run beside this)
   __shared__ int sh[1024];
   __shared__ int carry;
+  const int nth = int(blockDim.x);
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
-  for (int64_t b0 = 0; b0 < S.B; b0 += 1024) {
+  for (int64_t b0 = 0; b0 < S.B; b0 += nth) {
     const int64_t b = b0 + threadIdx.x;
     const int chunks = b < S.B ? (tree_ptr[b + 1] - tree_ptr[b] + kChunk - 1) / kChunk : 0;
     sh[threadIdx.x] = chunks;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
+    for (int o = 1; o < nth; o <<= 1) {
       const int v = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
       __syncthreads();
       sh[threadIdx.x] += v;
@@ -432,10 +452,14 @@ __global__ __launch_bounds__(1024) void k_items(SparseState S, const int32_t* __
       }
     }
     __syncthreads();
-    if (threadIdx.x == 1023) carry += sh[1023];
+    if (threadIdx.x == nth - 1) carry += sh[nth - 1];
     __syncthreads();
   }
   if (threadIdx.x == 0) S.tree_item0[S.B] = carry < S.max_items ? carry : S.max_items;
+}
+
+__global__ __launch_bounds__(1024) void k_items(SparseState S, const int32_t* __restrict__ tree_ptr) {
+  items_body(S, tree_ptr);
 }
 
 // dW2 root-column partials per work item (<= kChunk nodes of one tree), on the MFMA:
@@ -505,11 +529,11 @@ __device__ inline void root_part_body(const SparseState& S, const float* __restr
 //                  32 at a time, rank inside the batch from per-column row bitmasks
 // No float atomics, no general sort; deterministic.  Every global load is issued
 // unconditionally (clamped index, select afterwards) so the loads of a thread overlap.
-__global__ __launch_bounds__(kRowBlock) void k_csc_hist(SparseState S) {
+// (bodies: kRowBlock threads; hsm / psm = the launch's dynamic shared memory)
+__device__ inline void csc_hist_body(const SparseState& S, int bid, int32_t* hsm) {   // hsm [F]
   if (!use_sparse(S)) return;
-  extern __shared__ __attribute__((aligned(16))) int32_t hsm[];   // [F]
   for (int64_t c = threadIdx.x; c < S.F; c += kRowBlock) hsm[c] = 0;
-  const int64_t i = int64_t(blockIdx.x) * kRowBlock + threadIdx.x;
+  const int64_t i = int64_t(bid) * kRowBlock + threadIdx.x;
   const int64_t ic = min<int64_t>(i, S.N - 1);
   const int n = i < S.N ? min(S.nnz[ic], kCap) : 0;
   int32_t cl[kCap];
@@ -523,18 +547,22 @@ __global__ __launch_bounds__(kRowBlock) void k_csc_hist(SparseState S) {
   for (int s = 0; s < kCap; ++s)
     if (s < n) atomicAdd(&hsm[cl[s]], 1);
   __syncthreads();
-  int32_t* out = S.hist + int64_t(blockIdx.x) * S.F;
+  int32_t* out = S.hist + int64_t(bid) * S.F;
   for (int64_t c = threadIdx.x; c < S.F; c += kRowBlock) out[c] = hsm[c];
+}
+__global__ __launch_bounds__(kRowBlock) void k_csc_hist(SparseState S) {
+  extern __shared__ __attribute__((aligned(16))) int32_t hsm[];
+  csc_hist_body(S, int(blockIdx.x), hsm);
 }
 
 // 64 columns x 4 row-block quarters per block; hist[r][c] becomes the exclusive prefix
 // of column c over row blocks < r.  Loads in groups of 8 (independent).
-__global__ __launch_bounds__(256) void k_csc_prefix(SparseState S, int R) {
+__device__ inline void csc_prefix_body(const SparseState& S, int R, int bid) {
   if (!use_sparse(S)) return;
   __shared__ int32_t part[4][64];
   const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int64_t c = min<int64_t>(int64_t(blockIdx.x) * 64 + cl, S.F - 1);
-  const bool live = int64_t(blockIdx.x) * 64 + cl < S.F;
+  const int64_t c = min<int64_t>(int64_t(bid) * 64 + cl, S.F - 1);
+  const bool live = int64_t(bid) * 64 + cl < S.F;
   const int rq = (R + 3) / 4, rb = q * rq, re = min(R, rb + rq);
   int32_t sum = 0;
   for (int r0 = rb; r0 < re; r0 += 8) {
@@ -560,16 +588,21 @@ __global__ __launch_bounds__(256) void k_csc_prefix(SparseState S, int R) {
   }
   if (live && q == 3) S.col_total[c] = run;
 }
+__global__ __launch_bounds__(256) void k_csc_prefix(SparseState S, int R) {
+  csc_prefix_body(S, R, int(blockIdx.x));
+}
 
 // column starts: exclusive scan of col_total, one 1024-thread block (thread = run of
 // consecutive columns, block scan of the run sums)
-__global__ __launch_bounds__(1024) void k_csc_colscan(SparseState S) {
+// (body: any block size >= 256)
+__device__ inline void csc_colscan_body(const SparseState& S) {
   if (!use_sparse(S)) return;
   __shared__ int32_t wsum[1024];
   const int64_t F = S.F;
-  const int64_t per = (F + 1023) / 1024;
+  const int nth = int(blockDim.x);
+  const int64_t per = (F + nth - 1) / nth;
   const int64_t c0 = threadIdx.x * per;
-  constexpr int kMaxPer = kSparseMaxF / 1024;
+  constexpr int kMaxPer = kSparseMaxF / 256;
   int32_t v[kMaxPer];
   int32_t local = 0;
 #pragma unroll
@@ -580,7 +613,7 @@ __global__ __launch_bounds__(1024) void k_csc_colscan(SparseState S) {
   }
   wsum[threadIdx.x] = local;
   __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
+  for (int o = 1; o < nth; o <<= 1) {
     const int32_t t = threadIdx.x >= o ? wsum[threadIdx.x - o] : 0;
     __syncthreads();
     wsum[threadIdx.x] += t;
@@ -598,13 +631,14 @@ __global__ __launch_bounds__(1024) void k_csc_colscan(SparseState S) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
-  if (!use_sparse(S)) return;
-  extern __shared__ __attribute__((aligned(16))) int32_t psm[];   // [F] counters, [F] row masks
+__global__ __launch_bounds__(1024) void k_csc_colscan(SparseState S) { csc_colscan_body(S); }
+
+__device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* psm) {
+  if (!use_sparse(S)) return;   // psm: [F] counters, [F] row masks
   int32_t* cnt = psm;
   uint32_t* rows = reinterpret_cast<uint32_t*>(psm + S.F);
   const int64_t F = S.F;
-  const int32_t* pre = S.hist + int64_t(blockIdx.x) * F;
+  const int32_t* pre = S.hist + int64_t(bid) * F;
   for (int64_t c0 = threadIdx.x; c0 < F; c0 += 4 * 256) {
     int32_t st[4], pr[4];
 #pragma unroll
@@ -624,7 +658,7 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
   }
   // all of the block's entries up front: thread t holds entries t + 256k (k < 32) of
   // the row block = slot t % 32 of rows (t / 32) + 8k
-  const int64_t r0 = int64_t(blockIdx.x) * kRowBlock;
+  const int64_t r0 = int64_t(bid) * kRowBlock;
   const int s = threadIdx.x % kCap;
   constexpr int kPer = kRowBlock * kCap / 256;   // 32
   int32_t col[kPer], nn[kPer];
@@ -678,6 +712,10 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
     }
     __syncthreads();
   }
+}
+__global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
+  extern __shared__ __attribute__((aligned(16))) int32_t psm[];
+  csc_place_body(S, int(blockIdx.x), psm);
 }
 
 // dW1 = [dZ1_td | dZ1_bu]^T X over the CSC of X: four waves per column (four columns per
@@ -797,6 +835,112 @@ __device__ inline void rootcols_body(const SparseState& S, const int32_t* __rest
     dw2_td[int64_t(ty) * K2 + H + cc] = t2[0][ty][tx];
     dw2_bu[int64_t(ty) * K2 + H + cc] = t2[1][ty][tx];
   }
+}
+
+// ---------------------------------------------------------------- batch preparation
+// The fused step's weight-independent preparation of one batch (bgcn_prepare_batch /
+// the next batch on the side lane) as six launches of 256-thread blocks, each carrying
+// the independent steps of three chains side by side (a lone launch on a lane costs
+// ~5 us however little it does):
+//   A  zero the K1 counters | node -> root map, tree pointers, flag reset | DropEdge bounds
+//   B  DropEdge select | tree work items | the pass over X (ELL compaction)
+//   C  K1 count | CSC column histograms
+//   D  K1 scan (decoupled look-back) | CSC per-column prefixes
+//   E  K1 fill + self loops + D^-1/2 | CSC column starts
+//   F  K1 normalisation + plans | CSC placement
+struct PrepArgs {
+  SparseState S;
+  GraphBatch gb;
+  DropList dl[2];
+  const int64_t *batch, *rootindex;
+  int32_t *node_root, *tree_ptr, *status;
+  const void* X;
+  int64_t ldx;
+  int64_t* eptr;
+  uint64_t seed;
+  uint4* zero[2];
+  int nzero[2];         // 16-byte words per zero range
+  int nz, nRP, nR, nbd[2], lists;
+  int nsel, ncomp;
+  int nce, R;
+  int ntile, nprefix;
+  int ne, nn, np;
+};
+
+__global__ __launch_bounds__(256) void k_prep_a(PrepArgs a) {
+  int b = int(blockIdx.x);
+  if (b < a.nz) {   // 16 B per thread, 4 KB per block
+    const int64_t w = int64_t(b) * 256 + threadIdx.x;
+    const int64_t w0 = a.nzero[0];
+    if (w < w0) a.zero[0][w] = make_uint4(0u, 0u, 0u, 0u);
+    else if (w - w0 < a.nzero[1]) a.zero[1][w - w0] = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
+  b -= a.nz;
+  if (b < a.nRP) {
+    prologue_batch_body(a.S, a.batch, a.rootindex, a.node_root, a.tree_ptr, b, a.nR);
+    return;
+  }
+  b -= a.nRP;
+  const int d = b < a.nbd[0] ? 0 : 1;
+  drop_bounds_body(a.dl[d], d, a.batch, a.S.N, a.S.B, a.eptr, a.status, d == 0 ? b : b - a.nbd[0]);
+}
+
+template <class TX>
+__global__ __launch_bounds__(256) void k_prep_b(PrepArgs a) {
+  int b = int(blockIdx.x);
+  if (b < a.nsel) {   // (tree, list) blocks first: they finish beside the pass over X
+    const int d = b / int(a.S.B);
+    drop_select_body(a.dl[d], d, int64_t(b % int(a.S.B)), a.batch, a.S.N, a.S.B, a.seed, a.eptr, 1,
+                     nullptr, a.status);
+    return;
+  }
+  b -= a.nsel;
+  if (b == 0) {
+    items_body(a.S, a.tree_ptr);
+    return;
+  }
+  compact_body<false, TX>(a.S, static_cast<const TX*>(a.X), a.ldx, nullptr, b - 1, a.ncomp);
+}
+
+__global__ __launch_bounds__(256) void k_prep_c(PrepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int32_t dsm[];
+  int b = int(blockIdx.x);
+  if (b < 2 * a.nce) {
+    graph_count_body(a.gb, a.gb.g[b / a.nce], b % a.nce);
+    return;
+  }
+  csc_hist_body(a.S, b - 2 * a.nce, dsm);
+}
+
+__global__ __launch_bounds__(256) void k_prep_d(PrepArgs a) {
+  int b = int(blockIdx.x);
+  if (b < 2 * a.ntile) {
+    graph_scan_body(a.gb, a.gb.g[b / a.ntile]);
+    return;
+  }
+  csc_prefix_body(a.S, a.R, b - 2 * a.ntile);
+}
+
+__global__ __launch_bounds__(256) void k_prep_e(PrepArgs a) {
+  int b = int(blockIdx.x);
+  const int per = a.ne + a.nn;
+  if (b < 2 * per) {
+    graph_fill_nodes_body(a.gb, a.gb.g[b / per], b % per, a.ne);
+    return;
+  }
+  csc_colscan_body(a.S);
+}
+
+__global__ __launch_bounds__(256) void k_prep_f(PrepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int32_t dsm[];
+  int b = int(blockIdx.x);
+  const int per = a.ne + a.nn + a.np;
+  if (b < 2 * per) {
+    graph_rank_norm_body(a.gb, a.gb.g[b / per], b % per, a.ne, a.nn);
+    return;
+  }
+  csc_place_body(a.S, b - 2 * per, dsm);
 }
 
 // ---------------------------------------------------------------- merged backward launches
@@ -964,6 +1108,88 @@ int sparse_csc(SparseState& S, hipStream_t s) {
   hipLaunchKernelGGL(k_csc_colscan, dim3(1), dim3(1024), 0, s, S);
   BGCN_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_csc_place, dim3(unsigned(R)), dim3(256), size_t(2 * S.F) * sizeof(int32_t), s, S);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree_on, int mode,
+                  hipStream_t s, bool x_part) {
+  const int64_t N = bt->num_nodes, B = bt->num_graphs;
+  BGCN_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int32_t), s));
+  PrepArgs a{};
+  SparseState& S = a.S;
+  S.mode = mode;
+  S.N = N; S.F = F; S.B = B;
+  S.max_items = int(N / kChunk + B + 1);
+  S.flags = p.x_flags; S.nnz = p.x_nnz; S.cols = p.x_cols; S.vals = p.x_vals;
+  S.item_tree = p.item_tree; S.item_chunk = p.item_chunk; S.tree_item0 = p.tree_item0;
+  S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
+  S.csc_slot = p.csc_slot; S.csc_val = p.csc_val;
+  a.batch = bt->batch; a.rootindex = bt->rootindex;
+  a.node_root = p.node_root; a.tree_ptr = p.tree_ptr; a.status = p.status;
+  a.X = bt->x; a.ldx = bt->ldx;
+  // DropEdge (dataset.py:68-90) in the masked form: dropped edges become self loops, which
+  // K1 removes - the graphs of the compacted lists, no kept count on the host
+  const int64_t Etd = bt->td_num_edges, Ebu = bt->bu_num_edges;
+  const bool drop = bt->td_droprate > 0.0 || bt->bu_droprate > 0.0;
+  const int64_t* td = bt->td_edge_index;
+  const int64_t* bu = bt->bu_edge_index;
+  a.lists = drop ? 2 : 0;
+  if (drop) {
+    BGCN_CHECK_ARG(p.dws && p.dws_bytes >= drop_ws_size(B), "drop workspace too small");
+    Carve c(p.dws, p.dws_bytes);
+    a.eptr = c.take<int64_t>(size_t(2 * (B + 1)));
+    a.dl[0] = DropList{td, Etd, p.td_drop, Etd, bt->td_droprate, 0u};
+    a.dl[1] = DropList{bu, Ebu, p.bu_drop, Ebu, bt->bu_droprate, 1u};
+    a.seed = bt->drop_seed;
+    if (td) td = p.td_drop;
+    if (bu) bu = p.bu_drop;
+  }
+  GraphArgs ga[2];
+  graph_pair_args(td, Etd, bu, Ebu, &p.td, &p.bu, p.status, p.gws, p.gws_bytes, ga);
+  size_t zb[2] = {0, 0};
+  BGCN_TRY(graph_batch_setup(ga, 2, N, degree_on, &a.gb, zb));
+  for (int k = 0; k < 2; ++k) {
+    a.zero[k] = reinterpret_cast<uint4*>(a.gb.g[k].cnt_t);
+    a.nzero[k] = int(zb[k] / 16);
+    BGCN_CHECK_ARG(zb[k] % 16 == 0 && (reinterpret_cast<uintptr_t>(a.zero[k]) & 15) == 0, "zero range");
+  }
+  const bool sparse = mode != 1;
+  const bool xp = sparse && x_part;   // the pass over X and the CSC of X in these launches
+  const int64_t Emax = std::max(Etd, Ebu);
+  a.nz = int((a.nzero[0] + a.nzero[1] + 255) / 256);
+  a.nR = int((N + 255) / 256);
+  a.nRP = a.nR + int((B + 1 + 255) / 256);
+  a.nbd[0] = drop ? int(Etd / 256 + 1) : 0;
+  a.nbd[1] = drop ? int(Ebu / 256 + 1) : 0;
+  a.nsel = drop ? int(2 * B) : 0;
+  a.ncomp = xp ? int(grid_for(N, bt->x_dtype == BGCN_DTYPE_BF16 ? 8 : 4)) : 0;
+  a.nce = graph_edge_blocks(Emax);
+  a.R = xp ? int((N + kRowBlock - 1) / kRowBlock) : 0;
+  a.ntile = int(graph_scan_tiles(N));
+  a.nprefix = xp ? int(grid_for(F, 64)) : 0;
+  a.ne = graph_edge_blocks(Emax);
+  a.nn = graph_node_blocks(N);
+  a.np = graph_pos_blocks(Emax, N);
+  const dim3 blk(256);
+  hipLaunchKernelGGL(k_prep_a, dim3(unsigned(a.nz + a.nRP + a.nbd[0] + a.nbd[1])), blk, 0, s, a);
+  BGCN_CHECK_LAUNCH();
+  timing_begin(7, s);
+  const unsigned nb = unsigned(a.nsel + 1 + a.ncomp);
+  if (bt->x_dtype == BGCN_DTYPE_BF16) hipLaunchKernelGGL(k_prep_b<bf16_t>, dim3(nb), blk, 0, s, a);
+  else hipLaunchKernelGGL(k_prep_b<float>, dim3(nb), blk, 0, s, a);
+  BGCN_CHECK_LAUNCH();
+  timing_end(7, s);
+  const size_t hist_smem = xp ? size_t(F) * sizeof(int32_t) : 0;
+  if (2 * a.nce + a.R > 0) {
+    hipLaunchKernelGGL(k_prep_c, dim3(unsigned(2 * a.nce + a.R)), blk, hist_smem, s, a);
+    BGCN_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(k_prep_d, dim3(unsigned(2 * a.ntile + a.nprefix)), blk, 0, s, a);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_prep_e, dim3(unsigned(2 * (a.ne + a.nn) + (xp ? 1 : 0))), blk, 0, s, a);
+  BGCN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_prep_f, dim3(unsigned(2 * (a.ne + a.nn + a.np) + a.R)), blk, 2 * hist_smem, s, a);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }

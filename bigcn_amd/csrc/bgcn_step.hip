@@ -126,14 +126,20 @@ static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_
   Prepared p;
   Carve c(buf, bytes);
   carve_prepared(c, N, B, F, b->td_num_edges, b->bu_num_edges, &p);
-  BGCN_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int32_t), gs));
   const int mode = (feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxFeat) ? 1 : 0;
-  // on one lane (s == gs) the pass over X goes first - beside the forward, whose gathers
-  // are L2-served, it costs the chain less than beside the backward (measured 0.322 vs
-  // 0.329 ms per step) - then DropEdge and K1, then the CSC of X.  BGCN_PREP_ORDER=0
-  // (read per call) restores the graph-first order for A/B runs.
-  const char* oe = std::getenv("BGCN_PREP_ORDER");
-  const bool x_first = !(oe && atoi(oe) == 0) && s == gs;
+  // one stream: the six merged launches (DropEdge, K1, the pass over X and the CSC of X
+  // side by side, bgcn_sparse.hip prep_pipeline).  BGCN_PREP_MERGED=0 (read per call)
+  // selects the separate launches for A/B runs: the pass over X first (beside the
+  // forward, whose gathers are L2-served, it costs the chain less than beside the
+  // backward: 0.322 vs 0.329 ms per step), then DropEdge and K1, then the CSC.
+  const char* me = std::getenv("BGCN_PREP_MERGED");
+  if (s == gs && !(me && atoi(me) == 0)) {
+    BGCN_TRY(prep_pipeline(p, b, F, degree_on, mode, s));
+    if (out) *out = p;
+    return BGCN_OK;
+  }
+  BGCN_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int32_t), gs));
+  const bool x_first = s == gs;
   if (x_first)
     BGCN_TRY(sparse_prepare(p, N, B, F, mode, b->batch, b->rootindex, b->x, b->x_dtype, b->ldx, s, 1));
   const int64_t* td = b->td_edge_index;
@@ -187,6 +193,7 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
   Prepared p;
   int graph_lane = -1;
+
   timing_begin(10, s);   // span classes: 8 next-batch preparation, 9 main chain, 10 step
   timing_begin(9, s);
   if (!a->prepared_ready) {
