@@ -51,7 +51,22 @@ AuxState* aux_state(int lane) {
     for (int k = 0; k < kAuxLanes; ++k) {
       if (a.stream[k]) continue;
       hipStream_t st;
-      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+      // BGCN_SIDE_CU_EVERY=k (A/B knob, read at lane creation): the lane may not use CU i
+      // when i % k == k - 1, leaving those CUs to the caller's chain
+      const char* ce = std::getenv("BGCN_SIDE_CU_EVERY");
+      const int every = ce ? atoi(ce) : 0;
+      if (every > 1) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return nullptr;
+        const int ncu = prop.multiProcessorCount;
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i)
+          if (i % every != every - 1) mask[i / 32] |= 1u << (i % 32);
+        if (hipExtStreamCreateWithCUMask(&st, uint32_t(mask.size()), mask.data()) != hipSuccess)
+          return nullptr;
+      } else if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        return nullptr;
+      }
       // fork / join events only order two streams of the same device: a device-scope
       // release suffices (what a kernel boundary on one stream gives).  The default
       // system-scope fence writes back and invalidates every XCD's L2 at each record

@@ -115,10 +115,6 @@ __global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __
 // all zero across the wave (the common case for bag-of-words rows) costs one ballot -
 // and Z1[i] = sum val * W1T[col] with each lane owning 2 of the 128 outputs.
 constexpr int kRowChunks = 20;  // float4 per lane per pass (F <= 5120 in one pass)
-// side-lane compaction grid: one block per 4 rows (8 bf16 rows), i.e. short-lived waves
-// handed out in address order - measured 111 vs 128 us beside the training chain for a
-// persistent 256-block grid, same step time (BGCN_PREP_BLOCKS caps it for A/B runs)
-constexpr unsigned kPrepBlocks = 0xffffffffu;
 
 // Z1[i] += sum_s val_s * W1T[col_s] for the (col, val) pairs of lane-held lists: lane s
 // (< cnt) holds pair s; the pairs reach the wave by scalar readlane, gathers unconditional
@@ -1163,7 +1159,28 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   a.nbd[0] = drop ? int(Etd / 256 + 1) : 0;
   a.nbd[1] = drop ? int(Ebu / 256 + 1) : 0;
   a.nsel = drop ? int(2 * B) : 0;
-  a.ncomp = xp ? int(grid_for(N, bt->x_dtype == BGCN_DTYPE_BF16 ? 8 : 4)) : 0;
+  {   // The pass over X is paced: with fp32 X one 4-wave block per CU strides over the
+      // rows (~20 MB of loads in flight, ~4 TB/s).  A wave per row over all rows drains X
+      // at 5.5 TB/s but floods the memory queues with ~100 MB of requests, and every load
+      // of the latency-bound training chain beside it then waits behind them: measured
+      // 0.293-0.295 ms per step paced vs 0.303-0.306 unpaced (twitter15; 224-288 blocks
+      // within 1%, 512 worse than either).  bf16 X (twice the rows per byte) keeps the
+      // full grid: paced it lengthens the side lane (synth1024_bf16 0.90 vs 0.87 ms).
+      // BGCN_PREP_BLOCKS (read per call) overrides: 0 = full grid, n = n blocks.
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+      return n > 0 ? n : 256;
+    }();
+    const bool bf = bt->x_dtype == BGCN_DTYPE_BF16;
+    a.ncomp = xp ? int(grid_for(N, bf ? 8 : 4)) : 0;
+    int cap = bf ? 0 : ncu;
+    const char* e = std::getenv("BGCN_PREP_BLOCKS");
+    if (e) cap = atoi(e);
+    if (cap > 0) a.ncomp = std::min(a.ncomp, cap);
+  }
   a.nce = graph_edge_blocks(Emax);
   a.R = xp ? int((N + kRowBlock - 1) / kRowBlock) : 0;
   a.ntile = int(graph_scan_tiles(N));
@@ -1212,12 +1229,8 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
   BGCN_CHECK_LAUNCH();
   if (mode == 1) return BGCN_OK;
   BGCN_TRY(sparse_items(S, p.tree_ptr, s));
-  static const unsigned prep_blocks = [] {
-    const char* e = std::getenv("BGCN_PREP_BLOCKS");   // A/B knob for the side-lane grid
-    return e ? unsigned(std::max(1, atoi(e))) : kPrepBlocks;
-  }();
   timing_begin(7, s);
-  const dim3 grid(std::min<unsigned>(grid_for(N, xdt == BGCN_DTYPE_BF16 ? 8 : 4), prep_blocks));
+  const dim3 grid(grid_for(N, xdt == BGCN_DTYPE_BF16 ? 8 : 4));
   if (xdt == BGCN_DTYPE_BF16)
     hipLaunchKernelGGL((k_compact_conv1<false, bf16_t>), grid, dim3(256), 0, s, S,
                        static_cast<const bf16_t*>(X), ldx, nullptr);
