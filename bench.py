@@ -71,7 +71,8 @@ KERNEL_CLASSES = {
     "auto": {0: "conv1: k_compact_conv1 (X read + compaction + gather) or gather from prepared ELL",
              2: "conv2 (sparse root gather)", 3: "k_bwd_mid: dW2 partials + root partials + dH1",
              5: "k_bwd_tail: dW1 over CSC(X) + dW2 root columns + reductions",
-             7: "k_prep_b: X read + BoW compaction of the next batch (beside its DropEdge select + tree items)"},
+             7: "k_prep_b: paced X read + BoW compaction of the next batch beside the training chain "
+                "(+ its DropEdge select, tree items)"},
 }
 SPARSE_CAP = 32
 # rocprofv3 kernel symbol of each timed class (for the PMC traffic lookup)
@@ -203,6 +204,53 @@ def aggregation_bench(b, iters: int = 10):
         res[name] = {"avg_ms": round(ms, 4), "bytes": nbytes, "achieved": round(gbs, 1),
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4)}
     return {"kernel": "bgcn_spmm F=5000 (A_hat . X), one pool batch", "N": N, "F": Fd, **res}
+
+
+def compaction_standalone(fused, b, wl, iters: int = 10):
+    """The preparation's pass over X (k_prep_b, timing class 7) alone on the GPU, paced
+    (the step's grid) and unpaced (a wave per row over all rows, BGCN_PREP_BLOCKS=0): the
+    kernel's capability next to the in-step (paced, beside the chain) figure of `roofline`."""
+    import ctypes
+    from bigcn_amd import _lib, ops
+    from bigcn_amd._lib import ptr, stream_handle
+    L = _lib.lib()
+    F = int(b.x.size(1))
+    d, keep = fused._desc(b)
+    buf = fused._prep_buffer(d, F)
+    mode = _lib.BGCN_FEAT_SPARSE
+    N = int(b.x.size(0))
+    xbytes = 2 if wl.get("xdtype") == "bf16" else 4
+    nbytes = N * F * xbytes + N * (SPARSE_CAP * 8.0 + 4.0)
+    out = {"kernel": "k_prep_b (X read + BoW compaction + DropEdge select + tree items), alone on the GPU",
+           "bytes_per_launch": nbytes}
+    old = os.environ.get("BGCN_PREP_BLOCKS")
+    try:
+        for name, env in (("paced", old), ("unpaced", "0")):
+            if env is None:
+                os.environ.pop("BGCN_PREP_BLOCKS", None)
+            else:
+                os.environ["BGCN_PREP_BLOCKS"] = env
+            for _ in range(2):
+                _lib.check(L.bgcn_prepare_batch(ctypes.byref(d), F, fused.degree_on, mode, ptr(buf),
+                                                buf.numel(), stream_handle()))
+            torch.cuda.synchronize()
+            ops.set_kernel_timing(True, [7])
+            for _ in range(iters):
+                _lib.check(L.bgcn_prepare_batch(ctypes.byref(d), F, fused.degree_on, mode, ptr(buf),
+                                                buf.numel(), stream_handle()))
+            torch.cuda.synchronize()
+            ops.set_kernel_timing(False)
+            ms, n = ops.kernel_timing(7)
+            avg = ms / max(n, 1)
+            gbs = nbytes / (avg * 1e-3) / 1e9
+            out[name] = {"avg_ms": round(avg, 4), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4)}
+    finally:
+        if old is None:
+            os.environ.pop("BGCN_PREP_BLOCKS", None)
+        else:
+            os.environ["BGCN_PREP_BLOCKS"] = old
+    return out
 
 
 def main():
@@ -390,6 +438,10 @@ def main():
     agg = None
     if world == 1 and args.aggregation:
         agg = aggregation_bench(pool[0])
+    comp = None
+    if world == 1 and args.path == "fused" and args.feat_mode == "auto":
+        with torch.cuda.stream(stream):
+            comp = compaction_standalone(fused, pool[0], wl)
     if rank == 0:
         value, dt, N_avg = main_res["value"], main_res["dt"], main_res["N_avg"]
         roof, kernels, final_loss = main_res["roof"], main_res["kernels"], main_res["loss"]
@@ -413,6 +465,8 @@ def main():
         }
         if agg is not None:
             out["aggregation_5000"] = agg
+        if comp is not None:
+            out["compaction_standalone"] = comp
         if drop_res is not None:
             out["dropedge_" + drop_res["where"]] = {
                 "value": round(drop_res["value"], 2), "unit": "trees/s",
