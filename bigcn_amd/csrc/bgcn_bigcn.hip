@@ -620,7 +620,10 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     BGCN_TRY(gemm_tn_x(w.dz1, 2 * H, a->x, a->x_dtype, a->ldx, a->td_dw1, a->bu_dw1, F, H, 2 * H, F,
                        N, w.tn_ws, w.tn_bytes, sparse ? x : s, sparse ? 6 : 1, gate));
   }
-  if (sparse && !have_csc) BGCN_TRY(aux_join(s, kLaneSide));   // CSC built on the side
+  if (sparse && !have_csc) {   // CSC built on the side (the join covers every branch so far)
+    BGCN_TRY(aux_join(s, kLaneSide));
+    forked = false;
+  }
 
   // ---- tail launch: dW1 over the CSC of X (sparse), the dW2 root columns, the dW2
   // partial reductions and the db1 column sums
@@ -638,9 +641,10 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   BGCN_TRY(bwd_tail_launch(t, s));
   timing_end(5, s);
   (void)side_busy;
-  (void)forked;
   timing_end(9, s);   // the main stream's own chain (span class, bgcn_train_step)
-  BGCN_TRY(aux_join(s, kLaneSide));
+  // join only what this backward forked (a next-batch preparation on the side lane is
+  // waited for by the next bgcn_train_step call instead)
+  if (forked) BGCN_TRY(aux_join(s, kLaneSide));
   return BGCN_OK;
 }
 

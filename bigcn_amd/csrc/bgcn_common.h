@@ -66,6 +66,11 @@ constexpr int kAuxLanes = 1;
 constexpr int kLaneSide = 0;
 int aux_fork(hipStream_t main, int lane, hipStream_t* branch);
 int aux_join(hipStream_t main, int lane);
+// the next-batch preparation of bgcn_train_step is not joined by its own call: its end is
+// recorded (aux_prep_done) and the caller's stream waits for it at the start of the next
+// call (aux_prep_wait) - no join at the end of a step
+int aux_prep_done(hipStream_t main);
+int aux_prep_wait(hipStream_t main);
 
 // kernel timing hook (bench.py): record HIP events around a launch of a class
 void timing_begin(int cls, hipStream_t s);

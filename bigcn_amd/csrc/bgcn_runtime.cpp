@@ -37,6 +37,8 @@ constexpr int kMaxDevices = 64;
 struct AuxState {
   hipStream_t stream[kAuxLanes] = {};
   hipEvent_t fork[kAuxLanes] = {}, join[kAuxLanes] = {};
+  hipEvent_t prep = nullptr;   // end of the side lane's last next-batch preparation
+  bool prep_pending = false;   // recorded, not yet waited for by a caller's stream
 };
 AuxState g_aux[kMaxDevices];
 std::mutex g_aux_mu;
@@ -75,6 +77,7 @@ AuxState* aux_state(int lane) {
       if (hipEventCreateWithFlags(&a.fork[k], kFlags) != hipSuccess ||
           hipEventCreateWithFlags(&a.join[k], kFlags) != hipSuccess)
         return nullptr;
+      if (!a.prep && hipEventCreateWithFlags(&a.prep, kFlags) != hipSuccess) return nullptr;
       a.stream[k] = st;
     }
   }
@@ -149,12 +152,38 @@ int aux_join(hipStream_t main, int lane) {
   if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
   BGCN_CHECK_HIP(hipEventRecord(a->join[lane], a->stream[lane]));
   BGCN_CHECK_HIP(hipStreamWaitEvent(main, a->join[lane], 0));
+  if (lane == kLaneSide) a->prep_pending = false;   // everything queued there is covered
+  return BGCN_OK;
+}
+
+int aux_prep_done(hipStream_t main) {
+  if (!main || serial_branches()) return BGCN_OK;
+  std::lock_guard<std::mutex> lk(g_aux_mu);
+  AuxState* a = aux_state(kLaneSide);
+  if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
+  BGCN_CHECK_HIP(hipEventRecord(a->prep, a->stream[kLaneSide]));
+  a->prep_pending = true;
+  return BGCN_OK;
+}
+
+int aux_prep_wait(hipStream_t main) {
+  if (!main || serial_branches()) return BGCN_OK;
+  std::lock_guard<std::mutex> lk(g_aux_mu);
+  AuxState* a = aux_state(kLaneSide);
+  if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
+  if (!a->prep_pending) return BGCN_OK;
+  BGCN_CHECK_HIP(hipStreamWaitEvent(main, a->prep, 0));
+  a->prep_pending = false;
   return BGCN_OK;
 }
 
 }  // namespace bgcn
 
 extern "C" int bgcn_abi_version(void) { return BGCN_ABI_VERSION; }
+
+extern "C" int bgcn_join_side(bgcn_stream_t stream) {
+  return bgcn::aux_join(reinterpret_cast<hipStream_t>(stream), bgcn::kLaneSide);
+}
 
 extern "C" const char* bgcn_last_error(void) { return bgcn::g_err.c_str(); }
 

@@ -193,6 +193,9 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
   Prepared p;
   int graph_lane = -1;
+  // the previous call's next-batch preparation (this call's batch) must be complete
+  // before this stream uses it
+  BGCN_TRY(aux_prep_wait(s));
 
   timing_begin(10, s);   // span classes: 8 next-batch preparation, 9 main chain, 10 step
   timing_begin(9, s);
@@ -219,6 +222,10 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
     BGCN_TRY(prepare_into(a->next, F, a->degree_on, a->feat_mode, a->next_prepared,
                           a->next_prepared_bytes, x, nullptr, x));
     timing_end(8, x);
+    // waited for by the next call, not joined by this one: the step's chain ends without a
+    // cross-stream wait (chain alone 197 -> 190 us; beside a preparation the join was
+    // free, the side lane ends first)
+    BGCN_TRY(aux_prep_done(s));
   }
   BGCN_TRY(train_step_body(a, p, w, s, graph_lane));
   timing_end(10, s);

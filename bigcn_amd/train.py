@@ -98,6 +98,7 @@ class FusedTrainStep:
         self._args = a
         self.status = torch.zeros(1, dtype=torch.int32, device=model.fc.weight.device)
         self._pending = None       # (batch, prepared buffer, feat_mode, tensors) from next_data
+        self._stream = None
         self._next_desc = None
 
     def grads(self):
@@ -152,6 +153,8 @@ class FusedTrainStep:
             prep, keep, d = pend[1], pend[3], pend[4]
             ready = 1
         else:
+            if pend is not None:   # a preparation no step consumes: order its end before
+                self._join_side()   # its buffer returns to the allocator
             d, keep = self._desc(data)
             prep = self._prep_buffer(d, F)
             ready = 0
@@ -185,7 +188,8 @@ class FusedTrainStep:
                                                         d.bu_num_edges), data.x.device)
         # every auxiliary-lane branch joins back into the caller's stream inside the call,
         # so the workspaces and converted inputs can return to the allocator afterwards
-        check(L.bgcn_train_step(ctypes.addressof(a), ptr(ws), ws.numel(), stream_handle()))
+        self._stream = stream_handle()   # the prepared buffers belong to this stream
+        check(L.bgcn_train_step(ctypes.addressof(a), ptr(ws), ws.numel(), self._stream))
         self._pending = nxt
         return loss.view(())
 
@@ -198,6 +202,25 @@ class FusedTrainStep:
         # updates nothing; check_status() reports why
         self.opt.step(grads=self.bucket.views(), grad_scale=1.0 / world, skip_flag=self.bucket.flag)
         return loss
+
+    def _join_side(self) -> None:
+        """The current stream waits for the library's auxiliary lane (a next-batch
+        preparation may still be running there when a step returns)."""
+        check(_lib.lib().bgcn_join_side(self._stream))
+
+    def discard_prefetch(self) -> None:
+        """Drop a prepared next batch that will not be trained on (after ordering the
+        current stream behind its preparation)."""
+        if self._pending is not None:
+            self._join_side()
+            self._pending = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "_pending", None) is not None:
+                self._join_side()
+        except Exception:   # interpreter shutdown: nothing left to order
+            pass
 
     def check_status(self) -> None:
         """Host sync: raise on a bad edge index / label / (feat_mode "sparse") an

@@ -319,12 +319,13 @@ int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree
  * td_w1 td_b1 td_w2 td_b2 bu_w1 bu_b1 bu_w2 bu_b2 fc_w [C, 256] fc_b [C] (the
  * reference state_dict layout).  *status (optional, zeroed by the call): bit 0 = an
  * edge index outside [0, N) (skipped), bit 1 = a label outside [0, C) (ignored),
- * bit 2 = a feature row with more than BGCN_SPARSE_CAP non-zeros under BGCN_FEAT_SPARSE.
+ * bit 2 = a feature row with more than BGCN_SPARSE_CAP non-zeros under BGCN_FEAT_SPARSE,
+ * bit 3 = an internal cross-workgroup hand-off timed out (results invalid; never expected).
  *   prepared / prepared_ready: the current batch's prepared buffer; when not ready the
  *   call prepares it first (on the same stream).
  *   next / next_prepared (optional): a batch to prepare during this step on the
  *   auxiliary lane; pass it as the next call's prepared buffer with prepared_ready = 1.
- *   status_flag (optional): receives float(status & 7) once the forward has seen every
+ *   status_flag (optional): receives float(status & 15) once the forward has seen every
  *   flag; placed at the tail of the flat gradient bucket it travels through the DP
  *   all-reduce, so bgcn_adam_step's skip_flag skips the update on EVERY rank when any
  *   rank's step was invalid.
@@ -356,6 +357,11 @@ size_t bgcn_train_step_workspace_size(int64_t num_nodes, int64_t num_graphs, int
                                       int64_t bu_num_edges);
 int bgcn_train_step(const bgcn_step_args* args, void* workspace, size_t workspace_bytes,
                     bgcn_stream_t stream);
+/* A next-batch preparation (args->next) may still run on the library's auxiliary lane
+ * when bgcn_train_step returns; the next bgcn_train_step call orders its stream after it.
+ * bgcn_join_side makes `stream` wait for all auxiliary-lane work - call it before
+ * releasing a next_prepared buffer that no later step will consume. */
+int bgcn_join_side(bgcn_stream_t stream);
 
 /* --------------------------------------------------------------------------
  * Optimiser step of the training loop: torch.optim.Adam with the reference's three
