@@ -81,7 +81,7 @@ ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2):
                  ("auto", 7): "bgcn::k_prep_b<float>",
                  ("dense", 0): "bgcn::k_gemm_xwt<true, false, float>", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
                  ("dense", 2): "bgcn::k_conv2_fwd<float>", ("dense", 3): "bgcn::k_dw2<float>"}
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
 def pmc_traffic(mode: str, cls: int, workload: str = "twitter15"):
