@@ -23,12 +23,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--job-us", type=float, default=300.0)
+    ap.add_argument("--policies", action="store_true",
+                    help="only the 590 MB HBM read under each buffer-load cache policy")
     args = ap.parse_args()
     import bench
     from bigcn_amd import BiGCN, FusedTrainStep, ops
     from bigcn_amd.optim import bigcn_adam
     L = ctypes.CDLL(os.path.join(ROOT, "tools", "libinterfere.so"))
-    for f in (L.ifr_alu, L.ifr_read, L.ifr_pages):
+    for f in (L.ifr_alu, L.ifr_read, L.ifr_pages, L.ifr_read_pol):
         f.restype = ctypes.c_int
     dev = torch.device("cuda", 0)
     wl = bench.WORKLOADS["twitter15"]
@@ -57,6 +59,14 @@ def main():
         "pages 590MB 64 blk": lambda r: L.ifr_pages(P(big), ctypes.c_int64(big.numel()), 64, r, P(sink), sh()),
         "pages 590MB 1024 blk": lambda r: L.ifr_pages(P(big), ctypes.c_int64(big.numel()), 1024, r, P(sink), sh()),
     }
+
+    if args.policies:
+        jobs = {}
+        for blk in (1024, 256):
+            for aux in (0, 1, 2, 3, 16, 17, 18, 19):
+                jobs[f"read 590MB pol {aux} {blk} blk"] = (
+                    lambda r, aux=aux, blk=blk: L.ifr_read_pol(P(big), ctypes.c_int64(big.numel()), blk, r, aux,
+                                                               P(sink), sh()))
 
     def time_job(job, reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
