@@ -15,6 +15,7 @@
 #include "bgcn_bwd.h"
 #include "bgcn_internal.h"
 #include "bgcn_sparse.h"
+#include "bgcn_trace.h"
 
 namespace bgcn {
 
@@ -133,6 +134,7 @@ __global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ 
                                                       const int64_t* __restrict__ rootindex,
                                                       int64_t N, int64_t B, float* __restrict__ head,
                                                       HeadArgs hd) {
+  BT_BEGIN
   __shared__ float4 red[2][kReadSlices][16];
   __shared__ float4 red2[2][4][16];
   __shared__ float4 hrow[4 * H / 4];
@@ -180,6 +182,7 @@ __global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ 
   if (hd.W == nullptr) return;
   __syncthreads();
   if (threadIdx.x < 64) head_row(hd, b, B, hrow[threadIdx.x]);
+  BT_END(5);
 }
 
 // dH2[i][d*H + f] = dhead[b(i)][r1 block of d][f] / cnt_b * [H2 > 0]; block partial
@@ -195,6 +198,7 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
                                                      float* __restrict__ dH2,
                                                      float* __restrict__ colpart,
                                                      int nblk, HeadGradJob hj) {
+  BT_BEGIN
   if (int(blockIdx.x) >= nblk) {
     head_grad_block(hj, int(blockIdx.x) - nblk);
     return;
@@ -245,6 +249,7 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
     for (int q = 1; q < 8; ++q) acc = f4add(acc, red[q][l]);
     st4(colpart + int64_t(blockIdx.x) * (2 * H) + c, acc);
   }
+  BT_END(6);
 }
 
 // out_td[c] = sum_p colpart[p][c], out_bu[c] = sum_p colpart[p][H + c]: one block per
@@ -677,3 +682,5 @@ extern "C" int bgcn_keep_words(uint64_t seed, int64_t num_nodes, int32_t num_wor
   return bgcn::keep_words_impl(seed, num_nodes, num_words, words,
                                reinterpret_cast<hipStream_t>(stream));
 }
+
+BT_READER(bigcn)

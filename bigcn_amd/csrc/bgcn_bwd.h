@@ -145,12 +145,12 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
   if (dense_active(gate) != (cfg.want_dense != 0)) return;
   const int S = cfg.S;
   const int64_t ldp = cfg.ldp;
-  const int grp = threadIdx.x >> 8;
+  const int grp = threadIdx.x >> 8, ngrp = int(blockDim.x >> 8);   // 256-thread groups
   float (*red)[64] = reinterpret_cast<float (*)[64]>(smem + grp * 4 * 64);
   const int64_t per = int64_t(H) * ldp;
   const int64_t ntiles = (2 * per + 63) / 64;
   const int q = (threadIdx.x >> 6) & 3, t = threadIdx.x & 63;
-  for (int64_t base = int64_t(bl) * 4; base < ntiles; base += int64_t(cfg.blocks) * 4) {
+  for (int64_t base = int64_t(bl) * ngrp; base < ntiles; base += int64_t(cfg.blocks) * ngrp) {
     const int64_t tile = base + grp;
     const int64_t idx = tile * 64 + t;
     const bool valid = tile < ntiles && idx < 2 * per;

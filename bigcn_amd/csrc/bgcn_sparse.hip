@@ -25,6 +25,7 @@
 #include "bgcn_graph_body.h"
 #include "bgcn_internal.h"
 #include "bgcn_sparse.h"
+#include "bgcn_trace.h"
 
 namespace bgcn {
 namespace {
@@ -244,10 +245,15 @@ __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* 
 // row reaches its quarter by shuffle (entries s and s + 16 per lane); past a row's count
 // the value is 0 and the (clamped) column still loads, so every load is unconditional.
 constexpr int kC1Rows = 4;
-__global__ __launch_bounds__(256) void k_conv1_gather(SparseState S, float* __restrict__ Z1) {
+#ifndef BGCN_C1_THREADS
+#define BGCN_C1_THREADS 256
+#endif
+constexpr int kC1Threads = BGCN_C1_THREADS;   // threads per block
+__global__ __launch_bounds__(kC1Threads) void k_conv1_gather(SparseState S, float* __restrict__ Z1) {
+  BT_BEGIN
   if (!use_sparse(S)) return;
   const int lane = threadIdx.x & 63, ql = lane & 15, qb = lane & 48;
-  const int64_t i = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * kC1Rows + (lane >> 4);
+  const int64_t i = (int64_t(blockIdx.x) * (kC1Threads / 64) + (threadIdx.x >> 6)) * kC1Rows + (lane >> 4);
   const bool live = i < S.N;
   const int64_t ic = live ? i : S.N - 1;
   const int cnt = live ? min(S.nnz[ic], kCap) : 0;
@@ -283,6 +289,49 @@ __global__ __launch_bounds__(256) void k_conv1_gather(SparseState S, float* __re
     st4(Z1 + i * (2 * H) + 8 * ql, a0);
     st4(Z1 + i * (2 * H) + 8 * ql + 4, a1);
   }
+  BT_END(1);
+}
+
+// The same product with two rows per wave: half-wave h (32 lanes) owns row 2w + h, lane
+// l of a half the outputs [4l, 4l + 4) - one 16-byte load per lane per entry, a wave
+// instruction still moves 1 KiB (two 512-byte W1^T rows).  The loop runs to the longer
+// of the two rows in steps of kStep entries (a wave-uniform bound), so a wave issues
+// fewer padded gathers than with four rows, and holds fewer registers (more waves per
+// SIMD).
+#ifndef BGCN_C1_MODE
+#define BGCN_C1_MODE 2   // 0: four rows per wave (k_conv1_gather); 1 / 2: two rows, steps of 8 / 4
+#endif
+template <int kStep>
+__global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __restrict__ Z1) {
+  BT_BEGIN
+  if (!use_sparse(S)) return;
+  const int lane = threadIdx.x & 63, hl = lane & 31, hb = lane & 32;
+  const int64_t i = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool live = i < S.N;
+  const int64_t ic = live ? i : S.N - 1;
+  const int cnt = live ? min(S.nnz[ic], kCap) : 0;
+  const int32_t cl = S.cols[ic * kCap + hl];
+  const float vl = S.vals[ic * kCap + hl];
+  int cmax = max(cnt, __shfl_xor(cnt, 32, 64));
+  cmax = __builtin_amdgcn_readfirstlane(cmax);
+  float4 acc = f4zero();
+  for (int s0 = 0; s0 < cmax; s0 += kStep) {
+    float4 w[kStep];
+    float x[kStep];
+#pragma unroll
+    for (int u = 0; u < kStep; ++u) {
+      const int sl = s0 + u;                          // uniform, < kCap
+      const int32_t c = __shfl(cl, hb + (sl & 31), 64);
+      const float v = __shfl(vl, hb + (sl & 31), 64);
+      x[u] = sl < cnt ? v : 0.f;
+      const int32_t cc = min(max(c, 0), int32_t(S.F - 1));
+      w[u] = ld4(S.w1t + int64_t(cc) * (2 * H) + 4 * hl);
+    }
+#pragma unroll
+    for (int u = 0; u < kStep; ++u) acc = f4fma(x[u], w[u], acc);
+  }
+  if (live) st4(Z1 + i * (2 * H) + 4 * hl, acc);
+  BT_END(1);
 }
 
 // ---------------------------------------------------------------- conv2 forward
@@ -304,6 +353,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
                                                       const int32_t* __restrict__ tree_ptr,
                                                       const int64_t* __restrict__ rootindex,
                                                       float* __restrict__ Z2, KeepSrc keep) {
+  BT_BEGIN
   if (!use_sparse(S)) return;
   const int item = blockIdx.x;
   if (item >= S.tree_item0[S.B]) return;
@@ -340,6 +390,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
     dst[0] = av * w.x; dst[1] = av * w.y; dst[2] = av * w.z; dst[3] = av * w.w;
   }
   __syncthreads();
+  BT_MARK(2, 0);
 
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
   float* hs = &Hs[wv * 32 * kC2Ld];   // this wave's staged 32 x 64 H1 tile
@@ -364,6 +415,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
       __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
     }
+    if (t == wv) BT_MARK(2, 1);
     const float* hrow = &hs[r32 * kC2Ld + 32 * h];
     const uint32_t ni = uint32_t(ok ? i : beg);
     // K order (lane half h): kk < 32 -> H1 column 32h + kk (keep word h); kk >= 32 ->
@@ -403,6 +455,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
         acc1 = mfma32x32x2(a[32 + j], bq[j * kC2Ld + 32], acc1);
       }
     }
+    if (t == wv) BT_MARK(2, 2);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int64_t ii = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -412,6 +465,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
       }
     }
   }
+  BT_END(2);
 }
 
 
@@ -729,7 +783,7 @@ template <int kDw1Split>                       // waves per column (1 or 4)
 __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ dZ1,
                                 float* __restrict__ dw1_td, float* __restrict__ dw1_bu, int bid,
                                 float* smem) {
-  constexpr int kDw1Cols = 16 / kDw1Split;   // columns per 1024-thread block
+  const int kDw1Cols = int(blockDim.x >> 6) / kDw1Split;   // columns per block
   if (!use_sparse(S)) return;
   float (*t1)[17] = reinterpret_cast<float (*)[17]>(smem);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -771,7 +825,7 @@ __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ 
   // per output row)
   const int tx = threadIdx.x % kDw1Cols;
   const int64_t cc = int64_t(bid) * kDw1Cols + tx;
-  for (int ty = threadIdx.x / kDw1Cols; ty < 2 * H && cc < F; ty += 1024 / kDw1Cols) {
+  for (int ty = threadIdx.x / kDw1Cols; ty < 2 * H && cc < F; ty += int(blockDim.x) / kDw1Cols) {
     float acc = t1[ty][tx * kDw1Split];
 #pragma unroll
     for (int k = 1; k < kDw1Split; ++k) acc += t1[ty][tx * kDw1Split + k];
@@ -791,7 +845,8 @@ __device__ inline void rootcols_body(const SparseState& S, const int32_t* __rest
   if (!use_sparse(S)) return;
   float (*t2)[H][17] = reinterpret_cast<float (*)[H][17]>(smem);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t c = int64_t(bid) * 16 + wave;
+  const int cpb = int(blockDim.x >> 6);   // columns per block (one wave each)
+  const int64_t c = int64_t(bid) * cpb + wave;
   float a2[2] = {0.f, 0.f};
   if (c < S.F) {
     const int64_t beg = S.col_start[c], end = S.col_end[c];
@@ -824,9 +879,9 @@ __device__ inline void rootcols_body(const SparseState& S, const int32_t* __rest
   t2[0][lane][wave] = a2[0];
   t2[1][lane][wave] = a2[1];
   __syncthreads();
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;   // 16 x 64
-  const int64_t cc = int64_t(bid) * 16 + tx;
-  if (cc < S.F) {
+  const int tx = threadIdx.x % cpb;
+  const int64_t cc = int64_t(bid) * cpb + tx;
+  for (int ty = threadIdx.x / cpb; ty < H && cc < S.F; ty += int(blockDim.x) / cpb) {
     const int64_t K2 = S.F + H;
     dw2_td[int64_t(ty) * K2 + H + cc] = t2[0][ty][tx];
     dw2_bu[int64_t(ty) * K2 + H + cc] = t2[1][ty][tx];
@@ -948,47 +1003,61 @@ constexpr int kMidSmem = kDw2Smem > kRootPartSmem ? (kDw2Smem > kDh1Smem ? kDw2S
 template <class TX>
 __global__ __launch_bounds__(256) void k_bwd_mid(BwdMidArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[kMidSmem];
+  BT_BEGIN
   int b = int(blockIdx.x);
   if (b < a.n_dw2) {
     dw2_body<TX>(static_cast<const TX*>(a.X), a.ldx, a.S.F, a.H1, a.dZ2, a.node_root, a.S.N, a.keep,
                  a.gate, a.dw2_dense, a.dw2_sparse, a.n_dw2_dense, b, smem);
+    BT_END(70);
     return;
   }
   b -= a.n_dw2;
   if (b < a.n_root) {
     root_part_body(a.S, a.dZ2, a.tree_ptr, b % a.S.max_items, b / a.S.max_items, smem);
+    BT_END(71);
     return;
   }
   b -= a.n_root;
   if (b < 2 * a.nblk_h) {
     dh1_body(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, b % a.nblk_h,
              b / a.nblk_h, smem);
+    BT_END(72);
     return;
   }
   colsum_job_block(a.db2, b - 2 * a.nblk_h);
+  BT_END(73);
 }
 
 constexpr int kTailSmem = kDw1Smem > kRootColsSmem ? (kDw1Smem > kRedSmem ? kDw1Smem : kRedSmem)
                                                    : (kRootColsSmem > kRedSmem ? kRootColsSmem : kRedSmem);
+#ifndef BGCN_TAIL_THREADS
+#define BGCN_TAIL_THREADS 512   // 1024-thread blocks ran one per CU: dW1 in two rounds
+#endif
+constexpr int kTailThreads = BGCN_TAIL_THREADS;   // threads per block of the tail launch
 template <int kDw1Split>
-__global__ __launch_bounds__(1024) void k_bwd_tail(BwdTailArgs a) {
+__global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[kTailSmem];
+  BT_BEGIN
   int b = int(blockIdx.x);
   if (b < a.n_dw1) {
     dw1_body<kDw1Split>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, b, smem);
+    BT_END(80);
     return;
   }
   b -= a.n_dw1;
   if (b < a.n_rootcols) {
     rootcols_body(a.S, a.node_root, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem);
+    BT_END(81);
     return;
   }
   b -= a.n_rootcols;
   if (b < a.red_dense.blocks + a.red_sparse.blocks) {
     reduce_dw2_body(a.dw2_part, a.S.F + H, a.dw2_td, a.dw2_bu, a.gate, a.red_dense, a.red_sparse, b, smem);
+    BT_END(82);
     return;
   }
   colsum_job_block(a.db1, b - a.red_dense.blocks - a.red_sparse.blocks);
+  BT_END(83);
 }
 
 }  // namespace
@@ -1010,13 +1079,18 @@ int bwd_tail_launch(BwdTailArgs& a, hipStream_t s) {
   const char* e = std::getenv("BGCN_DW1_SPLIT");
   const bool sparse = a.S.mode != 1;
   const int split = e ? atoi(e) : (a.S.N >= 65536 ? 4 : 1);
-  a.n_dw1 = sparse ? int(split == 4 ? (a.S.F + 3) / 4 : (a.S.F + 15) / 16) : 0;
-  a.n_rootcols = sparse ? int((a.S.F + 15) / 16) : 0;
-  const int n = a.n_dw1 + a.n_rootcols + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(1024);
+  constexpr int wpb = kTailThreads / 64;   // waves per block
+  const int cols1 = split == 4 ? wpb / 4 : wpb;
+  a.n_dw1 = sparse ? int((a.S.F + cols1 - 1) / cols1) : 0;
+  a.n_rootcols = sparse ? int((a.S.F + wpb - 1) / wpb) : 0;
+  // the reduction configurations are sized in 1024-thread blocks (4 groups of 256)
+  a.red_dense.blocks *= 1024 / kTailThreads;
+  a.red_sparse.blocks *= 1024 / kTailThreads;
+  const int n = a.n_dw1 + a.n_rootcols + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(kTailThreads);
   if (split == 4)
-    hipLaunchKernelGGL(k_bwd_tail<4>, dim3(unsigned(n)), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_bwd_tail<4>, dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
   else
-    hipLaunchKernelGGL(k_bwd_tail<1>, dim3(unsigned(n)), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_bwd_tail<1>, dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -1159,13 +1233,15 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   a.nbd[0] = drop ? int(Etd / 256 + 1) : 0;
   a.nbd[1] = drop ? int(Ebu / 256 + 1) : 0;
   a.nsel = drop ? int(2 * B) : 0;
-  {   // The pass over X is paced: with fp32 X one 4-wave block per CU strides over the
-      // rows (~20 MB of loads in flight, ~4 TB/s).  A wave per row over all rows drains X
-      // at 5.5 TB/s but floods the memory queues with ~100 MB of requests, and every load
-      // of the latency-bound training chain beside it then waits behind them: measured
-      // 0.293-0.295 ms per step paced vs 0.303-0.306 unpaced (twitter15; 224-288 blocks
-      // within 1%, 512 worse than either).  bf16 X (twice the rows per byte) keeps the
-      // full grid: paced it lengthens the side lane (synth1024_bf16 0.90 vs 0.87 ms).
+  {   // The pass over X is paced: with fp32 X 1.5 4-wave blocks per CU stride over the
+      // rows (~30 MB of loads in flight, ~4.5 TB/s).  A wave per row over all rows drains
+      // X at 5.5 TB/s but floods the memory queues with ~100 MB of requests, and every
+      // load of the latency-bound training chain beside it then waits behind them:
+      // measured 0.293-0.295 ms per step paced vs 0.303-0.306 unpaced (twitter15; 224-288
+      // blocks within 1%, 512 worse than either).  With the shorter chain of 512-thread
+      // aggregation / tail blocks, 384 blocks: 0.2964-0.2966 vs 0.304-0.308 at 256
+      // (profiles/r02_pace_ab.txt).  bf16 X (twice the rows per byte) keeps the full
+      // grid: paced it lengthens the side lane (synth1024_bf16 0.90 vs 0.87 ms).
       // BGCN_PREP_BLOCKS (read per call) overrides: 0 = full grid, n = n blocks.
     static const int ncu = [] {
       int dev = 0, n = 0;
@@ -1176,7 +1252,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
     }();
     const bool bf = bt->x_dtype == BGCN_DTYPE_BF16;
     a.ncomp = xp ? int(grid_for(N, bf ? 8 : 4)) : 0;
-    int cap = bf ? 0 : ncu;
+    int cap = bf ? 0 : ncu + ncu / 2;
     const char* e = std::getenv("BGCN_PREP_BLOCKS");
     if (e) cap = atoi(e);
     if (cap > 0) a.ncomp = std::min(a.ncomp, cap);
@@ -1243,7 +1319,14 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
 }
 
 int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
-  hipLaunchKernelGGL(k_conv1_gather, dim3(grid_for(S.N, 4 * kC1Rows)), dim3(256), 0, s, S, Z1);
+#if BGCN_C1_MODE == 1
+  hipLaunchKernelGGL(k_conv1_rows2<8>, dim3(grid_for(S.N, 8)), dim3(256), 0, s, S, Z1);
+#elif BGCN_C1_MODE == 2
+  hipLaunchKernelGGL(k_conv1_rows2<4>, dim3(grid_for(S.N, 8)), dim3(256), 0, s, S, Z1);
+#else
+  hipLaunchKernelGGL(k_conv1_gather, dim3(grid_for(S.N, (kC1Threads / 64) * kC1Rows)), dim3(kC1Threads), 0, s,
+                     S, Z1);
+#endif
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -1251,3 +1334,5 @@ int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
 
 
 }  // namespace bgcn
+
+BT_READER(sparse)

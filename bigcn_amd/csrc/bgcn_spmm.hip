@@ -20,6 +20,7 @@
 // Up to two problems (the fused step's TD and BU graphs) share one launch
 // (blockIdx.y / blockIdx.z = problem).
 #include "bgcn_internal.h"
+#include "bgcn_trace.h"
 
 namespace bgcn {
 
@@ -117,11 +118,15 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
 // the long rows longs[j], j = block, block + nlongblk, ...: the 64 groups sum entries
 // q, q + 64, ... of the row (8 in flight) and combine their partials in LDS in group
 // order (deterministic; a row's sum does not depend on which block takes it).
-constexpr int kRowsThreads = 1024;
+#ifndef BGCN_ROWS_THREADS
+#define BGCN_ROWS_THREADS 512   // 1024-thread blocks ran one per CU (block trace)
+#endif
+constexpr int kRowsThreads = BGCN_ROWS_THREADS;
 constexpr int64_t kPlanMaxEntries = int64_t(1) << 17;   // capacity (E + N) up to which plans are used
 constexpr int kRowsGroups = kRowsThreads / 16;
 
 __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
+  BT_BEGIN
   constexpr int LANES = 16;
   const SpmmProb& P = sb.p[blockIdx.y];
   const int lane = threadIdx.x % LANES, grp = threadIdx.x / LANES;
@@ -170,6 +175,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_
       }
     }
     if (cur >= 0) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+    BT_END(3);
     return;
   }
   // long rows: one block per row
@@ -203,6 +209,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_
     }
     __syncthreads();
   }
+  if (nl > int(blockIdx.x - nchunk)) BT_END(4);
 }
 
 // Fixup, F <= 128: one block per SG = 256/LANES chunk boundaries, sub-group s checking
@@ -553,3 +560,5 @@ extern "C" int bgcn_spmm(const int32_t* ptr, const int32_t* row, const int32_t* 
                          epilogue, workspace, workspace_bytes,
                          reinterpret_cast<hipStream_t>(stream));
 }
+
+BT_READER(spmm)
