@@ -1074,11 +1074,13 @@ int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s) {
 }
 
 int bwd_tail_launch(BwdTailArgs& a, hipStream_t s) {
-  // one wave per column at Twitter-sized batches, four from 64k rows (longer columns);
+  // one wave per column (with 1024-thread blocks, one per CU, four waves per column won
+  // from 64k rows; with 512-thread blocks one wave wins at every size: synth1024_bf16
+  // 0.839 vs 0.850-0.859 ms, weibo_bf16 0.690 vs 0.697, profiles/r02_split_ab.txt);
   // BGCN_DW1_SPLIT=1/4 forces either (read per call: tests compare both)
   const char* e = std::getenv("BGCN_DW1_SPLIT");
   const bool sparse = a.S.mode != 1;
-  const int split = e ? atoi(e) : (a.S.N >= 65536 ? 4 : 1);
+  const int split = e ? atoi(e) : 1;
   constexpr int wpb = kTailThreads / 64;   // waves per block
   const int cols1 = split == 4 ? wpb / 4 : wpb;
   a.n_dw1 = sparse ? int((a.S.F + cols1 - 1) / cols1) : 0;

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
 #define BGCN_ROWS_THREADS 512   // 1024-thread blocks ran one per CU (block trace)
 #endif
 constexpr int kRowsThreads = BGCN_ROWS_THREADS;
-constexpr int64_t kPlanMaxEntries = int64_t(1) << 17;   // capacity (E + N) up to which plans are used
+constexpr int64_t kPlanMaxEntries = int64_t(1) << 30;   // capacity (E + N) up to which plans are used
 constexpr int kRowsGroups = kRowsThreads / 16;
 
 __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
@@ -489,8 +489,9 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   }
   // The plan pays off while long rows are few and short (one block each): measured on the
   // fused step beside the next batch's preparation, Twitter15-sized batches (E + N = 55k)
-  // 0.356 vs 0.362 ms per step, Weibo-sized ones (188k) 0.85 vs 0.77 ms - there a few
-  // blocks summing thousands of entries each become the tail under memory contention.
+  // 0.356 vs 0.362 ms per step; with 1024-thread row blocks (one per CU) Weibo-sized
+  // ones (188k) lost (0.85 vs 0.77 ms), with 512-thread blocks they win too (weibo_bf16
+  // 0.698-0.700 vs 0.719, synth1024_bf16 0.853 vs 0.867: profiles/r02_plan_ab.txt).
   // BGCN_SPMM_PLAN=0/1 forces either form (A/B runs).
   const char* pe = std::getenv("BGCN_SPMM_PLAN");   // read per call: tests switch it
   const int plan_env = pe ? atoi(pe) : -1;
