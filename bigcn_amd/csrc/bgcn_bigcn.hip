@@ -328,8 +328,13 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   t.kchunk2 = kc;
   t.S2 = int((N + kc - 1) / kc);
   if (t.S2 < 1) t.S2 = 1;
-  // sparse path: relu(H1) block of dW2 over 256-node splits (partial rows of 64)
-  t.kchunkh = 128;
+  // sparse path: relu(H1) block of dW2 over node splits of >= 128 nodes (partial rows of
+  // 64), at most ~kDw2MaxSplits splits: every split writes a 2 x 64 x 64 partial that the
+  // tail re-reads (118k nodes: 922 splits = 30 MB of partials at 128 nodes each)
+#ifndef BGCN_DW2_MAX_SPLITS
+#define BGCN_DW2_MAX_SPLITS 256
+#endif
+  t.kchunkh = std::max<int64_t>(128, ((N + BGCN_DW2_MAX_SPLITS - 1) / BGCN_DW2_MAX_SPLITS + BK - 1) / BK * BK);
   t.Sh = int((N + t.kchunkh - 1) / t.kchunkh);
   if (t.Sh < 1) t.Sh = 1;
   const size_t dense_part = size_t(2) * t.S2 * H * (H + F), sparse_part = size_t(2) * t.Sh * H * H;
