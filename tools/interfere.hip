@@ -97,3 +97,15 @@ extern "C" int ifr_read_pol(const void* buf, int64_t bytes, int blocks, int reps
   }
   return hipGetLastError();
 }
+
+// device buffers with an allocation flag (0 = hipMalloc default / coarse-grained,
+// 1 = fine-grained, 3 = uncached): does the placement of a streamed buffer change what
+// its stream costs the chain (cache pollution)?
+extern "C" void* ifr_alloc(int64_t bytes, int flags) {
+  void* p = nullptr;
+  if (flags == 0) { if (hipMalloc(&p, bytes) != hipSuccess) return nullptr; }
+  else if (hipExtMallocWithFlags(&p, bytes, unsigned(flags)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 1, bytes) != hipSuccess) return nullptr;
+  return p;
+}
+extern "C" int ifr_free(void* p) { return hipFree(p); }

@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--job-us", type=float, default=300.0)
+    ap.add_argument("--placement", action="store_true",
+                    help="only the 590 MB HBM read from buffers of each allocation flag")
     ap.add_argument("--policies", action="store_true",
                     help="only the 590 MB HBM read under each buffer-load cache policy")
     args = ap.parse_args()
@@ -32,6 +34,7 @@ def main():
     L = ctypes.CDLL(os.path.join(ROOT, "tools", "libinterfere.so"))
     for f in (L.ifr_alu, L.ifr_read, L.ifr_pages, L.ifr_read_pol):
         f.restype = ctypes.c_int
+    L.ifr_alloc.restype = ctypes.c_void_p
     dev = torch.device("cuda", 0)
     wl = bench.WORKLOADS["twitter15"]
     pool = bench.make_pool(wl, 0, 2, dev, (0.0, 0.0))
@@ -67,6 +70,18 @@ def main():
                 jobs[f"read 590MB pol {aux} {blk} blk"] = (
                     lambda r, aux=aux, blk=blk: L.ifr_read_pol(P(big), ctypes.c_int64(big.numel()), blk, r, aux,
                                                                P(sink), sh()))
+
+    if args.placement:
+        jobs = {}
+        for flag, nm in ((0, "coarse"), (1, "fine"), (3, "uncached")):
+            ptr = L.ifr_alloc(ctypes.c_int64(590 << 20), flag)
+            if not ptr:
+                print(f"alloc flag {flag} failed", flush=True)
+                continue
+            for blk in (1024, 256):
+                jobs[f"read 590MB {nm} {blk} blk"] = (
+                    lambda r, ptr=ptr, blk=blk: L.ifr_read(ctypes.c_void_p(ptr), ctypes.c_int64(590 << 20), blk, r,
+                                                           P(sink), sh()))
 
     def time_job(job, reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
