@@ -185,6 +185,121 @@ __global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ 
   BT_END(5);
 }
 
+// The same readout over tree work items (sparse path: S.item_* exist), so a large tree
+// no longer bounds the launch.  Block = one item (<= kChunk nodes of one tree), 512
+// threads = 2 directions x 16 row slices x 16 lanes x float4, eight row loads in flight
+// per slice.  A tree of one item finishes in its block; otherwise every item stores its
+// partial (rpart[item][2H]) and the tree's last arrival (rtick[b], zeroed by the
+// prologue, re-zeroed by the last arrival) adds the partials in item order: a fixed
+// order whichever block arrives last (deterministic).  Blocks from max_items on cover
+// trees without nodes (mean 0, root row 0, head on the bias).
+constexpr int kRoSlices = 16;
+__global__ __launch_bounds__(512) void k_readout_items(SparseState S, const float* __restrict__ H1,
+                                                       const float* __restrict__ H2,
+                                                       const int32_t* __restrict__ tree_ptr,
+                                                       const int64_t* __restrict__ rootindex,
+                                                       int64_t N, int64_t B, float* __restrict__ head,
+                                                       float* __restrict__ rpart, HeadArgs hd) {
+  BT_BEGIN
+  __shared__ float4 red[2][kRoSlices][16];
+  __shared__ float4 hrow[4 * H / 4];
+  const int blk = int(blockIdx.x);
+  int64_t b, beg, end;
+  int item0 = 0, nit = 1;
+  if (blk < S.max_items) {
+    if (blk >= S.tree_item0[S.B]) return;
+    b = S.item_tree[blk];
+    beg = int64_t(tree_ptr[b]) + int64_t(S.item_chunk[blk]) * kChunk;
+    end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
+    item0 = S.tree_item0[b];
+    nit = S.tree_item0[b + 1] - item0;
+  } else {
+    b = blk - S.max_items;
+    if (b >= B || tree_ptr[b + 1] > tree_ptr[b]) return;   // trees with nodes have items
+    beg = end = tree_ptr[b];
+  }
+  const int d = threadIdx.x >> 8, t = threadIdx.x & 255;
+  const int lane = t & 15, slice = t >> 4;
+  const int dd = (threadIdx.x >> 4) & 1, ll = threadIdx.x & 15;   // wave 0: (dir, lane)
+  // wave 0 issues the tree's tail operands first (root row of H1, the head's W / bias /
+  // label), so they arrive under the row loads instead of after them
+  HeadRegs hreg;
+  float4 hroot = f4zero();
+  int64_t root = 0;
+  if (threadIdx.x < 64) {
+    if (hd.W != nullptr) head_load(hd, b, hreg);
+    root = rootindex[b];
+    hroot = ld4(H1 + (root >= 0 && root < N ? root : 0) * (2 * H) + dd * H + ll * 4);
+  }
+  const float* src = H2 + d * H + lane * 4;
+  float4 s = f4zero();
+  for (int64_t i = beg + slice; i < end; i += 8 * kRoSlices) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld4(src + min<int64_t>(i + u * kRoSlices, end - 1) * (2 * H));
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i + u * kRoSlices < end) s = f4add(s, f4relu(v[u]));
+  }
+  red[d][slice][lane] = s;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;   // wave 0 finishes the item (and the tree)
+  float4 acc = f4zero();
+  if (threadIdx.x < 32) {
+    acc = red[dd][0][ll];
+#pragma unroll
+    for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, red[dd][q][ll]);
+  }
+  if (nit > 1) {
+    // partials go out as agent-scope atomic stores (write-through past the XCD's L2) and
+    // are read back by the last arrival with agent-scope atomic loads: no L2 write-back /
+    // invalidate (a __threadfence per block cost the launch 13.7 -> 48 us)
+    float* p = rpart + int64_t(blk) * (2 * H) + dd * H + ll * 4;
+    if (threadIdx.x < 32) {
+      __hip_atomic_store(p + 0, acc.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 1, acc.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 2, acc.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 3, acc.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);   // the stores are acknowledged before the ticket
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    int tk = 0;
+    if (threadIdx.x == 0)
+      tk = __hip_atomic_fetch_add(&S.rtick[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tk = __shfl(tk, 0, 64);
+    if (tk != nit - 1) return;
+    if (threadIdx.x < 32) {
+      const float* q0 = rpart + int64_t(item0) * (2 * H) + dd * H + ll * 4;
+      for (int q = 0; q < nit; ++q) {
+        const float* pq = q0 + int64_t(q) * (2 * H);
+        const float4 v = make_float4(__hip_atomic_load(pq + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(pq + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(pq + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        acc = q == 0 ? v : f4add(acc, v);
+      }
+    }
+  }
+  const int64_t t0 = tree_ptr[b], t1 = tree_ptr[b + 1];
+  const int base = (dd == 1 ? 0 : 2 * H) + ll * 4;   // BU first (:128)
+  if (threadIdx.x < 32) {
+    const float cnt = float(t1 - t0 > 0 ? t1 - t0 : 1);
+    acc = make_float4(acc.x / cnt, acc.y / cnt, acc.z / cnt, acc.w / cnt);
+    st4(head + b * (4 * H) + base, acc);
+    hrow[base / 4] = acc;
+  } else {
+    const float4 hr = (t1 > t0 && root >= 0 && root < N) ? hroot : f4zero();
+    st4(head + b * (4 * H) + base + H, hr);
+    hrow[(base + H) / 4] = hr;
+  }
+  if (hd.W == nullptr) return;
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): wave 0's hrow writes have landed
+  __builtin_amdgcn_wave_barrier();
+  head_row(hd, b, B, hrow[threadIdx.x], hreg);
+  BT_END(5);
+}
+
 // dH2[i][d*H + f] = dhead[b(i)][r1 block of d][f] / cnt_b * [H2 > 0]; block partial
 // column sums -> colpart[blk][2H].  256 threads = 8 row phases x 32 lanes x float4; a
 // block covers kReadBwdRows rows, every thread's rows are loaded before use.  Blocks
@@ -289,6 +404,8 @@ struct FusedWs {
   float *z1, *z2, *d2, *dz2, *dh1, *dz1;  // [N, 2H]
   float* colpart;                         // [nblk, 2H] db1 partials (k_dh1)
   float* colpart2;                        // [nblk, 2H] db2 partials (k_readout_bwd)
+  float* rpart;                           // [max_items, 2H] readout partials (k_readout_items)
+  int32_t* rtick;                         // [B] readout arrival counters
   float* spmm_ws; size_t spmm_bytes;
   float* dw2_part;                        // [2][S2][H][H+F]
   float* tn_ws; size_t tn_bytes;
@@ -321,6 +438,8 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
                                  (N + kReadBwdRows - 1) / kReadBwdRows);
   t.colpart = c.take<float>(size_t(nblk) * 2 * H);
   t.colpart2 = c.take<float>(size_t(nblk) * 2 * H);
+  t.rpart = c.take<float>(size_t(N / kChunk + B + 1) * 2 * H);   // max_items (carve_sparse)
+  t.rtick = c.take<int32_t>(size_t(B));
   t.S2 = dw2_splits(N, F);
   int64_t kc = (N + t.S2 - 1) / t.S2;
   kc = (kc + BK - 1) / BK * BK;
@@ -334,7 +453,8 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
 #ifndef BGCN_DW2_MAX_SPLITS
 #define BGCN_DW2_MAX_SPLITS 256
 #endif
-  t.kchunkh = std::max<int64_t>(128, ((N + BGCN_DW2_MAX_SPLITS - 1) / BGCN_DW2_MAX_SPLITS + BK - 1) / BK * BK);
+  // (whole 64-row dH1 tiles: the split's dH1 block forms its dW2 partial, bgcn_bwd.h)
+  t.kchunkh = std::max<int64_t>(128, ((N + BGCN_DW2_MAX_SPLITS - 1) / BGCN_DW2_MAX_SPLITS + 63) / 64 * 64);
   t.Sh = int((N + t.kchunkh - 1) / t.kchunkh);
   if (t.Sh < 1) t.Sh = 1;
   const size_t dense_part = size_t(2) * t.S2 * H * (H + F), sparse_part = size_t(2) * t.Sh * H * H;
@@ -432,6 +552,7 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
   sp.vals = a->x_vals;
   carve_sparse(c, N, B, F, &sp);
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
+  if (sp.mode != 1) sp.rtick = w.rtick;   // item readout (tree items exist on the sparse path)
   w.spmm_bytes = ws_bytes - align_up(c.off, 256) - 256;
   w.spmm_ws = c.take<float>(1);
   for (int d = 0; d < 2; ++d)
@@ -555,8 +676,13 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
   timing_end(2, s);
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z2, a->h2, a->td_b2, a->bu_b2, BGCN_EPI_NONE, w, s));
   const HeadArgs no_head{};
-  hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B)), dim3(1024), 0, s, a->h1, a->h2,
-                     a->tree_ptr, a->rootindex, N, B, a->head_in, head ? *head : no_head);
+  if (sparse)
+    hipLaunchKernelGGL(k_readout_items, dim3(unsigned(sp.max_items + B)), dim3(512), 0, s, sp, a->h1,
+                       a->h2, a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart,
+                       head ? *head : no_head);
+  else
+    hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B)), dim3(1024), 0, s, a->h1, a->h2,
+                       a->tree_ptr, a->rootindex, N, B, a->head_in, head ? *head : no_head);
   BGCN_CHECK_LAUNCH();
   if (forked) BGCN_TRY(aux_join(s, kLaneSide));
   return BGCN_OK;
@@ -602,7 +728,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   // ---- middle launch: dW2 partials (the dense config, gated, and the sparse path's
   // relu(H1) block), the dW2 root-column partials, dH1 through dropout and relu (+ db1
   // partials) and the db2 column sums.  One dependent launch instead of four.
-  const int64_t nblk_h = (N + kDh1Rows - 1) / kDh1Rows;
+  const int64_t nblk_h = w.Sh;   // dH1 (+ relu(H1) dW2 partial) blocks: one per node split
   const int gxd = int(grid_for(H + F, 64));
   BwdMidArgs m{};
   m.S = sp;
@@ -611,8 +737,9 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   m.dw2_dense = Dw2Cfg{w.kchunk2, w.S2, gxd, 1, H + F, w.dw2_part};
   m.dw2_sparse = Dw2Cfg{w.kchunkh, w.Sh, 1, 0, int64_t(H), w.dw2_part};
   m.n_dw2_dense = dense_launched(a, sp) ? gxd * w.S2 * 2 : 0;
-  m.n_dw2 = m.n_dw2_dense + (sparse ? w.Sh * 2 : 0);
+  m.n_dw2 = m.n_dw2_dense;   // the sparse relu(H1) block is formed by the dH1 blocks
   m.W2td = a->td_w2; m.W2bu = a->bu_w2; m.dH1 = w.dh1; m.colpart = w.colpart; m.nblk_h = int(nblk_h);
+  m.rows_h = w.kchunkh;
   m.db2 = ColsumJob{w.colpart2, int(nblk_r), a->td_db2, a->bu_db2};
   timing_begin(3, s);
   BGCN_TRY(bwd_mid_launch(m, a->x_dtype, s));

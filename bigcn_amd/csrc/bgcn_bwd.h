@@ -176,20 +176,30 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
 }
 
 // dH1[i][d*H + c] = (dZ2_d[i] . W2_d[:, c]) * keep(d,i,c) * s * [H1 > 0], c < H,
-// + block partial column sums.  A 64-row x 64-column tile per (block, direction) on the
-// fp32 MFMA (32x32x2): four waves as 2 row halves x 2 column halves, K = H = 64 in 32
-// steps.  The K order is permuted (lane half h owns k in [32h, 32h+32)) so each lane's
-// dZ2 operand is one contiguous 128-byte run; W2 rows come straight from L2.
-// Device body, 256 threads: row block bx of direction d; smem: kDh1Smem floats.
+// + block partial column sums, over `rows` consecutive nodes (64-row tiles) of direction
+// d per block.  A 64-row x 64-column tile on the fp32 MFMA (32x32x2): four waves as
+// 2 row halves x 2 column halves, K = H = 64 in 32 steps.  The K order is permuted (lane
+// half h owns k in [32h, 32h+32)) so each lane's dZ2 operand is one contiguous 128-byte
+// run.  dZ2 tiles and W2[:, :64] are staged in LDS with coalesced float4 loads (rows
+// padded to 65 floats: conflict-free operand reads).
+//
+// dw2part != nullptr (the sparse path, gated off when the dense path runs): the same
+// block also forms the relu(H1) block of dW2 over its rows,
+//   part[d][bx][o][c] = sum_i dZ2_d[i][o] * keep(d,i,c) * s * relu(H1_d[i][c]),
+// from the operands the dH1 tile already holds: each lane's 16 (row, c) values of H1 and
+// of the keep words are exactly its B operands of a 32x32x2 chain whose K order is the
+// accumulator row order acc_row(q, h); the dZ2^T operands are read from the staged tile
+// in that order.  Two row-half waves are combined in LDS (fixed order).  One block per
+// node split (the tail reduces the splits), so the separate dW2 role - its own loads of
+// dZ2 and H1 and its own keep hashing - is gone from the launch.
+// Device body, 256 threads; smem: kDh1Smem floats.
 constexpr int kDh1Rows = 64;
 constexpr int kDh1Smem = kDh1Rows * (H + 1) + H * (H + 1) + 2 * H;
 __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __restrict__ H1,
                                 const float* __restrict__ W2td, const float* __restrict__ W2bu,
                                 int64_t ldw2, int64_t N, KeepSrc keep, float* __restrict__ dH1,
-                                float* __restrict__ colpart, int bx, int d, float* smem) {
-  // dZ2 tile (64 rows x 64) and W2[:, :64] staged in LDS with coalesced float4 loads
-  // (a direct per-lane operand load touches 64 cache lines per instruction); rows are
-  // padded to 65 floats so the MFMA operand reads are bank-conflict free.
+                                float* __restrict__ colpart, int64_t rows, float* __restrict__ dw2part,
+                                int nsplit, int bx, int d, float* smem) {
   float* Ds = smem;
   float* Ws = smem + kDh1Rows * (H + 1);
   float (*red)[H] = reinterpret_cast<float (*)[H]>(smem + kDh1Rows * (H + 1) + H * (H + 1));
@@ -197,59 +207,119 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
   const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int rh = wid & 1, ch = wid >> 1;
   const int r = l & 31, h = l >> 5;
-  const int64_t blk0 = int64_t(bx) * kDh1Rows;
-  const int64_t row0 = blk0 + rh * 32;
   const int c = ch * 32 + r;  // output column of this lane (within H)
-  {
-    float4 dv[4], wv[4];
+  const int64_t beg = int64_t(bx) * rows, end = min<int64_t>(beg + rows, N);
+  const int ntile = int((end - beg + kDh1Rows - 1) / kDh1Rows);
+  const float sc = keep.scale();
+  const bool want_dw2 = dw2part != nullptr;
+
+  float4 dv[4];
+  float hv[16];
+  auto gload = [&](int64_t blk0) {   // one tile's dZ2 rows and this lane's H1 values
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {   // element e = tid + 256u of a 64 x 16 float4 grid
+    for (int u = 0; u < 4; ++u) {    // element e = tid + 256u of a 64 x 16 float4 grid
       const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
       dv[u] = ld4(dZ2 + min<int64_t>(blk0 + rr, N - 1) * (2 * H) + d * H + q);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t i = min<int64_t>(blk0 + rh * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, N - 1);
+      hv[q] = H1[i * (2 * H) + d * H + c];
+    }
+  };
+  {
+    float4 wv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
       wv[u] = ld4(W2 + int64_t(rr) * ldw2 + q);
     }
+    gload(beg);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
+      float* ww = &Ws[rr * (H + 1) + q];
+      ww[0] = wv[u].x; ww[1] = wv[u].y; ww[2] = wv[u].z; ww[3] = wv[u].w;
+    }
+  }
+  f32x16 pw0 = {}, pw1 = {};   // dW2 partial: o in [0, 32) / [32, 64), columns ch*32 + r
+  float cs = 0.f;
+  for (int t = 0; t < ntile; ++t) {
+    const int64_t blk0 = beg + int64_t(t) * kDh1Rows;
+    const int64_t row0 = blk0 + rh * 32;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
       float* dd = &Ds[rr * (H + 1) + q];
       dd[0] = dv[u].x; dd[1] = dv[u].y; dd[2] = dv[u].z; dd[3] = dv[u].w;
-      float* ww = &Ws[rr * (H + 1) + q];
-      ww[0] = wv[u].x; ww[1] = wv[u].y; ww[2] = wv[u].z; ww[3] = wv[u].w;
     }
-  }
-  float hv[16];
-  uint32_t wd[16];
+    // this tile's per-lane operands, reduced before the next tile's loads reuse hv:
+    // a2 = keep * s * relu(H1) (dW2's B operand), bit q of km = kept and H1 > 0 (dH1)
+    float a2[16];
+    uint32_t km = 0;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int64_t i = min<int64_t>(row0 + (q & 3) + 8 * (q >> 2) + 4 * h, N - 1);
-    hv[q] = H1[i * (2 * H) + d * H + c];
-    wd[q] = keep.get(uint32_t(d), uint32_t(i), uint32_t(c >> 5));
-  }
-  __syncthreads();
-  // lane half h owns k in [32h, 32h + 32) (permuted K, same for A and B)
-  const float* ap = &Ds[(rh * 32 + r) * (H + 1) + 32 * h];
-  const float* bp = &Ws[(32 * h) * (H + 1) + c];
-  f32x16 acc = {};
-#pragma unroll
-  for (int kk = 0; kk < 32; ++kk) acc = mfma32x32x2(ap[kk], bp[kk * (H + 1)], acc);
-
-  const float sc = keep.scale();
-  float cs = 0.f;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-    const float g = (((wd[q] >> (c & 31)) & 1u) && hv[q] > 0.f) ? acc[q] * sc : 0.f;
-    if (i < N) {
-      dH1[i * (2 * H) + d * H + c] = g;
-      cs += g;
+    for (int q = 0; q < 16; ++q) {
+      const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(i, N - 1)), uint32_t(c >> 5));
+      const bool kept = ((wd >> (c & 31)) & 1u) && i < N;
+      a2[q] = kept ? sc * fmaxf(hv[q], 0.f) : 0.f;
+      km |= uint32_t(kept && hv[q] > 0.f) << q;
     }
+    __syncthreads();
+    // lane half h owns k in [32h, 32h + 32) (permuted K, same for A and B)
+    const float* ap = &Ds[(rh * 32 + r) * (H + 1) + 32 * h];
+    const float* bp = &Ws[(32 * h) * (H + 1) + c];
+    f32x16 acc = {};
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) acc = mfma32x32x2(ap[kk], bp[kk * (H + 1)], acc);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      const float g = ((km >> q) & 1u) ? acc[q] * sc : 0.f;
+      if (i < N) {
+        dH1[i * (2 * H) + d * H + c] = g;
+        cs += g;
+      }
+    }
+    if (want_dw2) {
+      // B[k = acc_row(q, h)][c] = a2[q] (this lane's); A[o][k] = dZ2[row0 + k][o] from LDS
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int k = (q & 3) + 8 * (q >> 2) + 4 * h;
+        const float* zr = &Ds[(rh * 32 + k) * (H + 1)];
+        pw0 = mfma32x32x2(zr[r], a2[q], pw0);
+        pw1 = mfma32x32x2(zr[32 + r], a2[q], pw1);
+      }
+    }
+    __syncthreads();   // Ds is rewritten by the next tile
+    if (t + 1 < ntile) gload(blk0 + kDh1Rows);
   }
   cs += __shfl_xor(cs, 32);
   if (h == 0) red[rh][c] = cs;
   __syncthreads();
   if (threadIdx.x < H)
-    colpart[int64_t(bx) * (2 * H) + d * H + threadIdx.x] =
-        red[0][threadIdx.x] + red[1][threadIdx.x];
+    colpart[int64_t(bx) * (2 * H) + d * H + threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x];
+  if (!want_dw2) return;
+  // combine the two row halves: rh = 1 parks its partial in LDS (Ds), rh = 0 adds and stores
+  float* P = Ds;   // [64 o][64 c]
+  if (rh == 1) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int o = acc_row(q, l);
+      P[o * H + c] = pw0[q];
+      P[(32 + o) * H + c] = pw1[q];
+    }
+  }
+  __syncthreads();
+  if (rh == 0) {
+    float* out = dw2part + (int64_t(d) * nsplit + bx) * (H * H);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int o = acc_row(q, l);
+      out[o * H + c] = pw0[q] + P[o * H + c];
+      out[(32 + o) * H + c] = pw1[q] + P[(32 + o) * H + c];
+    }
+  }
 }
 
 

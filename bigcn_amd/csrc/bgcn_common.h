@@ -215,6 +215,14 @@ __device__ __forceinline__ float xs(const bf16_t* p) { return bf2f(*p); }
 // entries ("long rows", BU star roots) are listed in longs[0 .. *nlong) and aggregated by
 // one block each.  No row is split, so no fixup pass follows.
 constexpr int kPlanChunk = 16;
+// The chunk grid itself is finer: chunk g owns the rows [row(g * kPlanGrid), row((g + 1) *
+// kPlanGrid)), at most kPlanGrid + kPlanChunk - 1 entries, so a group's gathers mostly fit
+// in one round of eight (a 16-entry grid took two dependent rounds per group).
+#ifndef BGCN_PLAN_GRID
+#define BGCN_PLAN_GRID 16
+#endif
+constexpr int kPlanGrid = BGCN_PLAN_GRID;
+static_assert(kPlanGrid <= kPlanChunk, "a chunk holds at most 2 * 16 - 1 entries");
 struct SpmmPlan {
   const int2* bnd;
   const int32_t* longs;

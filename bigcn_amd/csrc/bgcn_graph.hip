@@ -223,7 +223,7 @@ __global__ void k_nodes(GraphBatch gb) {
 // chunk bounds of a plan: lo = the entry where chunk g starts (a long row at the boundary
 // is skipped), hi = where it ends (a long row is excluded)
 __device__ __forceinline__ int2 plan_bounds(const int32_t* ptr, const int32_t* row, int64_t nnz, int64_t g) {
-  const int64_t p0 = g * kPlanChunk, p1 = p0 + kPlanChunk;
+  const int64_t p0 = g * kPlanGrid, p1 = p0 + kPlanGrid;
   int lo = int(nnz), hi = int(nnz);
   if (p0 < nnz) {
     const int32_t r = row[p0];
@@ -239,7 +239,7 @@ __global__ void k_normalize(GraphBatch gb) {
   const int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   // the plans' chunk bounds, chunk g = thread p (the first ngroups threads; rows are
   // final here, k_nodes wrote the self loops)
-  if (G.bnd_t && p < (G.E + gb.N + kPlanChunk - 1) / kPlanChunk) {
+  if (G.bnd_t && p < (G.E + gb.N + kPlanGrid - 1) / kPlanGrid) {
     G.bnd_t[p] = plan_bounds(G.t_ptr, G.t_row, G.t_ptr[gb.N], p);
     G.bnd_s[p] = plan_bounds(G.s_ptr, G.s_row, G.s_ptr[gb.N], p);
   }
@@ -278,7 +278,7 @@ size_t graph_carve(Carve& c, int64_t E, int64_t N, GraphIO* G, size_t* zero_byte
   t.tmp_s = c.take<int32_t>(cap);
   t.bsum = c.take<int32_t>(size_t(nb) * 4);
   t.dinv = c.take<float>(n);
-  const size_t ng = (cap + kPlanChunk - 1) / kPlanChunk;
+  const size_t ng = (cap + kPlanGrid - 1) / kPlanGrid;
   t.bnd_t = c.take<int2>(ng);
   t.bnd_s = c.take<int2>(ng);
   t.long_t = c.take<int32_t>(n);

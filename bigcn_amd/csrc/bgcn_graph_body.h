@@ -294,7 +294,7 @@ __device__ __forceinline__ int32_t row_of(const int32_t* ptr, int64_t N, int64_t
   return int32_t(lo);
 }
 __device__ __forceinline__ int2 plan_bounds_ptr(const int32_t* ptr, int64_t N, int64_t nnz, int64_t g) {
-  const int64_t p0 = g * kPlanChunk, p1 = p0 + kPlanChunk;
+  const int64_t p0 = g * kPlanGrid, p1 = p0 + kPlanGrid;
   int lo = int(nnz), hi = int(nnz);
   if (p0 < nnz) {
     const int32_t r = row_of(ptr, N, p0);
@@ -307,7 +307,7 @@ __device__ __forceinline__ int2 plan_bounds_ptr(const int32_t* ptr, int64_t N, i
 
 __device__ __forceinline__ int2 plan_bounds_row(const int32_t* ptr, const int32_t* row, int64_t nnz,
                                                int64_t g) {
-  const int64_t p0 = g * kPlanChunk, p1 = p0 + kPlanChunk;
+  const int64_t p0 = g * kPlanGrid, p1 = p0 + kPlanGrid;
   int lo = int(nnz), hi = int(nnz);
   if (p0 < nnz) {
     const int32_t r = row[p0];
@@ -363,7 +363,7 @@ __device__ inline void graph_rank_norm_body(const GraphBatch& gb, const GraphIO&
   }
   const int64_t p = int64_t(bid - ne - nn) * blockDim.x + threadIdx.x;
   const int64_t nnz = G.t_ptr[N];   // == s_ptr[N]
-  if (G.bnd_t && p < (G.E + N + kPlanChunk - 1) / kPlanChunk) {
+  if (G.bnd_t && p < (G.E + N + kPlanGrid - 1) / kPlanGrid) {
     // grouped: every row entry is already final (fill_nodes), read the row of a slot;
     // general: this launch is still placing entries, find the row from the pointers
     G.bnd_t[p] = graph_grouped_t(G) ? plan_bounds_row(G.t_ptr, G.t_row, nnz, p)

@@ -80,7 +80,26 @@ struct HeadArgs {
 // One wave, row b of the head: h = head_in[b][4l .. 4l+3] held by lane l.
 //   z = h W^T + bias ; logp = z - logsumexp(z) ; loss_row = -logp[y] ;
 //   dz = (softmax - onehot(y)) / B ; dhead = dz W.  Dot products butterfly-reduced.
-__device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4 h) {
+// The head's operands (W rows, bias, label) are loaded by head_load, unconditionally
+// from clamped rows, so a caller can issue them long before the row is known: loaded
+// inside the dependent chain each was one more full memory latency (C + 2 of them).
+struct HeadRegs {
+  float4 w[kMaxClasses];
+  float bias[kMaxClasses];
+  int64_t y;
+};
+__device__ inline void head_load(const HeadArgs& hd, int64_t b, HeadRegs& r) {
+  const int l = threadIdx.x & 63;
+  const int cm = hd.C - 1;
+#pragma unroll
+  for (int c = 0; c < kMaxClasses; ++c) {
+    const int cc = c < cm ? c : cm;
+    r.w[c] = ld4(hd.W + int64_t(cc) * kHeadIn + 4 * l);
+    r.bias[c] = hd.bias[cc];
+  }
+  r.y = hd.y[b];
+}
+__device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4 h, const HeadRegs& r) {
   const int l = threadIdx.x & 63;
   const int C = hd.C;
   float z[kMaxClasses];
@@ -88,11 +107,11 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
   for (int c = 0; c < kMaxClasses; ++c) {
     z[c] = 0.f;
     if (c < C) {  // C is uniform: the shuffles stay convergent
-      const float4 w = ld4(hd.W + int64_t(c) * kHeadIn + 4 * l);
+      const float4 w = r.w[c];
       float p = fmaf(h.x, w.x, fmaf(h.y, w.y, fmaf(h.z, w.z, h.w * w.w)));
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
-      z[c] = p + hd.bias[c];
+      z[c] = p + r.bias[c];
     }
   }
   float m = z[0];
@@ -104,7 +123,7 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
   for (int c = 0; c < kMaxClasses; ++c)
     if (c < C) se += expf(z[c] - m);
   const float lse = m + logf(se);
-  const int64_t yb = hd.y[b];
+  const int64_t yb = r.y;
   const bool yok = yb >= 0 && yb < C;
   if (!yok && l == 0 && hd.status) atomicOr(hd.status, 2);
   const float inv_b = 1.0f / float(B);
@@ -119,13 +138,18 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
         hd.dz[b * C + c] = g;
         if (c == yb) hd.loss_row[b] = -lp;
       }
-      dh = f4fma(g, ld4(hd.W + int64_t(c) * kHeadIn + 4 * l), dh);
+      dh = f4fma(g, r.w[c], dh);
     }
   }
   if (l == 0 && !yok) hd.loss_row[b] = 0.f;
   if (l == 0 && b == 0 && hd.in_status && hd.status && *hd.in_status) atomicOr(hd.status, *hd.in_status);
   if (l == 0 && b == 0 && hd.in_xflags && hd.status && *hd.in_xflags) atomicOr(hd.status, 4);
   st4(hd.dhead + b * kHeadIn + 4 * l, dh);
+}
+__device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4 h) {
+  HeadRegs r;
+  head_load(hd, b, r);
+  head_row(hd, b, B, h, r);
 }
 
 // ---- small reductions carried by extra blocks of a launch the caller's stream makes

@@ -29,6 +29,7 @@ struct SparseState {
   uint32_t* rbits;      // [2][N] forward's root keep masks (bit s: root non-zero s kept)
   float* csc_val;       // [N*kCap] X value of each csc_slot entry
   int32_t* zero_word = nullptr;   // zeroed by the prologue (the train step's status word)
+  int32_t* rtick = nullptr;       // [B] readout arrival counters, zeroed by the prologue
 };
 
 constexpr int kRowBlock = kCscRowBlock;   // rows per block of the CSC counting sort
@@ -77,7 +78,8 @@ struct BwdMidArgs {
   int n_root;                    // (set by launcher)
   const float *W2td, *W2bu;      // dH1
   float *dH1, *colpart;
-  int nblk_h;
+  int nblk_h;                    // dH1 blocks per direction (node splits of rows_h nodes)
+  int64_t rows_h;
   ColsumJob db2;
 };
 struct BwdTailArgs {

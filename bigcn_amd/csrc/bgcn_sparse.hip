@@ -101,6 +101,8 @@ __global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __
                                                   int nR) {
   const int blk = blockIdx.x;
   if (blk == 0 && threadIdx.x == 0 && S.zero_word) *S.zero_word = 0;
+  if (blk == 0 && S.rtick)
+    for (int64_t b = threadIdx.x; b < S.B; b += blockDim.x) S.rtick[b] = 0;
   if (blk < nT) {
     if (S.mode == 1) return;
     transpose_tile(S, blk % nTx, (blk / nTx) % 2, blk / (2 * nTx), w1td, w1bu, w2td, w2bu);
@@ -1001,10 +1003,19 @@ __global__ __launch_bounds__(256) void k_prep_f(PrepArgs a) {
 constexpr int kMidSmem = kDw2Smem > kRootPartSmem ? (kDw2Smem > kDh1Smem ? kDw2Smem : kDh1Smem)
                                                   : (kRootPartSmem > kDh1Smem ? kRootPartSmem : kDh1Smem);
 template <class TX>
-__global__ __launch_bounds__(256) void k_bwd_mid(BwdMidArgs a) {
+__global__ __launch_bounds__(256, 3) void k_bwd_mid(BwdMidArgs a) {   // 4 waves per SIMD: one round for the whole grid
   __shared__ __attribute__((aligned(16))) float smem[kMidSmem];
   BT_BEGIN
   int b = int(blockIdx.x);
+  if (b < 2 * a.nblk_h) {   // longest-lived role first
+    // the relu(H1) block of dW2 rides along when the sparse path is the one running
+    float* part = (a.S.mode != 1 && !dense_active(a.gate)) ? a.dw2_sparse.part : nullptr;
+    dh1_body(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, a.rows_h, part,
+             a.nblk_h, b % a.nblk_h, b / a.nblk_h, smem);
+    BT_END(72);
+    return;
+  }
+  b -= 2 * a.nblk_h;
   if (b < a.n_dw2) {
     dw2_body<TX>(static_cast<const TX*>(a.X), a.ldx, a.S.F, a.H1, a.dZ2, a.node_root, a.S.N, a.keep,
                  a.gate, a.dw2_dense, a.dw2_sparse, a.n_dw2_dense, b, smem);
@@ -1018,13 +1029,7 @@ __global__ __launch_bounds__(256) void k_bwd_mid(BwdMidArgs a) {
     return;
   }
   b -= a.n_root;
-  if (b < 2 * a.nblk_h) {
-    dh1_body(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, b % a.nblk_h,
-             b / a.nblk_h, smem);
-    BT_END(72);
-    return;
-  }
-  colsum_job_block(a.db2, b - 2 * a.nblk_h);
+  colsum_job_block(a.db2, b);
   BT_END(73);
 }
 
@@ -1136,7 +1141,7 @@ int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root
   const int nT = S.mode == 1 ? 0 : nTx * 2 * 4;
   const int nR = batch_part ? int((S.N + 255) / 256) : 0;
   const int nP = batch_part ? int((S.B + 1 + 255) / 256) : 0;
-  const int nZ = (nT + nR + nP == 0 && S.zero_word) ? 1 : 0;
+  const int nZ = (nT + nR + nP == 0 && (S.zero_word || S.rtick)) ? 1 : 0;
   if (nT + nR + nP + nZ == 0) return BGCN_OK;
   hipLaunchKernelGGL(k_prologue, dim3(unsigned(nT + nR + nP + nZ)), dim3(256), 0, s, S, a->td_w1, a->bu_w1,
                      a->td_w2, a->bu_w2, a->batch, a->rootindex, node_root, a->tree_ptr, nTx, nT, nR);

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_
   __shared__ float4 red[kRowsGroups][LANES];
   if (int64_t(blockIdx.x) < nchunk) {
     const int64_t g = int64_t(blockIdx.x) * kRowsGroups + grp;
-    if (g >= P.ngroups) return;
+    if (g >= (P.capacity + kPlanGrid - 1) / kPlanGrid) return;
     const int2 bd = P.plan.bnd[g];
     const int n = bd.y - bd.x;                       // <= 2 * LANES - 1; <= 0: no rows
     if (n <= 0) return;
@@ -497,7 +497,8 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   const int plan_env = pe ? atoi(pe) : -1;
   planned = planned && (plan_env == 1 || (plan_env != 0 && capmax <= kPlanMaxEntries));
   if (planned) {   // K1's plans: complete rows per chunk, long rows per block, no fixup
-    const int64_t nchunk = (gmax + kRowsGroups - 1) / kRowsGroups;
+    const int64_t gplan = (capmax + kPlanGrid - 1) / kPlanGrid;   // K1's chunk grid
+    const int64_t nchunk = (gplan + kRowsGroups - 1) / kRowsGroups;
     const int nlongblk = int(std::min<int64_t>(256, std::max<int64_t>(1, capmax / (kPlanChunk + 1))));
     hipLaunchKernelGGL(k_spmm_rows, dim3(unsigned(nchunk + nlongblk), gy), dim3(kRowsThreads), 0, stream,
                        sb, nchunk, nlongblk);
