@@ -148,6 +148,23 @@ __device__ __forceinline__ float2 conv1_row(const SparseState& S, int cnt, int32
 // per lane: the whole row, F <= kSparseMaxF), already in flight.
 static_assert(kRowChunks * 64 * 4 >= kSparseMaxF, "one pass per row");
 template <class TX> constexpr int row_chunks() { return kRowChunks * 4 / XChunk<TX>::kElems; }
+// Two ways to place a row's non-zeros in ascending column order.  Per element: a ballot
+// per element position of the 16-byte piece, every lane counting the set lanes below it
+// (E ballots per piece).  By prefix: each lane's non-zero mask, then the exclusive prefix
+// of the per-lane counts - one ballot when no lane holds two non-zeros (the common case
+// for bag-of-words rows), else by the counts' bit planes - and a loop over the lane's own
+// non-zeros.  The prefix form halves the kernel's registers (205 -> 126-138) and moves bf16
+// X at 5.9 instead of 4.3 TB/s alone on the GPU (a bf16 piece holds 8 elements: 8 ballots
+// per piece).  Beside the training chain the faster pass costs the chain more: fp32 keeps
+// the per-element form (twitter15 0.289 vs 0.298-0.316 ms per step), bf16 takes the
+// prefix form paced at one block per CU (weibo_bf16 0.646 vs 0.669 ms, synth1024_bf16
+// 0.793 vs 0.811: profiles/r02_compact_ab.txt).  BGCN_COMPACT_PREFIX: 1 bf16 only, 2 both.
+#ifndef BGCN_COMPACT_PREFIX
+#define BGCN_COMPACT_PREFIX 1
+#endif
+template <class TX> constexpr bool compact_by_prefix() {
+  return BGCN_COMPACT_PREFIX >= 2 || (BGCN_COMPACT_PREFIX == 1 && sizeof(TX) == 2);
+}
 template <bool kConv1, class TX>
 __device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, const u32x4* r,
                                             int32_t* s_col, float* s_val, float* __restrict__ Z1) {
@@ -156,6 +173,7 @@ __device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, con
   const int lane = threadIdx.x & 63;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   int cnt = 0;
+  if constexpr (!compact_by_prefix<TX>()) {
 #pragma unroll
   for (int u = 0; u < row_chunks<TX>(); ++u) {
     const u32x4 ru = r[u];                           // past the row: 0 (range-checked load)
@@ -179,6 +197,43 @@ __device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, con
         ++pos;
       }
     }
+  }
+  } else {
+#pragma unroll
+  for (int u = 0; u < row_chunks<TX>(); ++u) {
+    const u32x4 ru = r[u];                           // past the row: 0 (range-checked load)
+    uint32_t mb = 0;                                 // this lane's non-zero elements
+#pragma unroll
+    for (int c = 0; c < E; ++c) mb |= uint32_t(XC::nz(ru, c)) << c;
+    const uint64_t any = __ballot(mb != 0u);
+    if (any == 0ull) continue;                       // wave-uniform skip
+    // ascending column order: lanes below me contribute all their non-zeros first - the
+    // exclusive prefix of the per-lane counts, one ballot when no lane holds two (the
+    // common case for bag-of-words rows), else by the counts' bit planes
+    const int n = __popc(mb);
+    int pos = cnt;
+    if (__ballot(n > 1) == 0ull) {
+      pos += __popcll(any & lt);
+      cnt += __popcll(any);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {                  // n <= 8
+        const uint64_t bk = __ballot((n >> k) & 1);
+        pos += __popcll(bk & lt) << k;
+        cnt += __popcll(bk) << k;
+      }
+    }
+    const int col0 = (u * 64 + lane) * E;
+    while (mb) {
+      const int c = __builtin_ctz(mb);
+      mb &= mb - 1u;
+      if (pos < kCap) {
+        s_col[pos] = col0 + c;
+        s_val[pos] = XC::elem(ru, c);
+      }
+      ++pos;
+    }
+  }
   }
   if (lane == 0) S.nnz[i] = cnt;
   if (cnt > kCap) {
@@ -1247,8 +1302,9 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
       // measured 0.293-0.295 ms per step paced vs 0.303-0.306 unpaced (twitter15; 224-288
       // blocks within 1%, 512 worse than either).  With the shorter chain of 512-thread
       // aggregation / tail blocks, 384 blocks: 0.2964-0.2966 vs 0.304-0.308 at 256
-      // (profiles/r02_pace_ab.txt).  bf16 X (twice the rows per byte) keeps the full
-      // grid: paced it lengthens the side lane (synth1024_bf16 0.90 vs 0.87 ms).
+      // (profiles/r02_pace_ab.txt).  bf16 X (the prefix compaction, compact_by_prefix):
+      // one block per CU - 192 / 256 / 320 / 512 / 1024 blocks / the full grid: weibo_bf16
+      // 0.667 / 0.646 / 0.661 / 0.709 / 0.688 / 0.697 ms (profiles/r02_compact_ab.txt).
       // BGCN_PREP_BLOCKS (read per call) overrides: 0 = full grid, n = n blocks.
     static const int ncu = [] {
       int dev = 0, n = 0;
@@ -1259,7 +1315,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
     }();
     const bool bf = bt->x_dtype == BGCN_DTYPE_BF16;
     a.ncomp = xp ? int(grid_for(N, bf ? 8 : 4)) : 0;
-    int cap = bf ? 0 : ncu + ncu / 2;
+    int cap = bf ? (compact_by_prefix<bf16_t>() ? ncu : 0) : ncu + ncu / 2;
     const char* e = std::getenv("BGCN_PREP_BLOCKS");
     if (e) cap = atoi(e);
     if (cap > 0) a.ncomp = std::min(a.ncomp, cap);
