@@ -177,32 +177,34 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
 
 // dH1[i][d*H + c] = (dZ2_d[i] . W2_d[:, c]) * keep(d,i,c) * s * [H1 > 0], c < H,
 // + block partial column sums, over `rows` consecutive nodes (64-row tiles) of direction
-// d per block.  A 64-row x 64-column tile on the fp32 MFMA (32x32x2): four waves as
-// 2 row halves x 2 column halves, K = H = 64 in 32 steps.  The K order is permuted (lane
-// half h owns k in [32h, 32h+32)) so each lane's dZ2 operand is one contiguous 128-byte
-// run.  dZ2 tiles and W2[:, :64] are staged in LDS with coalesced float4 loads (rows
-// padded to 65 floats: conflict-free operand reads).
+// d per block.  A 64-row x 64-column tile per 256-thread block, four waves as 2 row halves
+// x 2 column halves, on the bf16 MFMA in split form (mfma_x3, bgcn_common.h: this launch
+// was bound by the f32-input MFMA, 64 cycles per 32x32x2).  The dZ2 tile and W2[:, :64]^T
+// are staged in LDS already split (hi / lo bf16, rows of 72 = 16-byte aligned), so every
+// operand fragment of dH1 is one 16-byte LDS read.
 //
 // dw2part != nullptr (the sparse path, gated off when the dense path runs): the same
 // block also forms the relu(H1) block of dW2 over its rows,
 //   part[d][bx][o][c] = sum_i dZ2_d[i][o] * keep(d,i,c) * s * relu(H1_d[i][c]),
 // from the operands the dH1 tile already holds: each lane's 16 (row, c) values of H1 and
-// of the keep words are exactly its B operands of a 32x32x2 chain whose K order is the
-// accumulator row order acc_row(q, h); the dZ2^T operands are read from the staged tile
-// in that order.  Two row-half waves are combined in LDS (fixed order).  One block per
-// node split (the tail reduces the splits), so the separate dW2 role - its own loads of
-// dZ2 and H1 and its own keep hashing - is gone from the launch.
+// of the keep words, in the accumulator row order acc_row(q, h), are its B fragments of
+// two 32x32x16 k-steps (element j of step s: row 16s + 8(j>>2) + 4h + (j&3)); the dZ2^T
+// fragments are read from the staged tile in that row order.  Two row-half waves are
+// combined in LDS (fixed order).  One block per node split (the tail reduces the splits).
 // Device body, 256 threads; smem: kDh1Smem floats.
 constexpr int kDh1Rows = 64;
-constexpr int kDh1Smem = kDh1Rows * (H + 1) + H * (H + 1) + 2 * H;
+constexpr int kDsLd = H + 8;   // bf16 row stride of the staged, split tiles
+constexpr int kDh1Smem = (4 * kDh1Rows * kDsLd) / 2 + 2 * H;
 __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __restrict__ H1,
                                 const float* __restrict__ W2td, const float* __restrict__ W2bu,
                                 int64_t ldw2, int64_t N, KeepSrc keep, float* __restrict__ dH1,
                                 float* __restrict__ colpart, int64_t rows, float* __restrict__ dw2part,
                                 int nsplit, int bx, int d, float* smem) {
-  float* Ds = smem;
-  float* Ws = smem + kDh1Rows * (H + 1);
-  float (*red)[H] = reinterpret_cast<float (*)[H]>(smem + kDh1Rows * (H + 1) + H * (H + 1));
+  __bf16* Dh = reinterpret_cast<__bf16*>(smem);   // dZ2 tile [row][o], hi / lo
+  __bf16* Dl = Dh + kDh1Rows * kDsLd;
+  __bf16* Wh = Dl + kDh1Rows * kDsLd;             // W2[:, :64]^T [c][o], hi / lo
+  __bf16* Wl = Wh + H * kDsLd;
+  float (*red)[H] = reinterpret_cast<float (*)[H]>(smem + 2 * kDh1Rows * kDsLd);
   const float* W2 = d == 0 ? W2td : W2bu;
   const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int rh = wid & 1, ch = wid >> 1;
@@ -236,10 +238,11 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
     }
     gload(beg);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 4; ++u) {     // W2[o = rr][c = q + t] -> W^T[c][o]
       const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      float* ww = &Ws[rr * (H + 1) + q];
-      ww[0] = wv[u].x; ww[1] = wv[u].y; ww[2] = wv[u].z; ww[3] = wv[u].w;
+      const float v[4] = {wv[u].x, wv[u].y, wv[u].z, wv[u].w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) split_bf16(v[t], Wh[(q + t) * kDsLd + rr], Wl[(q + t) * kDsLd + rr]);
     }
   }
   f32x16 pw0 = {}, pw1 = {};   // dW2 partial: o in [0, 32) / [32, 64), columns ch*32 + r
@@ -250,28 +253,41 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      float* dd = &Ds[rr * (H + 1) + q];
-      dd[0] = dv[u].x; dd[1] = dv[u].y; dd[2] = dv[u].z; dd[3] = dv[u].w;
+      const float v[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) split_bf16(v[k], Dh[rr * kDsLd + q + k], Dl[rr * kDsLd + q + k]);
     }
-    // this tile's per-lane operands, reduced before the next tile's loads reuse hv:
-    // a2 = keep * s * relu(H1) (dW2's B operand), bit q of km = kept and H1 > 0 (dH1)
-    float a2[16];
+    // this tile's per-lane operands: a2 = keep * s * relu(H1) split (dW2's B fragments in
+    // accumulator row order), bit q of km = kept and H1 > 0 (dH1)
+    bf16x8 a2h[2], a2l[2];
     uint32_t km = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
       const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(i, N - 1)), uint32_t(c >> 5));
       const bool kept = ((wd >> (c & 31)) & 1u) && i < N;
-      a2[q] = kept ? sc * fmaxf(hv[q], 0.f) : 0.f;
+      __bf16 x, y;
+      split_bf16(kept ? sc * fmaxf(hv[q], 0.f) : 0.f, x, y);
+      a2h[q >> 3][q & 7] = x;
+      a2l[q >> 3][q & 7] = y;
       km |= uint32_t(kept && hv[q] > 0.f) << q;
+      if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // four keep hashes in flight
     }
     __syncthreads();
-    // lane half h owns k in [32h, 32h + 32) (permuted K, same for A and B)
-    const float* ap = &Ds[(rh * 32 + r) * (H + 1) + 32 * h];
-    const float* bp = &Ws[(32 * h) * (H + 1) + c];
+    // dH1: A = dZ2 rows (row rh*32 + r, o = 16s + 8h + j), B = W2^T (column c)
     f32x16 acc = {};
+    const __bf16* ah = &Dh[(rh * 32 + r) * kDsLd + 8 * h];
+    const __bf16* al = &Dl[(rh * 32 + r) * kDsLd + 8 * h];
+    const __bf16* bh = &Wh[c * kDsLd + 8 * h];
+    const __bf16* bl = &Wl[c * kDsLd + 8 * h];
 #pragma unroll
-    for (int kk = 0; kk < 32; ++kk) acc = mfma32x32x2(ap[kk], bp[kk * (H + 1)], acc);
+    for (int s = 0; s < 4; ++s) {
+      acc = mfma_x3(*reinterpret_cast<const bf16x8*>(ah + 16 * s), *reinterpret_cast<const bf16x8*>(al + 16 * s),
+                    *reinterpret_cast<const bf16x8*>(bh + 16 * s), *reinterpret_cast<const bf16x8*>(bl + 16 * s),
+                    acc);
+      if (s == 1) __builtin_amdgcn_sched_barrier(0);   // two k-steps' fragments live at a time
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -282,16 +298,24 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
       }
     }
     if (want_dw2) {
-      // B[k = acc_row(q, h)][c] = a2[q] (this lane's); A[o][k] = dZ2[row0 + k][o] from LDS
+      // dW2: A = dZ2^T (o = r / 32 + r, rows in the a2 fragments' order), B = a2
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int k = (q & 3) + 8 * (q >> 2) + 4 * h;
-        const float* zr = &Ds[(rh * 32 + k) * (H + 1)];
-        pw0 = mfma32x32x2(zr[r], a2[q], pw0);
-        pw1 = mfma32x32x2(zr[32 + r], a2[q], pw1);
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 z0h, z0l, z1h, z1l;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = rh * 32 + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+          z0h[j] = Dh[k * kDsLd + r];
+          z0l[j] = Dl[k * kDsLd + r];
+          z1h[j] = Dh[k * kDsLd + 32 + r];
+          z1l[j] = Dl[k * kDsLd + 32 + r];
+        }
+        pw0 = mfma_x3(z0h, z0l, a2h[s], a2l[s], pw0);
+        pw1 = mfma_x3(z1h, z1l, a2h[s], a2l[s], pw1);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    __syncthreads();   // Ds is rewritten by the next tile
+    __syncthreads();   // the staged tile is rewritten by the next tile
     if (t + 1 < ntile) gload(blk0 + kDh1Rows);
   }
   cs += __shfl_xor(cs, 32);
@@ -300,8 +324,8 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
   if (threadIdx.x < H)
     colpart[int64_t(bx) * (2 * H) + d * H + threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x];
   if (!want_dw2) return;
-  // combine the two row halves: rh = 1 parks its partial in LDS (Ds), rh = 0 adds and stores
-  float* P = Ds;   // [64 o][64 c]
+  // combine the two row halves: rh = 1 parks its partial in LDS, rh = 0 adds and stores
+  float* P = smem;   // [64 o][64 c] over the staged tiles (free after the loop's barrier)
   if (rh == 1) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {

@@ -117,6 +117,28 @@ __device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// fp32 products on the bf16 MFMA.  The f32-input MFMA issues at the FP32 vector rate, 1/16
+// of the bf16 one; x = hi + lo with hi = bf16(x), lo = bf16(x - hi) keeps 16 of x's 24
+// mantissa bits, and a.b ~ ah.bh + ah.bl + al.bh (al.bl and the two residuals dropped,
+// each <= 2^-18 |a b|): ~1e-5 relative per product, accumulated in fp32.  Used where the
+// result feeds only linear steps (the backward's dH1 / dW2 products): a forward product
+// that feeds a relu flips its sign for entries near zero (measured on conv2: not used).
+// Lane map of 32x32x16: lane (h = l >> 5, r = l & 31) holds A[r][8h + j] and B[8h + j][r].
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {
+  hi = __bf16(x);
+  lo = __bf16(x - float(hi));
+}
+// acc += a.b for split operands (three bf16 products, small terms first)
+__device__ __forceinline__ f32x16 mfma_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 c) {
+  c = mfma_bf16(al, bh, c);
+  c = mfma_bf16(ah, bl, c);
+  return mfma_bf16(ah, bh, c);
+}
+
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 // streaming (non-temporal) 16-byte load: data read once, kept out of the caches' LRU

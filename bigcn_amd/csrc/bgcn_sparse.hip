@@ -592,26 +592,37 @@ __device__ inline void root_part_body(const SparseState& S, const float* __restr
   }
   __syncthreads();
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
-  const int64_t n0 = beg + wv * 64 + 32 * h;
   f32x16 acc0 = {}, acc1 = {};
   if (beg + wv * 64 < end) {
+    // bf16 MFMA: A = the 0/1 keep bits (exact in bf16), B = dZ2 split hi + lo (two
+    // products, error <= 2^-18 relative); k-step s takes nodes n0 + 16s + 8h + j
+    const int64_t n0 = beg + wv * 64;
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      float b0[16], b1[16], av[16];
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 a, b0h, b0l, b1h, b1l;
+      float z0[8], z1[8];
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const int64_t node = n0 + half * 16 + kk;
+      for (int j = 0; j < 8; ++j) {
+        const int64_t node = n0 + 16 * s + 8 * h + j;
+        const float* zr = dZ2 + (node < end ? node : beg) * (2 * H) + d * H;
+        z0[j] = zr[r32];
+        z1[j] = zr[32 + r32];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t node = n0 + 16 * s + 8 * h + j;
         const bool ok = node < end;
-        const float* zr = dZ2 + (ok ? node : beg) * (2 * H) + d * H;
-        b0[kk] = ok ? zr[r32] : 0.f;
-        b1[kk] = ok ? zr[32 + r32] : 0.f;
-        av[kk] = (ok && ((bits[node - beg] >> r32) & 1u)) ? 1.f : 0.f;
+        a[j] = __bf16((ok && ((bits[node - beg] >> r32) & 1u)) ? 1.f : 0.f);
+        __bf16 x, y;
+        split_bf16(ok ? z0[j] : 0.f, x, y);
+        b0h[j] = x; b0l[j] = y;
+        split_bf16(ok ? z1[j] : 0.f, x, y);
+        b1h[j] = x; b1l[j] = y;
       }
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        acc0 = mfma32x32x2(av[kk], b0[kk], acc0);
-        acc1 = mfma32x32x2(av[kk], b1[kk], acc1);
-      }
+      acc0 = mfma_bf16(a, b0l, acc0);
+      acc0 = mfma_bf16(a, b0h, acc0);
+      acc1 = mfma_bf16(a, b1l, acc1);
+      acc1 = mfma_bf16(a, b1h, acc1);
     }
   }
 #pragma unroll
