@@ -562,7 +562,7 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
     sp.item_tree = prep->item_tree; sp.item_chunk = prep->item_chunk; sp.tree_item0 = prep->tree_item0;
     sp.hist = prep->hist; sp.col_total = prep->col_total;
     sp.col_start = prep->col_start; sp.col_end = prep->col_end;
-    sp.csc_slot = prep->csc_slot; sp.csc_val = prep->csc_val;
+    sp.csc = prep->csc;
   }
   // dense kernels run when feat_mode == dense (no gate) or when the sparse path overflowed
   // (auto); under BGCN_FEAT_SPARSE they are not launched (dense_launched)

@@ -296,8 +296,7 @@ struct Prepared {
   int32_t *x_flags, *x_nnz, *x_cols;
   float* x_vals;
   int32_t *hist, *col_total, *col_start, *col_end;
-  uint32_t* csc_slot;
-  float* csc_val;
+  uint2* csc;   // [N * kCap] (slot, value bits) grouped by column, rows in order
   void* gws;
   size_t gws_bytes;
   int64_t *td_drop, *bu_drop;            // [2, E] masked DropEdge lists (device DropEdge)

@@ -25,9 +25,9 @@ struct SparseState {
   int32_t* hist;        // [R][F] per-row-block column counts -> prefixes (R = N / kRowBlock)
   int32_t* col_total;   // [F]
   int32_t *col_start, *col_end;  // [F]
-  uint32_t* csc_slot;   // [N*kCap] slots (i*kCap + s) grouped by column, rows in order
+  uint2* csc;           // [N*kCap] (slot i*kCap + s, value bits) grouped by column, rows in
+                        // order: one 8-byte store per placed entry (the placement scatters)
   uint32_t* rbits;      // [2][N] forward's root keep masks (bit s: root non-zero s kept)
-  float* csc_val;       // [N*kCap] X value of each csc_slot entry
   int32_t* zero_word = nullptr;   // zeroed by the prologue (the train step's status word)
   int32_t* rtick = nullptr;       // [B] readout arrival counters, zeroed by the prologue
 };

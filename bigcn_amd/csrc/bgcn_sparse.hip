@@ -780,11 +780,13 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
   const int s = threadIdx.x % kCap;
   constexpr int kPer = kRowBlock * kCap / 256;   // 32
   int32_t col[kPer], nn[kPer];
+  float val[kPer];
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {   // issue all 64 loads first ...
+  for (int k = 0; k < kPer; ++k) {   // issue all 96 loads first ...
     const int64_t ic = min<int64_t>(r0 + threadIdx.x / kCap + 8 * k, S.N - 1);
     nn[k] = S.nnz[ic];
     col[k] = S.cols[ic * kCap + s];
+    val[k] = S.vals[ic * kCap + s];
   }
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {   // ... then mask the padding slots
@@ -815,8 +817,7 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
         const uint32_t m = rows[cc];
         rank[k] = __popc(m & ((1u << rr[k]) - 1u));
         const int64_t i = r0 + bt * kBatchRows + rr[k];
-        S.csc_slot[cnt[cc] + rank[k]] = uint32_t(i * kCap + s);
-        S.csc_val[cnt[cc] + rank[k]] = S.vals[i * kCap + s];
+        S.csc[cnt[cc] + rank[k]] = make_uint2(uint32_t(i * kCap + s), __float_as_uint(val[4 * bt + k]));
       }
     }
     __syncthreads();
@@ -863,8 +864,9 @@ __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ 
     const int64_t beg = S.col_start[c], end = S.col_end[c];
     for (int64_t u0 = beg + 64 * part; u0 < end; u0 += 64 * kDw1Split) {
       const int64_t u = min<int64_t>(u0 + lane, end - 1);   // clamped: duplicates, x masked
-      const uint32_t slot = S.csc_slot[u];
-      const float xv = S.csc_val[u];
+      const uint2 ent = S.csc[u];
+      const uint32_t slot = ent.x;
+      const float xv = __uint_as_float(ent.y);
       const int n = int(min<int64_t>(64, end - u0));
       const float x_l = lane < n ? xv : 0.f;
       const int32_t i_l = int32_t(slot / kCap);
@@ -921,7 +923,7 @@ __device__ inline void rootcols_body(const SparseState& S, const int32_t* __rest
     for (int64_t u0 = beg; u0 < end; u0 += 64) {
       const int64_t u = u0 + lane;
       const bool ok = u < end;
-      const uint32_t slot = S.csc_slot[ok ? u : beg];
+      const uint32_t slot = S.csc[ok ? u : beg].x;
       const int32_t i_l = int32_t(slot / kCap);
       const int32_t s_l = int32_t(slot % kCap);
       const bool root_l = ok && node_root[i_l] == i_l;
@@ -1187,9 +1189,8 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   t.col_total = c.take<int32_t>(size_t(F));
   t.col_start = c.take<int32_t>(size_t(F));
   t.col_end = c.take<int32_t>(size_t(F));
-  t.csc_slot = c.take<uint32_t>(slots);
+  t.csc = c.take<uint2>(slots);
   t.rbits = c.take<uint32_t>(size_t(2) * N);
-  t.csc_val = c.take<float>(slots);
   if (S) {
     t.mode = S->mode;
     t.flags = S->flags;
@@ -1267,7 +1268,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   S.flags = p.x_flags; S.nnz = p.x_nnz; S.cols = p.x_cols; S.vals = p.x_vals;
   S.item_tree = p.item_tree; S.item_chunk = p.item_chunk; S.tree_item0 = p.tree_item0;
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
-  S.csc_slot = p.csc_slot; S.csc_val = p.csc_val;
+  S.csc = p.csc;
   a.batch = bt->batch; a.rootindex = bt->rootindex;
   a.node_root = p.node_root; a.tree_ptr = p.tree_ptr; a.status = p.status;
   a.X = bt->x; a.ldx = bt->ldx;
@@ -1371,7 +1372,7 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
   S.flags = p.x_flags; S.nnz = p.x_nnz; S.cols = p.x_cols; S.vals = p.x_vals;
   S.item_tree = p.item_tree; S.item_chunk = p.item_chunk; S.tree_item0 = p.tree_item0;
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
-  S.csc_slot = p.csc_slot; S.csc_val = p.csc_val;
+  S.csc = p.csc;
   if (!(part & 1)) return mode == 1 ? BGCN_OK : sparse_csc(S, s);
   const int nR = int((N + 255) / 256), nP = int((B + 1 + 255) / 256);
   hipLaunchKernelGGL(k_prologue, dim3(unsigned(nR + nP)), dim3(256), 0, s, S, nullptr, nullptr,

@@ -100,8 +100,7 @@ size_t carve_prepared(Carve& c, int64_t N, int64_t B, int64_t F, int64_t Etd, in
   t.col_total = c.take<int32_t>(size_t(F));
   t.col_start = c.take<int32_t>(size_t(F));
   t.col_end = c.take<int32_t>(size_t(F));
-  t.csc_slot = c.take<uint32_t>(size_t(N) * BGCN_SPARSE_CAP);
-  t.csc_val = c.take<float>(size_t(N) * BGCN_SPARSE_CAP);
+  t.csc = c.take<uint2>(size_t(N) * BGCN_SPARSE_CAP);
   t.td_drop = c.take<int64_t>(size_t(2 * Etd));
   t.bu_drop = c.take<int64_t>(size_t(2 * Ebu));
   t.dws_bytes = drop_ws_size(B);
