@@ -62,10 +62,29 @@ __device__ __forceinline__ bool edge_kept(const int64_t* ei, int64_t E, int64_t 
 // count: edge e = bid * blockDim + thread.  Run-start counters are wave-aggregated
 // (ballot + popcount, one atomic per wave): in a propagation tree nearly every edge
 // starts a run, and per-edge atomics on one address serialise.
+// Per-node counts are wave-aggregated too: the edges of one node come in runs (a BU star
+// root's children, a TD parent's), and a run inside a wave adds its length with one
+// atomic from its first lane instead of one atomic per edge on the same address.
+__device__ __forceinline__ void add_runs(int32_t* __restrict__ cnt, bool keep, int64_t key) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t pkey = __shfl_up(key, 1, kWave);
+  const bool pkeep = __shfl_up(int(keep), 1, kWave) != 0;
+  const bool lead = keep && (lane == 0 || !pkeep || pkey != key);
+  const uint64_t km = __ballot(keep), lm = __ballot(lead);
+  if (lead) {
+    const uint64_t after = lane == kWave - 1 ? 0ull : (lm >> (lane + 1)) << (lane + 1);
+    const int next = after ? __builtin_ctzll(after) : kWave;   // the next run's first lane
+    const uint64_t span = (next == kWave ? ~0ull : ((1ull << next) - 1ull)) & ~((1ull << lane) - 1ull);
+    atomicAdd(&cnt[key], __popcll(km & span));
+  }
+}
+
 __device__ inline void graph_count_body(const GraphBatch& gb, const GraphIO& G, int bid) {
   const int64_t e = int64_t(bid) * blockDim.x + threadIdx.x;
   const int64_t N = gb.N;
   bool start_t = false, start_s = false;
+  bool kept = false;
+  int64_t ksrc = 0, kdst = 0;
   if (e < G.E) {
     int64_t src, dst;
     bool valid;
@@ -85,8 +104,9 @@ __device__ inline void graph_count_body(const GraphBatch& gb, const GraphIO& G, 
           atomicOr(&G.flags[2], 1);
       }
     } else {
-      atomicAdd(&G.cnt_t[dst], 1);
-      atomicAdd(&G.cnt_s[src], 1);
+      kept = true;
+      ksrc = src;
+      kdst = dst;
       int64_t psrc = -1, pdst = -1;
       if (e > 0) {
         bool pv;
@@ -98,6 +118,8 @@ __device__ inline void graph_count_body(const GraphBatch& gb, const GraphIO& G, 
       if (start_s) G.run_s[src] = int32_t(e);
     }
   }
+  add_runs(G.cnt_t, kept, kdst);
+  add_runs(G.cnt_s, kept, ksrc);
   const int nt = __popcll(__ballot(start_t)), ns = __popcll(__ballot(start_s));
   if ((threadIdx.x & (kWave - 1)) == 0) {
     if (nt) atomicAdd(&G.flags[0], nt);
