@@ -675,18 +675,24 @@ __global__ __launch_bounds__(kRowBlock) void k_csc_hist(SparseState S) {
 
 // 64 columns x 4 row-block quarters per block; hist[r][c] becomes the exclusive prefix
 // of column c over row blocks < r.  Loads in groups of 8 (independent).
+// per column: exclusive prefix of the row-block counts.  A 256-thread block takes
+// kPrefixCols columns x kPrefixSegs segments of the row blocks (each segment summed, then
+// rewritten as prefixes, eight loads in flight); the segment totals are combined in
+// segment order.  16 x 16: a Weibo / 1024-node batch has 370-460 row blocks, and with 4
+// segments of a column per thread the two passes took ~30 dependent load rounds.
+constexpr int kPrefixCols = 16, kPrefixSegs = 256 / kPrefixCols;
 __device__ inline void csc_prefix_body(const SparseState& S, int R, int bid) {
   if (!use_sparse(S)) return;
-  __shared__ int32_t part[4][64];
-  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int64_t c = min<int64_t>(int64_t(bid) * 64 + cl, S.F - 1);
-  const bool live = int64_t(bid) * 64 + cl < S.F;
-  const int rq = (R + 3) / 4, rb = q * rq, re = min(R, rb + rq);
+  __shared__ int32_t part[kPrefixSegs][kPrefixCols];
+  const int cl = threadIdx.x % kPrefixCols, q = threadIdx.x / kPrefixCols;
+  const int64_t c = min<int64_t>(int64_t(bid) * kPrefixCols + cl, S.F - 1);
+  const bool live = int64_t(bid) * kPrefixCols + cl < S.F;
+  const int rq = (R + kPrefixSegs - 1) / kPrefixSegs, rb = q * rq, re = min(R, rb + rq);
   int32_t sum = 0;
   for (int r0 = rb; r0 < re; r0 += 8) {
     int32_t v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = S.hist[int64_t(min(r0 + u, re - 1)) * S.F + c];
+    for (int u = 0; u < 8; ++u) v[u] = S.hist[int64_t(max(min(r0 + u, re - 1), 0)) * S.F + c];
 #pragma unroll
     for (int u = 0; u < 8; ++u) sum += r0 + u < re ? v[u] : 0;
   }
@@ -697,14 +703,14 @@ __device__ inline void csc_prefix_body(const SparseState& S, int R, int bid) {
   for (int r0 = rb; r0 < re; r0 += 8) {
     int32_t v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = S.hist[int64_t(min(r0 + u, re - 1)) * S.F + c];
+    for (int u = 0; u < 8; ++u) v[u] = S.hist[int64_t(max(min(r0 + u, re - 1), 0)) * S.F + c];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (live && r0 + u < re) S.hist[int64_t(r0 + u) * S.F + c] = run;
       run += r0 + u < re ? v[u] : 0;
     }
   }
-  if (live && q == 3) S.col_total[c] = run;
+  if (live && q == kPrefixSegs - 1) S.col_total[c] = run;
 }
 __global__ __launch_bounds__(256) void k_csc_prefix(SparseState S, int R) {
   csc_prefix_body(S, R, int(blockIdx.x));
@@ -1247,7 +1253,7 @@ int sparse_csc(SparseState& S, hipStream_t s) {
   const int R = int((S.N + kRowBlock - 1) / kRowBlock);
   hipLaunchKernelGGL(k_csc_hist, dim3(unsigned(R)), dim3(kRowBlock), size_t(S.F) * sizeof(int32_t), s, S);
   BGCN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_csc_prefix, dim3(grid_for(S.F, 64)), dim3(256), 0, s, S, R);
+  hipLaunchKernelGGL(k_csc_prefix, dim3(grid_for(S.F, kPrefixCols)), dim3(256), 0, s, S, R);
   BGCN_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_csc_colscan, dim3(1), dim3(1024), 0, s, S);
   BGCN_CHECK_LAUNCH();
@@ -1335,7 +1341,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   a.nce = graph_edge_blocks(Emax);
   a.R = xp ? int((N + kRowBlock - 1) / kRowBlock) : 0;
   a.ntile = int(graph_scan_tiles(N));
-  a.nprefix = xp ? int(grid_for(F, 64)) : 0;
+  a.nprefix = xp ? int(grid_for(F, kPrefixCols)) : 0;
   a.ne = graph_edge_blocks(Emax);
   a.nn = graph_node_blocks(N);
   a.np = graph_pos_blocks(Emax, N);
