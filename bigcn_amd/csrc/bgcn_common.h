@@ -132,6 +132,25 @@ __device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {
   hi = __bf16(x);
   lo = __bf16(x - float(hi));
 }
+// fp32-grade form (for products that feed a relu, where 1e-5 relative flips signs of
+// entries near zero): x = hi + mid + lo keeps all 24 bits, and a.b takes the six products
+// down to 2^-16 |a b| (al.bh, am.bm, ah.bl, am.bh, ah.bm, ah.bh, small terms first) - the
+// dropped ones are below 2^-24 |a b|, fp32's own rounding.
+__device__ __forceinline__ void split3_bf16(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = __bf16(x);
+  const float r = x - float(hi);
+  mid = __bf16(r);
+  lo = __bf16(r - float(mid));
+}
+__device__ __forceinline__ f32x16 mfma_x6(bf16x8 ah, bf16x8 am, bf16x8 al, bf16x8 bh, bf16x8 bm,
+                                          bf16x8 bl, f32x16 c) {
+  c = mfma_bf16(al, bh, c);
+  c = mfma_bf16(am, bm, c);
+  c = mfma_bf16(ah, bl, c);
+  c = mfma_bf16(am, bh, c);
+  c = mfma_bf16(ah, bm, c);
+  return mfma_bf16(ah, bh, c);
+}
 // acc += a.b for split operands (three bf16 products, small terms first)
 __device__ __forceinline__ f32x16 mfma_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x16 c) {
   c = mfma_bf16(al, bh, c);

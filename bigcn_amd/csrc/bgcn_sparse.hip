@@ -395,17 +395,23 @@ __global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __res
 // conv2 lin on the sparse path, one work item (<= kChunk nodes of one tree) per block:
 //   Z2_d[i] = [keep * 2 relu(H1_d[i]) | kept_d(i, s)] . [W2_d^T[0:64] ; Wr_b]
 //   Wr_b[s] = 2 relu(x_root,col_s) W2_d^T[64 + col_s]      (s < nnz(root), else 0)
-// i.e. one [nodes x (64 + nnz(root))] x [. x 64] product on the fp32 MFMA per item, with
-// the dropout-masked relu(H1) and the per-node root keep bits (0/1) generated in
-// registers and the tree's root block of W2^T staged in LDS.  The root keep masks are
-// stored in S.rbits for the dW2 root columns of the backward.  Each wave stages its
-// 32-row H1 tile through LDS (coalesced).  K order per lane half h: H1 columns
-// [32h, 32h+32), then root slots 2j + h (so each lane hashes only its own slots and the
-// steps past the root's non-zeros are skipped); B rows 32 apart for the two halves with
-// an odd row stride (bank-conflict free).
-constexpr int kC2Ld = H + 1;         // odd row stride: rows 32 apart hit disjoint banks
-constexpr int kC2Slot0 = H;          // slot rows: even slots at 64 + s/2, odd at 96 + s/2
-constexpr int kC2Rows = H + 2 * (kCap / 2) + 16;   // 112 (rows 80..95 unused padding)
+// i.e. one [nodes x (64 + nnz(root))] x [. x 64] product per item, with the dropout-masked
+// relu(H1) and the per-node root keep bits (0/1) generated in registers and the block's B
+// operand staged once in LDS.  The root keep masks are stored in S.rbits for the dW2 root
+// columns of the backward.  Each wave stages its 32-row H1 tile through LDS (coalesced).
+//
+// The product runs on the bf16 MFMA in the fp32-grade split form (mfma_x6, bgcn_common.h):
+// the f32-input MFMA issues at the FP32 vector rate and bounds this kernel at Weibo /
+// 1024-node sizes; the three-product form (~1e-5 relative) flips relu'(H2) for entries
+// near zero, hence six.  B is staged transposed and pre-split (hi / mid / lo bf16 [o][k]):
+// k < 64 the H1 columns (W2^T rows), k in [64, 96) the root slots (slot 2j + h at
+// 64 + 16h + j, value 2 relu(x_root) W2^T[64 + col]).  K order: lane half h owns H1
+// columns [32h, 32h + 32) (k-step s: columns 32h + 8s + j) and root slots 2j + h (k-step
+// t: slots 2(8t + j) + h), so each lane hashes only its own keep words and the steps past
+// the root's non-zeros are skipped; the keep bits are exact in bf16 (three products).
+constexpr int kC2Ld = H + 1;             // f32 row stride of the staged H1 tiles
+constexpr int kC2K = H + kCap;           // B rows: 64 H1 columns + 32 root slot positions
+constexpr int kC2Ld16 = kC2K + 8;        // bf16 row stride of the split B (16-byte aligned)
 __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float* __restrict__ H1,
                                                       const int32_t* __restrict__ tree_ptr,
                                                       const int64_t* __restrict__ rootindex,
@@ -414,7 +420,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   if (!use_sparse(S)) return;
   const int item = blockIdx.x;
   if (item >= S.tree_item0[S.B]) return;
-  __shared__ float Bs[kC2Rows * kC2Ld];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3][H * kC2Ld16];   // hi, mid, lo
   __shared__ float Hs[4 * 32 * kC2Ld];
   __shared__ uint32_t rk[kCap];
   const int d = blockIdx.y;
@@ -423,28 +429,37 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   const int64_t end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
   const int64_t r = rootindex[b];
   const int rn = S.nnz[r];
-  const int mh = (rn + 1) / 2;   // root slot steps per lane half
+  const int mh = (rn + 1) / 2;   // root slot pairs (slot 2j + h, j < mh)
   const float sc = keep.scale();
   const int64_t K2 = S.F + H;
   const float* w2t = S.w2t + int64_t(d) * K2 * H;
   // B fill with unconditional loads (clamped slot / column; see k_dh1), selects after
   if (threadIdx.x < kCap)
     rk[threadIdx.x] = threadIdx.x < rn ? uint32_t(H + S.cols[r * kCap + threadIdx.x]) : 0u;
-  for (int e = threadIdx.x; e < H * (H / 4); e += 256) {
+  for (int e = threadIdx.x; e < H * (H / 4); e += 256) {   // W2^T rows k < 64, 4 outputs each
     const int k = e >> 4, q = (e & 15) * 4;
     const float4 v = ld4(w2t + int64_t(k) * H + q);
-    float* dst = &Bs[k * kC2Ld + q];
-    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int o = (q + u) * kC2Ld16 + k;
+      split3_bf16(vv[u], Bs[0][o], Bs[1][o], Bs[2][o]);
+    }
   }
-  for (int e = threadIdx.x; e < kCap * (H / 4); e += 256) {
+  for (int e = threadIdx.x; e < kCap * (H / 4); e += 256) {  // root slots (zero past rn)
     const int s = e >> 4, q = (e & 15) * 4;
     const int64_t slot = r * kCap + s;              // always inside the row's ELL list
     const int32_t col = min(max(S.cols[slot], 0), int32_t(S.F - 1));
     const float val = S.vals[slot];
     const float4 w = ld4(w2t + int64_t(H + col) * H + q);
     const float av = s < rn ? sc * fmaxf(val, 0.f) : 0.f;
-    float* dst = &Bs[(kC2Slot0 + (s & 1) * 32 + (s >> 1)) * kC2Ld + q];
-    dst[0] = av * w.x; dst[1] = av * w.y; dst[2] = av * w.z; dst[3] = av * w.w;
+    const float vv[4] = {av * w.x, av * w.y, av * w.z, av * w.w};
+    const int k = H + (s & 1) * (kCap / 2) + (s >> 1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int o = (q + u) * kC2Ld16 + k;
+      split3_bf16(vv[u], Bs[0][o], Bs[1][o], Bs[2][o]);
+    }
   }
   __syncthreads();
   BT_MARK(2, 0);
@@ -475,14 +490,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
     if (t == wv) BT_MARK(2, 1);
     const float* hrow = &hs[r32 * kC2Ld + 32 * h];
     const uint32_t ni = uint32_t(ok ? i : beg);
-    // K order (lane half h): kk < 32 -> H1 column 32h + kk (keep word h); kk >= 32 ->
-    // root slot 2(kk - 32) + h.  Each lane hashes only its own slots, and the steps past
-    // the root's non-zeros (uniform per block) are skipped.
     const uint32_t wd = keep.get(uint32_t(d), ni, uint32_t(h));
-    float a[48];
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk)
-      a[kk] = ((wd >> kk) & 1u) ? sc * fmaxf(hrow[kk], 0.f) : 0.f;
     uint32_t m = 0;
 #pragma unroll
     for (int j = 0; j < kCap / 2; ++j) {
@@ -493,25 +501,51 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
         bit = sl < rn ? (keep.get(uint32_t(d), ni, k >> 5) >> (k & 31)) & 1u : 0u;
       }
       m |= bit << (2 * j + h);
-      a[32 + j] = bit ? 1.f : 0.f;
+    }
+    f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {   // H1 columns 32h + 8s + j
+      bf16x8 ah, am, al;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = 8 * s + j;
+        const float a = ((wd >> kk) & 1u) ? sc * fmaxf(hrow[kk], 0.f) : 0.f;
+        __bf16 x, y, z;
+        split3_bf16(a, x, y, z);
+        ah[j] = x; am[j] = y; al[j] = z;
+      }
+      const int k = 32 * h + 8 * s;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int o = (32 * half + r32) * kC2Ld16 + k;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(&Bs[0][o]);
+        const bf16x8 bm = *reinterpret_cast<const bf16x8*>(&Bs[1][o]);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(&Bs[2][o]);
+        if (half == 0) acc0 = mfma_x6(ah, am, al, bh, bm, bl, acc0);
+        else acc1 = mfma_x6(ah, am, al, bh, bm, bl, acc1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {   // root slots 2(8tt + j) + h
+      if (8 * tt < mh) {
+        bf16x8 ar;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ar[j] = __bf16(((m >> (2 * (8 * tt + j) + h)) & 1u) ? 1.f : 0.f);
+        const int k = H + (kCap / 2) * h + 8 * tt;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int o = (32 * half + r32) * kC2Ld16 + k;
+          f32x16 c = half == 0 ? acc0 : acc1;
+          c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[2][o]), c);
+          c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[1][o]), c);
+          c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[0][o]), c);
+          if (half == 0) acc0 = c; else acc1 = c;
+        }
+      }
     }
     m |= __shfl_xor(m, 32);
     if (h == 0 && ok) S.rbits[int64_t(d) * S.N + i] = m;
-    f32x16 acc0 = {}, acc1 = {};
-    const float* bp = &Bs[(32 * h) * kC2Ld + r32];            // rows 32h + kk
-    const float* bq = &Bs[(kC2Slot0 + 32 * h) * kC2Ld + r32];  // slot rows of this half
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) {
-      acc0 = mfma32x32x2(a[kk], bp[kk * kC2Ld], acc0);
-      acc1 = mfma32x32x2(a[kk], bp[kk * kC2Ld + 32], acc1);
-    }
-#pragma unroll
-    for (int j = 0; j < kCap / 2; ++j) {
-      if (j < mh) {
-        acc0 = mfma32x32x2(a[32 + j], bq[j * kC2Ld], acc0);
-        acc1 = mfma32x32x2(a[32 + j], bq[j * kC2Ld + 32], acc1);
-      }
-    }
     if (t == wv) BT_MARK(2, 2);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
