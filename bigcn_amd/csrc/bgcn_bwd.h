@@ -199,7 +199,8 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
                                 const float* __restrict__ W2td, const float* __restrict__ W2bu,
                                 int64_t ldw2, int64_t N, KeepSrc keep, float* __restrict__ dH1,
                                 float* __restrict__ colpart, int64_t rows, float* __restrict__ dw2part,
-                                int nsplit, int bx, int d, float* smem) {
+                                int nsplit, int bx, int d, float* smem,
+                                const __bf16* __restrict__ w2d = nullptr) {
   __bf16* Dh = reinterpret_cast<__bf16*>(smem);   // dZ2 tile [row][o], hi / lo
   __bf16* Dl = Dh + kDh1Rows * kDsLd;
   __bf16* Wh = Dl + kDh1Rows * kDsLd;             // W2[:, :64]^T [c][o], hi / lo
@@ -229,7 +230,22 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
       hv[q] = H1[i * (2 * H) + d * H + c];
     }
   };
-  {
+  if (w2d) {   // the prologue's split image ([2][c][o], hi / lo): 16-byte copies
+    static_assert(kDsLd == kW2dLd, "dH1's W rows are the prologue image's rows");
+    const __bf16* src = w2d + int64_t(d) * 2 * H * kW2dLd;
+    uint4 cv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = threadIdx.x + 256 * u, part = e >> 9, c = (e >> 3) & 63, q = (e & 7) * 8;
+      cv[u] = *reinterpret_cast<const uint4*>(src + (int64_t(part) * H + c) * kW2dLd + q);
+    }
+    gload(beg);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = threadIdx.x + 256 * u, part = e >> 9, c = (e >> 3) & 63, q = (e & 7) * 8;
+      *reinterpret_cast<uint4*>((part ? Wl : Wh) + c * kDsLd + q) = cv[u];
+    }
+  } else {
     float4 wv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {

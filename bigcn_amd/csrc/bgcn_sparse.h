@@ -6,6 +6,8 @@
 namespace bgcn {
 
 constexpr int kCap = 32;     // max non-zeros per feature row on the sparse path
+constexpr int kW2sLd = 64 + kCap + 8;   // bf16 row strides of the split W2 images (16-byte
+constexpr int kW2dLd = 64 + 8;          // aligned rows; conv2's also holds 32 root slots)
 constexpr int kChunk = kChunkItems;  // nodes per tree work item (conv2, dW2 root partials)
 
 struct SparseState {
@@ -19,6 +21,10 @@ struct SparseState {
   // step scratch
   float* w1t;      // [F][128]     = [W1_td ; W1_bu]^T
   float* w2t;      // [2][64+F][64] = W2_d^T
+  // W2_d[:, :64] split for the bf16 MFMA once per step by the prologue (the blocks of
+  // conv2 / the middle launch copy them instead of splitting per block):
+  __bf16* w2s;     // [2][3][64 o][kW2sLd] hi / mid / lo of W2_d[o][k], k < 64 (conv2's B)
+  __bf16* w2d;     // [2][2][64 c][kW2dLd] hi / lo of W2_d[o][c] at [c][o] (dH1's B)
   int max_items;
   int32_t *item_tree, *item_chunk, *tree_item0;
   float* root_part;  // [2][max_items][kCap][64]

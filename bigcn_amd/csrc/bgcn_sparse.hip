@@ -87,6 +87,32 @@ __device__ inline void prologue_batch_body(const SparseState& S, const int64_t* 
   tree_ptr[b] = int32_t(lo);
 }
 
+// W2_d[:, :64] split for the bf16 MFMA (kSplitBlocks 256-thread blocks per direction, one
+// element per thread): conv2's image [3][o][k] (hi / mid / lo) and the middle launch's
+// [2][c][o] (hi / lo).
+constexpr int kSplitBlocks = H * H / 256;
+__device__ inline void split_w2_block(const SparseState& S, int sb, const float* __restrict__ w2td,
+                                      const float* __restrict__ w2bu) {
+  const int d = sb / kSplitBlocks;
+  const float* W2 = d == 0 ? w2td : w2bu;
+  const int64_t ld = S.F + H;
+  __bf16* cs = S.w2s + int64_t(d) * 3 * H * kW2sLd;
+  __bf16* ds = S.w2d + int64_t(d) * 2 * H * kW2dLd;
+  {
+    const int e = (sb % kSplitBlocks) * 256 + threadIdx.x;
+    const int o = e >> 6, k = e & 63;
+    __bf16 x, y, z;
+    const float v = W2[int64_t(o) * ld + k];
+    split3_bf16(v, x, y, z);
+    cs[o * kW2sLd + k] = x;
+    cs[H * kW2sLd + o * kW2sLd + k] = y;
+    cs[2 * H * kW2sLd + o * kW2sLd + k] = z;
+    split_bf16(v, x, y);
+    ds[k * kW2dLd + o] = x;
+    ds[H * kW2dLd + k * kW2dLd + o] = y;
+  }
+}
+
 // Forward prologue, one launch: the weight transposes (sparse path), node -> root map,
 // tree pointers (binary search in the sorted batch vector) and the overflow-flag reset.
 // Block ranges: [0, nT) transposes, [nT, nT + nR) node_root, then tree_ptr.
@@ -108,7 +134,12 @@ __global__ __launch_bounds__(256) void k_prologue(SparseState S, const float* __
     transpose_tile(S, blk % nTx, (blk / nTx) % 2, blk / (2 * nTx), w1td, w1bu, w2td, w2bu);
     return;
   }
-  prologue_batch_body(S, batch, rootindex, node_root, tree_ptr, blk - nT, nR);
+  const int nS = nT > 0 ? 2 * kSplitBlocks : 0;   // the split W2 images ride with the transposes
+  if (blk < nT + nS) {
+    split_w2_block(S, blk - nT, w2td, w2bu);
+    return;
+  }
+  prologue_batch_body(S, batch, rootindex, node_root, tree_ptr, blk - nT - nS, nR);
 }
 
 // ---------------------------------------------------------------- X compaction + conv1
@@ -436,14 +467,13 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   // B fill with unconditional loads (clamped slot / column; see k_dh1), selects after
   if (threadIdx.x < kCap)
     rk[threadIdx.x] = threadIdx.x < rn ? uint32_t(H + S.cols[r * kCap + threadIdx.x]) : 0u;
-  for (int e = threadIdx.x; e < H * (H / 4); e += 256) {   // W2^T rows k < 64, 4 outputs each
-    const int k = e >> 4, q = (e & 15) * 4;
-    const float4 v = ld4(w2t + int64_t(k) * H + q);
-    const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int o = (q + u) * kC2Ld16 + k;
-      split3_bf16(vv[u], Bs[0][o], Bs[1][o], Bs[2][o]);
+  {   // k < 64: the prologue's split image of W2_d[:, :64] (16-byte copies, 8 per row part)
+    static_assert(kC2Ld16 == kW2sLd, "conv2's B rows are the prologue image's rows");
+    const __bf16* src = S.w2s + int64_t(d) * 3 * H * kW2sLd;
+    for (int e = threadIdx.x; e < 3 * H * 8; e += 256) {
+      const int part = e / (H * 8), o = (e / 8) % H, q = (e % 8) * 8;
+      *reinterpret_cast<uint4*>(&Bs[part][o * kC2Ld16 + q]) =
+          *reinterpret_cast<const uint4*>(src + (int64_t(part) * H + o) * kW2sLd + q);
     }
   }
   for (int e = threadIdx.x; e < kCap * (H / 4); e += 256) {  // root slots (zero past rn)
@@ -1128,7 +1158,7 @@ __global__ __launch_bounds__(256, 3) void k_bwd_mid(BwdMidArgs a) {   // 4 waves
     // the relu(H1) block of dW2 rides along when the sparse path is the one running
     float* part = (a.S.mode != 1 && !dense_active(a.gate)) ? a.dw2_sparse.part : nullptr;
     dh1_body(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, a.rows_h, part,
-             a.nblk_h, b % a.nblk_h, b / a.nblk_h, smem);
+             a.nblk_h, b % a.nblk_h, b / a.nblk_h, smem, a.S.mode != 1 ? a.S.w2d : nullptr);
     BT_END(72);
     return;
   }
@@ -1228,6 +1258,8 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   t.max_items = int(N / kChunk + B + 1);
   t.w1t = c.take<float>(size_t(F) * 2 * H);
   t.w2t = c.take<float>(size_t(2) * (F + H) * H);
+  t.w2s = c.take<__bf16>(size_t(2) * 3 * H * kW2sLd);
+  t.w2d = c.take<__bf16>(size_t(2) * 2 * H * kW2dLd);
   t.item_tree = c.take<int32_t>(size_t(t.max_items));
   t.item_chunk = c.take<int32_t>(size_t(t.max_items));
   t.tree_item0 = c.take<int32_t>(size_t(B + 1));
@@ -1255,11 +1287,12 @@ int sparse_prologue(SparseState& S, const bgcn_bigcn_args* a, int32_t* node_root
                     bool batch_part) {
   const int nTx = int((S.F + H + 31) / 32);
   const int nT = S.mode == 1 ? 0 : nTx * 2 * 4;
+  const int nS = nT > 0 ? 2 * kSplitBlocks : 0;
   const int nR = batch_part ? int((S.N + 255) / 256) : 0;
   const int nP = batch_part ? int((S.B + 1 + 255) / 256) : 0;
   const int nZ = (nT + nR + nP == 0 && (S.zero_word || S.rtick)) ? 1 : 0;
   if (nT + nR + nP + nZ == 0) return BGCN_OK;
-  hipLaunchKernelGGL(k_prologue, dim3(unsigned(nT + nR + nP + nZ)), dim3(256), 0, s, S, a->td_w1, a->bu_w1,
+  hipLaunchKernelGGL(k_prologue, dim3(unsigned(nT + nS + nR + nP + nZ)), dim3(256), 0, s, S, a->td_w1, a->bu_w1,
                      a->td_w2, a->bu_w2, a->batch, a->rootindex, node_root, a->tree_ptr, nTx, nT, nR);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
