@@ -645,6 +645,7 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
   if (sparse && a->save_for_backward) {
     hipStream_t x;
     BGCN_TRY(aux_fork(s, kLaneSide, &x));
+    sp.root_map = w.node_root;
     BGCN_TRY(sparse_csc(sp, x));
     forked = true;
   }
@@ -721,6 +722,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   bool forked = false;
   if (sparse && !have_csc) {
     BGCN_TRY(aux_fork(s, kLaneSide, &x));
+    sp.root_map = w.node_root;
     BGCN_TRY(sparse_csc(sp, x));
     forked = true;
   }

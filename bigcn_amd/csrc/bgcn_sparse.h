@@ -36,7 +36,10 @@ struct SparseState {
   uint32_t* rbits;      // [2][N] forward's root keep masks (bit s: root non-zero s kept)
   int32_t* zero_word = nullptr;   // zeroed by the prologue (the train step's status word)
   int32_t* rtick = nullptr;       // [B] readout arrival counters, zeroed by the prologue
+  const int32_t* root_map = nullptr;   // node -> its tree's root (the CSC placement flags root rows)
 };
+// CSC slot bit 31: the entry's row is a tree root (its column gets a dW2 root-column term)
+constexpr uint32_t kCscRootFlag = 0x80000000u;
 
 constexpr int kRowBlock = kCscRowBlock;   // rows per block of the CSC counting sort
 constexpr int64_t kSparseMaxF = kSparseMaxFeat;  // LDS bound of the CSC kernels (2 x 4 B x F)

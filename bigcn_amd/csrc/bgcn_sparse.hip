@@ -860,12 +860,14 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
   constexpr int kPer = kRowBlock * kCap / 256;   // 32
   int32_t col[kPer], nn[kPer];
   float val[kPer];
+  uint32_t rootbits = 0u;   // bit k: row of entry k is a tree root
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {   // issue all 96 loads first ...
+  for (int k = 0; k < kPer; ++k) {   // issue all loads first ...
     const int64_t ic = min<int64_t>(r0 + threadIdx.x / kCap + 8 * k, S.N - 1);
     nn[k] = S.nnz[ic];
     col[k] = S.cols[ic * kCap + s];
     val[k] = S.vals[ic * kCap + s];
+    rootbits |= uint32_t(S.root_map[ic] == int32_t(ic)) << k;
   }
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {   // ... then mask the padding slots
@@ -896,7 +898,8 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
         const uint32_t m = rows[cc];
         rank[k] = __popc(m & ((1u << rr[k]) - 1u));
         const int64_t i = r0 + bt * kBatchRows + rr[k];
-        S.csc[cnt[cc] + rank[k]] = make_uint2(uint32_t(i * kCap + s), __float_as_uint(val[4 * bt + k]));
+        const uint32_t flag = ((rootbits >> (4 * bt + k)) & 1u) ? kCscRootFlag : 0u;
+        S.csc[cnt[cc] + rank[k]] = make_uint2(uint32_t(i * kCap + s) | flag, __float_as_uint(val[4 * bt + k]));
       }
     }
     __syncthreads();
@@ -926,25 +929,28 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
 // entries per column; the split measured 14 us slower there), slow at Weibo size (~225).
 constexpr int kDw1Depth = 16;
 // Device body, 1024 threads, column block bid; smem: kDw1Smem floats.
-constexpr int kDw1Smem = 2 * H * 17;
+constexpr int kDw1Smem = 2 * 2 * H * 17;   // dW1 and the dW2 root-column partials
 template <int kDw1Split>                       // waves per column (1 or 4)
 __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ dZ1,
-                                float* __restrict__ dw1_td, float* __restrict__ dw1_bu, int bid,
-                                float* smem) {
+                                float* __restrict__ dw1_td, float* __restrict__ dw1_bu,
+                                const int64_t* __restrict__ batch, float* __restrict__ dw2_td,
+                                float* __restrict__ dw2_bu, float scale, int bid, float* smem) {
   const int kDw1Cols = int(blockDim.x >> 6) / kDw1Split;   // columns per block
   if (!use_sparse(S)) return;
   float (*t1)[17] = reinterpret_cast<float (*)[17]>(smem);
+  float (*t2)[17] = reinterpret_cast<float (*)[17]>(smem + 2 * H * 17);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int part = wave % kDw1Split;
   const int64_t F = S.F;
   const int64_t c = int64_t(bid) * kDw1Cols + wave / kDw1Split;
-  float2 a1 = make_float2(0.f, 0.f);
+  const int rd = lane >> 5, ro = (2 * lane) & (H - 1);   // this lane's (direction, output pair)
+  float2 a1 = make_float2(0.f, 0.f), a2 = make_float2(0.f, 0.f);
   if (c < F) {
     const int64_t beg = S.col_start[c], end = S.col_end[c];
     for (int64_t u0 = beg + 64 * part; u0 < end; u0 += 64 * kDw1Split) {
       const int64_t u = min<int64_t>(u0 + lane, end - 1);   // clamped: duplicates, x masked
       const uint2 ent = S.csc[u];
-      const uint32_t slot = ent.x;
+      const uint32_t slot = ent.x & ~kCscRootFlag;
       const float xv = __uint_as_float(ent.y);
       const int n = int(min<int64_t>(64, end - u0));
       const float x_l = lane < n ? xv : 0.f;
@@ -965,75 +971,59 @@ __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ 
           a1.y = fmaf(x[v], gv[v].y, a1.y);
         }
       }
+      // dW2 root columns: dW2_d[:, 64 + c] = sum over the root rows holding column c (tree
+      // order = CSC row order) of 2 relu(x) * sum_items root_part[d][item][slot] - the
+      // root entries (rare) are flagged in the CSC record, so this pass over the column
+      // finds them (a separate role re-read every column and gathered node_root per entry)
+      uint64_t m = __ballot(lane < n && (ent.x & kCscRootFlag));
+      while (m) {   // in row (= tree) order
+        const int j = __builtin_ctzll(m);
+        m &= m - 1;
+        const int32_t i = __builtin_amdgcn_readlane(i_l, j);     // j is wave-uniform
+        const int32_t sl = int32_t(__builtin_amdgcn_readlane(int32_t(slot), j) % kCap);
+        const float f = scale * fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(x_l), j)), 0.f);
+        const int b = int(batch[i]);
+        float2 sum = make_float2(0.f, 0.f);
+        const int it0 = S.tree_item0[b], it1 = S.tree_item0[b + 1];
+        for (int it = it0; it < it1; it += 4) {   // four item partials in flight, in item order
+          float2 v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[q] = *reinterpret_cast<const float2*>(
+                S.root_part + (int64_t(rd) * S.max_items + min(it + q, it1 - 1)) * (kCap * H) + sl * H + ro);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (it + q < it1) {
+              sum.x += v[q].x;
+              sum.y += v[q].y;
+            }
+        }
+        a2.x = fmaf(f, sum.x, a2.x);
+        a2.y = fmaf(f, sum.y, a2.y);
+      }
     }
   }
   t1[2 * lane][wave] = a1.x;
   t1[2 * lane + 1][wave] = a1.y;
+  t2[2 * lane][wave] = a2.x;
+  t2[2 * lane + 1][wave] = a2.y;
   __syncthreads();
   // combine the column's partials in wave order, then store (kDw1Cols consecutive columns
-  // per output row)
+  // per output row); every root column is written (zero when no root holds it)
   const int tx = threadIdx.x % kDw1Cols;
   const int64_t cc = int64_t(bid) * kDw1Cols + tx;
+  const int64_t K2 = F + H;
   for (int ty = threadIdx.x / kDw1Cols; ty < 2 * H && cc < F; ty += int(blockDim.x) / kDw1Cols) {
-    float acc = t1[ty][tx * kDw1Split];
+    float acc = t1[ty][tx * kDw1Split], acc2 = t2[ty][tx * kDw1Split];
 #pragma unroll
-    for (int k = 1; k < kDw1Split; ++k) acc += t1[ty][tx * kDw1Split + k];
+    for (int k = 1; k < kDw1Split; ++k) {
+      acc += t1[ty][tx * kDw1Split + k];
+      acc2 += t2[ty][tx * kDw1Split + k];
+    }
     float* dst = ty < H ? dw1_td + int64_t(ty) * F : dw1_bu + int64_t(ty - H) * F;
     dst[cc] = acc;
-  }
-}
-
-// dW2 root columns: dW2_d[:, 64 + c] = sum over the root rows holding column c (tree
-// order = CSC row order) of 2 relu(x) * sum_items root_part[d][item][slot]; every column
-// is written (zero when no root holds it).  A wave per column; only root rows are read.
-// Device body, 1024 threads, column block bid; smem: kRootColsSmem floats.
-constexpr int kRootColsSmem = 2 * H * 17;
-__device__ inline void rootcols_body(const SparseState& S, const int32_t* __restrict__ node_root,
-                                     const int64_t* __restrict__ batch, float* __restrict__ dw2_td,
-                                     float* __restrict__ dw2_bu, float scale, int bid, float* smem) {
-  if (!use_sparse(S)) return;
-  float (*t2)[H][17] = reinterpret_cast<float (*)[H][17]>(smem);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int cpb = int(blockDim.x >> 6);   // columns per block (one wave each)
-  const int64_t c = int64_t(bid) * cpb + wave;
-  float a2[2] = {0.f, 0.f};
-  if (c < S.F) {
-    const int64_t beg = S.col_start[c], end = S.col_end[c];
-    for (int64_t u0 = beg; u0 < end; u0 += 64) {
-      const int64_t u = u0 + lane;
-      const bool ok = u < end;
-      const uint32_t slot = S.csc[ok ? u : beg].x;
-      const int32_t i_l = int32_t(slot / kCap);
-      const int32_t s_l = int32_t(slot % kCap);
-      const bool root_l = ok && node_root[i_l] == i_l;
-      uint64_t m = __ballot(root_l);
-      while (m) {   // root rows (rare), in row (= tree) order
-        const int j = __builtin_ctzll(m);
-        m &= m - 1;
-        const int32_t i = __builtin_amdgcn_readlane(i_l, j);     // j is wave-uniform
-        const int32_t sl = __builtin_amdgcn_readlane(s_l, j);
-        const float xv = S.vals[int64_t(i) * kCap + sl];
-        const int b = int(batch[i]);
-        const float f = scale * fmaxf(xv, 0.f);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          float sum = 0.f;
-          for (int it = S.tree_item0[b]; it < S.tree_item0[b + 1]; ++it)
-            sum += S.root_part[(int64_t(d) * S.max_items + it) * (kCap * H) + sl * H + lane];
-          a2[d] = fmaf(f, sum, a2[d]);
-        }
-      }
-    }
-  }
-  t2[0][lane][wave] = a2[0];
-  t2[1][lane][wave] = a2[1];
-  __syncthreads();
-  const int tx = threadIdx.x % cpb;
-  const int64_t cc = int64_t(bid) * cpb + tx;
-  for (int ty = threadIdx.x / cpb; ty < H && cc < S.F; ty += int(blockDim.x) / cpb) {
-    const int64_t K2 = S.F + H;
-    dw2_td[int64_t(ty) * K2 + H + cc] = t2[0][ty][tx];
-    dw2_bu[int64_t(ty) * K2 + H + cc] = t2[1][ty][tx];
+    float* dst2 = ty < H ? dw2_td + int64_t(ty) * K2 : dw2_bu + int64_t(ty - H) * K2;
+    dst2[H + cc] = acc2;
   }
 }
 
@@ -1180,8 +1170,7 @@ __global__ __launch_bounds__(256, 3) void k_bwd_mid(BwdMidArgs a) {   // 4 waves
   BT_END(73);
 }
 
-constexpr int kTailSmem = kDw1Smem > kRootColsSmem ? (kDw1Smem > kRedSmem ? kDw1Smem : kRedSmem)
-                                                   : (kRootColsSmem > kRedSmem ? kRootColsSmem : kRedSmem);
+constexpr int kTailSmem = kDw1Smem > kRedSmem ? kDw1Smem : kRedSmem;
 #ifndef BGCN_TAIL_THREADS
 #define BGCN_TAIL_THREADS 512   // 1024-thread blocks ran one per CU: dW1 in two rounds
 #endif
@@ -1192,17 +1181,11 @@ __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
   BT_BEGIN
   int b = int(blockIdx.x);
   if (b < a.n_dw1) {
-    dw1_body<kDw1Split>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, b, smem);
+    dw1_body<kDw1Split>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem);
     BT_END(80);
     return;
   }
   b -= a.n_dw1;
-  if (b < a.n_rootcols) {
-    rootcols_body(a.S, a.node_root, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem);
-    BT_END(81);
-    return;
-  }
-  b -= a.n_rootcols;
   if (b < a.red_dense.blocks + a.red_sparse.blocks) {
     reduce_dw2_body(a.dw2_part, a.S.F + H, a.dw2_td, a.dw2_bu, a.gate, a.red_dense, a.red_sparse, b, smem);
     BT_END(82);
@@ -1236,11 +1219,11 @@ int bwd_tail_launch(BwdTailArgs& a, hipStream_t s) {
   constexpr int wpb = kTailThreads / 64;   // waves per block
   const int cols1 = split == 4 ? wpb / 4 : wpb;
   a.n_dw1 = sparse ? int((a.S.F + cols1 - 1) / cols1) : 0;
-  a.n_rootcols = sparse ? int((a.S.F + wpb - 1) / wpb) : 0;
+  a.n_rootcols = 0;   // the dW2 root columns ride with the dW1 waves (dw1_body)
   // the reduction configurations are sized in 1024-thread blocks (4 groups of 256)
   a.red_dense.blocks *= 1024 / kTailThreads;
   a.red_sparse.blocks *= 1024 / kTailThreads;
-  const int n = a.n_dw1 + a.n_rootcols + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(kTailThreads);
+  const int n = a.n_dw1 + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(kTailThreads);
   if (split == 4)
     hipLaunchKernelGGL(k_bwd_tail<4>, dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
   else
@@ -1351,6 +1334,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   S.item_tree = p.item_tree; S.item_chunk = p.item_chunk; S.tree_item0 = p.tree_item0;
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
   S.csc = p.csc;
+  S.root_map = p.node_root;
   a.batch = bt->batch; a.rootindex = bt->rootindex;
   a.node_root = p.node_root; a.tree_ptr = p.tree_ptr; a.status = p.status;
   a.X = bt->x; a.ldx = bt->ldx;
@@ -1455,6 +1439,7 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
   S.item_tree = p.item_tree; S.item_chunk = p.item_chunk; S.tree_item0 = p.tree_item0;
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
   S.csc = p.csc;
+  S.root_map = p.node_root;
   if (!(part & 1)) return mode == 1 ? BGCN_OK : sparse_csc(S, s);
   const int nR = int((N + 255) / 256), nP = int((B + 1 + 255) / 256);
   hipLaunchKernelGGL(k_prologue, dim3(unsigned(nR + nP)), dim3(256), 0, s, S, nullptr, nullptr,
