@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_adam_step",
     "bgcn_prepare_workspace_size", "bgcn_prepare_batch",
     "bgcn_train_step_workspace_size", "bgcn_train_step", "bgcn_join_side",
+    "bgcn_weight_images_size",
 )
 
 
@@ -108,6 +109,7 @@ class StepArgs(Structure):
         ("prepared", c_void_p), ("prepared_bytes", c_size_t), ("prepared_ready", c_int32),
         ("next", POINTER(BatchDesc)), ("next_prepared", c_void_p), ("next_prepared_bytes", c_size_t),
         ("status_flag", c_void_p),
+        ("images", c_void_p), ("images_current", c_int32),
     ]
 
 
@@ -148,6 +150,7 @@ _SIGS = {
     "bgcn_bigcn_backward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
     "bgcn_keep_words": (c_int, [c_uint64, c_int64, c_int32, c_void_p, c_void_p]),
     "bgcn_adam_step": (c_int, [c_void_p, c_void_p]),
+    "bgcn_weight_images_size": (c_size_t, [c_int64]),
     "bgcn_drop_edges_workspace_size": (c_size_t, [c_int64]),
     "bgcn_drop_edges": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_int64, c_void_p, c_int64, c_double,
                                 c_void_p, c_int64, c_void_p, c_int64, c_int64, c_uint64, c_int32, c_void_p,
@@ -185,7 +188,7 @@ def load_library(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.bgcn_abi_version() != 2:
+        if lib.bgcn_abi_version() != 3:
             raise ImportError("libbgcn.so ABI version mismatch")
         _lib = lib
         return lib

@@ -537,7 +537,7 @@ static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool 
 // Workspace + sparse state of one call.  The sparse path's per-row lists and its
 // overflow flag live in caller-owned buffers (saved from forward to backward).
 static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w, SparseState& sp,
-                 const int32_t*& gate, const Prepared* prep) {
+                 const int32_t*& gate, const Prepared* prep, const WeightImages* img) {
   const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
   BGCN_CHECK_ARG(ws && ws_bytes >= bigcn_ws_size(N, B, F, H), "workspace too small");
   BGCN_CHECK_ARG(a->feat_mode == BGCN_FEAT_DENSE ||
@@ -552,6 +552,9 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
   sp.vals = a->x_vals;
   carve_sparse(c, N, B, F, &sp);
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
+  if (img) {
+    sp.w1t = img->w1t; sp.w2t = img->w2t; sp.w2s = img->w2s; sp.w2d = img->w2d;
+  }
   if (sp.mode != 1) sp.rtick = w.rtick;   // item readout (tree items exist on the sparse path)
   w.spmm_bytes = ws_bytes - align_up(c.off, 256) - 256;
   w.spmm_ws = c.take<float>(1);
@@ -586,14 +589,15 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
                         const int32_t* gate, hipStream_t s, const HeadArgs* head, bool forked);
 
 int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
-                       int graph_lane, const HeadArgs* head, const Prepared* prep) {
+                       int graph_lane, const HeadArgs* head, const Prepared* prep,
+                       const WeightImages* img, bool img_current) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->head_in && a->td_w1 && a->bu_w1 && a->td_w2 && a->bu_w2, "null pointer");
   const int64_t N = a->num_nodes, F = a->in_feats;
   FusedWs w;
   SparseState sp{};
   const int32_t* gate = nullptr;
-  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate, prep));
+  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate, prep, img));
   KeepSrc keep = make_keep(a);
   const bool sparse = sp.mode != 1;
 
@@ -602,7 +606,10 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
     // only the weight transposes and conv1's gather from the ELL remain (the prologue
     // also clears the step's status word, which the head ORs into)
     sp.zero_word = head ? head->status : nullptr;
-    BGCN_TRY(sparse_prologue(sp, a, w.node_root, s, false));
+    if (sparse && img && img_current)
+      sp.conv1_clears = 1;   // nothing left for the prologue but its two clears
+    else
+      BGCN_TRY(sparse_prologue(sp, a, w.node_root, s, false));
     if (sparse) {
       timing_begin(0, s);
       BGCN_TRY(sparse_conv1_gather(sp, w.z1, s));
@@ -693,7 +700,8 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
 // -> dW1.  Side lane, forked as soon as its inputs exist: db2, the dW2 chain (relu(H1)
 // block, root partials, root columns), db1 and the gated dense dW1; joined at the end.
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
-                        const Prepared* prep, bool side_busy, const HeadGradJob* head) {
+                        const Prepared* prep, bool side_busy, const HeadGradJob* head,
+                        const WeightImages* img) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->dhead_in && a->td_dw1 && a->bu_dw1 && a->td_dw2 && a->bu_dw2 && a->td_db1 &&
                      a->bu_db1 && a->td_db2 && a->bu_db2,
@@ -702,7 +710,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   FusedWs w;
   SparseState sp{};
   const int32_t* gate = nullptr;
-  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate, prep));
+  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate, prep, img));
   KeepSrc keep = make_keep(a);
   const bool sparse = sp.mode != 1;
   const bool have_csc = a->save_for_backward || prep != nullptr;

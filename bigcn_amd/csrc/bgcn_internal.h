@@ -271,16 +271,20 @@ __device__ inline void head_grad_block(const HeadGradJob& j, int hb) {
 // ---- fused encoder (bgcn_bigcn.hip); graph_lane: see bigcn_forward_impl
 size_t bigcn_ws_size(int64_t N, int64_t B, int64_t F, int64_t hid);
 struct Prepared;
+struct WeightImages;
+// img (bgcn_train_step): the caller's weight-image buffer replaces the workspace's copies;
+// img_current: it already holds the current weights' images (no prologue launch)
 int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
                        int graph_lane, const HeadArgs* head = nullptr,
-                       const Prepared* prep = nullptr);
+                       const Prepared* prep = nullptr, const WeightImages* img = nullptr,
+                       bool img_current = false);
 // side_busy: the side lane carries other long work (a next-batch preparation); the dW2
 // chain then stays on the caller's stream
 // head (bgcn_train_step): the classifier head's weight gradients, run as extra blocks of
 // the readout backward
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
                         const Prepared* prep = nullptr, bool side_busy = false,
-                        const HeadGradJob* head = nullptr);
+                        const HeadGradJob* head = nullptr, const WeightImages* img = nullptr);
 
 // ---- prepared batch (bgcn_step.hip): the weight-independent state of one batch
 // (sizes shared with bgcn_sparse.h: tree work items of kChunkItems nodes, CSC row blocks)

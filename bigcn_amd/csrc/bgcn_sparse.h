@@ -37,7 +37,18 @@ struct SparseState {
   int32_t* zero_word = nullptr;   // zeroed by the prologue (the train step's status word)
   int32_t* rtick = nullptr;       // [B] readout arrival counters, zeroed by the prologue
   const int32_t* root_map = nullptr;   // node -> its tree's root (the CSC placement flags root rows)
+  int conv1_clears = 0;           // conv1's block 0 clears zero_word / rtick (no prologue launch)
 };
+// The weight images of the sparse path in a caller-owned persistent buffer
+// (bgcn_weight_images_size): kept current by bgcn_adam_step, so a step whose images are
+// current launches no prologue (its transposes and splits were the Adam's tile epilogue).
+struct WeightImages {
+  float* w1t;      // [F][128]
+  float* w2t;      // [2][F+64][64]
+  __bf16* w2s;     // [2][3][64][kW2sLd]
+  __bf16* w2d;     // [2][2][64][kW2dLd]
+};
+size_t carve_images(Carve& c, int64_t F, WeightImages* im);
 // CSC slot bit 31: the entry's row is a tree root (its column gets a dW2 root-column term)
 constexpr uint32_t kCscRootFlag = 0x80000000u;
 

@@ -32,6 +32,16 @@ namespace {
 
 __device__ __forceinline__ bool use_sparse(const SparseState& S) { return S.mode != 1 && S.flags[0] == 0; }
 
+// the prologue's clears when its launch is skipped (weight images current): the step's
+// status word and the readout tickets, by conv1's block 0 (both are first used by the
+// readout, two launches later)
+__device__ __forceinline__ void conv1_clears(const SparseState& S) {
+  if (!S.conv1_clears || blockIdx.x != 0) return;
+  if (threadIdx.x == 0 && S.zero_word) *S.zero_word = 0;
+  if (S.rtick)
+    for (int64_t b = threadIdx.x; b < S.B; b += blockDim.x) S.rtick[b] = 0;
+}
+
 // ---------------------------------------------------------------- weight transposes
 // W1T[c][d*64 + o] = W1_d[o][c] (c < F) and W2T_d[k][o] = W2_d[o][k] (k < 64+F):
 // 32 x 32 tiles through LDS; blockIdx.z: 0/1 = W1 td/bu, 2/3 = W2 td/bu.
@@ -339,6 +349,7 @@ constexpr int kC1Rows = 4;
 constexpr int kC1Threads = BGCN_C1_THREADS;   // threads per block
 __global__ __launch_bounds__(kC1Threads) void k_conv1_gather(SparseState S, float* __restrict__ Z1) {
   BT_BEGIN
+  conv1_clears(S);
   if (!use_sparse(S)) return;
   const int lane = threadIdx.x & 63, ql = lane & 15, qb = lane & 48;
   const int64_t i = (int64_t(blockIdx.x) * (kC1Threads / 64) + (threadIdx.x >> 6)) * kC1Rows + (lane >> 4);
@@ -392,6 +403,7 @@ __global__ __launch_bounds__(kC1Threads) void k_conv1_gather(SparseState S, floa
 template <int kStep>
 __global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __restrict__ Z1) {
   BT_BEGIN
+  conv1_clears(S);
   if (!use_sparse(S)) return;
   const int lane = threadIdx.x & 63, hl = lane & 31, hb = lane & 32;
   const int64_t i = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
@@ -1233,6 +1245,16 @@ int bwd_tail_launch(BwdTailArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- host side
+size_t carve_images(Carve& c, int64_t F, WeightImages* im) {
+  WeightImages t;
+  t.w1t = c.take<float>(size_t(F) * 2 * H);
+  t.w2t = c.take<float>(size_t(2) * (F + H) * H);
+  t.w2s = c.take<__bf16>(size_t(2) * 3 * H * kW2sLd);
+  t.w2d = c.take<__bf16>(size_t(2) * 2 * H * kW2dLd);
+  if (im) *im = t;
+  return c.off;
+}
+
 size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   SparseState t{};
   t.N = N;
@@ -1476,5 +1498,11 @@ int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
 
 
 }  // namespace bgcn
+
+extern "C" size_t bgcn_weight_images_size(int64_t in_feats) {
+  if (in_feats <= 0) return 0;
+  bgcn::Carve c(nullptr, 0);
+  return bgcn::carve_images(c, in_feats, nullptr) + 256;
+}
 
 BT_READER(sparse)

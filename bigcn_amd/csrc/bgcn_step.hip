@@ -190,6 +190,7 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
   Carve c(ws, ws_bytes);
   carve_step(c, N, B, F, C, &w);
   BGCN_CHECK_ARG(c.ok(), "workspace too small");
+  BGCN_CHECK_ARG(a->images || !a->images_current, "images_current without an image buffer");
   Prepared p;
   int graph_lane = -1;
   // the previous call's next-batch preparation (this call's batch) must be complete
@@ -254,13 +255,19 @@ static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w
   // dhead per tree); the prepared batch's K1 status is folded into *status
   const HeadArgs hd{a->params[8], a->params[9], a->y, int(C), a->logp, w.dz, w.loss_row, w.dhead,
                     a->status, p.status, a->feat_mode == BGCN_FEAT_SPARSE ? p.x_flags : nullptr};
-  BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, graph_lane, &hd, &p));
+  WeightImages im{};
+  if (a->images) {
+    Carve ci(a->images, bgcn_weight_images_size(F));
+    carve_images(ci, F, &im);
+  }
+  const WeightImages* img = a->images ? &im : nullptr;
+  BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, graph_lane, &hd, &p, img, a->images_current != 0));
   // fc weight/bias gradients, the loss mean and the validity flag: extra blocks of the
   // readout backward (joins the side lane at its end; with a next-batch preparation on
   // the side lane the dW2 chain stays on this stream, which balances the two)
   const HeadGradJob hj{w.head, w.dz, B, int(C), w.loss_row, a->grads[8], a->grads[9], a->loss,
                        a->status, a->status_flag};
-  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr, &hj);
+  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr, &hj, img);
 }
 
 }  // namespace bgcn

@@ -29,7 +29,12 @@ class AdamArgs(ctypes.Structure):
                 ("count", ctypes.c_int), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
                 ("bias_correction1", ctypes.c_float), ("bias_correction2_sqrt", ctypes.c_float),
-                ("grad_scale", ctypes.c_float), ("skip_flag", ctypes.c_void_p)]
+                ("grad_scale", ctypes.c_float), ("skip_flag", ctypes.c_void_p),
+                ("images", ctypes.c_void_p), ("images_in_feats", ctypes.c_int64),
+                ("image_role", ctypes.c_int32 * MAX_TENSORS)]
+
+# BGCN_IMAGE_* (include/bgcn.h): which weight image a conv weight's update also writes
+IMAGE_TD_W1, IMAGE_BU_W1, IMAGE_TD_W2, IMAGE_BU_W2 = 1, 2, 3, 4
 
 
 class FusedAdam:
@@ -65,11 +70,14 @@ class FusedAdam:
 
     @torch.no_grad()
     def step(self, grads: Optional[Sequence[torch.Tensor]] = None, grad_scale: float = 1.0,
-             skip_flag: Optional[torch.Tensor] = None) -> None:
+             skip_flag: Optional[torch.Tensor] = None, images=None) -> None:
         """``grads`` overrides ``p.grad`` (e.g. views of a reduced flat DP bucket).
         ``skip_flag``: a one-element fp32 device tensor; when it holds a non-zero value at
         execution time the launch updates nothing (an invalid training step, decided on
         the device without a host sync; the step counter still advances).
+        ``images``: ``(buffer, in_feats, {id(param): IMAGE_*})`` - the updates of those
+        conv weights also write the weight images a :class:`FusedTrainStep` reads
+        (``bgcn_weight_images_size``), so its next step derives nothing from the weights.
 
         Learning rates are read from ``param_groups`` on every call, so schedulers that
         edit ``group['lr']`` (as with torch.optim.Adam) take effect."""
@@ -88,11 +96,13 @@ class FusedAdam:
             a = AdamArgs()
             keep = []
             groups = []         # param_groups index of each table entry (lr refreshed per step)
+            entries = []        # params() index of each table entry
             k = 0
             for gi, p in enumerate(self.params()):
                 gr = gs[gi]
                 if gr is None:
                     continue
+                entries.append(gi)
                 gr = gr.contiguous()
                 keep.append(gr)
                 m, v = self.state[p]
@@ -103,7 +113,7 @@ class FusedAdam:
                 k += 1
             a.count = k
             a.beta1, a.beta2, a.eps, a.weight_decay = b1, b2, self.eps, self.weight_decay
-            cached = (key, a, keep, groups)
+            cached = (key, a, keep, groups, entries)
             self._cache = cached if cacheable else None
         a, groups = cached[1], cached[3]
         if a.count == 0:
@@ -117,7 +127,19 @@ class FusedAdam:
         a.bias_correction1 = 1.0 - b1 ** t
         a.bias_correction2_sqrt = math.sqrt(1.0 - b2 ** t)
         a.grad_scale = grad_scale
+        if images is not None:
+            buf, F, roles = images
+            a.images, a.images_in_feats = ptr(buf), int(F)
+            ps = self.params()
+            for k, gi in enumerate(self._entries(cached)):
+                a.image_role[k] = roles.get(id(ps[gi]), 0)
+        else:
+            a.images, a.images_in_feats = None, 0
         check(_lib.lib().bgcn_adam_step(ctypes.addressof(a), stream_handle()))
+
+    def _entries(self, cached):
+        """params() index of each table entry (gradients that are None have no entry)."""
+        return cached[4]
 
     def _group_of(self, p) -> int:
         for gi, g in enumerate(self.param_groups):

@@ -26,7 +26,7 @@ from ._lib import BatchDesc, StepArgs, check, ptr, stream_handle, workspace
 from .bigcn import BiGCN, _draw_seed, _num_graphs
 from .dp import GradBucket
 from .ops import _FEAT_MODES, check_encoder_shapes, degree_code, features, x_dtype_code
-from .optim import FusedAdam, bigcn_adam
+from .optim import IMAGE_BU_W1, IMAGE_BU_W2, IMAGE_TD_W1, IMAGE_TD_W2, FusedAdam, bigcn_adam
 
 
 def _step_feat_mode(feat_mode: str, data) -> int:
@@ -100,6 +100,37 @@ class FusedTrainStep:
         self._pending = None       # (batch, prepared buffer, feat_mode, tensors) from next_data
         self._stream = None
         self._next_desc = None
+        # Weight images (W1^T, W2^T, the bf16 splits of W2[:, :64]) in a persistent buffer:
+        # the fused Adam writes them with every update, so a step whose weights are those the
+        # last update wrote launches no prologue.  They count as current while the weights'
+        # version counters, storage and the optimiser's step count are what they were right
+        # after that update (any torch in-place edit - load_state_dict, copy_ under no_grad -
+        # or an optimiser step without the images makes the next step re-derive them).
+        # Edits through ``p.data`` bypass the version counter: call invalidate_images().
+        w = self.step_params
+        self._img_params = (w[0], w[4], w[2], w[6])
+        self._img_roles = {id(w[0]): IMAGE_TD_W1, id(w[4]): IMAGE_BU_W1,
+                           id(w[2]): IMAGE_TD_W2, id(w[6]): IMAGE_BU_W2}
+        self._images = None
+        self._images_F = None
+        self._images_key = None
+
+    def _image_key(self):
+        return (self.opt.step_count, tuple(p._version for p in self._img_params),
+                tuple(p.data_ptr() for p in self._img_params))
+
+    def invalidate_images(self) -> None:
+        """Make the next step re-derive the weight images from the parameters (needed only
+        after writing parameters behind torch's version counters, e.g. via ``p.data``)."""
+        self._images_key = None
+
+    def _image_buffer(self, F: int):
+        if self._images is None or self._images_F != F:
+            n = _lib.lib().bgcn_weight_images_size(F)
+            self._images = workspace(n, self.status.device)
+            self._images_F = F
+            self._images_key = None
+        return self._images
 
     def grads(self):
         """{parameter: gradient view} of the last step (before the DP all-reduce)."""
@@ -182,6 +213,9 @@ class FusedTrainStep:
         loss = torch.empty(1, dtype=torch.float32, device=data.x.device)
         a.loss, a.logp, a.status = ptr(loss), ptr(logp), ptr(self.status)
         a.status_flag = ptr(self.bucket.flag)
+        img = self._image_buffer(F)
+        a.images = ptr(img)
+        a.images_current = int(self._images_key is not None and self._images_key == self._image_key())
         L = _lib.lib()
         N, B = d.num_nodes, d.num_graphs
         ws = workspace(L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
@@ -200,7 +234,11 @@ class FusedTrainStep:
         self.bucket.allreduce_sum_(self.group)
         # an invalid step (status bits, any rank: the flag is summed by the all-reduce)
         # updates nothing; check_status() reports why
-        self.opt.step(grads=self.bucket.views(), grad_scale=1.0 / world, skip_flag=self.bucket.flag)
+        self.opt.step(grads=self.bucket.views(), grad_scale=1.0 / world, skip_flag=self.bucket.flag,
+                      images=(self._images, self._images_F, self._img_roles))
+        # the images now hold the updated weights (or, after an invalid step, the unchanged
+        # ones: the launch skipped params and images alike)
+        self._images_key = self._image_key()
         return loss
 
     def _join_side(self) -> None:

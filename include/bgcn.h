@@ -47,7 +47,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 2
+#define BGCN_ABI_VERSION 3
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -349,7 +349,17 @@ typedef struct bgcn_step_args {
   const bgcn_batch* next;        /* or NULL                                  */
   void* next_prepared; size_t next_prepared_bytes;
   float* status_flag;            /* [1] or NULL                              */
+  /* weight images (optional): the transposed / split copies of the conv weights the
+   * step's sparse-path kernels read (bgcn_weight_images_size).  images_current = 1: the
+   * buffer already holds them for the CURRENT params (written by bgcn_adam_step with the
+   * same buffer, params untouched since) and the step skips deriving them; 0: the step
+   * derives them into the buffer. */
+  void* images; int32_t images_current;
 } bgcn_step_args;
+
+/* Bytes of a weight-image buffer for in_feats = F (W1^T [F][128], W2^T [2][F+64][64]
+ * and the bf16 split images of W2[:, :64]); persistent, caller-owned. */
+size_t bgcn_weight_images_size(int64_t in_feats);
 
 /* workspace of the step itself (the prepared buffers are separate) */
 size_t bgcn_train_step_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,
@@ -385,7 +395,19 @@ typedef struct bgcn_adam_args {
   float beta1, beta2, eps, weight_decay;
   float bias_correction1, bias_correction2_sqrt, grad_scale;
   const float* skip_flag;        /* [1] or NULL                              */
+  /* weight images (optional): with images set, the tensors whose image_role is one of
+   * BGCN_IMAGE_* (conv weights [64][F] / [64][F+64]) are updated tile by tile and their
+   * updated values also written into the image buffer of a step with in_feats =
+   * images_in_feats, which the next bgcn_train_step then uses with images_current = 1
+   * (an invalid step leaves params and images untouched alike). */
+  void* images; int64_t images_in_feats;
+  int32_t image_role[BGCN_ADAM_MAX_TENSORS];
 } bgcn_adam_args;
+#define BGCN_IMAGE_NONE 0
+#define BGCN_IMAGE_TD_W1 1
+#define BGCN_IMAGE_BU_W1 2
+#define BGCN_IMAGE_TD_W2 3
+#define BGCN_IMAGE_BU_W2 4
 int bgcn_adam_step(const bgcn_adam_args* args, bgcn_stream_t stream);
 
 /* Materialise the in-kernel dropout keep bits (for tests / debugging):

@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = _lib.load_library()
     for name in _declared_functions():
         assert hasattr(lib, name), name
-    assert lib.bgcn_abi_version() == 2
+    assert lib.bgcn_abi_version() == 3
 
 
 def test_workspace_queries_without_gpu():
@@ -42,6 +42,9 @@ def test_workspace_queries_without_gpu():
     assert lib.bgcn_bigcn_workspace_size(1000, 8, 5000, 64) > lib.bgcn_bigcn_workspace_size(100, 8, 5000, 64)
     n = lib.bgcn_train_step_workspace_size(1000, 8, 5000, 4, 990, 990)
     assert n > lib.bgcn_bigcn_workspace_size(1000, 8, 5000, 64)
+    # weight images: W1^T [F][128] + W2^T [2][F+64][64] fp32 + the bf16 split images
+    assert lib.bgcn_weight_images_size(5000) >= 4 * (5000 * 128 + 2 * 5064 * 64)
+    assert lib.bgcn_weight_images_size(0) == 0
 
 
 def test_invalid_arguments_fail_before_any_device_work():
@@ -96,3 +99,7 @@ def test_constants_match_header():
         m = re.search(rf"#define {name} (\d+)", text)
         assert m, name
         assert int(m.group(1)) == getattr(_lib, name), name
+    from bigcn_amd import optim
+    for name in ("TD_W1", "BU_W1", "TD_W2", "BU_W2"):
+        m = re.search(rf"#define BGCN_IMAGE_{name} (\d+)", text)
+        assert m and int(m.group(1)) == getattr(optim, "IMAGE_" + name), name

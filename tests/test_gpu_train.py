@@ -185,6 +185,53 @@ def test_next_batch_prefetch_matches_plain_steps(mode):
     s2.check_status()
 
 
+@pytest.mark.parametrize("mode", ["auto", "sparse", "dense"])
+def test_weight_images_kept_by_adam_match_derived(mode):
+    """Five full steps (step + fused Adam).  With the weight images (W1^T, W2^T, the bf16
+    splits of W2[:, :64]) written by the Adam's tile epilogue, the steps after the first
+    launch no prologue; losses, gradients and parameters are bitwise those of steps that
+    re-derive the images from the weights every time.  A load_state_dict between steps
+    (version counters) makes the next step re-derive them; zeroing the kept images shows
+    that a current step really reads them."""
+    from bigcn_amd import FusedTrainStep
+    batches = [_synth(60 + k, 24, 150) for k in range(3)]
+    p = O.make_params(5000, 64, 64, 4, seed=18)
+    p2 = O.make_params(5000, 64, 64, 4, seed=19)
+    runs = []
+    for keep in (True, False):
+        m = _model(p, mode)
+        m.train()
+        step = FusedTrainStep(m)
+        out, current = [], []
+        for it in range(5):
+            if it == 3:
+                m.load_state_dict({k: v.float() for k, v in p2.items()})
+            if not keep:
+                step.invalidate_images()
+            current.append(step._images_key is not None and step._images_key == step._image_key())
+            loss = step(batches[it % 3], seed=100 + it)
+            out.append((loss.clone(), [v.clone() for v in step.grads().values()]))
+        out.append([v.clone() for v in m.state_dict().values()])
+        runs.append((out, current))
+    (a, ca), (b, cb) = runs
+    assert ca == [False, True, True, False, True]
+    assert cb == [False] * 5
+    for (l1, g1), (l2, g2) in zip(a[:5], b[:5]):
+        assert torch.equal(l1, l2)
+        for x, y in zip(g1, g2):
+            assert torch.equal(x, y)
+    for x, y in zip(a[5], b[5]):
+        assert torch.equal(x, y)
+    if mode != "dense":   # negative control: a current step reads the kept images
+        m = _model(p, mode)
+        m.train()
+        step = FusedTrainStep(m)
+        step(batches[0], seed=100)
+        ref = step.forward_backward(batches[1], seed=101).clone()
+        step._images.zero_()
+        assert not torch.equal(step.forward_backward(batches[1], seed=101), ref)
+
+
 @pytest.mark.parametrize("mode", ["auto", "dense"])
 @pytest.mark.parametrize("training", [False, True])
 def test_pheme_768_dense_features(training, mode):
