@@ -51,10 +51,17 @@ class GradBucket:
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
         self.numels = [p.numel() for p in self.params]
         dev = self.params[0].device
-        n = sum(self.numels)
+        # every view starts on a 16-byte boundary (the kernels' float4 paths; a Weibo head
+        # bias of 2 elements would otherwise misalign every parameter after it); the gaps
+        # stay zero through the all-reduce
+        offs, n = [], 0
+        for k in self.numels:
+            offs.append(n)
+            n += (k + 3) // 4 * 4
+        self._packed = all(k % 4 == 0 for k in self.numels)   # no gaps: one cat fills it
         self.flat = torch.zeros(n + (1 if status_slot else 0), dtype=torch.float32, device=dev)
         self.flag = self.flat[n:] if status_slot else None
-        self._views = [v.view_as(p) for v, p in zip(torch.split(self.flat[:n], self.numels), self.params)]
+        self._views = [self.flat[o:o + k].view_as(p) for o, k, p in zip(offs, self.numels, self.params)]
 
     def views(self) -> List[torch.Tensor]:
         """Persistent per-parameter views of the flat bucket (parameter order): kernels
@@ -74,7 +81,11 @@ class GradBucket:
         views of the reduced bucket in parameter order (the caller divides by world)."""
         grads = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(n, device=self.flat.device)
                  for p, n in zip(self.params, self.numels)]
-        torch.cat(grads, out=self.flat[:sum(self.numels)])
+        if self._packed:
+            torch.cat(grads, out=self.flat[:sum(self.numels)])
+        else:
+            for v, g in zip(self._views, grads):
+                v.view(-1).copy_(g)
         self.allreduce_sum_(group)
         return self._views
 

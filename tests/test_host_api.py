@@ -50,3 +50,20 @@ def test_fused_step_bucket_carries_the_status_slot():
     assert st.bucket.flag.numel() == 1
     assert st.bucket.flag.data_ptr() == st.bucket.flat.data_ptr() + 4 * n
     assert sum(v.numel() for v in st.bucket.views()) == n
+
+
+def test_bucket_views_are_16_byte_aligned():
+    """Net's 2-class head bias would misalign every later view of a packed bucket: the
+    views start on 16-byte boundaries (float4 paths of the step and the fused Adam), the
+    gaps stay zero, reduce_sum fills the views."""
+    from bigcn_amd import FusedTrainStep, Net
+    m = Net(16, 64, 64)
+    st = FusedTrainStep(m)
+    b = st.bucket
+    assert all(v.data_ptr() % 16 == 0 for v in b.views())
+    assert b.flag.data_ptr() == b.flat.data_ptr() + 4 * (b.flat.numel() - 1)
+    for p in b.params:
+        p.grad = torch.full_like(p, 2.0)
+    views = b.reduce_sum()
+    assert all(bool((v == 2.0).all()) for v in views)
+    assert float(b.flat[:-1].sum()) == 2.0 * sum(p.numel() for p in b.params)
