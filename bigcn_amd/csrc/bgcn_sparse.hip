@@ -1039,6 +1039,128 @@ __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ 
   }
 }
 
+// dW1 by output slices, XCD-aware (the default form).  The 128-wide dZ1 row splits into
+// kSlices slices of kSliceW outputs; the blocks of XCD x (blocks are dispatched to the
+// XCDs round-robin: block b runs on XCD b % 8) take slice x % kSlices of every column of
+// their column groups, so an XCD's L2 serves the gathers of ONE slice of dZ1 - N x 128 B
+// (3.9 MB at Twitter size) instead of the whole 15.7 MB table, most of which the
+// column-per-wave form fetched from the Infinity Cache (PMC: 140 MB per launch, the
+// fabric-bound ~7 TB/s).  A wave takes one (column, slice): kSliceGroups entries per
+// gather instruction (kSliceLanes lanes x 16 B per entry), kSliceDepth rounds in flight;
+// the lane groups' partials are combined by a fixed xor-shuffle tree (deterministic).  The
+// dW2 root columns ride along as in dw1_body (same per-output order, same values).
+#ifndef BGCN_DW1_SLICES
+#define BGCN_DW1_SLICES 4
+#endif
+#ifndef BGCN_DW1_DEPTH
+#define BGCN_DW1_DEPTH 4
+#endif
+constexpr int kSlices = BGCN_DW1_SLICES;
+constexpr int kSliceW = 2 * H / kSlices;          // outputs per slice
+constexpr int kSliceLanes = kSliceW / 4;          // lanes per entry (one float4 each)
+constexpr int kSliceGroups = 64 / kSliceLanes;    // entries per gather instruction
+constexpr int kSliceDepth = BGCN_DW1_DEPTH;
+static_assert(8 % kSlices == 0 && kSliceW <= H && kSliceLanes >= 1, "slices");
+__device__ __forceinline__ float4 shfl4(float4 v, int src) {
+  return make_float4(__shfl(v.x, src, 64), __shfl(v.y, src, 64), __shfl(v.z, src, 64), __shfl(v.w, src, 64));
+}
+__device__ __forceinline__ float4 shfl_xor4(float4 v, int m) {
+  return make_float4(__shfl_xor(v.x, m, 64), __shfl_xor(v.y, m, 64), __shfl_xor(v.z, m, 64),
+                     __shfl_xor(v.w, m, 64));
+}
+// blocks of the sliced form for F columns with W waves (= columns) per block
+__host__ __device__ inline int dw1_sliced_blocks(int64_t F, int W) {
+  const int64_t groups = (F + W - 1) / W, reps = 8 / kSlices;
+  return int(8 * ((groups + reps - 1) / reps));
+}
+__device__ inline void dw1_sliced_body(const SparseState& S, const float* __restrict__ dZ1,
+                                       float* __restrict__ dw1_td, float* __restrict__ dw1_bu,
+                                       const int64_t* __restrict__ batch, float* __restrict__ dw2_td,
+                                       float* __restrict__ dw2_bu, float scale, int bid, float* smem) {
+  if (!use_sparse(S)) return;
+  const int W = int(blockDim.x >> 6);
+  const int x = bid & 7, sl_ = x % kSlices;
+  const int64_t cg = int64_t(bid >> 3) * (8 / kSlices) + x / kSlices;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane / kSliceLanes, q = lane % kSliceLanes;
+  const int so = kSliceW * sl_, d = so / H, oo = so % H + 4 * q;   // slice start, direction, my outputs
+  const int64_t F = S.F;
+  const int64_t c = cg * W + wave;
+  float4 a1 = f4zero(), a2 = f4zero();
+  if (c < F) {
+    const int64_t beg = S.col_start[c], end = S.col_end[c];
+    for (int64_t u0 = beg; u0 < end; u0 += 64) {
+      const int64_t u = min<int64_t>(u0 + lane, end - 1);   // clamped: duplicates, x masked
+      const uint2 ent = S.csc[u];
+      const uint32_t slot = ent.x & ~kCscRootFlag;
+      const int n = int(min<int64_t>(64, end - u0));
+      const float x_l = lane < n ? __uint_as_float(ent.y) : 0.f;
+      const int32_t i_l = int32_t(slot / kCap);
+      for (int j0 = 0; j0 < n; j0 += kSliceGroups * kSliceDepth) {
+        float4 gv[kSliceDepth];
+        float xx[kSliceDepth];
+#pragma unroll
+        for (int v = 0; v < kSliceDepth; ++v) {
+          const int j = j0 + v * kSliceGroups + g;
+          const int jc = j < n ? j : n - 1;
+          const int32_t i = __shfl(i_l, jc, 64);
+          const float xv = __shfl(x_l, jc, 64);
+          xx[v] = j < n ? xv : 0.f;
+          gv[v] = ld4(dZ1 + int64_t(i) * (2 * H) + so + 4 * q);
+        }
+#pragma unroll
+        for (int v = 0; v < kSliceDepth; ++v) a1 = f4fma(xx[v], gv[v], a1);
+      }
+      uint64_t m = __ballot(lane < n && (ent.x & kCscRootFlag));
+      while (m) {   // root entries, in row (= tree) order; lane group 0 holds the slice
+        const int j = __builtin_ctzll(m);
+        m &= m - 1;
+        const int32_t i = __builtin_amdgcn_readlane(i_l, j);
+        const int32_t sl = int32_t(__builtin_amdgcn_readlane(int32_t(slot), j) % kCap);
+        const float f = scale * fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(x_l), j)), 0.f);
+        if (g != 0) continue;
+        const int b = int(batch[i]);
+        float4 sum = f4zero();
+        const int it0 = S.tree_item0[b], it1 = S.tree_item0[b + 1];
+        for (int it = it0; it < it1; it += 4) {   // four item partials in flight, in item order
+          float4 v[4];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq)
+            v[qq] = ld4(S.root_part + (int64_t(d) * S.max_items + min(it + qq, it1 - 1)) * (kCap * H) + sl * H + oo);
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq)
+            if (it + qq < it1) sum = f4add(sum, v[qq]);
+        }
+        a2 = f4fma(f, sum, a2);
+      }
+    }
+  }
+#pragma unroll
+  for (int off = kSliceLanes; off < 64; off <<= 1) a1 = f4add(a1, shfl_xor4(a1, off));
+  float* t1 = smem;                                 // [kSliceW][W + 1]
+  float* t2 = smem + kSliceW * (W + 1);
+  if (g == 0) {
+    const float v1[4] = {a1.x, a1.y, a1.z, a1.w}, v2[4] = {a2.x, a2.y, a2.z, a2.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t1[(4 * q + j) * (W + 1) + wave] = v1[j];
+      t2[(4 * q + j) * (W + 1) + wave] = v2[j];
+    }
+  }
+  __syncthreads();
+  const int64_t K2 = F + H;
+  float* w1 = d == 0 ? dw1_td : dw1_bu;
+  float* w2 = d == 0 ? dw2_td : dw2_bu;
+  for (int e = threadIdx.x; e < kSliceW * W; e += int(blockDim.x)) {
+    const int ol = e / W, tx = e % W;
+    const int64_t cc = cg * W + tx;
+    if (cc >= F) continue;
+    const int o = so % H + ol;
+    w1[int64_t(o) * F + cc] = t1[ol * (W + 1) + tx];
+    w2[int64_t(o) * K2 + H + cc] = t2[ol * (W + 1) + tx];
+  }
+}
+
 // ---------------------------------------------------------------- batch preparation
 // The fused step's weight-independent preparation of one batch (bgcn_prepare_batch /
 // the next batch on the side lane) as six launches of 256-thread blocks, each carrying
@@ -1187,13 +1309,16 @@ constexpr int kTailSmem = kDw1Smem > kRedSmem ? kDw1Smem : kRedSmem;
 #define BGCN_TAIL_THREADS 512   // 1024-thread blocks ran one per CU: dW1 in two rounds
 #endif
 constexpr int kTailThreads = BGCN_TAIL_THREADS;   // threads per block of the tail launch
-template <int kDw1Split>
+template <int kDw1Split>   // 0: dw1_sliced_body, else dw1_body's waves per column
 __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[kTailSmem];
   BT_BEGIN
   int b = int(blockIdx.x);
   if (b < a.n_dw1) {
-    dw1_body<kDw1Split>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem);
+    if constexpr (kDw1Split == 0)
+      dw1_sliced_body(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem);
+    else
+      dw1_body<kDw1Split>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem);
     BT_END(80);
     return;
   }
@@ -1225,12 +1350,13 @@ int bwd_tail_launch(BwdTailArgs& a, hipStream_t s) {
   // from 64k rows; with 512-thread blocks one wave wins at every size: synth1024_bf16
   // 0.839 vs 0.850-0.859 ms, weibo_bf16 0.690 vs 0.697, profiles/r02_split_ab.txt);
   // BGCN_DW1_SPLIT=1/4 forces either (read per call: tests compare both)
+  // default: the XCD-aware output slices (dw1_sliced_body), BGCN_DW1_SPLIT=0
   const char* e = std::getenv("BGCN_DW1_SPLIT");
   const bool sparse = a.S.mode != 1;
-  const int split = e ? atoi(e) : 1;
+  const int split = e ? atoi(e) : 0;
   constexpr int wpb = kTailThreads / 64;   // waves per block
   const int cols1 = split == 4 ? wpb / 4 : wpb;
-  a.n_dw1 = sparse ? int((a.S.F + cols1 - 1) / cols1) : 0;
+  a.n_dw1 = !sparse ? 0 : split == 0 ? dw1_sliced_blocks(a.S.F, wpb) : int((a.S.F + cols1 - 1) / cols1);
   a.n_rootcols = 0;   // the dW2 root columns ride with the dW1 waves (dw1_body)
   // the reduction configurations are sized in 1024-thread blocks (4 groups of 256)
   a.red_dense.blocks *= 1024 / kTailThreads;
@@ -1238,8 +1364,10 @@ int bwd_tail_launch(BwdTailArgs& a, hipStream_t s) {
   const int n = a.n_dw1 + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(kTailThreads);
   if (split == 4)
     hipLaunchKernelGGL(k_bwd_tail<4>, dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
-  else
+  else if (split == 1)
     hipLaunchKernelGGL(k_bwd_tail<1>, dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_bwd_tail<0>, dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }

@@ -452,14 +452,14 @@ def test_planned_and_merge_path_aggregation_match_oracle(plan, monkeypatch):
 
 
 def test_dw1_column_split_matches(monkeypatch):
-    """dW1 over the CSC of X with one wave per column (Twitter-sized batches) and with
-    four waves per column (from 64k rows): the same gradients up to summation order, and
-    every other gradient bit for bit."""
+    """dW1 over the CSC of X by XCD-aware output slices (the default, "0"), with one wave
+    per column and with four waves per column: the same gradients up to summation order,
+    and every other gradient (the dW2 root columns included) bit for bit."""
     from bigcn_amd import FusedTrainStep
     b = _synth(48, 64, 200)
     p = O.make_params(5000, 64, 64, 4, seed=29)
     res = {}
-    for split in ("1", "4"):
+    for split in ("0", "1", "4"):
         monkeypatch.setenv("BGCN_DW1_SPLIT", split)
         step = FusedTrainStep(_model(p))
         step.forward_backward(b, seed=3)
@@ -468,8 +468,10 @@ def test_dw1_column_split_matches(monkeypatch):
     for k in KEYS:
         if k.endswith("conv1.lin.weight"):
             close(res["4"][k], res["1"][k], what=k)
+            close(res["0"][k], res["1"][k], what=k)
         else:
             assert torch.equal(res["1"][k], res["4"][k]), k
+            assert torch.equal(res["1"][k], res["0"][k]), k
 
 
 def test_inplace_x_edit_after_collate_skips_update():
