@@ -39,6 +39,16 @@ inline int propagate(int rc) { return rc; }
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // Simple bump allocator over a caller-provided workspace.
+// Blocks are dispatched to the 8 XCDs round-robin (block b of a 1-D grid runs on XCD b % 8).
+// xcd_contig(b, R) renumbers blocks [0, R) so that each XCD takes a contiguous range of
+// logical blocks (XCD x: [x q + min(x, r), ...), q = R / 8, r = R % 8): work items that
+// share data (adjacent rows of one tree) then share one XCD's L2.  A 2-D grid keeps the
+// mapping for every row when gridDim.x is a multiple of 8.
+__host__ __device__ inline int xcd_contig(int b, int R) {
+  const int q = R / 8, r = R % 8, x = b % 8, i = b / 8;
+  return x * q + (x < r ? x : r) + i;
+}
+
 struct Carve {
   char* base;
   size_t cap;

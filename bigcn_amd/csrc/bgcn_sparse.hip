@@ -837,13 +837,9 @@ __global__ __launch_bounds__(1024) void k_csc_colscan(SparseState S) { csc_colsc
 // dispatcher hands blocks to the XCDs round-robin) take consecutive row blocks, whose
 // entries of a column are adjacent in the CSC, so a line of it is mostly written from one
 // XCD's L2 instead of from all eight (the placement's stores are scattered by column).
-__device__ __forceinline__ int xcd_row_block(int b, int R) {
-  const int q = R / 8, r = R % 8, x = b % 8, i = b / 8;
-  return x * q + min(x, r) + i;
-}
 __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* psm) {
   if (!use_sparse(S)) return;   // psm: [F] counters, [F] row masks
-  bid = xcd_row_block(bid, int((S.N + kRowBlock - 1) / kRowBlock));
+  bid = xcd_contig(bid, int((S.N + kRowBlock - 1) / kRowBlock));
   int32_t* cnt = psm;
   uint32_t* rows = reinterpret_cast<uint32_t*>(psm + S.F);
   const int64_t F = S.F;

@@ -134,7 +134,9 @@ __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_
   const int base_lane = ((threadIdx.x & 63) / LANES) * LANES;
   __shared__ float4 red[kRowsGroups][LANES];
   if (int64_t(blockIdx.x) < nchunk) {
-    const int64_t g = int64_t(blockIdx.x) * kRowsGroups + grp;
+    // XCD-contiguous chunk ranges: a tree's rows and the neighbours they gather stay in one
+    // L2 (the launch pads gridDim.x to a multiple of 8)
+    const int64_t g = int64_t(xcd_contig(int(blockIdx.x), int(nchunk))) * kRowsGroups + grp;
     if (g >= (P.capacity + kPlanGrid - 1) / kPlanGrid) return;
     const int2 bd = P.plan.bnd[g];
     const int n = bd.y - bd.x;                       // <= 2 * LANES - 1; <= 0: no rows
@@ -499,7 +501,8 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   if (planned) {   // K1's plans: complete rows per chunk, long rows per block, no fixup
     const int64_t gplan = (capmax + kPlanGrid - 1) / kPlanGrid;   // K1's chunk grid
     const int64_t nchunk = (gplan + kRowsGroups - 1) / kRowsGroups;
-    const int nlongblk = int(std::min<int64_t>(256, std::max<int64_t>(1, capmax / (kPlanChunk + 1))));
+    int nlongblk = int(std::min<int64_t>(256, std::max<int64_t>(1, capmax / (kPlanChunk + 1))));
+    nlongblk += int((8 - (nchunk + nlongblk) % 8) % 8);   // gridDim.x % 8 == 0 (xcd_contig)
     hipLaunchKernelGGL(k_spmm_rows, dim3(unsigned(nchunk + nlongblk), gy), dim3(kRowsThreads), 0, stream,
                        sb, nchunk, nlongblk);
   } else if (F == 64) {
