@@ -256,8 +256,8 @@ def compaction_standalone(fused, b, wl, iters: int = 10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="twitter15", choices=sorted(WORKLOADS))
     ap.add_argument("--pool", type=int, default=4)
     ap.add_argument("--cpu-trees", type=int, default=32)
