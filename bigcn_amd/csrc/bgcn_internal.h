@@ -75,6 +75,7 @@ struct HeadArgs {
   int32_t* status;       // bit 1: label out of range
   const int32_t* in_status;  // OR-ed into *status once (prepared batch's K1 flags), or nullptr
   const int32_t* in_xflags;  // BGCN_FEAT_SPARSE: the compaction's overflow flag (-> bit 2)
+  int publish = 0;       // dhead stored write-through (agent-scope atomics) for other CUs
 };
 
 // One wave, row b of the head: h = head_in[b][4l .. 4l+3] held by lane l.
@@ -83,28 +84,33 @@ struct HeadArgs {
 // The head's operands (W rows, bias, label) are loaded by head_load, unconditionally
 // from clamped rows, so a caller can issue them long before the row is known: loaded
 // inside the dependent chain each was one more full memory latency (C + 2 of them).
+// MC: classes held in registers (>= hd.C): 4 covers Twitter (4) and Weibo (2) and holds 60
+// fewer registers than kMaxClasses
+template <int MC = kMaxClasses>
 struct HeadRegs {
-  float4 w[kMaxClasses];
-  float bias[kMaxClasses];
+  float4 w[MC];
+  float bias[MC];
   int64_t y;
 };
-__device__ inline void head_load(const HeadArgs& hd, int64_t b, HeadRegs& r) {
+template <int MC>
+__device__ inline void head_load(const HeadArgs& hd, int64_t b, HeadRegs<MC>& r) {
   const int l = threadIdx.x & 63;
   const int cm = hd.C - 1;
 #pragma unroll
-  for (int c = 0; c < kMaxClasses; ++c) {
+  for (int c = 0; c < MC; ++c) {
     const int cc = c < cm ? c : cm;
     r.w[c] = ld4(hd.W + int64_t(cc) * kHeadIn + 4 * l);
     r.bias[c] = hd.bias[cc];
   }
   r.y = hd.y[b];
 }
-__device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4 h, const HeadRegs& r) {
+template <int MC>
+__device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4 h, const HeadRegs<MC>& r) {
   const int l = threadIdx.x & 63;
   const int C = hd.C;
-  float z[kMaxClasses];
+  float z[MC];
 #pragma unroll
-  for (int c = 0; c < kMaxClasses; ++c) {
+  for (int c = 0; c < MC; ++c) {
     z[c] = 0.f;
     if (c < C) {  // C is uniform: the shuffles stay convergent
       const float4 w = r.w[c];
@@ -116,11 +122,11 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
   }
   float m = z[0];
 #pragma unroll
-  for (int c = 1; c < kMaxClasses; ++c)
+  for (int c = 1; c < MC; ++c)
     if (c < C) m = fmaxf(m, z[c]);
   float se = 0.f;
 #pragma unroll
-  for (int c = 0; c < kMaxClasses; ++c)
+  for (int c = 0; c < MC; ++c)
     if (c < C) se += expf(z[c] - m);
   const float lse = m + logf(se);
   const int64_t yb = r.y;
@@ -129,7 +135,7 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
   const float inv_b = 1.0f / float(B);
   float4 dh = f4zero();
 #pragma unroll
-  for (int c = 0; c < kMaxClasses; ++c) {
+  for (int c = 0; c < MC; ++c) {
     if (c < C) {
       const float lp = z[c] - lse;
       const float g = yok ? (expf(lp) - (c == yb ? 1.f : 0.f)) * inv_b : 0.f;
@@ -144,10 +150,18 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
   if (l == 0 && !yok) hd.loss_row[b] = 0.f;
   if (l == 0 && b == 0 && hd.in_status && hd.status && *hd.in_status) atomicOr(hd.status, *hd.in_status);
   if (l == 0 && b == 0 && hd.in_xflags && hd.status && *hd.in_xflags) atomicOr(hd.status, 4);
-  st4(hd.dhead + b * kHeadIn + 4 * l, dh);
+  if (hd.publish) {   // read in the same launch by the tree's other item blocks
+    float* p = hd.dhead + b * kHeadIn + 4 * l;
+    __hip_atomic_store(p + 0, dh.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, dh.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 2, dh.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 3, dh.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    st4(hd.dhead + b * kHeadIn + 4 * l, dh);
+  }
 }
 __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4 h) {
-  HeadRegs r;
+  HeadRegs<kMaxClasses> r;
   head_load(hd, b, r);
   head_row(hd, b, B, h, r);
 }

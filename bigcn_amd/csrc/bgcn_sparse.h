@@ -101,6 +101,8 @@ struct BwdMidArgs {
   int nblk_h;                    // dH1 blocks per direction (node splits of rows_h nodes)
   int64_t rows_h;
   ColsumJob db2;
+  HeadGradJob hg{};               // the classifier head's weight gradients (readout fused)
+  int n_hg = 0;
 };
 struct BwdTailArgs {
   SparseState S;

@@ -1296,8 +1296,12 @@ __global__ __launch_bounds__(256, 3) void k_bwd_mid(BwdMidArgs a) {   // 4 waves
     return;
   }
   b -= a.n_root;
-  colsum_job_block(a.db2, b);
-  BT_END(73);
+  if (b < colsum_job_blocks(256)) {
+    colsum_job_block(a.db2, b);
+    BT_END(73);
+    return;
+  }
+  head_grad_block(a.hg, b - colsum_job_blocks(256));
 }
 
 constexpr int kTailSmem = kDw1Smem > kRedSmem ? kDw1Smem : kRedSmem;
@@ -1332,7 +1336,7 @@ __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
 
 int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s) {
   a.n_root = (a.S.mode != 1) ? 2 * a.S.max_items : 0;
-  const int n = a.n_dw2 + a.n_root + 2 * a.nblk_h + colsum_job_blocks(256);
+  const int n = a.n_dw2 + a.n_root + 2 * a.nblk_h + colsum_job_blocks(256) + a.n_hg;
   if (x_dtype == BGCN_DTYPE_BF16)
     hipLaunchKernelGGL(k_bwd_mid<bf16_t>, dim3(unsigned(n)), dim3(256), 0, s, a);
   else

@@ -474,6 +474,39 @@ def test_dw1_column_split_matches(monkeypatch):
             assert torch.equal(res["1"][k], res["0"][k]), k
 
 
+@pytest.mark.parametrize("mode", ["auto", "sparse"])
+def test_fused_readout_backward_matches(monkeypatch, mode):
+    """The readout backward fused into the item readout (dH2 from the kept sign bits after
+    the tree's head releases its item blocks, per-item db2 partials, head weight gradients
+    in the middle launch) against the separate k_readout_bwd launch: loss, logp and every
+    gradient bit for bit except db2 (partials grouped by item instead of by 64 rows:
+    summation order).  Trees of up to ~1500 nodes span several items, so item blocks wait
+    for their tree's head; the status word stays clean (no spin time-out)."""
+    from bigcn_amd import FusedTrainStep
+    b = _synth(49, 48, 300)
+    if mode == "auto":
+        _unhinted(b)   # the device-gated dense fallback launched (and gated off)
+    p = O.make_params(5000, 64, 64, 4, seed=33)
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("BGCN_READOUT_FUSED", fused)
+        m = _model(p, mode)
+        m.train()
+        step = FusedTrainStep(m)
+        logp = torch.empty(b.num_graphs, 4, device=DEV)
+        loss = step.forward_backward(b, seed=8, logp=logp)
+        step.check_status()
+        g = step.grads()
+        res[fused] = (loss.clone(), logp.clone(), {k: g[prm].clone() for k, prm in zip(KEYS, step.step_params)})
+    assert torch.equal(res["1"][0], res["0"][0])
+    assert torch.equal(res["1"][1], res["0"][1])
+    for k in KEYS:
+        if k.endswith("conv2.bias"):
+            close(res["1"][2][k], res["0"][2][k], what=k)
+        else:
+            assert torch.equal(res["1"][2][k], res["0"][2][k]), k
+
+
 def test_inplace_x_edit_after_collate_skips_update():
     """The host nnz hint (collate / synth_batch) is bound to the x tensor object, so an
     in-place edit that overfills a row goes unseen by the hint.  The step then flags
