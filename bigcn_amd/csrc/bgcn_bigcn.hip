@@ -227,8 +227,8 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
       return;
     }
     b = S.item_tree[blk];
-    beg = int64_t(tree_ptr[b]) + int64_t(S.item_chunk[blk]) * kChunk;
-    end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
+    beg = S.item_beg[blk];
+    end = S.item_end[blk];
     item0 = S.tree_item0[b];
     nit = S.tree_item0[b + 1] - item0;
   } else {
@@ -648,7 +648,8 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
     for (int o = 0; o < 2; ++o) w.plan[d][o] = prep ? prep->plan[d][o] : SpmmPlan{nullptr, nullptr, nullptr};
   if (prep) {   // the batch's weight-independent state lives in the prepared buffer
     w.node_root = prep->node_root;
-    sp.item_tree = prep->item_tree; sp.item_chunk = prep->item_chunk; sp.tree_item0 = prep->tree_item0;
+    sp.item_tree = prep->item_tree; sp.tree_item0 = prep->tree_item0;
+    sp.item_beg = prep->item_beg; sp.item_end = prep->item_end; sp.item_root = prep->item_root;
     sp.hist = prep->hist; sp.col_total = prep->col_total;
     sp.col_start = prep->col_start; sp.col_end = prep->col_end;
     sp.csc = prep->csc;
@@ -734,7 +735,7 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
   if (sparse) {
     hipStream_t xi;
     BGCN_TRY(aux_fork(s, kLaneSide, &xi));
-    BGCN_TRY(sparse_items(sp, a->tree_ptr, xi));
+    BGCN_TRY(sparse_items(sp, a->tree_ptr, a->rootindex, xi));
     side_busy = side_busy || xi != s;
   }
   // conv1 lin, TD and BU in one pass over X: sparse (compaction + gather) or dense MFMA

@@ -310,7 +310,7 @@ struct Prepared {
   SpmmPlan plan[2][2];                   // [td, bu][t (forward), s (backward)]
   int64_t td_cap, bu_cap;                // E + N
   int32_t *tree_ptr, *node_root, *status;
-  int32_t *item_tree, *item_chunk, *tree_item0;
+  int32_t *item_tree, *item_beg, *item_end, *item_root, *tree_item0;   // items: tree, node range, root
   int32_t *x_flags, *x_nnz, *x_cols;
   float* x_vals;
   int32_t *hist, *col_total, *col_start, *col_end;

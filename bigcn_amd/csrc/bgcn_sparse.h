@@ -26,7 +26,8 @@ struct SparseState {
   __bf16* w2s;     // [2][3][64 o][kW2sLd] hi / mid / lo of W2_d[o][k], k < 64 (conv2's B)
   __bf16* w2d;     // [2][2][64 c][kW2dLd] hi / lo of W2_d[o][c] at [c][o] (dH1's B)
   int max_items;
-  int32_t *item_tree, *item_chunk, *tree_item0;
+  int32_t *item_tree, *tree_item0;
+  int32_t *item_beg, *item_end, *item_root;   // item node range [beg, end), its tree's root
   float* root_part;  // [2][max_items][kCap][64]
   int32_t* hist;        // [R][F] per-row-block column counts -> prefixes (R = N / kRowBlock)
   int32_t* col_total;   // [F]
@@ -69,7 +70,7 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
 int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s);
 int sparse_compact_conv1(SparseState& S, const void* X, int xdt, int64_t ldx, float* Z1,
                          hipStream_t s);
-int sparse_items(SparseState& S, const int32_t* tree_ptr, hipStream_t s);
+int sparse_items(SparseState& S, const int32_t* tree_ptr, const int64_t* rootindex, hipStream_t s);
 int sparse_conv2(SparseState& S, const float* H1, const int32_t* tree_ptr, const int64_t* rootindex,
                  float* Z2, KeepSrc keep, hipStream_t s);
 int sparse_csc(SparseState& S, hipStream_t s);

@@ -467,10 +467,8 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   __shared__ float Hs[4 * 32 * kC2Ld];
   __shared__ uint32_t rk[kCap];
   const int d = blockIdx.y;
-  const int b = S.item_tree[item];
-  const int64_t beg = int64_t(tree_ptr[b]) + int64_t(S.item_chunk[item]) * kChunk;
-  const int64_t end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
-  const int64_t r = rootindex[b];
+  const int64_t beg = S.item_beg[item], end = S.item_end[item];
+  const int64_t r = S.item_root[item];
   const int rn = S.nnz[r];
   const int mh = (rn + 1) / 2;   // root slot pairs (slot 2j + h, j < mh)
   const float sc = keep.scale();
@@ -608,7 +606,8 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
 // non-zeros s (the 2 relu(x) factor is applied in k_dw_cols).
 // one block: items per tree = ceil(n_b / kChunk), exclusive scan over trees (1024 at a
 // time with a carry), then every tree writes its item descriptors.
-__device__ inline void items_body(const SparseState& S, const int32_t* __restrict__ tree_ptr) {
+__device__ inline void items_body(const SparseState& S, const int32_t* __restrict__ tree_ptr,
+                                  const int64_t* __restrict__ rootindex) {
   if (S.mode == 1) return;   // (not the overflow flag: the pass over X may run beside this)
   __shared__ int sh[1024];
   __shared__ int carry;
@@ -617,7 +616,8 @@ __device__ inline void items_body(const SparseState& S, const int32_t* __restric
   __syncthreads();
   for (int64_t b0 = 0; b0 < S.B; b0 += nth) {
     const int64_t b = b0 + threadIdx.x;
-    const int chunks = b < S.B ? (tree_ptr[b + 1] - tree_ptr[b] + kChunk - 1) / kChunk : 0;
+    const int t0 = b < S.B ? tree_ptr[b] : 0, t1 = b < S.B ? tree_ptr[b + 1] : 0;
+    const int chunks = (t1 - t0 + kChunk - 1) / kChunk;
     sh[threadIdx.x] = chunks;
     __syncthreads();
     for (int o = 1; o < nth; o <<= 1) {
@@ -629,9 +629,15 @@ __device__ inline void items_body(const SparseState& S, const int32_t* __restric
     const int first = carry + sh[threadIdx.x] - chunks;
     if (b < S.B) {
       S.tree_item0[b] = first < S.max_items ? first : S.max_items;
+      // the item's node range and root stored with it: its readers skip the tree_ptr /
+      // rootindex level of their dependent load chains
+      const int64_t r = rootindex[b];
+      const int32_t root = int32_t(r >= 0 && r < S.N ? r : 0);
       for (int q = 0; q < chunks && first + q < S.max_items; ++q) {
         S.item_tree[first + q] = int32_t(b);
-        S.item_chunk[first + q] = q;
+        S.item_beg[first + q] = t0 + q * kChunk;
+        S.item_end[first + q] = min(t0 + (q + 1) * kChunk, t1);
+        S.item_root[first + q] = root;
       }
     }
     __syncthreads();
@@ -641,8 +647,9 @@ __device__ inline void items_body(const SparseState& S, const int32_t* __restric
   if (threadIdx.x == 0) S.tree_item0[S.B] = carry < S.max_items ? carry : S.max_items;
 }
 
-__global__ __launch_bounds__(1024) void k_items(SparseState S, const int32_t* __restrict__ tree_ptr) {
-  items_body(S, tree_ptr);
+__global__ __launch_bounds__(1024) void k_items(SparseState S, const int32_t* __restrict__ tree_ptr,
+                                                const int64_t* __restrict__ rootindex) {
+  items_body(S, tree_ptr, rootindex);
 }
 
 // dW2 root-column partials per work item (<= kChunk nodes of one tree), on the MFMA:
@@ -659,9 +666,7 @@ __device__ inline void root_part_body(const SparseState& S, const float* __restr
   if (item >= S.tree_item0[S.B]) return;
   uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
   float (*red)[kCap * H] = reinterpret_cast<float (*)[kCap * H]>(smem + kChunk);
-  const int b = S.item_tree[item];
-  const int64_t beg = int64_t(tree_ptr[b]) + int64_t(S.item_chunk[item]) * kChunk;
-  const int64_t end = min<int64_t>(beg + kChunk, int64_t(tree_ptr[b + 1]));
+  const int64_t beg = S.item_beg[item], end = S.item_end[item];
   for (int t = threadIdx.x; t < kChunk; t += 256) {
     const int64_t i = beg + t;
     bits[t] = i < end ? S.rbits[int64_t(d) * S.N + i] : 0u;
@@ -1217,7 +1222,7 @@ __global__ __launch_bounds__(256) void k_prep_b(PrepArgs a) {
   }
   b -= a.nsel;
   if (b == 0) {
-    items_body(a.S, a.tree_ptr);
+    items_body(a.S, a.tree_ptr, a.rootindex);
     return;
   }
   compact_body<false, TX>(a.S, static_cast<const TX*>(a.X), a.ldx, nullptr, b - 1, a.ncomp);
@@ -1394,7 +1399,9 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   t.w2s = c.take<__bf16>(size_t(2) * 3 * H * kW2sLd);
   t.w2d = c.take<__bf16>(size_t(2) * 2 * H * kW2dLd);
   t.item_tree = c.take<int32_t>(size_t(t.max_items));
-  t.item_chunk = c.take<int32_t>(size_t(t.max_items));
+  t.item_beg = c.take<int32_t>(size_t(t.max_items));
+  t.item_end = c.take<int32_t>(size_t(t.max_items));
+  t.item_root = c.take<int32_t>(size_t(t.max_items));
   t.tree_item0 = c.take<int32_t>(size_t(B + 1));
   t.root_part = c.take<float>(size_t(2) * t.max_items * kCap * H);
   const size_t slots = size_t(N) * kCap;
@@ -1443,8 +1450,8 @@ int sparse_compact_conv1(SparseState& S, const void* X, int xdt, int64_t ldx, fl
   return BGCN_OK;
 }
 
-int sparse_items(SparseState& S, const int32_t* tree_ptr, hipStream_t s) {
-  hipLaunchKernelGGL(k_items, dim3(1), dim3(1024), 0, s, S, tree_ptr);
+int sparse_items(SparseState& S, const int32_t* tree_ptr, const int64_t* rootindex, hipStream_t s) {
+  hipLaunchKernelGGL(k_items, dim3(1), dim3(1024), 0, s, S, tree_ptr, rootindex);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -1481,7 +1488,8 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   S.N = N; S.F = F; S.B = B;
   S.max_items = int(N / kChunk + B + 1);
   S.flags = p.x_flags; S.nnz = p.x_nnz; S.cols = p.x_cols; S.vals = p.x_vals;
-  S.item_tree = p.item_tree; S.item_chunk = p.item_chunk; S.tree_item0 = p.tree_item0;
+  S.item_tree = p.item_tree; S.tree_item0 = p.tree_item0;
+  S.item_beg = p.item_beg; S.item_end = p.item_end; S.item_root = p.item_root;
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
   S.csc = p.csc;
   S.root_map = p.node_root;
@@ -1586,7 +1594,8 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
   S.N = N; S.F = F; S.B = B;
   S.max_items = int(N / kChunk + B + 1);
   S.flags = p.x_flags; S.nnz = p.x_nnz; S.cols = p.x_cols; S.vals = p.x_vals;
-  S.item_tree = p.item_tree; S.item_chunk = p.item_chunk; S.tree_item0 = p.tree_item0;
+  S.item_tree = p.item_tree; S.tree_item0 = p.tree_item0;
+  S.item_beg = p.item_beg; S.item_end = p.item_end; S.item_root = p.item_root;
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
   S.csc = p.csc;
   S.root_map = p.node_root;
@@ -1596,7 +1605,7 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
                      nullptr, nullptr, batch, rootindex, p.node_root, p.tree_ptr, 1, 0, nR);
   BGCN_CHECK_LAUNCH();
   if (mode == 1) return BGCN_OK;
-  BGCN_TRY(sparse_items(S, p.tree_ptr, s));
+  BGCN_TRY(sparse_items(S, p.tree_ptr, rootindex, s));
   timing_begin(7, s);
   const dim3 grid(grid_for(N, xdt == BGCN_DTYPE_BF16 ? 8 : 4));
   if (xdt == BGCN_DTYPE_BF16)

@@ -89,7 +89,9 @@ size_t carve_prepared(Carve& c, int64_t N, int64_t B, int64_t F, int64_t Etd, in
   t.status = c.take<int32_t>(1);
   const int64_t max_items = N / kChunkItems + B + 1;
   t.item_tree = c.take<int32_t>(size_t(max_items));
-  t.item_chunk = c.take<int32_t>(size_t(max_items));
+  t.item_beg = c.take<int32_t>(size_t(max_items));
+  t.item_end = c.take<int32_t>(size_t(max_items));
+  t.item_root = c.take<int32_t>(size_t(max_items));
   t.tree_item0 = c.take<int32_t>(size_t(B + 1));
   t.x_flags = c.take<int32_t>(8);
   t.x_nnz = c.take<int32_t>(size_t(N));
