@@ -507,6 +507,30 @@ def test_fused_readout_backward_matches(monkeypatch, mode):
             assert torch.equal(res["1"][2][k], res["0"][2][k]), k
 
 
+def test_train_step_more_than_four_classes():
+    """C = 7: the readout holds every class's head operands (k_readout_items<16>) and the
+    readout backward stays a separate launch (the fused form is sized for <= 4 classes);
+    loss, logp and every gradient match the oracle."""
+    from bigcn_amd import BiGCN, FusedTrainStep
+    b = _synth(50, 24, 300)
+    b.y = (b.y * 7 + torch.arange(b.y.numel(), device=DEV)) % 7
+    p = O.make_params(5000, 64, 64, 7, seed=34)
+    m = BiGCN(5000, 64, 64).to(DEV)
+    m.fc = torch.nn.Linear(4 * 64, 7).to(DEV)
+    m.load_state_dict({k: v.float() for k, v in p.items()})
+    m.eval()
+    step = FusedTrainStep(m)
+    logp = torch.empty(b.num_graphs, 7, device=DEV)
+    loss = step.forward_backward(b, logp=logp)
+    rlogp, rloss, rgrads, _ = _oracle(b, p, False)
+    close(logp, rlogp, what="logp")
+    close(loss, rloss, what="loss")
+    g = step.grads()
+    for k, prm in zip(KEYS, step.step_params):
+        close(g[prm], rgrads[k], what=k)
+    step.check_status()
+
+
 def test_inplace_x_edit_after_collate_skips_update():
     """The host nnz hint (collate / synth_batch) is bound to the x tensor object, so an
     in-place edit that overfills a row goes unseen by the hint.  The step then flags
