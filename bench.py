@@ -141,26 +141,43 @@ def make_pool(wl, rank, pool, device, drop=None):
     return out
 
 
-def cpu_baseline(wl, trees: int, steps: int):
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: the affinity set (BASELINE.md protocol), capped
+    by OMP_NUM_THREADS - the GPU box's CPU share is 16 per GPU (OMP_NUM_THREADS=16 there)
+    while os.sched_getaffinity reports the whole machine's cores."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        cap = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    except ValueError:
+        cap = 16
+    return max(1, min(n, cap if cap > 0 else n))
+
+
+def cpu_baseline(wl, trees: int, steps: int, warmup: int = 1, repeats: int = 3):
     """The oracle (op-for-op plain-PyTorch restatement of the reference step) on the
     host cores: Python root loops, materialised [N, 5064] concat, aten dropout, autograd,
-    Adam with 3 groups."""
+    Adam with 3 groups.  BASELINE.md protocol: B = 128 trees, the median of `repeats`
+    timed repeats; the warm-up and the steps per repeat are cut to fit the bench's time
+    budget (the line states both)."""
     from bigcn_amd.data import synth_batch, synth_tree_sizes
     from oracle import bigcn_oracle as O
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores = cpu_threads()
     torch.set_num_threads(cores)
     rng = np.random.default_rng(777)
     sizes = synth_tree_sizes(rng, trees, wl["mean"], wl["sigma"])
     b = synth_batch(rng, sizes, wl["feats"], wl["classes"], *wl["drop"], device="cpu")
-    batch = {"x": b.x, "edge_index": b.edge_index, "BU_edge_index": b.BU_edge_index, "batch": b.batch,
-             "rootindex": b.rootindex, "y": b.y}
+    batch = {"x": b.x.float(), "edge_index": b.edge_index, "BU_edge_index": b.BU_edge_index,
+             "batch": b.batch, "rootindex": b.rootindex, "y": b.y}
     p = {k: v.requires_grad_(True) for k, v in O.make_params(wl["feats"], 64, 64, wl["classes"]).items()}
     opt = O.make_optimizer(p)
-    O.train_step(p, opt, batch, training=True)        # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(warmup):
         O.train_step(p, opt, batch, training=True)
-    dt = time.perf_counter() - t0
+    rates = []
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            O.train_step(p, opt, batch, training=True)
+        rates.append(trees * steps / (time.perf_counter() - t0))
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as f:
@@ -170,10 +187,28 @@ def cpu_baseline(wl, trees: int, steps: int):
                     break
     except OSError:
         pass
-    return {"value": round(trees * steps / dt, 3), "unit": "trees/s", "cores": cores, "kind": "port",
-            "sample": f"{steps} timed steps (+1 warm-up) of {trees} trees ({int(sizes.sum())} nodes), "
-                      f"same tree/feature distribution; oracle/bigcn_oracle.py train_step, torch "
-                      f"{torch.__version__} on {cpu}, {cores} threads; baseline only"}
+    return {"value": round(float(np.median(rates)), 3), "unit": "trees/s", "cores": cores, "kind": "port",
+            "repeats": [round(r, 3) for r in rates],
+            "sample": f"median of {repeats} repeats x {steps} timed steps (+{warmup} warm-up) of one "
+                      f"{trees}-tree batch ({int(sizes.sum())} nodes), the workload's tree/feature "
+                      f"distribution, fp32; oracle/bigcn_oracle.py train_step, torch {torch.__version__} "
+                      f"on {cpu}, {cores} threads; baseline only.  Deviation from BASELINE.md's "
+                      f"protocol (3 warm-up, >= 10 timed steps per repeat): cut to keep the default "
+                      f"bench run within minutes"}
+
+
+def step_roofline(N_avg: float, wl, sec_per_step: float):
+    """Whole-step HBM fraction: the algorithmic bytes of one step that no design can avoid -
+    X read ONCE (N * F * s; the step's every other access is O(N * 128) or L2-served) - over
+    the measured step time, against 8 TB/s.  BASELINE.md's per-tree figure counts X twice
+    (forward and dW1, 2 * N * F * s), which this build's single pass does not need; both
+    fractions are given."""
+    xbytes = 2 if wl.get("xdtype") == "bf16" else 4
+    once = N_avg * wl["feats"] * xbytes
+    gbs = once / sec_per_step / 1e9
+    return {"bytes_per_step": round(once), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "frac_baseline_md_bytes": round(2 * gbs / PEAK_HBM_GBS, 4),
+            "what": "X read once per step / ms_per_step; frac_baseline_md_bytes counts 2*N*F*s (BASELINE.md)"}
 
 
 def aggregation_bench(b, iters: int = 10):
@@ -260,8 +295,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="twitter15", choices=sorted(WORKLOADS))
     ap.add_argument("--pool", type=int, default=4)
-    ap.add_argument("--cpu-trees", type=int, default=32)
-    ap.add_argument("--cpu-steps", type=int, default=10)
+    ap.add_argument("--cpu-trees", type=int, default=128)
+    ap.add_argument("--cpu-steps", type=int, default=2, help="CPU baseline: timed steps per repeat")
+    ap.add_argument("--cpu-warmup", type=int, default=1)
+    ap.add_argument("--cpu-repeats", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--feat-mode", default="auto", choices=["auto", "dense"],
@@ -282,6 +319,9 @@ def main():
                          "draw is then neither repeated nor timed)")
     ap.add_argument("--compare-dropedge", type=int, default=1,
                     help="at N=1 also time the other DropEdge placement and report it beside the main line")
+    ap.add_argument("--dropin", type=int, default=1,
+                    help="at N=1 also time the drop-in path (model(data), loss.backward(), the "
+                         "optimiser: --path autograd) and report it beside the main line")
     args = ap.parse_args()
 
     from bigcn_amd import BiGCN, FusedTrainStep, Net
@@ -315,12 +355,12 @@ def main():
     fused = FusedTrainStep(model, opt, tddroprate=drops[0], budroprate=drops[1],
                            drop_seed=4242 + rank)       # bgcn_train_step + all-reduce + Adam
 
-    ctx = {"pool": pool, "fused": fused}                # swapped for the DropEdge comparison run
+    ctx = {"pool": pool, "fused": fused, "path": args.path}   # swapped for the comparison runs
 
     def step(i):
         pool, fused = ctx["pool"], ctx["fused"]
         b = pool[i % len(pool)]
-        if args.path == "fused":                        # K1 + fwd + head + loss + bwd in one call;
+        if ctx["path"] == "fused":                      # K1 + fwd + head + loss + bwd in one call;
             nxt = pool[(i + 1) % len(pool)] if args.prefetch else None   # the next batch's
             return fused(b, next_data=nxt)              # preparation overlaps this step
         b.__dict__.pop("_bgcn_graphs", None)          # gcn_norm/CSR rebuilt every step (as GCNConv does)
@@ -367,6 +407,8 @@ def main():
         if timing and dominant:
             ops.set_kernel_timing(True, dominant)
         torch.cuda.synchronize()
+        if ctx["path"] == "fused":
+            ctx["fused"].run_report(reset=True)         # validity of the timed steps only
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
@@ -398,7 +440,7 @@ def main():
                 continue
             avg_ms = ms / n
             n_nodes = N_avg if where == "timed loop" else N_warm
-            bound, work = kernel_work(mode, c, n_nodes, wl["feats"], args.prefetch and args.path == "fused",
+            bound, work = kernel_work(mode, c, n_nodes, wl["feats"], args.prefetch and ctx["path"] == "fused",
                                       2 if wl.get("xdtype") == "bf16" else 4)
             ent = {"avg_ms": round(avg_ms, 4), "launches": n, "measured": where}
             if bound == "mfma":
@@ -423,8 +465,14 @@ def main():
                         "kernel": KERNEL_CLASSES[mode][c], "bytes_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
         value = wl["trees"] * world * steps / dt
+        # the step's validity (one host read after the timed region): the OR of the timed
+        # steps' status words and the optimiser updates skipped as invalid, max over ranks
+        report = ctx["fused"].run_report() if ctx["path"] == "fused" else {"status": 0, "invalid_steps": 0}
+        v = torch.tensor([report["status"], report["invalid_steps"]], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
         return {"value": value, "dt": dt, "N_avg": N_avg, "roof": roof, "kernels": kernels,
-                "loss": float(loss.item())}
+                "loss": float(loss.item()), "status": int(v[0]), "invalid_steps": int(v[1])}
 
     main_res = run(args.feat_mode, args.steps, args.warmup)
     dense_res = None
@@ -439,6 +487,15 @@ def main():
         drop_res = run(args.feat_mode, max(3, args.steps // 2), 2)
         drop_res["where"] = "device" if other else "host_once_untimed"
         ctx["pool"], ctx["fused"] = pool, fused
+    dropin_res = None
+    if world == 1 and args.path == "fused" and args.dropin:
+        # the north_star drop-in form: the reference's loop body verbatim on the per-op
+        # modules (gcn_norm/CSR rebuilt every step as GCNConv does), DropEdge applied by the
+        # host DataLoader as in the reference (once per pool batch here, untimed)
+        ctx["pool"] = make_pool(wl, rank, args.pool, dev, None)
+        ctx["path"] = "autograd"
+        dropin_res = run(args.feat_mode, max(5, args.steps // 2), 3)
+        ctx["pool"], ctx["path"] = pool, args.path
     agg = None
     if world == 1 and args.aggregation:
         agg = aggregation_bench(pool[0])
@@ -452,7 +509,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            cpu = cpu_baseline(wl, args.cpu_trees, args.cpu_steps)
+            cpu = cpu_baseline(wl, args.cpu_trees, args.cpu_steps, args.cpu_warmup, args.cpu_repeats)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "trees/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
@@ -462,7 +519,10 @@ def main():
             "config": {"workload": wl["desc"], "trees_per_gpu": wl["trees"], "feat_path": args.feat_mode,
                        "global_batch": wl["trees"] * world, "avg_nodes_per_batch": round(N_avg, 1),
                        "in_feats": wl["feats"], "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "final_loss": round(final_loss, 5),
+            "roofline": roof, "cpu_baseline": cpu,
+            "invalid_steps": main_res["invalid_steps"], "status": main_res["status"],
+            "step_roofline": step_roofline(N_avg, wl, dt / args.steps),
+            "kernels": kernels, "final_loss": round(final_loss, 5),
             "feat_mode": args.feat_mode, "step_path": args.path, "prefetch_next_batch": bool(args.prefetch),
             "dropedge": ("device, re-drawn every step (timed)" if device_drop
                          else "host, applied once per pool batch at synthesis (not timed)"),
@@ -475,6 +535,14 @@ def main():
             out["dropedge_" + drop_res["where"]] = {
                 "value": round(drop_res["value"], 2), "unit": "trees/s",
                 "ms_per_step": round(drop_res["dt"] / max(3, args.steps // 2) * 1e3, 4)}
+        if dropin_res is not None:
+            n = max(5, args.steps // 2)
+            out["dropin_path"] = {
+                "value": round(dropin_res["value"], 2), "unit": "trees/s",
+                "ms_per_step": round(dropin_res["dt"] / n * 1e3, 4), "steps": n,
+                "what": "--path autograd: model(data) -> F.nll_loss -> loss.backward() -> optimiser "
+                        "step per batch (BiGCN_Twitter.py:183-189 verbatim on the drop-in GCNConv / "
+                        "scatter_mean modules), host DropEdge once per pool batch (untimed)"}
         if dense_res is not None:
             out["dense_path"] = {"value": round(dense_res["value"], 2), "unit": "trees/s",
                                  "ms_per_step": round(dense_res["dt"] / max(3, args.steps // 2) * 1e3, 4),
@@ -483,6 +551,10 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if main_res["invalid_steps"] or main_res["status"]:
+        log(f"INVALID: {main_res['invalid_steps']} timed step(s) skipped by the optimiser, "
+            f"status bits {main_res['status']:#x}")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

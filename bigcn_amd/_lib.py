@@ -29,9 +29,9 @@ BGCN_FEAT_AUTO = 0
 BGCN_FEAT_DENSE = 1
 BGCN_FEAT_SPARSE = 2
 BGCN_SPARSE_CAP = 32
-BGCN_SPARSE_CAP = 32
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1
+ABI_VERSION = 4   # BGCN_ABI_VERSION of include/bgcn.h
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
@@ -110,6 +110,7 @@ class StepArgs(Structure):
         ("next", POINTER(BatchDesc)), ("next_prepared", c_void_p), ("next_prepared_bytes", c_size_t),
         ("status_flag", c_void_p),
         ("images", c_void_p), ("images_current", c_int32),
+        ("status_seen", c_void_p),
     ]
 
 
@@ -188,7 +189,7 @@ def load_library(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.bgcn_abi_version() != 3:
+        if lib.bgcn_abi_version() != ABI_VERSION:
             raise ImportError("libbgcn.so ABI version mismatch")
         _lib = lib
         return lib

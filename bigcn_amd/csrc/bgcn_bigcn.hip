@@ -667,9 +667,10 @@ static bool dense_launched(const bgcn_bigcn_args* a, const SparseState& sp) {
 
 // The readout backward rides in k_readout_items (train step, sparse path) when every item
 // block can be resident at once (its waiting blocks must not hold the slots their tree's
-// head block needs); BGCN_READOUT_FUSED=0 (read per call) keeps k_readout_bwd.
-static bool readout_fused(const SparseState& sp, int64_t B, bool have_head, int C) {
-  if (sp.mode == 1 || !have_head || C > 4) return false;   // (k_readout_items<4>)
+// head block needs) and the step has a status word (a timed-out wait must invalidate the
+// step); BGCN_READOUT_FUSED=0 (read per call) keeps k_readout_bwd.
+static bool readout_fused(const SparseState& sp, int64_t B, bool have_head, bool have_status, int C) {
+  if (sp.mode == 1 || !have_head || !have_status || C > 4) return false;   // (k_readout_items<4>)
   const char* e = std::getenv("BGCN_READOUT_FUSED");
   if (e && atoi(e) == 0) return false;
   static const int64_t slots = [] {
@@ -791,7 +792,8 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z2, a->h2, a->td_b2, a->bu_b2, BGCN_EPI_NONE, w, s));
   const HeadArgs no_head{};
   if (sparse) {
-    const bool fuse = readout_fused(sp, B, head != nullptr && head->W != nullptr, head ? head->C : 0);
+    const bool fuse = readout_fused(sp, B, head != nullptr && head->W != nullptr,
+                                    head != nullptr && head->status != nullptr, head ? head->C : 0);
     HeadArgs hd = head ? *head : no_head;
     hd.publish = fuse ? 1 : 0;
     if (hd.C <= 4)
@@ -838,7 +840,8 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   const int nhead = head ? head->C + 1 : 0;
   // fused into the forward's k_readout_items (dH2 and per-item db2 partials are written;
   // the head's weight gradients move to extra blocks of the middle launch)
-  const bool rfused = readout_fused(sp, B, head != nullptr && head->head != nullptr, head ? head->C : 0);
+  const bool rfused = readout_fused(sp, B, head != nullptr && head->head != nullptr,
+                                    head != nullptr && head->status != nullptr, head ? head->C : 0);
   if (!rfused) {
     hipLaunchKernelGGL(k_readout_bwd, dim3(unsigned(nblk_r + nhead)), dim3(256), 0, s, a->dhead_in, a->h2,
                        a->batch, a->tree_ptr, N, B, w.d2, w.colpart2, int(nblk_r), head ? *head : no_head);

@@ -225,6 +225,7 @@ struct HeadGradJob {
   float* loss;           // [1]
   const int32_t* status;  // or nullptr
   float* status_flag;    // or nullptr
+  int32_t* status_seen = nullptr;   // sticky OR of the step statuses, or nullptr
 };
 __device__ inline void head_grad_block(const HeadGradJob& j, int hb) {
   __shared__ float4 r4[4][64];
@@ -278,7 +279,9 @@ __device__ inline void head_grad_block(const HeadGradJob& j, int hb) {
   }
   if (t == 0) {
     *j.loss = ls[0] / float(B);
-    if (j.status_flag) *j.status_flag = j.status ? float(*j.status & 15) : 0.0f;
+    const int32_t st = j.status ? *j.status & 15 : 0;
+    if (j.status_flag) *j.status_flag = float(st);
+    if (j.status_seen && st) atomicOr(j.status_seen, st);
   }
 }
 

@@ -160,7 +160,10 @@ __device__ void adam_image_tile(const bgcn_adam_tensor& T, const AdamConst& c, i
 }
 
 __global__ __launch_bounds__(256) void k_adam(bgcn_adam_args a, WeightImages im) {
-  if (a.skip_flag && *a.skip_flag != 0.0f) return;   // invalid step (any rank): no update
+  if (a.skip_flag && *a.skip_flag != 0.0f) {   // invalid step (any rank): no update
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.skip_count) atomicAdd(a.skip_count, 1);
+    return;
+  }
   // locate this block's tensor (at most BGCN_ADAM_MAX_TENSORS, uniform scan)
   int k = 0;
   while (k + 1 < a.count && int64_t(blockIdx.x) >= a.block_start[k + 1]) ++k;

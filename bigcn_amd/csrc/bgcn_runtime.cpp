@@ -38,7 +38,8 @@ struct AuxState {
   hipStream_t stream[kAuxLanes] = {};
   hipEvent_t fork[kAuxLanes] = {}, join[kAuxLanes] = {};
   hipEvent_t prep = nullptr;   // end of the side lane's last next-batch preparation
-  bool prep_pending = false;   // recorded, not yet waited for by a caller's stream
+  bool prep_pending = false;   // recorded, not yet waited for by the stream that queued it
+  hipStream_t prep_owner = nullptr;   // the caller's stream whose step queued it
 };
 AuxState g_aux[kMaxDevices];
 std::mutex g_aux_mu;
@@ -152,7 +153,10 @@ int aux_join(hipStream_t main, int lane) {
   if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
   BGCN_CHECK_HIP(hipEventRecord(a->join[lane], a->stream[lane]));
   BGCN_CHECK_HIP(hipStreamWaitEvent(main, a->join[lane], 0));
-  if (lane == kLaneSide) a->prep_pending = false;   // everything queued there is covered
+  // everything queued on the lane is now ordered before `main` - but only the stream that
+  // queued the preparation may stop waiting for it (another stream's join, e.g. an eval
+  // forward, says nothing about the training stream)
+  if (lane == kLaneSide && main == a->prep_owner) a->prep_pending = false;
   return BGCN_OK;
 }
 
@@ -163,6 +167,7 @@ int aux_prep_done(hipStream_t main) {
   if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
   BGCN_CHECK_HIP(hipEventRecord(a->prep, a->stream[kLaneSide]));
   a->prep_pending = true;
+  a->prep_owner = main;
   return BGCN_OK;
 }
 
@@ -173,7 +178,7 @@ int aux_prep_wait(hipStream_t main) {
   if (!a) return fail(BGCN_EHIP, "auxiliary stream unavailable");
   if (!a->prep_pending) return BGCN_OK;
   BGCN_CHECK_HIP(hipStreamWaitEvent(main, a->prep, 0));
-  a->prep_pending = false;
+  if (main == a->prep_owner) a->prep_pending = false;   // other streams keep waiting too
   return BGCN_OK;
 }
 

@@ -37,6 +37,7 @@ struct SparseState {
   uint32_t* rbits;      // [2][N] forward's root keep masks (bit s: root non-zero s kept)
   int32_t* zero_word = nullptr;   // zeroed by the prologue (the train step's status word)
   int32_t* rtick = nullptr;       // [B] readout arrival counters, zeroed by the prologue
+  int32_t* bstatus = nullptr;     // batch status word (bit 0: a batch id outside [0, B)), or nullptr
   const int32_t* root_map = nullptr;   // node -> its tree's root (the CSC placement flags root rows)
   int conv1_clears = 0;           // conv1's block 0 clears zero_word / rtick (no prologue launch)
 };

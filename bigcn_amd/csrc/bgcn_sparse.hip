@@ -82,6 +82,9 @@ __device__ inline void prologue_batch_body(const SparseState& S, const int64_t* 
     const int64_t i = int64_t(bid) * blockDim.x + threadIdx.x;
     if (i >= S.N) return;
     const int64_t b = batch[i];
+    // a node in no tree would keep stale backward rows (the readout never visits it):
+    // flagged as a bad index, which invalidates the step
+    if ((b < 0 || b >= S.B) && S.bstatus) atomicOr(S.bstatus, 1);
     const int64_t bc = b < 0 ? 0 : (b >= S.B ? S.B - 1 : b);
     const int64_t r = rootindex[bc];
     node_root[i] = int32_t((b >= 0 && b < S.B && r >= 0 && r < S.N) ? r : 0);
@@ -1493,6 +1496,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
   S.csc = p.csc;
   S.root_map = p.node_root;
+  S.bstatus = p.status;
   a.batch = bt->batch; a.rootindex = bt->rootindex;
   a.node_root = p.node_root; a.tree_ptr = p.tree_ptr; a.status = p.status;
   a.X = bt->x; a.ldx = bt->ldx;
@@ -1599,6 +1603,7 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
   S.csc = p.csc;
   S.root_map = p.node_root;
+  S.bstatus = p.status;
   if (!(part & 1)) return mode == 1 ? BGCN_OK : sparse_csc(S, s);
   const int nR = int((N + 255) / 256), nP = int((B + 1 + 255) / 256);
   hipLaunchKernelGGL(k_prologue, dim3(unsigned(nR + nP)), dim3(256), 0, s, S, nullptr, nullptr,

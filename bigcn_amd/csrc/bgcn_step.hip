@@ -268,7 +268,7 @@ static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w
   // readout backward (joins the side lane at its end; with a next-batch preparation on
   // the side lane the dW2 chain stays on this stream, which balances the two)
   const HeadGradJob hj{w.head, w.dz, B, int(C), w.loss_row, a->grads[8], a->grads[9], a->loss,
-                       a->status, a->status_flag};
+                       a->status, a->status_flag, a->status_seen};
   return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr, &hj, img);
 }
 

@@ -31,7 +31,7 @@ class AdamArgs(ctypes.Structure):
                 ("bias_correction1", ctypes.c_float), ("bias_correction2_sqrt", ctypes.c_float),
                 ("grad_scale", ctypes.c_float), ("skip_flag", ctypes.c_void_p),
                 ("images", ctypes.c_void_p), ("images_in_feats", ctypes.c_int64),
-                ("image_role", ctypes.c_int32 * MAX_TENSORS)]
+                ("image_role", ctypes.c_int32 * MAX_TENSORS), ("skip_count", ctypes.c_void_p)]
 
 # BGCN_IMAGE_* (include/bgcn.h): which weight image a conv weight's update also writes
 IMAGE_TD_W1, IMAGE_BU_W1, IMAGE_TD_W2, IMAGE_BU_W2 = 1, 2, 3, 4
@@ -70,11 +70,14 @@ class FusedAdam:
 
     @torch.no_grad()
     def step(self, grads: Optional[Sequence[torch.Tensor]] = None, grad_scale: float = 1.0,
-             skip_flag: Optional[torch.Tensor] = None, images=None) -> None:
+             skip_flag: Optional[torch.Tensor] = None, images=None,
+             skip_count: Optional[torch.Tensor] = None) -> None:
         """``grads`` overrides ``p.grad`` (e.g. views of a reduced flat DP bucket).
         ``skip_flag``: a one-element fp32 device tensor; when it holds a non-zero value at
         execution time the launch updates nothing (an invalid training step, decided on
         the device without a host sync; the step counter still advances).
+        ``skip_count``: a one-element int32 device tensor incremented on the device by
+        every skipped update (the number of invalid steps of a run, read once).
         ``images``: ``(buffer, in_feats, {id(param): IMAGE_*})`` - the updates of those
         conv weights also write the weight images a :class:`FusedTrainStep` reads
         (``bgcn_weight_images_size``), so its next step derives nothing from the weights.
@@ -124,6 +127,9 @@ class FusedAdam:
             if skip_flag.dtype != torch.float32 or skip_flag.numel() != 1 or skip_flag.device != self.params()[0].device:
                 raise ValueError("skip_flag must be a one-element fp32 tensor on the parameters' device")
         a.skip_flag = ptr(skip_flag)
+        if skip_count is not None and (skip_count.dtype != torch.int32 or skip_count.numel() != 1):
+            raise ValueError("skip_count must be a one-element int32 tensor")
+        a.skip_count = ptr(skip_count)
         a.bias_correction1 = 1.0 - b1 ** t
         a.bias_correction2_sqrt = math.sqrt(1.0 - b2 ** t)
         a.grad_scale = grad_scale

@@ -97,6 +97,11 @@ class FusedTrainStep:
         a.degree_on = self.degree_on
         self._args = a
         self.status = torch.zeros(1, dtype=torch.int32, device=model.fc.weight.device)
+        # validity over many steps without a host sync per step: the OR of every step's
+        # status (bgcn_step_args.status_seen) and the number of updates the fused Adam
+        # skipped (bgcn_adam_args.skip_count); read by run_report()
+        self.status_seen = torch.zeros(1, dtype=torch.int32, device=model.fc.weight.device)
+        self.skipped = torch.zeros(1, dtype=torch.int32, device=model.fc.weight.device)
         self._pending = None       # (batch, prepared buffer, feat_mode, tensors) from next_data
         self._stream = None
         self._next_desc = None
@@ -213,6 +218,7 @@ class FusedTrainStep:
         loss = torch.empty(1, dtype=torch.float32, device=data.x.device)
         a.loss, a.logp, a.status = ptr(loss), ptr(logp), ptr(self.status)
         a.status_flag = ptr(self.bucket.flag)
+        a.status_seen = ptr(self.status_seen)
         img = self._image_buffer(F)
         a.images = ptr(img)
         a.images_current = int(self._images_key is not None and self._images_key == self._image_key())
@@ -220,11 +226,19 @@ class FusedTrainStep:
         N, B = d.num_nodes, d.num_graphs
         ws = workspace(L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
                                                         d.bu_num_edges), data.x.device)
-        # every auxiliary-lane branch joins back into the caller's stream inside the call,
-        # so the workspaces and converted inputs can return to the allocator afterwards
+        # every branch the step forks joins back into the caller's stream inside the call
+        # (the workspace can return to the allocator afterwards), except the next batch's
+        # preparation, which outlives the call: its buffer is held in self._pending until
+        # the next call (or _join_side()) has ordered a stream behind it
         self._stream = stream_handle()   # the prepared buffers belong to this stream
-        check(L.bgcn_train_step(ctypes.addressof(a), ptr(ws), ws.numel(), self._stream))
-        self._pending = nxt
+        self._pending = nxt              # held before the call: a failure below may leave
+        try:                             # the preparation queued on the side lane
+            check(L.bgcn_train_step(ctypes.addressof(a), ptr(ws), ws.numel(), self._stream))
+        except Exception:
+            if nxt is not None:
+                self._join_side()        # nothing may still write the buffer once it is freed
+                self._pending = None
+            raise
         return loss.view(())
 
     def __call__(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None,
@@ -235,7 +249,7 @@ class FusedTrainStep:
         # an invalid step (status bits, any rank: the flag is summed by the all-reduce)
         # updates nothing; check_status() reports why
         self.opt.step(grads=self.bucket.views(), grad_scale=1.0 / world, skip_flag=self.bucket.flag,
-                      images=(self._images, self._images_F, self._img_roles))
+                      images=(self._images, self._images_F, self._img_roles), skip_count=self.skipped)
         # the images now hold the updated weights (or, after an invalid step, the unchanged
         # ones: the launch skipped params and images alike)
         self._images_key = self._image_key()
@@ -260,12 +274,25 @@ class FusedTrainStep:
         except Exception:   # interpreter shutdown: nothing left to order
             pass
 
+    def run_report(self, reset: bool = False) -> dict:
+        """Host sync: validity of every step since construction (or the last reset):
+        ``status`` = the OR of the steps' status words (0: every step valid) and
+        ``invalid_steps`` = the optimiser updates skipped because a step was invalid (on
+        any rank).  Steps run through forward_backward() alone count in ``status`` only."""
+        out = {"status": int(self.status_seen.item()), "invalid_steps": int(self.skipped.item())}
+        if reset:
+            self.status_seen.zero_()
+            self.skipped.zero_()
+        return out
+
     def check_status(self) -> None:
-        """Host sync: raise on a bad edge index / label / (feat_mode "sparse") an
-        over-full feature row seen by the last step."""
+        """Host sync: raise on a bad edge index / batch id / label / (feat_mode "sparse")
+        an over-full feature row / an internal time-out seen by the last step.  Any of them
+        makes the step invalid: __call__'s optimiser update was skipped."""
         s = int(self.status.item())
         if s & 1:
-            raise IndexError("edge_index contains an index out of range [0, num_nodes)")
+            raise IndexError("edge_index or batch contains an index out of range "
+                             "([0, num_nodes) / [0, num_graphs))")
         if s & 2:
             raise IndexError("label out of range [0, num_classes)")
         if s & 4:

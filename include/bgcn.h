@@ -47,7 +47,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 3
+#define BGCN_ABI_VERSION 4
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -318,9 +318,12 @@ int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree
  * data-parallel bucket; the all-reduce and bgcn_adam_step follow.  Parameter order:
  * td_w1 td_b1 td_w2 td_b2 bu_w1 bu_b1 bu_w2 bu_b2 fc_w [C, 256] fc_b [C] (the
  * reference state_dict layout).  *status (optional, zeroed by the call): bit 0 = an
- * edge index outside [0, N) (skipped), bit 1 = a label outside [0, C) (ignored),
+ * edge index outside [0, N) or a batch id outside [0, B), bit 1 = a label outside [0, C),
  * bit 2 = a feature row with more than BGCN_SPARSE_CAP non-zeros under BGCN_FEAT_SPARSE,
- * bit 3 = an internal cross-workgroup hand-off timed out (results invalid; never expected).
+ * bit 3 = an internal cross-workgroup hand-off timed out (never expected).  ANY set bit
+ * makes the step's results invalid: through status_flag the optimiser skips the update.
+ * status_seen (optional, never cleared by the library): every step ORs its status into
+ * it, so a training loop can check the validity of many steps with one host read.
  *   prepared / prepared_ready: the current batch's prepared buffer; when not ready the
  *   call prepares it first (on the same stream).
  *   next / next_prepared (optional): a batch to prepare during this step on the
@@ -355,6 +358,7 @@ typedef struct bgcn_step_args {
    * same buffer, params untouched since) and the step skips deriving them; 0: the step
    * derives them into the buffer. */
   void* images; int32_t images_current;
+  int32_t* status_seen;          /* [1] or NULL: OR of every step's status     */
 } bgcn_step_args;
 
 /* Bytes of a weight-image buffer for in_feats = F (W1^T [F][128], W2^T [2][F+64][64]
@@ -380,7 +384,8 @@ int bgcn_join_side(bgcn_stream_t stream);
  * grad_scale multiplies every gradient first (1/world for a summed DP bucket).
  * bias_correction1 = 1 - beta1^t, bias_correction2_sqrt = sqrt(1 - beta2^t).
  * skip_flag (optional): when *skip_flag != 0 on the device the launch leaves every
- * parameter and moment untouched (an invalid step, see bgcn_step_args.status_flag).
+ * parameter and moment untouched (an invalid step, see bgcn_step_args.status_flag) and
+ * adds one to *skip_count (optional).
  * block_start is scratch filled by the library.
  * -------------------------------------------------------------------------- */
 #define BGCN_ADAM_MAX_TENSORS 16
@@ -402,6 +407,9 @@ typedef struct bgcn_adam_args {
    * (an invalid step leaves params and images untouched alike). */
   void* images; int64_t images_in_feats;
   int32_t image_role[BGCN_ADAM_MAX_TENSORS];
+  /* skip_count (optional): incremented on the device each time skip_flag skips the
+   * update, so the number of invalid steps of a run is one host read at its end */
+  int32_t* skip_count;
 } bgcn_adam_args;
 #define BGCN_IMAGE_NONE 0
 #define BGCN_IMAGE_TD_W1 1

@@ -1,0 +1,205 @@
+"""Oracle parity at the FULL sizes of the BASELINE configurations, on the bench's exact
+workloads (``bench.WORKLOADS`` / ``bench.make_pool``: 128 trees of LogNormal sizes, 5000-dim
+bag-of-words X, device DropEdge where the workload draws it), and the cross-workgroup
+hand-offs of the step under the load the bench puts beside them.
+
+Reference loop body: ``model/Twitter/BiGCN_Twitter.py:168-169`` (batch_size 128) and
+``:183-189`` (model -> nll_loss -> backward); Weibo head ``model/Weibo/BiGCN_Weibo.py:76-89``.
+
+Every step here runs as the bench runs it: ``FusedTrainStep`` on a non-default stream with
+``next_data`` set, so the next batch's preparation (DropEdge, K1, the pass over X) runs on
+the side lane beside the checked step's chain.  The oracle (``oracle/bigcn_oracle.py``,
+fp64, CPU) gets the same inputs: the DropEdge lists its restatement of the device draw
+keeps for the step's drop seed, and the in-kernel dropout draw materialised by
+``keep_words``.
+
+Tolerances (fp32 / bf16-split kernels vs the fp64 oracle), both per tensor:
+  * max-scaled:  max|a - b| <= 1e-4 * max|b|
+  * elementwise: |a - b| <= 1e-4 * (|b| + rms(b))   for EVERY element - small entries
+    (e.g. the dW1 column of a rare word) are held to the same relative bar.
+"""
+import numpy as np
+import pytest
+import torch
+
+import bench
+from oracle import bigcn_oracle as O
+from test_gpu_bigcn import DEV, _oracle, close
+from test_gpu_train import KEYS, _model
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def close_elem(a, b, tol=TOL, what=""):
+    """|a - b| <= tol * (|b| + rms(b)) elementwise."""
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    if b.numel() == 0:
+        return
+    rms = float(b.pow(2).mean().sqrt())
+    bound = tol * (b.abs() + rms)
+    err = (a - b).abs()
+    bad = err > bound
+    if bool(bad.any()):
+        worst = int(torch.argmax(err / bound.clamp_min(1e-300)))
+        raise AssertionError(f"{what}: {int(bad.sum())} of {b.numel()} elements exceed "
+                             f"{tol:g}*(|b|+rms); worst at {worst}: {float(a.flatten()[worst]):.6e} vs "
+                             f"{float(b.flatten()[worst]):.6e} (rms {rms:.3e})")
+
+
+def _oracle_batch(b, drops, drop_seed):
+    """The batch the oracle trains on: the kept DropEdge lists of the device draw."""
+    B = b.num_graphs
+    batch = b.batch.cpu().numpy()
+    ref = type("RefBatch", (), {})()
+    ref.x, ref.batch, ref.rootindex, ref.y = b.x, b.batch, b.rootindex, b.y
+    ei, bu = b.edge_index, b.BU_edge_index
+    if drops[0] > 0:
+        ei = torch.as_tensor(O.drop_edges(ei.cpu().numpy(), batch, B, drops[0], drop_seed, 0))
+    if drops[1] > 0:
+        bu = torch.as_tensor(O.drop_edges(bu.cpu().numpy(), batch, B, drops[1], drop_seed, 1))
+    ref.edge_index, ref.BU_edge_index = ei, bu
+    return ref
+
+
+@pytest.mark.parametrize("workload", ["twitter15", "weibo_bf16", "synth1024_bf16"])
+def test_full_size_step_matches_oracle(workload):
+    """BASELINE configs[1] (twitter15: 128 trees x mean 256, fp32, DropEdge 0.2/0.2),
+    configs[2] (weibo_bf16: 128 x mean 816, bf16 X, 2-class Net, no DropEdge) and the
+    per-GPU shape of configs[4] (synth1024_bf16: 128 x mean 1024, bf16 X, DropEdge): loss,
+    log-probs and all ten gradients of the bench's step against the fp64 oracle."""
+    from bigcn_amd import FusedTrainStep
+    from bigcn_amd.ops import keep_words, unpack_keep
+    wl = bench.WORKLOADS[workload]
+    drops = wl["drop"]
+    pool = bench.make_pool(wl, 0, 2, DEV, drop=(0.0, 0.0))    # undropped: DropEdge on the device
+    C, F = wl["classes"], wl["feats"]
+    p = O.make_params(F, 64, 64, C, seed=31)
+    m = _model(p, "auto", classes=C)
+    m.train()
+    step = FusedTrainStep(m, tddroprate=drops[0], budroprate=drops[1], drop_seed=4242)
+    b = pool[1]
+    logp = torch.empty(b.num_graphs, C, device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step.forward_backward(pool[0], seed=11, next_data=pool[1])       # prepares pool[1] beside it
+        loss = step.forward_backward(b, seed=12, logp=logp, next_data=pool[0])
+        grads = [step.grads()[prm].clone() for prm in step.step_params]
+        step.discard_prefetch()
+    torch.cuda.synchronize()
+    step.check_status()
+    assert step.run_report()["status"] == 0
+    N = b.x.size(0)
+    assert N > 25000, N                                                  # really full size
+    mk = unpack_keep(keep_words(12, N, F, DEV).cpu(), 64 + F)
+    ref = _oracle_batch(b, drops, step.last_drop_seed)
+    if drops[0] > 0:
+        assert ref.edge_index.size(1) < b.edge_index.size(1)
+    rlogp, rloss, rgrads, _ = _oracle(ref, p, True, mk[0], mk[1])
+    del mk
+    close(loss, rloss, what="loss")
+    close(logp, rlogp, what="logp")
+    close_elem(logp, rlogp, what="logp")
+    for k, g in zip(KEYS, grads):
+        close(g, rgrads[k], what=k)
+        close_elem(g, rgrads[k], what=k)
+
+
+def test_readout_handoffs_under_prefetch_load(monkeypatch):
+    """The fused readout backward's cross-workgroup hand-offs (item partials to the tree's
+    last arrival, dhead from the head block to the tree's other item blocks) with the
+    next batch's paced pass over X running beside them, exactly as in the bench: twenty
+    consecutive full-size twitter15 steps with BGCN_READOUT_FUSED=1 equal the separate
+    k_readout_bwd launch (=0) bit for bit - loss and every gradient except db2, whose
+    partials are grouped by item instead of by row block (summation order) - and no step
+    sets a status bit (no spin time-out, no K1 look-back time-out).  Then twenty steps with
+    the fused Adam: no update skipped."""
+    from bigcn_amd import FusedTrainStep
+    wl = bench.WORKLOADS["twitter15"]
+    pool = bench.make_pool(wl, 0, 4, DEV, drop=(0.0, 0.0))
+    p = O.make_params(5000, 64, 64, 4, seed=32)
+    runs = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("BGCN_READOUT_FUSED", fused)
+        m = _model(p)
+        m.train()
+        step = FusedTrainStep(m, tddroprate=0.2, budroprate=0.2, drop_seed=77)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        out = []
+        with torch.cuda.stream(s):
+            for i in range(20):
+                loss = step.forward_backward(pool[i % 4], seed=500 + i, next_data=pool[(i + 1) % 4])
+                out.append((loss.clone(), [step.grads()[prm].clone() for prm in step.step_params]))
+            step.discard_prefetch()
+        torch.cuda.synchronize()
+        assert step.run_report()["status"] == 0, fused
+        runs[fused] = out
+    for i, ((l1, g1), (l0, g0)) in enumerate(zip(runs["1"], runs["0"])):
+        assert torch.equal(l1, l0), i
+        for k, a, c in zip(KEYS, g1, g0):
+            if k.endswith("conv2.bias"):
+                close(a, c, what=f"step {i} {k}")
+            else:
+                assert torch.equal(a, c), (i, k)
+    monkeypatch.setenv("BGCN_READOUT_FUSED", "1")
+    m = _model(p)
+    m.train()
+    step = FusedTrainStep(m, tddroprate=0.2, budroprate=0.2, drop_seed=78)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for i in range(20):
+            step(pool[i % 4], seed=900 + i, next_data=pool[(i + 1) % 4])
+        step.discard_prefetch()
+    torch.cuda.synchronize()
+    rep = step.run_report()
+    assert rep == {"status": 0, "invalid_steps": 0}, rep
+    assert step.opt.step_count == 20
+
+
+def test_run_report_counts_invalid_steps():
+    """An invalid step (a label out of range: status bit 1) is counted by the fused Adam's
+    skip counter and ORed into the sticky status, without a host sync in the loop."""
+    from bigcn_amd import FusedTrainStep
+    from test_gpu_bigcn import _synth
+    good = _synth(70, 8, 60)
+    bad = _synth(71, 8, 60)
+    bad.y = bad.y.clone()
+    bad.y[2] = 9
+    p = O.make_params(5000, 64, 64, 4, seed=33)
+    m = _model(p)
+    m.train()
+    step = FusedTrainStep(m)
+    for b in (good, bad, good, bad, bad):
+        step(b, seed=1)
+    rep = step.run_report(reset=True)
+    assert rep == {"status": 2, "invalid_steps": 3}, rep
+    step(good, seed=2)
+    assert step.run_report() == {"status": 0, "invalid_steps": 0}
+
+
+def test_batch_ids_out_of_range_invalidate_the_step():
+    """A node whose batch id lies outside [0, num_graphs) belongs to no tree (the readout
+    never visits it, so its backward rows would be stale): status bit 0, the update is
+    skipped, check_status raises IndexError."""
+    from bigcn_amd import FusedTrainStep
+    from test_gpu_bigcn import _synth
+    b = _synth(72, 6, 40)
+    b.batch = b.batch.clone()
+    b.batch[-1] = b.num_graphs + 3                      # sorted order kept: last node, last tree
+    p = O.make_params(5000, 64, 64, 4, seed=34)
+    m = _model(p)
+    m.train()
+    step = FusedTrainStep(m)
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    step(b, seed=3)
+    torch.cuda.synchronize()
+    with pytest.raises(IndexError):
+        step.check_status()
+    assert step.run_report()["invalid_steps"] == 1
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k]), k
