@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_adam_step",
     "bgcn_prepare_workspace_size", "bgcn_prepare_batch",
     "bgcn_train_step_workspace_size", "bgcn_train_step", "bgcn_join_side",
-    "bgcn_weight_images_size",
+    "bgcn_weight_images_size", "bgcn_train_step_saved",
 )
 
 
@@ -162,6 +162,8 @@ _SIGS = {
     "bgcn_train_step_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64, c_int64, c_int64]),
     "bgcn_train_step": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_join_side": (c_int, [c_void_p]),
+    "bgcn_train_step_saved": (c_int, [c_void_p, c_size_t, c_int64, c_int64, c_int64, c_int64,
+                                      POINTER(c_void_p), POINTER(c_void_p)]),
     "bgcn_set_kernel_timing": (c_int, [c_int]),
     "bgcn_kernel_timing": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),
 }

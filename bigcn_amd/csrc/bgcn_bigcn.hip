@@ -401,7 +401,8 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
                                                      int nblk, HeadGradJob hj) {
   BT_BEGIN
   if (int(blockIdx.x) >= nblk) {
-    head_grad_block(hj, int(blockIdx.x) - nblk);
+    __shared__ __attribute__((aligned(16))) float hsm[kHeadGradSmem];
+    head_grad_block(hj, int(blockIdx.x) - nblk, hsm);
     return;
   }
   constexpr int kPer = kReadBwdRows / 8;

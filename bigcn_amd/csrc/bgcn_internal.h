@@ -185,8 +185,11 @@ constexpr int kColsumGroups = 16;
 __host__ __device__ constexpr int colsum_job_blocks(int threads) {
   return 128 * kColsumGroups / threads;
 }
-__device__ inline void colsum_job_block(const ColsumJob& j, int jb) {
-  __shared__ float red[kColsumGroups * 64];
+// sm: kColsumSmem floats of the caller's shared memory (a merged launch passes its role
+// buffer, so the job adds no LDS of its own to the launch)
+constexpr int kColsumSmem = kColsumGroups * 64;
+__device__ inline void colsum_job_block(const ColsumJob& j, int jb, float* sm) {
+  float* red = sm;
   const int cpb = int(blockDim.x) / kColsumGroups;    // columns per block (<= 64)
   const int cl = threadIdx.x % cpb, g = threadIdx.x / cpb;
   const int c = jb * cpb + cl;
@@ -227,10 +230,12 @@ struct HeadGradJob {
   float* status_flag;    // or nullptr
   int32_t* status_seen = nullptr;   // sticky OR of the step statuses, or nullptr
 };
-__device__ inline void head_grad_block(const HeadGradJob& j, int hb) {
-  __shared__ float4 r4[4][64];
-  __shared__ float ls[256];
-  __shared__ float dbp[kMaxClasses][64];
+// sm: kHeadGradSmem floats of the caller's shared memory (16-byte aligned)
+constexpr int kHeadGradSmem = 4 * 64 * 4 + 256 + kMaxClasses * 64;
+__device__ inline void head_grad_block(const HeadGradJob& j, int hb, float* sm) {
+  float4 (*r4)[64] = reinterpret_cast<float4 (*)[64]>(sm);
+  float* ls = sm + 4 * 64 * 4;
+  float (*dbp)[64] = reinterpret_cast<float (*)[64]>(sm + 4 * 64 * 4 + 256);
   const int t = threadIdx.x;
   const int64_t B = j.B;
   const int C = j.C;

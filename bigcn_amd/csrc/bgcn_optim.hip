@@ -145,15 +145,16 @@ __device__ void adam_image_tile(const bgcn_adam_tensor& T, const AdamConst& c, i
     const int o0 = ob + 4 * qq;
     float* dst = w1 ? im.w1t + kr * (2 * H) + d * H + o0 : im.w2t + (int64_t(d) * K + kr) * H + o0;
     st4(dst, v);
-    if (!w1 && kr < H) {   // the middle launch's split image [c][o] (c = kr)
-      __bf16* ds = im.w2d + int64_t(d) * 2 * H * kW2dLd + kr * kW2dLd + o0;
+    if (!w1 && kr < H) {   // the middle launch's split image [c][o] (c = kr): hi / mid / lo
+      __bf16* ds = im.w2d + int64_t(d) * 3 * H * kW2dLd + kr * kW2dLd + o0;
       const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        __bf16 x, y;
-        split_bf16(vv[j], x, y);
+        __bf16 x, y, z;
+        split3_bf16(vv[j], x, y, z);
         ds[j] = x;
         ds[H * kW2dLd + j] = y;
+        ds[2 * H * kW2dLd + j] = z;
       }
     }
   }

@@ -24,7 +24,7 @@ struct SparseState {
   // W2_d[:, :64] split for the bf16 MFMA once per step by the prologue (the blocks of
   // conv2 / the middle launch copy them instead of splitting per block):
   __bf16* w2s;     // [2][3][64 o][kW2sLd] hi / mid / lo of W2_d[o][k], k < 64 (conv2's B)
-  __bf16* w2d;     // [2][2][64 c][kW2dLd] hi / lo of W2_d[o][c] at [c][o] (dH1's B)
+  __bf16* w2d;     // [2][3][64 c][kW2dLd] hi / mid / lo of W2_d[o][c] at [c][o] (dH1's B)
   int max_items;
   int32_t *item_tree, *tree_item0;
   int32_t *item_beg, *item_end, *item_root;   // item node range [beg, end), its tree's root
@@ -48,7 +48,7 @@ struct WeightImages {
   float* w1t;      // [F][128]
   float* w2t;      // [2][F+64][64]
   __bf16* w2s;     // [2][3][64][kW2sLd]
-  __bf16* w2d;     // [2][2][64][kW2dLd]
+  __bf16* w2d;     // [2][3][64][kW2dLd]
 };
 size_t carve_images(Carve& c, int64_t F, WeightImages* im);
 // CSC slot bit 31: the entry's row is a tree root (its column gets a dW2 root-column term)

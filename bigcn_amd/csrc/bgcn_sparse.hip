@@ -101,8 +101,8 @@ __device__ inline void prologue_batch_body(const SparseState& S, const int64_t* 
 }
 
 // W2_d[:, :64] split for the bf16 MFMA (kSplitBlocks 256-thread blocks per direction, one
-// element per thread): conv2's image [3][o][k] (hi / mid / lo) and the middle launch's
-// [2][c][o] (hi / lo).
+// element per thread): conv2's image [3][o][k] and the middle launch's [3][c][o] (hi / mid /
+// lo: both feed fp32-grade six-product MFMAs).
 constexpr int kSplitBlocks = H * H / 256;
 __device__ inline void split_w2_block(const SparseState& S, int sb, const float* __restrict__ w2td,
                                       const float* __restrict__ w2bu) {
@@ -110,7 +110,7 @@ __device__ inline void split_w2_block(const SparseState& S, int sb, const float*
   const float* W2 = d == 0 ? w2td : w2bu;
   const int64_t ld = S.F + H;
   __bf16* cs = S.w2s + int64_t(d) * 3 * H * kW2sLd;
-  __bf16* ds = S.w2d + int64_t(d) * 2 * H * kW2dLd;
+  __bf16* ds = S.w2d + int64_t(d) * 3 * H * kW2dLd;
   {
     const int e = (sb % kSplitBlocks) * 256 + threadIdx.x;
     const int o = e >> 6, k = e & 63;
@@ -120,9 +120,10 @@ __device__ inline void split_w2_block(const SparseState& S, int sb, const float*
     cs[o * kW2sLd + k] = x;
     cs[H * kW2sLd + o * kW2sLd + k] = y;
     cs[2 * H * kW2sLd + o * kW2sLd + k] = z;
-    split_bf16(v, x, y);
+    split3_bf16(v, x, y, z);
     ds[k * kW2dLd + o] = x;
     ds[H * kW2dLd + k * kW2dLd + o] = y;
+    ds[2 * H * kW2dLd + k * kW2dLd + o] = z;
   }
 }
 
@@ -1275,8 +1276,12 @@ __global__ __launch_bounds__(256) void k_prep_f(PrepArgs a) {
 // middle (256 threads): dW2 partials (dense / relu(H1) block), dW2 root partials, dH1,
 // db2 column sums;  tail (1024 threads): dW1 over the CSC, dW2 root columns, the dW2
 // partial reduction, db1 column sums.  Roles by block range, in that order.
-constexpr int kMidSmem = kDw2Smem > kRootPartSmem ? (kDw2Smem > kDh1Smem ? kDw2Smem : kDh1Smem)
-                                                  : (kRootPartSmem > kDh1Smem ? kRootPartSmem : kDh1Smem);
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+#if BGCN_DH1_PS
+constexpr int kMidSmem = cmax(cmax(cmax(kDw2Smem, kRootPartSmem), cmax(kDh1SmemPs, kColsumSmem)), kHeadGradSmem);
+#else
+constexpr int kMidSmem = cmax(cmax(cmax(kDw2Smem, kRootPartSmem), cmax(kDh1Smem, kColsumSmem)), kHeadGradSmem);
+#endif
 template <class TX>
 __global__ __launch_bounds__(256, 3) void k_bwd_mid(BwdMidArgs a) {   // 4 waves per SIMD: one round for the whole grid
   __shared__ __attribute__((aligned(16))) float smem[kMidSmem];
@@ -1285,8 +1290,16 @@ __global__ __launch_bounds__(256, 3) void k_bwd_mid(BwdMidArgs a) {   // 4 waves
   if (b < 2 * a.nblk_h) {   // longest-lived role first
     // the relu(H1) block of dW2 rides along when the sparse path is the one running
     float* part = (a.S.mode != 1 && !dense_active(a.gate)) ? a.dw2_sparse.part : nullptr;
+#if BGCN_DH1_PS
+    dh1_body_ps(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, a.rows_h, part,
+                a.nblk_h, b % a.nblk_h, b / a.nblk_h, smem, a.S.mode != 1 ? a.S.w2d : nullptr);
+#elif BGCN_DH1_OLD
+    dh1_body_old(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, a.rows_h, part,
+                 a.nblk_h, b % a.nblk_h, b / a.nblk_h, smem, a.S.mode != 1 ? a.S.w2d : nullptr);
+#else
     dh1_body(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, a.rows_h, part,
              a.nblk_h, b % a.nblk_h, b / a.nblk_h, smem, a.S.mode != 1 ? a.S.w2d : nullptr);
+#endif
     BT_END(72);
     return;
   }
@@ -1305,14 +1318,14 @@ __global__ __launch_bounds__(256, 3) void k_bwd_mid(BwdMidArgs a) {   // 4 waves
   }
   b -= a.n_root;
   if (b < colsum_job_blocks(256)) {
-    colsum_job_block(a.db2, b);
+    colsum_job_block(a.db2, b, smem);
     BT_END(73);
     return;
   }
-  head_grad_block(a.hg, b - colsum_job_blocks(256));
+  head_grad_block(a.hg, b - colsum_job_blocks(256), smem);
 }
 
-constexpr int kTailSmem = kDw1Smem > kRedSmem ? kDw1Smem : kRedSmem;
+constexpr int kTailSmem = cmax(cmax(kDw1Smem, kRedSmem), kColsumSmem);
 #ifndef BGCN_TAIL_THREADS
 #define BGCN_TAIL_THREADS 512   // 1024-thread blocks ran one per CU: dW1 in two rounds
 #endif
@@ -1336,7 +1349,7 @@ __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
     BT_END(82);
     return;
   }
-  colsum_job_block(a.db1, b - a.red_dense.blocks - a.red_sparse.blocks);
+  colsum_job_block(a.db1, b - a.red_dense.blocks - a.red_sparse.blocks, smem);
   BT_END(83);
 }
 
@@ -1386,7 +1399,7 @@ size_t carve_images(Carve& c, int64_t F, WeightImages* im) {
   t.w1t = c.take<float>(size_t(F) * 2 * H);
   t.w2t = c.take<float>(size_t(2) * (F + H) * H);
   t.w2s = c.take<__bf16>(size_t(2) * 3 * H * kW2sLd);
-  t.w2d = c.take<__bf16>(size_t(2) * 2 * H * kW2dLd);
+  t.w2d = c.take<__bf16>(size_t(2) * 3 * H * kW2dLd);
   if (im) *im = t;
   return c.off;
 }
@@ -1400,7 +1413,7 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   t.w1t = c.take<float>(size_t(F) * 2 * H);
   t.w2t = c.take<float>(size_t(2) * (F + H) * H);
   t.w2s = c.take<__bf16>(size_t(2) * 3 * H * kW2sLd);
-  t.w2d = c.take<__bf16>(size_t(2) * 2 * H * kW2dLd);
+  t.w2d = c.take<__bf16>(size_t(2) * 3 * H * kW2dLd);
   t.item_tree = c.take<int32_t>(size_t(t.max_items));
   t.item_beg = c.take<int32_t>(size_t(t.max_items));
   t.item_end = c.take<int32_t>(size_t(t.max_items));

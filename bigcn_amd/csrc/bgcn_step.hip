@@ -293,6 +293,22 @@ extern "C" size_t bgcn_train_step_workspace_size(int64_t num_nodes, int64_t num_
                                   bu_num_edges);
 }
 
+extern "C" int bgcn_train_step_saved(void* workspace, size_t workspace_bytes, int64_t num_nodes,
+                                     int64_t num_graphs, int64_t in_feats, int64_t num_classes, float** h1,
+                                     float** h2) {
+  using namespace bgcn;
+  BGCN_CHECK_ARG(num_nodes > 0 && num_graphs > 0 && in_feats > 0 && num_classes >= 1, "bad sizes");
+  BGCN_CHECK_ARG(workspace && h1 && h2 &&
+                     workspace_bytes >= train_step_ws_size(num_nodes, num_graphs, in_feats, num_classes, 0, 0),
+                 "workspace too small");
+  StepWs w;
+  Carve c(workspace, workspace_bytes);
+  carve_step(c, num_nodes, num_graphs, in_feats, num_classes, &w);
+  *h1 = w.h1;
+  *h2 = w.h2;
+  return BGCN_OK;
+}
+
 extern "C" int bgcn_train_step(const bgcn_step_args* args, void* workspace, size_t workspace_bytes,
                                bgcn_stream_t stream) {
   return bgcn::train_step_impl(args, workspace, workspace_bytes,

@@ -231,6 +231,7 @@ class FusedTrainStep:
         # preparation, which outlives the call: its buffer is held in self._pending until
         # the next call (or _join_side()) has ordered a stream behind it
         self._stream = stream_handle()   # the prepared buffers belong to this stream
+        self._last = (ws, N, B, F)       # the saved activations of this step (saved_activations)
         self._pending = nxt              # held before the call: a failure below may leave
         try:                             # the preparation queued on the side lane
             check(L.bgcn_train_step(ctypes.addressof(a), ptr(ws), ws.numel(), self._stream))
@@ -273,6 +274,27 @@ class FusedTrainStep:
                 self._join_side()
         except Exception:   # interpreter shutdown: nothing left to order
             pass
+
+    def saved_activations(self):
+        """(H1, H2) of the last step: the pre-relu conv1 / conv2 outputs, [N, 128] fp32
+        device tensors (TD columns [0, 64), BU [64, 128)), views of the step's workspace
+        (valid until the next step) - the per-stage intermediates the reference's
+        explain_PHEME.py:91-162 dumps."""
+        if getattr(self, "_last", None) is None:
+            raise RuntimeError("no step has run yet")
+        ws, N, B, F = self._last
+        h1, h2 = ctypes.c_void_p(), ctypes.c_void_p()
+        check(_lib.lib().bgcn_train_step_saved(ptr(ws), ws.numel(), N, B, F, self.num_classes,
+                                               ctypes.byref(h1), ctypes.byref(h2)))
+        base = ws.data_ptr()
+        n = N * 128
+        out = []
+        for p_ in (h1.value, h2.value):
+            off = p_ - base
+            if off % 4 or off < 0 or off + 4 * n > ws.numel():
+                raise RuntimeError("activation view outside the step workspace")
+            out.append(ws[off:off + 4 * n].view(torch.float32).view(N, 128))
+        return tuple(out)
 
     def run_report(self, reset: bool = False) -> dict:
         """Host sync: validity of every step since construction (or the last reset):

@@ -371,6 +371,14 @@ size_t bgcn_train_step_workspace_size(int64_t num_nodes, int64_t num_graphs, int
                                       int64_t bu_num_edges);
 int bgcn_train_step(const bgcn_step_args* args, void* workspace, size_t workspace_bytes,
                     bgcn_stream_t stream);
+/* The saved pre-activation conv outputs of the last step run in a step workspace (the
+ * fused step's form of the per-stage dumps of explain_PHEME.py:91-162): h1 = conv1 output
+ * H1 (pre-relu, also the detached x2), h2 = conv2 output H2 (pre-relu), each [N, 128]
+ * fp32 with TD in columns [0, 64) and BU in [64, 128).  Pointers into `workspace` (valid
+ * until it is reused); the sizes must be those of the step. */
+int bgcn_train_step_saved(void* workspace, size_t workspace_bytes, int64_t num_nodes,
+                          int64_t num_graphs, int64_t in_feats, int64_t num_classes, float** h1,
+                          float** h2);
 /* A next-batch preparation (args->next) may still run on the library's auxiliary lane
  * when bgcn_train_step returns; the next bgcn_train_step call orders its stream after it.
  * bgcn_join_side makes `stream` wait for all auxiliary-lane work - call it before

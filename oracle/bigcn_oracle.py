@@ -160,21 +160,41 @@ def make_params(in_feats: int = 5000, hid: int = 64, out: int = 64, num_classes:
     return p
 
 
+def _relu(h: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
+    """``F.relu``; with ``mask`` (bool, h's shape) the relu' decision is injected: h * mask.
+    Only entries where h is within rounding of zero (a tie: +-1e-9 where the value is O(1))
+    can differ from relu(h) - by at most that entry's magnitude in the forward value - but
+    their gradient flips from 0 to 1 or back.  Parity tests at full size pass the kernel's
+    own decisions so the comparison measures arithmetic error, not ties (test_gpu_fullsize)."""
+    if mask is None:
+        return F.relu(h)
+    return h * mask.to(h.dtype)
+
+
 def direction_forward(p: Dict[str, torch.Tensor], prefix: str, x: torch.Tensor,
                       edge_index: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor,
                       training: bool = False, keep_mask: Optional[torch.Tensor] = None,
-                      degree_on: str = "col", stages: Optional[dict] = None) -> torch.Tensor:
+                      degree_on: str = "col", stages: Optional[dict] = None,
+                      relu_masks=None) -> torch.Tensor:
     """``TDrumorGCN.forward`` (``BiGCN_Twitter.py:26-67``) == ``BUrumorGCN.forward``
     (``:77-114``) with the direction's edge_index.  ``keep_mask`` ([N, hid+F] bool)
     injects the dropout draw of ``:54`` (``F.dropout(p=0.5)`` keeps with prob 0.5 and
-    scales by 2); ``None`` in training mode uses torch's own RNG like the reference."""
+    scales by 2); ``None`` in training mode uses torch's own RNG like the reference.
+    ``relu_masks`` (optional ``(m1 [N, hid], m2 [N, out])`` bool): the relu' decisions of
+    the relu over conv1's columns of the concat (``:53``) and of the relu after conv2
+    (``:57``), see ``_relu``."""
     w1, b1 = p[f"{prefix}.conv1.lin.weight"], p[f"{prefix}.conv1.bias"]
     w2, b2 = p[f"{prefix}.conv2.lin.weight"], p[f"{prefix}.conv2.bias"]
+    m1, m2 = relu_masks if relu_masks is not None else (None, None)
     x1 = copy.copy(x.float())                                            # :28
     h = gcn_conv(x, edge_index, w1, b1, degree_on=degree_on)             # :42
     x2 = copy.copy(h)                                                    # :44  detached leaf
     h = torch.cat((h, root_extend(x1, batch, rootindex)), 1)             # :46-51
-    h = F.relu(h)                                                        # :53
+    if m1 is None:
+        h = F.relu(h)                                                    # :53
+    else:   # the same relu, its decision on conv1's columns injected
+        hid = m1.size(1)
+        h = torch.cat((_relu(h[:, :hid], m1), F.relu(h[:, hid:])), 1)
     if training:                                                         # :54
         if keep_mask is None:
             h = F.dropout(h, training=True)
@@ -184,7 +204,9 @@ def direction_forward(p: Dict[str, torch.Tensor], prefix: str, x: torch.Tensor,
         stages[f"{prefix}.h1"] = x2.detach().clone()
         stages[f"{prefix}.a2"] = h.detach().clone()
     h = gcn_conv(h, edge_index, w2, b2, degree_on=degree_on)             # :56
-    h = F.relu(h)                                                        # :57
+    if stages is not None:
+        stages[f"{prefix}.h2"] = h.detach().clone()
+    h = _relu(h, m2)                                                     # :57
     if stages is not None:
         stages[f"{prefix}.r1"] = h.detach().clone()
     h = torch.cat((h, root_extend(x2, batch, rootindex)), 1)             # :59-63
@@ -196,13 +218,15 @@ def direction_forward(p: Dict[str, torch.Tensor], prefix: str, x: torch.Tensor,
 
 def bigcn_forward(p: Dict[str, torch.Tensor], x, td_edge_index, bu_edge_index, batch, rootindex,
                   training: bool = False, td_mask=None, bu_mask=None, degree_on: str = "col",
-                  stages: Optional[dict] = None) -> torch.Tensor:
+                  stages: Optional[dict] = None, relu_masks: Optional[dict] = None) -> torch.Tensor:
     """``BiGCN.forward`` (``BiGCN_Twitter.py:125-131``): TD first, BU second, concat
-    **BU first** (``:128``), fc, log_softmax."""
+    **BU first** (``:128``), fc, log_softmax.  ``relu_masks``: {prefix: (m1, m2)}, see
+    ``direction_forward``."""
+    rm = relu_masks or {}
     td = direction_forward(p, "TDrumorGCN", x, td_edge_index, batch, rootindex, training, td_mask,
-                           degree_on, stages)
+                           degree_on, stages, rm.get("TDrumorGCN"))
     bu = direction_forward(p, "BUrumorGCN", x, bu_edge_index, batch, rootindex, training, bu_mask,
-                           degree_on, stages)
+                           degree_on, stages, rm.get("BUrumorGCN"))
     h = torch.cat((bu, td), 1)
     if stages is not None:
         stages["head_in"] = h.detach().clone()
@@ -246,11 +270,11 @@ def params_requiring_grad(p: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]
 
 def reference_grads(p: Dict[str, torch.Tensor], batch: dict, training: bool = False,
                     td_mask=None, bu_mask=None, degree_on: str = "col",
-                    stages: Optional[dict] = None):
+                    stages: Optional[dict] = None, relu_masks: Optional[dict] = None):
     """Forward + NLL + backward on fresh leaf copies of ``p``; returns (loss, logp, grads)."""
     q = params_requiring_grad(p)
     logp = bigcn_forward(q, batch["x"], batch["edge_index"], batch["BU_edge_index"], batch["batch"],
-                         batch["rootindex"], training, td_mask, bu_mask, degree_on, stages)
+                         batch["rootindex"], training, td_mask, bu_mask, degree_on, stages, relu_masks)
     loss = bigcn_loss(logp, batch["y"])
     loss.backward()
     return loss.detach(), logp.detach(), {k: v.grad.detach().clone() for k, v in q.items()}

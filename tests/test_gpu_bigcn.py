@@ -76,12 +76,12 @@ def _synth(seed, B, mean, F=5000, droprates=(0.2, 0.2), root_random=False):
     return synth_batch(rng, sizes, F, 4, *droprates, device=DEV, root_random=root_random)
 
 
-def _oracle(b, p, training, td_mask=None, bu_mask=None, degree_on="col"):
+def _oracle(b, p, training, td_mask=None, bu_mask=None, degree_on="col", relu_masks=None):
     batch = {"x": b.x.double().cpu(), "edge_index": b.edge_index.cpu(), "BU_edge_index": b.BU_edge_index.cpu(),
              "batch": b.batch.cpu(), "rootindex": b.rootindex.cpu(), "y": b.y.cpu()}
     pd = {k: v.double() for k, v in p.items()}
     st = {}
-    loss, logp, grads = O.reference_grads(pd, batch, training, td_mask, bu_mask, degree_on, st)
+    loss, logp, grads = O.reference_grads(pd, batch, training, td_mask, bu_mask, degree_on, st, relu_masks)
     return logp, loss, grads, st
 
 

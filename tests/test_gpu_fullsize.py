@@ -17,6 +17,14 @@ Tolerances (fp32 / bf16-split kernels vs the fp64 oracle), both per tensor:
   * max-scaled:  max|a - b| <= 1e-4 * max|b|
   * elementwise: |a - b| <= 1e-4 * (|b| + rms(b))   for EVERY element - small entries
     (e.g. the dW1 column of a rare word) are held to the same relative bar.
+
+relu' ties.  An entry of H1 or H2 within rounding of zero takes relu' = 1 in one precision
+and 0 in another; that one flip moves dW1 by ~1e-4 of its max (Weibo size: the
+reference's OWN fp32 path differs from fp64 by 3.2e-4 on TD conv1's weight through a
+single tie, tools/prec_probe.py).  The oracle therefore takes the kernel's relu'
+decisions (``relu_masks``, from the step's saved H1 / H2), and the test asserts that
+every decision differing from the fp64 sign is a tie (|h| <= 1e-5 max|h|).  The saved H1 /
+H2 themselves are compared with the oracle's stages at the same tolerances.
 """
 import numpy as np
 import pytest
@@ -29,6 +37,17 @@ from test_gpu_train import KEYS, _model
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
+
+
+def errors(a, b):
+    """(max-scaled error, worst elementwise error ratio |a-b| / (|b| + rms(b)))."""
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    if b.numel() == 0:
+        return 0.0, 0.0
+    err = (a - b).abs()
+    rms = float(b.pow(2).mean().sqrt())
+    return float(err.max()) / max(float(b.abs().max()), 1e-300), float((err / (b.abs() + rms).clamp_min(1e-300)).max())
 
 
 def close_elem(a, b, tol=TOL, what=""):
@@ -88,6 +107,7 @@ def test_full_size_step_matches_oracle(workload):
         step.forward_backward(pool[0], seed=11, next_data=pool[1])       # prepares pool[1] beside it
         loss = step.forward_backward(b, seed=12, logp=logp, next_data=pool[0])
         grads = [step.grads()[prm].clone() for prm in step.step_params]
+        h1, h2 = (t.clone() for t in step.saved_activations())
         step.discard_prefetch()
     torch.cuda.synchronize()
     step.check_status()
@@ -98,14 +118,29 @@ def test_full_size_step_matches_oracle(workload):
     ref = _oracle_batch(b, drops, step.last_drop_seed)
     if drops[0] > 0:
         assert ref.edge_index.size(1) < b.edge_index.size(1)
-    rlogp, rloss, rgrads, _ = _oracle(ref, p, True, mk[0], mk[1])
+    h1, h2 = h1.cpu(), h2.cpu()
+    masks = {d: (h1[:, 64 * k:64 * (k + 1)] > 0, h2[:, 64 * k:64 * (k + 1)] > 0)
+             for k, d in enumerate(("TDrumorGCN", "BUrumorGCN"))}
+    rlogp, rloss, rgrads, st = _oracle(ref, p, True, mk[0], mk[1], relu_masks=masks)
     del mk
-    close(loss, rloss, what="loss")
-    close(logp, rlogp, what="logp")
-    close_elem(logp, rlogp, what="logp")
-    for k, g in zip(KEYS, grads):
-        close(g, rgrads[k], what=k)
-        close_elem(g, rgrads[k], what=k)
+    table = {k: errors(g, rgrads[k]) for k, g in zip(KEYS, grads)}
+    table["logp"] = errors(logp, rlogp)
+    table["loss"] = errors(loss, rloss)
+    ties = {}
+    for k, d in enumerate(("TDrumorGCN", "BUrumorGCN")):
+        for name, mine in (("h1", h1), ("h2", h2)):
+            r = st[f"{d}.{name}"]
+            got = mine[:, 64 * k:64 * (k + 1)]
+            table[f"{d}.{name} (saved)"] = errors(got, r)
+            flip = (got > 0) != (r > 0)
+            ties[f"{d}.{name}"] = int(flip.sum())
+            assert bool((r[flip].abs() <= 1e-5 * r.abs().max()).all()), \
+                f"{d}.{name}: a relu' decision differs from the fp64 sign away from zero"
+    print(f"\n{workload} N={N}: (max-scaled, elementwise) error vs the fp64 oracle; relu' ties {ties}")
+    for k, (e1, e2) in table.items():
+        print(f"  {k:32s} {e1:.2e} {e2:.2e}")
+    bad = {k: v for k, v in table.items() if v[0] > TOL or v[1] > TOL}
+    assert not bad, f"{workload}: beyond {TOL:g}: {bad}"
 
 
 def test_readout_handoffs_under_prefetch_load(monkeypatch):

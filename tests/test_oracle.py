@@ -123,6 +123,29 @@ def test_oracle_fp32_matches_golden(name):
         np.testing.assert_allclose(v.numpy(), g["grad:" + k], rtol=1e-4, atol=1e-6, err_msg=k)
 
 
+def test_injected_relu_decisions():
+    """relu_masks equal to the oracle's own relu' decisions reproduce the plain oracle
+    exactly; a flipped decision changes the step."""
+    g = load_golden("bigcn_train_mixed.npz")
+    b = golden_batch(g)
+    p = {k: v.double() for k, v in golden_params(g).items()}
+    batch = {"x": b.x.double(), "edge_index": b.edge_index, "BU_edge_index": b.BU_edge_index,
+             "batch": b.batch, "rootindex": b.rootindex, "y": b.y}
+    tdm, bum = torch.as_tensor(g["td_keep"]), torch.as_tensor(g["bu_keep"])
+    st = {}
+    _, logp, grads = O.reference_grads(p, batch, True, tdm, bum, stages=st)
+    masks = {d: (st[f"{d}.h1"] > 0, st[f"{d}.h2"] > 0) for d in ("TDrumorGCN", "BUrumorGCN")}
+    _, logp2, grads2 = O.reference_grads(p, batch, True, tdm, bum, relu_masks=masks)
+    assert torch.equal(logp, logp2)
+    for k in grads:
+        assert torch.equal(grads[k], grads2[k]), k
+    m1, m2 = masks["TDrumorGCN"]
+    m2 = m2.clone()
+    m2[0, 0] = ~m2[0, 0]                      # one flipped decision of TD's conv2 relu
+    _, _, grads3 = O.reference_grads(p, batch, True, tdm, bum, relu_masks={"TDrumorGCN": (m1, m2)})
+    assert not torch.equal(grads["TDrumorGCN.conv2.bias"], grads3["TDrumorGCN.conv2.bias"])
+
+
 def test_train_step_runs_adam_groups():
     g = load_golden("bigcn_train_mixed.npz")
     b = golden_batch(g)
