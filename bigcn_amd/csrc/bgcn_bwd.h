@@ -183,8 +183,12 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
 // with cancellation, so the three-product form's 2^-16 relative error per product grew to
 // 1.2e-4 of max|dW1| at Weibo size (the fp32 reference path: 1e-6); with six products dW1
 // is fp32-grade at every size (tests/test_gpu_fullsize.py).  The dZ2 tile is staged in LDS
-// as fp32 (rows of 68 floats) and split three ways per fragment in registers; W2[:, :64]^T
-// comes split three ways from the weight image (rows of 72 bf16, 16-byte aligned).
+// split three ways (hi / mid / lo, rows of 72 bf16 = 16-byte aligned, each element split
+// once by the staging thread) and W2[:, :64]^T comes split three ways from the weight
+// image, so every operand fragment is one 16-byte LDS read.  55 KB of LDS: two blocks per
+// CU (splitting per fragment in registers instead fit three per CU in 45 KB but took
+// longer: twitter15 0.280 vs 0.276 ms, the two column-half waves split every element
+// twice; round 2's three-product form 0.273).
 //
 // dw2part != nullptr (the sparse path, gated off when the dense path runs): the same
 // block also forms the relu(H1) block of dW2 over its rows,
@@ -201,406 +205,26 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
 #define BGCN_DH1_X6 1   // 0: the three-product form (A/B only: not fp32-grade)
 #endif
 constexpr int kDh1Rows = 64;
-constexpr int kDsLd = H + 8;   // bf16 row stride of the W2^T split image rows
-constexpr int kDzLd = H + 4;   // fp32 row stride of the staged dZ2 tile (16-byte aligned rows)
-constexpr int kDh1Smem = kDh1Rows * kDzLd + (3 * H * kDsLd) / 2 + 2 * H;
-static_assert(kDh1Rows * kDzLd >= H * H, "the dW2 combine reuses the dZ2 tile");
-__device__ __forceinline__ void split3_x8(float4 a, float4 b, bf16x8& h, bf16x8& m, bf16x8& l) {
-  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    __bf16 x, y, z;
-    split3_bf16(v[j], x, y, z);
-    h[j] = x;
-    m[j] = y;
-    l[j] = z;
-  }
-}
+constexpr int kDsLd = H + 8;   // bf16 row stride of the staged, split tiles
+constexpr int kDh1Smem = (6 * kDh1Rows * kDsLd) / 2 + 2 * H;
+// dH1[i][d*H + c] = (dZ2_d[i] . W2_d[:, c]) * keep(d,i,c) * s * [H1 > 0], c < H,
+// + block partial column sums, over `rows` consecutive nodes (64-row tiles) of direction
+// d per block.  A 64-row x 64-column tile per 256-thread block, four waves as 2 row halves
+// x 2 column halves, on the bf16 MFMA in split form (mfma_x3, bgcn_common.h: this launch
+// was bound by the f32-input MFMA, 64 cycles per 32x32x2).  The dZ2 tile and W2[:, :64]^T
+// are staged in LDS already split (hi / lo bf16, rows of 72 = 16-byte aligned), so every
+// operand fragment of dH1 is one 16-byte LDS read.
+//
+// dw2part != nullptr (the sparse path, gated off when the dense path runs): the same
+// block also forms the relu(H1) block of dW2 over its rows,
+//   part[d][bx][o][c] = sum_i dZ2_d[i][o] * keep(d,i,c) * s * relu(H1_d[i][c]),
+// from the operands the dH1 tile already holds: each lane's 16 (row, c) values of H1 and
+// of the keep words, in the accumulator row order acc_row(q, h), are its B fragments of
+// two 32x32x16 k-steps (element j of step s: row 16s + 8(j>>2) + 4h + (j&3)); the dZ2^T
+// fragments are read from the staged tile in that row order.  Two row-half waves are
+// combined in LDS (fixed order).  One block per node split (the tail reduces the splits).
+// Device body, 256 threads; smem: kDh1Smem floats.
 __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __restrict__ H1,
-                                const float* __restrict__ W2td, const float* __restrict__ W2bu,
-                                int64_t ldw2, int64_t N, KeepSrc keep, float* __restrict__ dH1,
-                                float* __restrict__ colpart, int64_t rows, float* __restrict__ dw2part,
-                                int nsplit, int bx, int d, float* smem,
-                                const __bf16* __restrict__ w2d = nullptr) {
-  float* Dz = smem;                                                   // dZ2 tile [row][o], fp32
-  __bf16* Wh = reinterpret_cast<__bf16*>(smem + kDh1Rows * kDzLd);    // W2[:, :64]^T [c][o]
-  __bf16* Wm = Wh + H * kDsLd;
-  __bf16* Wl = Wm + H * kDsLd;
-  float (*red)[H] = reinterpret_cast<float (*)[H]>(smem + kDh1Rows * kDzLd + (3 * H * kDsLd) / 2);
-  const float* W2 = d == 0 ? W2td : W2bu;
-  const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int rh = wid & 1, ch = wid >> 1;
-  const int r = l & 31, h = l >> 5;
-  const int c = ch * 32 + r;  // output column of this lane (within H)
-  const int64_t beg = int64_t(bx) * rows, end = min<int64_t>(beg + rows, N);
-  const int ntile = int((end - beg + kDh1Rows - 1) / kDh1Rows);
-  const float sc = keep.scale();
-  const bool want_dw2 = dw2part != nullptr;
-
-  float4 dv[4];
-  float hv[16];
-  auto gload = [&](int64_t blk0) {   // one tile's dZ2 rows and this lane's H1 values
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {    // element e = tid + 256u of a 64 x 16 float4 grid
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      dv[u] = ld4(dZ2 + min<int64_t>(blk0 + rr, N - 1) * (2 * H) + d * H + q);
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int64_t i = min<int64_t>(blk0 + rh * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, N - 1);
-      hv[q] = H1[i * (2 * H) + d * H + c];
-    }
-  };
-  if (w2d) {   // the weight image ([2][3][c][o], hi / mid / lo): 16-byte copies
-    static_assert(kDsLd == kW2dLd, "dH1's W rows are the weight image's rows");
-    const __bf16* src = w2d + int64_t(d) * 3 * H * kW2dLd;
-    uint4 cv[6];
-#pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      const int e = threadIdx.x + 256 * u, part = e >> 9, cc = (e >> 3) & 63, q = (e & 7) * 8;
-      cv[u] = *reinterpret_cast<const uint4*>(src + (int64_t(part) * H + cc) * kW2dLd + q);
-    }
-    gload(beg);
-#pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      const int e = threadIdx.x + 256 * u, part = e >> 9, cc = (e >> 3) & 63, q = (e & 7) * 8;
-      *reinterpret_cast<uint4*>(Wh + (int64_t(part) * H + cc) * kDsLd + q) = cv[u];
-    }
-  } else {
-    float4 wv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      wv[u] = ld4(W2 + int64_t(rr) * ldw2 + q);
-    }
-    gload(beg);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {     // W2[o = rr][c = q + t] -> W^T[c][o]
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      const float v[4] = {wv[u].x, wv[u].y, wv[u].z, wv[u].w};
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        split3_bf16(v[t], Wh[(q + t) * kDsLd + rr], Wm[(q + t) * kDsLd + rr], Wl[(q + t) * kDsLd + rr]);
-    }
-  }
-  f32x16 pw0 = {}, pw1 = {};   // dW2 partial: o in [0, 32) / [32, 64), columns ch*32 + r
-  float cs = 0.f;
-  for (int t = 0; t < ntile; ++t) {
-    const int64_t blk0 = beg + int64_t(t) * kDh1Rows;
-    const int64_t row0 = blk0 + rh * 32;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      st4(&Dz[rr * kDzLd + q], dv[u]);
-    }
-    // this tile's per-lane operands: a2 = keep * s * relu(H1) split (dW2's B fragments in
-    // accumulator row order), bit q of km = kept and H1 > 0 (dH1)
-    bf16x8 a2h[2], a2l[2];
-    uint32_t km = 0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(i, N - 1)), uint32_t(c >> 5));
-      const bool kept = ((wd >> (c & 31)) & 1u) && i < N;
-      __bf16 x, y;
-      split_bf16(kept ? sc * fmaxf(hv[q], 0.f) : 0.f, x, y);
-      a2h[q >> 3][q & 7] = x;
-      a2l[q >> 3][q & 7] = y;
-      km |= uint32_t(kept && hv[q] > 0.f) << q;
-      if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // four keep hashes in flight
-    }
-    __syncthreads();
-    // dH1: A = dZ2 rows (row rh*32 + r, o = 16s + 8h + j, split here), B = W2^T (column c)
-    f32x16 acc = {};
-    const float* ar = &Dz[(rh * 32 + r) * kDzLd + 8 * h];
-    const __bf16* bh = &Wh[c * kDsLd + 8 * h];
-    const __bf16* bm = &Wm[c * kDsLd + 8 * h];
-    const __bf16* bl = &Wl[c * kDsLd + 8 * h];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 xh, xm, xl;
-      split3_x8(ld4(ar + 16 * s), ld4(ar + 16 * s + 4), xh, xm, xl);
-#if BGCN_DH1_X6
-      acc = mfma_x6(xh, xm, xl, *reinterpret_cast<const bf16x8*>(bh + 16 * s),
-                    *reinterpret_cast<const bf16x8*>(bm + 16 * s), *reinterpret_cast<const bf16x8*>(bl + 16 * s),
-                    acc);
-#else   // A/B: the three-product form (hi + mid = the two-way split)
-      (void)xl;
-      acc = mfma_x3(xh, xm, *reinterpret_cast<const bf16x8*>(bh + 16 * s),
-                    *reinterpret_cast<const bf16x8*>(bm + 16 * s), acc);
-#endif
-      __builtin_amdgcn_sched_barrier(0);   // one k-step's fragments live at a time
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      const float g = ((km >> q) & 1u) ? acc[q] * sc : 0.f;
-      if (i < N) {
-        dH1[i * (2 * H) + d * H + c] = g;
-        cs += g;
-      }
-    }
-    if (want_dw2) {
-      // dW2: A = dZ2^T (o = r / 32 + r, rows in the a2 fragments' order), B = a2
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 z0h, z0l, z1h, z1l;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = rh * 32 + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
-          __bf16 x, y;
-          split_bf16(Dz[k * kDzLd + r], x, y);
-          z0h[j] = x;
-          z0l[j] = y;
-          split_bf16(Dz[k * kDzLd + 32 + r], x, y);
-          z1h[j] = x;
-          z1l[j] = y;
-        }
-        pw0 = mfma_x3(z0h, z0l, a2h[s], a2l[s], pw0);
-        pw1 = mfma_x3(z1h, z1l, a2h[s], a2l[s], pw1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __syncthreads();   // the staged tile is rewritten by the next tile
-    if (t + 1 < ntile) gload(blk0 + kDh1Rows);
-  }
-  cs += __shfl_xor(cs, 32);
-  if (h == 0) red[rh][c] = cs;
-  __syncthreads();
-  if (threadIdx.x < H)
-    colpart[int64_t(bx) * (2 * H) + d * H + threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x];
-  if (!want_dw2) return;
-  // combine the two row halves: rh = 1 parks its partial in LDS, rh = 0 adds and stores
-  float* P = smem;   // [64 o][64 c] over the staged tile (free after the loop's barrier)
-  if (rh == 1) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int o = acc_row(q, l);
-      P[o * H + c] = pw0[q];
-      P[(32 + o) * H + c] = pw1[q];
-    }
-  }
-  __syncthreads();
-  if (rh == 0) {
-    float* out = dw2part + (int64_t(d) * nsplit + bx) * (H * H);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int o = acc_row(q, l);
-      out[o * H + c] = pw0[q] + P[o * H + c];
-      out[(32 + o) * H + c] = pw1[q] + P[(32 + o) * H + c];
-    }
-  }
-}
-
-
-#if BGCN_DH1_OLD   // A/B only: round 2's pre-split staging (three products)
-// dH1[i][d*H + c] = (dZ2_d[i] . W2_d[:, c]) * keep(d,i,c) * s * [H1 > 0], c < H,
-// + block partial column sums, over `rows` consecutive nodes (64-row tiles) of direction
-// d per block.  A 64-row x 64-column tile per 256-thread block, four waves as 2 row halves
-// x 2 column halves, on the bf16 MFMA in split form (mfma_x3, bgcn_common.h: this launch
-// was bound by the f32-input MFMA, 64 cycles per 32x32x2).  The dZ2 tile and W2[:, :64]^T
-// are staged in LDS already split (hi / lo bf16, rows of 72 = 16-byte aligned), so every
-// operand fragment of dH1 is one 16-byte LDS read.
-//
-// dw2part != nullptr (the sparse path, gated off when the dense path runs): the same
-// block also forms the relu(H1) block of dW2 over its rows,
-//   part[d][bx][o][c] = sum_i dZ2_d[i][o] * keep(d,i,c) * s * relu(H1_d[i][c]),
-// from the operands the dH1 tile already holds: each lane's 16 (row, c) values of H1 and
-// of the keep words, in the accumulator row order acc_row(q, h), are its B fragments of
-// two 32x32x16 k-steps (element j of step s: row 16s + 8(j>>2) + 4h + (j&3)); the dZ2^T
-// fragments are read from the staged tile in that row order.  Two row-half waves are
-// combined in LDS (fixed order).  One block per node split (the tail reduces the splits).
-// Device body, 256 threads; smem: kDh1Smem floats.
-__device__ inline void dh1_body_old(const float* __restrict__ dZ2, const float* __restrict__ H1,
-                                const float* __restrict__ W2td, const float* __restrict__ W2bu,
-                                int64_t ldw2, int64_t N, KeepSrc keep, float* __restrict__ dH1,
-                                float* __restrict__ colpart, int64_t rows, float* __restrict__ dw2part,
-                                int nsplit, int bx, int d, float* smem,
-                                const __bf16* __restrict__ w2d = nullptr) {
-  __bf16* Dh = reinterpret_cast<__bf16*>(smem);   // dZ2 tile [row][o], hi / lo
-  __bf16* Dl = Dh + kDh1Rows * kDsLd;
-  __bf16* Wh = Dl + kDh1Rows * kDsLd;             // W2[:, :64]^T [c][o], hi / lo
-  __bf16* Wl = Wh + H * kDsLd;
-  float (*red)[H] = reinterpret_cast<float (*)[H]>(smem + 2 * kDh1Rows * kDsLd);
-  const float* W2 = d == 0 ? W2td : W2bu;
-  const int wid = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int rh = wid & 1, ch = wid >> 1;
-  const int r = l & 31, h = l >> 5;
-  const int c = ch * 32 + r;  // output column of this lane (within H)
-  const int64_t beg = int64_t(bx) * rows, end = min<int64_t>(beg + rows, N);
-  const int ntile = int((end - beg + kDh1Rows - 1) / kDh1Rows);
-  const float sc = keep.scale();
-  const bool want_dw2 = dw2part != nullptr;
-
-  float4 dv[4];
-  float hv[16];
-  auto gload = [&](int64_t blk0) {   // one tile's dZ2 rows and this lane's H1 values
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {    // element e = tid + 256u of a 64 x 16 float4 grid
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      dv[u] = ld4(dZ2 + min<int64_t>(blk0 + rr, N - 1) * (2 * H) + d * H + q);
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int64_t i = min<int64_t>(blk0 + rh * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, N - 1);
-      hv[q] = H1[i * (2 * H) + d * H + c];
-    }
-  };
-  if (w2d) {   // the prologue's split image ([2][c][o], hi / lo): 16-byte copies
-    
-    const __bf16* src = w2d + int64_t(d) * 3 * H * kW2dLd;
-    uint4 cv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = threadIdx.x + 256 * u, part = e >> 9, c = (e >> 3) & 63, q = (e & 7) * 8;
-      cv[u] = *reinterpret_cast<const uint4*>(src + (int64_t(part) * H + c) * kW2dLd + q);
-    }
-    gload(beg);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = threadIdx.x + 256 * u, part = e >> 9, c = (e >> 3) & 63, q = (e & 7) * 8;
-      *reinterpret_cast<uint4*>((part ? Wl : Wh) + c * kDsLd + q) = cv[u];
-    }
-  } else {
-    float4 wv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      wv[u] = ld4(W2 + int64_t(rr) * ldw2 + q);
-    }
-    gload(beg);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {     // W2[o = rr][c = q + t] -> W^T[c][o]
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      const float v[4] = {wv[u].x, wv[u].y, wv[u].z, wv[u].w};
-#pragma unroll
-      for (int t = 0; t < 4; ++t) split_bf16(v[t], Wh[(q + t) * kDsLd + rr], Wl[(q + t) * kDsLd + rr]);
-    }
-  }
-  f32x16 pw0 = {}, pw1 = {};   // dW2 partial: o in [0, 32) / [32, 64), columns ch*32 + r
-  float cs = 0.f;
-  for (int t = 0; t < ntile; ++t) {
-    const int64_t blk0 = beg + int64_t(t) * kDh1Rows;
-    const int64_t row0 = blk0 + rh * 32;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = threadIdx.x + 256 * u, rr = e >> 4, q = (e & 15) * 4;
-      const float v[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) split_bf16(v[k], Dh[rr * kDsLd + q + k], Dl[rr * kDsLd + q + k]);
-    }
-    // this tile's per-lane operands: a2 = keep * s * relu(H1) split (dW2's B fragments in
-    // accumulator row order), bit q of km = kept and H1 > 0 (dH1)
-    bf16x8 a2h[2], a2l[2];
-    uint32_t km = 0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(i, N - 1)), uint32_t(c >> 5));
-      const bool kept = ((wd >> (c & 31)) & 1u) && i < N;
-      __bf16 x, y;
-      split_bf16(kept ? sc * fmaxf(hv[q], 0.f) : 0.f, x, y);
-      a2h[q >> 3][q & 7] = x;
-      a2l[q >> 3][q & 7] = y;
-      km |= uint32_t(kept && hv[q] > 0.f) << q;
-      if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // four keep hashes in flight
-    }
-    __syncthreads();
-    // dH1: A = dZ2 rows (row rh*32 + r, o = 16s + 8h + j), B = W2^T (column c)
-    f32x16 acc = {};
-    const __bf16* ah = &Dh[(rh * 32 + r) * kDsLd + 8 * h];
-    const __bf16* al = &Dl[(rh * 32 + r) * kDsLd + 8 * h];
-    const __bf16* bh = &Wh[c * kDsLd + 8 * h];
-    const __bf16* bl = &Wl[c * kDsLd + 8 * h];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      acc = mfma_x3(*reinterpret_cast<const bf16x8*>(ah + 16 * s), *reinterpret_cast<const bf16x8*>(al + 16 * s),
-                    *reinterpret_cast<const bf16x8*>(bh + 16 * s), *reinterpret_cast<const bf16x8*>(bl + 16 * s),
-                    acc);
-      if (s == 1) __builtin_amdgcn_sched_barrier(0);   // two k-steps' fragments live at a time
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      const float g = ((km >> q) & 1u) ? acc[q] * sc : 0.f;
-      if (i < N) {
-        dH1[i * (2 * H) + d * H + c] = g;
-        cs += g;
-      }
-    }
-    if (want_dw2) {
-      // dW2: A = dZ2^T (o = r / 32 + r, rows in the a2 fragments' order), B = a2
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 z0h, z0l, z1h, z1l;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = rh * 32 + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
-          z0h[j] = Dh[k * kDsLd + r];
-          z0l[j] = Dl[k * kDsLd + r];
-          z1h[j] = Dh[k * kDsLd + 32 + r];
-          z1l[j] = Dl[k * kDsLd + 32 + r];
-        }
-        pw0 = mfma_x3(z0h, z0l, a2h[s], a2l[s], pw0);
-        pw1 = mfma_x3(z1h, z1l, a2h[s], a2l[s], pw1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __syncthreads();   // the staged tile is rewritten by the next tile
-    if (t + 1 < ntile) gload(blk0 + kDh1Rows);
-  }
-  cs += __shfl_xor(cs, 32);
-  if (h == 0) red[rh][c] = cs;
-  __syncthreads();
-  if (threadIdx.x < H)
-    colpart[int64_t(bx) * (2 * H) + d * H + threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x];
-  if (!want_dw2) return;
-  // combine the two row halves: rh = 1 parks its partial in LDS, rh = 0 adds and stores
-  float* P = smem;   // [64 o][64 c] over the staged tiles (free after the loop's barrier)
-  if (rh == 1) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int o = acc_row(q, l);
-      P[o * H + c] = pw0[q];
-      P[(32 + o) * H + c] = pw1[q];
-    }
-  }
-  __syncthreads();
-  if (rh == 0) {
-    float* out = dw2part + (int64_t(d) * nsplit + bx) * (H * H);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int o = acc_row(q, l);
-      out[o * H + c] = pw0[q] + P[o * H + c];
-      out[(32 + o) * H + c] = pw1[q] + P[(32 + o) * H + c];
-    }
-  }
-}
-
-
-#endif
-
-#if BGCN_DH1_PS   // A/B: pre-split three-way staging (six products)
-constexpr int kDh1SmemPs = (6 * kDh1Rows * kDsLd) / 2 + 2 * H;
-// dH1[i][d*H + c] = (dZ2_d[i] . W2_d[:, c]) * keep(d,i,c) * s * [H1 > 0], c < H,
-// + block partial column sums, over `rows` consecutive nodes (64-row tiles) of direction
-// d per block.  A 64-row x 64-column tile per 256-thread block, four waves as 2 row halves
-// x 2 column halves, on the bf16 MFMA in split form (mfma_x3, bgcn_common.h: this launch
-// was bound by the f32-input MFMA, 64 cycles per 32x32x2).  The dZ2 tile and W2[:, :64]^T
-// are staged in LDS already split (hi / lo bf16, rows of 72 = 16-byte aligned), so every
-// operand fragment of dH1 is one 16-byte LDS read.
-//
-// dw2part != nullptr (the sparse path, gated off when the dense path runs): the same
-// block also forms the relu(H1) block of dW2 over its rows,
-//   part[d][bx][o][c] = sum_i dZ2_d[i][o] * keep(d,i,c) * s * relu(H1_d[i][c]),
-// from the operands the dH1 tile already holds: each lane's 16 (row, c) values of H1 and
-// of the keep words, in the accumulator row order acc_row(q, h), are its B fragments of
-// two 32x32x16 k-steps (element j of step s: row 16s + 8(j>>2) + 4h + (j&3)); the dZ2^T
-// fragments are read from the staged tile in that row order.  Two row-half waves are
-// combined in LDS (fixed order).  One block per node split (the tail reduces the splits).
-// Device body, 256 threads; smem: kDh1Smem floats.
-__device__ inline void dh1_body_ps(const float* __restrict__ dZ2, const float* __restrict__ H1,
                                 const float* __restrict__ W2td, const float* __restrict__ W2bu,
                                 int64_t ldw2, int64_t N, KeepSrc keep, float* __restrict__ dH1,
                                 float* __restrict__ colpart, int64_t rows, float* __restrict__ dw2part,
@@ -708,11 +332,17 @@ __device__ inline void dh1_body_ps(const float* __restrict__ dZ2, const float* _
     const __bf16* bl = &Wl[c * kDsLd + 8 * h];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
+#if BGCN_DH1_X6
       acc = mfma_x6(*reinterpret_cast<const bf16x8*>(ah + 16 * s), *reinterpret_cast<const bf16x8*>(am + 16 * s),
                     *reinterpret_cast<const bf16x8*>(al + 16 * s), *reinterpret_cast<const bf16x8*>(bh + 16 * s),
                     *reinterpret_cast<const bf16x8*>(bm + 16 * s), *reinterpret_cast<const bf16x8*>(bl + 16 * s),
                     acc);
-      __builtin_amdgcn_sched_barrier(0);
+#else   // A/B: the three-product form (hi + mid = the two-way split)
+      (void)al; (void)bl;
+      acc = mfma_x3(*reinterpret_cast<const bf16x8*>(ah + 16 * s), *reinterpret_cast<const bf16x8*>(am + 16 * s),
+                    *reinterpret_cast<const bf16x8*>(bh + 16 * s), *reinterpret_cast<const bf16x8*>(bm + 16 * s), acc);
+#endif
+      __builtin_amdgcn_sched_barrier(0);   // one k-step's fragments live at a time
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -774,6 +404,5 @@ __device__ inline void dh1_body_ps(const float* __restrict__ dZ2, const float* _
 }
 
 
-#endif
 
 }  // namespace bgcn

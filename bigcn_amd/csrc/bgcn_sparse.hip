@@ -1277,29 +1277,17 @@ __global__ __launch_bounds__(256) void k_prep_f(PrepArgs a) {
 // db2 column sums;  tail (1024 threads): dW1 over the CSC, dW2 root columns, the dW2
 // partial reduction, db1 column sums.  Roles by block range, in that order.
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-#if BGCN_DH1_PS
-constexpr int kMidSmem = cmax(cmax(cmax(kDw2Smem, kRootPartSmem), cmax(kDh1SmemPs, kColsumSmem)), kHeadGradSmem);
-#else
 constexpr int kMidSmem = cmax(cmax(cmax(kDw2Smem, kRootPartSmem), cmax(kDh1Smem, kColsumSmem)), kHeadGradSmem);
-#endif
 template <class TX>
-__global__ __launch_bounds__(256, 3) void k_bwd_mid(BwdMidArgs a) {   // 4 waves per SIMD: one round for the whole grid
+__global__ __launch_bounds__(256, 2) void k_bwd_mid(BwdMidArgs a) {   // LDS: two blocks per CU (dh1_body)
   __shared__ __attribute__((aligned(16))) float smem[kMidSmem];
   BT_BEGIN
   int b = int(blockIdx.x);
   if (b < 2 * a.nblk_h) {   // longest-lived role first
     // the relu(H1) block of dW2 rides along when the sparse path is the one running
     float* part = (a.S.mode != 1 && !dense_active(a.gate)) ? a.dw2_sparse.part : nullptr;
-#if BGCN_DH1_PS
-    dh1_body_ps(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, a.rows_h, part,
-                a.nblk_h, b % a.nblk_h, b / a.nblk_h, smem, a.S.mode != 1 ? a.S.w2d : nullptr);
-#elif BGCN_DH1_OLD
-    dh1_body_old(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, a.rows_h, part,
-                 a.nblk_h, b % a.nblk_h, b / a.nblk_h, smem, a.S.mode != 1 ? a.S.w2d : nullptr);
-#else
     dh1_body(a.dZ2, a.H1, a.W2td, a.W2bu, a.S.F + H, a.S.N, a.keep, a.dH1, a.colpart, a.rows_h, part,
              a.nblk_h, b % a.nblk_h, b / a.nblk_h, smem, a.S.mode != 1 ? a.S.w2d : nullptr);
-#endif
     BT_END(72);
     return;
   }
