@@ -42,6 +42,14 @@ WORKLOADS = {
                       desc="Twitter15-shaped synthetic: 128 trees/GPU, LogNormal(0.8) sizes mean 256 "
                            "clamped [2,8192], 5000-dim BoW x, DropEdge 0.2/0.2 re-drawn every step, "
                            "dropout 0.5, fp32"),
+    # twitter15 with a tail of long posts: 1 % of the rows hold 40-300 distinct words (the
+    # reference caps no row, Process/getTwittergraph.py:16-24).  Rows past the 32-entry ELL
+    # spill their tail to the batch's spill pool; the step stays on the sparse path.
+    "twitter15_tail": dict(trees=128, mean=256, sigma=0.8, feats=5000, classes=4, drop=(0.2, 0.2),
+                           long_rows=(0.01, 40, 300),
+                           desc="twitter15 with 1% of the rows holding 40-300 non-zeros (uniform): "
+                                "128 trees/GPU, LogNormal(0.8) sizes mean 256, 5000-dim BoW x, "
+                                "DropEdge 0.2/0.2 re-drawn every step, dropout 0.5, fp32"),
     # BASELINE.json configs[2]: Weibo, 5000-dim BoW, batch 128, bf16.  Weibo trees average
     # ~816 nodes; the reference's Weibo script drops no edges
     # (BiGCN_Weibo.py:199-200) and has the 2-class head (Net, :76-89).  x is stored bf16
@@ -137,7 +145,8 @@ def make_pool(wl, rank, pool, device, drop=None):
         rng = np.random.default_rng(20250205 + 1 + 1000 * rank + i)
         sizes = synth_tree_sizes(rng, wl["trees"], wl["mean"], wl["sigma"])
         xdt = torch.bfloat16 if wl.get("xdtype") == "bf16" else torch.float32
-        out.append(synth_batch(rng, sizes, wl["feats"], wl["classes"], *drop, device=device, dtype=xdt))
+        out.append(synth_batch(rng, sizes, wl["feats"], wl["classes"], *drop, device=device, dtype=xdt,
+                               long_rows=wl.get("long_rows")))
     return out
 
 
@@ -165,7 +174,8 @@ def cpu_baseline(wl, trees: int, steps: int, warmup: int = 1, repeats: int = 3):
     torch.set_num_threads(cores)
     rng = np.random.default_rng(777)
     sizes = synth_tree_sizes(rng, trees, wl["mean"], wl["sigma"])
-    b = synth_batch(rng, sizes, wl["feats"], wl["classes"], *wl["drop"], device="cpu")
+    b = synth_batch(rng, sizes, wl["feats"], wl["classes"], *wl["drop"], device="cpu",
+                    long_rows=wl.get("long_rows"))
     batch = {"x": b.x.float(), "edge_index": b.edge_index, "BU_edge_index": b.BU_edge_index,
              "batch": b.batch, "rootindex": b.rootindex, "y": b.y}
     p = {k: v.requires_grad_(True) for k, v in O.make_params(wl["feats"], 64, 64, wl["classes"]).items()}

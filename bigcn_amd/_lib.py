@@ -29,6 +29,7 @@ BGCN_FEAT_AUTO = 0
 BGCN_FEAT_DENSE = 1
 BGCN_FEAT_SPARSE = 2
 BGCN_SPARSE_CAP = 32
+BGCN_SPARSE_SPILL_PER_ROW = 32   # spill pool capacity per row (rows over the ELL cap)
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1
 ABI_VERSION = 4   # BGCN_ABI_VERSION of include/bgcn.h

@@ -573,7 +573,7 @@ int check_args(const bgcn_bigcn_args* a) {
   BGCN_CHECK_ARG(a->td.t_ptr && a->bu.t_ptr && a->td.s_ptr && a->bu.s_ptr, "null graph");
   BGCN_CHECK_ARG(a->feat_mode == BGCN_FEAT_AUTO || a->feat_mode == BGCN_FEAT_DENSE ||
                      a->feat_mode == BGCN_FEAT_SPARSE, "bad feat_mode");
-  BGCN_CHECK_ARG(a->feat_mode != BGCN_FEAT_SPARSE || a->in_feats <= kSparseMaxF,
+  BGCN_CHECK_ARG(a->feat_mode != BGCN_FEAT_SPARSE || (a->in_feats <= kSparseMaxF && a->num_nodes <= kSparseMaxN),
                  "BGCN_FEAT_SPARSE needs in_feats <= 5120");
   return BGCN_OK;
 }
@@ -632,7 +632,7 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
                  "sparse feature buffers required unless feat_mode == BGCN_FEAT_DENSE");
   Carve c(ws, ws_bytes);
   carve_fused(c, N, B, F, &w);
-  sp.mode = (a->feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxF) ? 1 : 0;
+  sp.mode = (a->feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxF || N > kSparseMaxN) ? 1 : 0;
   sp.flags = a->x_flags;
   sp.nnz = a->x_nnz;
   sp.cols = a->x_cols;
@@ -654,6 +654,8 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
     sp.hist = prep->hist; sp.col_total = prep->col_total;
     sp.col_start = prep->col_start; sp.col_end = prep->col_end;
     sp.csc = prep->csc;
+    sp.ovf_off = prep->x_ovf_off; sp.ovf = prep->x_ovf; sp.ovf_cap = prep->ovf_cap;
+    sp.long_rows = prep->x_long;
   }
   // dense kernels run when feat_mode == dense (no gate) or when the sparse path overflowed
   // (auto); under BGCN_FEAT_SPARSE they are not launched (dense_launched)
@@ -907,6 +909,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   t.dZ1 = w.dz1; t.dw1_td = a->td_dw1; t.dw1_bu = a->bu_dw1;
   t.node_root = w.node_root; t.batch = a->batch; t.dw2_td = a->td_dw2; t.dw2_bu = a->bu_dw2;
   t.keep_scale = keep.scale(); t.dw2_part = w.dw2_part; t.gate = gate;
+  t.keep = keep; t.dZ2 = w.dz2;
   // 1024-thread blocks, 4 output tiles of 64 each
   t.red_dense = RedCfg{w.S2, H + F, 1,
                        dense_launched(a, sp) ? int(std::min<unsigned>(grid_for(2 * H * (H + F), 256), 256)) : 0};

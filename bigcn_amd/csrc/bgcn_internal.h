@@ -321,8 +321,12 @@ struct Prepared {
   int32_t *item_tree, *item_beg, *item_end, *item_root, *tree_item0;   // items: tree, node range, root
   int32_t *x_flags, *x_nnz, *x_cols;
   float* x_vals;
+  int32_t* x_ovf_off;                    // [N] spill pool offsets (rows over the ELL cap)
+  int32_t* x_long;                       // [N] list of the rows over the ELL cap
+  uint2* x_ovf;                          // [ovf_cap] spilled (col, value bits)
+  int64_t ovf_cap;
   int32_t *hist, *col_total, *col_start, *col_end;
-  uint2* csc;   // [N * kCap] (slot, value bits) grouped by column, rows in order
+  uint2* csc;   // [N * (kCap + kSpillPerRow)] (slot, value bits) grouped by column, rows in order
   void* gws;
   size_t gws_bytes;
   int64_t *td_drop, *bu_drop;            // [2, E] masked DropEdge lists (device DropEdge)

@@ -5,7 +5,14 @@
 
 namespace bgcn {
 
-constexpr int kCap = 32;     // max non-zeros per feature row on the sparse path
+constexpr int kCap = 32;     // non-zeros per feature row held in the ELL list
+// A row of more than kCap non-zeros keeps its first kCap in the ELL list and spills the
+// rest, in column order, to a per-batch pool of (col, value bits) pairs (kSpillPerRow
+// entries per row of capacity: a batch may hold N * (kCap + kSpillPerRow) non-zeros).
+// Every product with X is a sum over non-zeros, so the spilled entries add their terms
+// in extra loops of the same kernels; only a batch whose spill exceeds the pool falls
+// back to the dense MFMA path.
+constexpr int kSpillPerRow = BGCN_SPARSE_SPILL_PER_ROW;
 constexpr int kW2sLd = 64 + kCap + 8;   // bf16 row strides of the split W2 images (16-byte
 constexpr int kW2dLd = 64 + 8;          // aligned rows; conv2's also holds 32 root slots)
 constexpr int kChunk = kChunkItems;  // nodes per tree work item (conv2, dW2 root partials)
@@ -14,10 +21,15 @@ struct SparseState {
   int mode;        // 0 auto, 1 dense (sparse kernels idle), 2 sparse preferred (same as auto)
   int64_t N, F, B;
   // saved with the activations (caller-owned)
-  int32_t* flags;  // [0] = some row has > kCap non-zeros -> dense path
+  int32_t* flags;  // [0] = the batch's spill exceeds the pool -> dense path; [1] = pool fill;
+                   // [2] = rows over kCap (long_rows)
   int32_t* nnz;    // [N]
   int32_t* cols;   // [N][kCap]
   float* vals;     // [N][kCap]
+  int32_t* ovf_off;   // [N] first pool entry of row i (valid when nnz[i] > kCap)
+  int32_t* long_rows; // [N] the rows over kCap (count in flags[2]; conv1's long-row blocks)
+  uint2* ovf;         // [ovf_cap] spilled (col, value bits), row by row, columns ascending
+  int64_t ovf_cap;
   // step scratch
   float* w1t;      // [F][128]     = [W1_td ; W1_bu]^T
   float* w2t;      // [2][64+F][64] = W2_d^T
@@ -32,8 +44,9 @@ struct SparseState {
   int32_t* hist;        // [R][F] per-row-block column counts -> prefixes (R = N / kRowBlock)
   int32_t* col_total;   // [F]
   int32_t *col_start, *col_end;  // [F]
-  uint2* csc;           // [N*kCap] (slot i*kCap + s, value bits) grouped by column, rows in
-                        // order: one 8-byte store per placed entry (the placement scatters)
+  uint2* csc;           // [N*(kCap+kSpillPerRow)] (slot i*kCap + s, value bits) grouped by
+                        // column, rows in order: one 8-byte store per placed entry (the
+                        // placement scatters); a spilled entry's slot is i*kCap | kCscSpillFlag
   uint32_t* rbits;      // [2][N] forward's root keep masks (bit s: root non-zero s kept)
   int32_t* zero_word = nullptr;   // zeroed by the prologue (the train step's status word)
   int32_t* rtick = nullptr;       // [B] readout arrival counters, zeroed by the prologue
@@ -51,8 +64,12 @@ struct WeightImages {
   __bf16* w2d;     // [2][3][64][kW2dLd]
 };
 size_t carve_images(Carve& c, int64_t F, WeightImages* im);
-// CSC slot bit 31: the entry's row is a tree root (its column gets a dW2 root-column term)
+// CSC slot bit 31: the entry's row is a tree root (its column gets a dW2 root-column term);
+// bit 30: a spilled entry (no ELL slot; its root term is summed over the tree directly)
 constexpr uint32_t kCscRootFlag = 0x80000000u;
+constexpr uint32_t kCscSpillFlag = 0x40000000u;
+constexpr uint32_t kCscSlotMask = 0x3fffffffu;
+constexpr int64_t kSparseMaxN = int64_t(1) << 25;   // slots i*kCap below bit 30
 
 constexpr int kRowBlock = kCscRowBlock;   // rows per block of the CSC counting sort
 constexpr int64_t kSparseMaxF = kSparseMaxFeat;  // LDS bound of the CSC kernels (2 x 4 B x F)
@@ -115,6 +132,8 @@ struct BwdTailArgs {
   const int64_t* batch;
   float *dw2_td, *dw2_bu;
   float keep_scale;
+  KeepSrc keep;                  // spilled root entries: keep bits recomputed
+  const float* dZ2;              // spilled root entries: summed over their tree
   const float* dw2_part;
   const int32_t* gate;
   RedCfg red_dense, red_sparse;

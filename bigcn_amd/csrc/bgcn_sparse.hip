@@ -210,9 +210,11 @@ template <class TX> constexpr int row_chunks() { return kRowChunks * 4 / XChunk<
 template <class TX> constexpr bool compact_by_prefix() {
   return BGCN_COMPACT_PREFIX >= 2 || (BGCN_COMPACT_PREFIX == 1 && sizeof(TX) == 2);
 }
-template <bool kConv1, class TX>
-__device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, const u32x4* r,
-                                            int32_t* s_col, float* s_val, float* __restrict__ Z1) {
+// Walk a row's non-zeros in ascending column order: emit(pos, col, val) for each, pos =
+// its rank in the row (lanes below a lane contribute all their non-zeros first); returns
+// the row's count (wave-uniform).
+template <class TX, class Emit>
+__device__ __forceinline__ int walk_row(const u32x4* r, Emit emit) {
   typedef XChunk<TX> XC;
   constexpr int E = XC::kElems;
   const int lane = threadIdx.x & 63;
@@ -223,7 +225,6 @@ __device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, con
   for (int u = 0; u < row_chunks<TX>(); ++u) {
     const u32x4 ru = r[u];                           // past the row: 0 (range-checked load)
     if (__ballot(XC::any(ru)) == 0ull) continue;     // wave-uniform skip
-    // ascending column order: lanes below me contribute all their non-zeros first
     int pos = cnt;
 #pragma unroll
     for (int c = 0; c < E; ++c) {
@@ -235,10 +236,7 @@ __device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, con
 #pragma unroll
     for (int c = 0; c < E; ++c) {
       if (XC::nz(ru, c)) {
-        if (pos < kCap) {
-          s_col[pos] = col0 + c;
-          s_val[pos] = XC::elem(ru, c);
-        }
+        emit(pos, col0 + c, XC::elem(ru, c));
         ++pos;
       }
     }
@@ -252,8 +250,7 @@ __device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, con
     for (int c = 0; c < E; ++c) mb |= uint32_t(XC::nz(ru, c)) << c;
     const uint64_t any = __ballot(mb != 0u);
     if (any == 0ull) continue;                       // wave-uniform skip
-    // ascending column order: lanes below me contribute all their non-zeros first - the
-    // exclusive prefix of the per-lane counts, one ballot when no lane holds two (the
+    // the exclusive prefix of the per-lane counts, one ballot when no lane holds two (the
     // common case for bag-of-words rows), else by the counts' bit planes
     const int n = __popc(mb);
     int pos = cnt;
@@ -272,29 +269,114 @@ __device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, con
     while (mb) {
       const int c = __builtin_ctz(mb);
       mb &= mb - 1u;
-      if (pos < kCap) {
-        s_col[pos] = col0 + c;
-        s_val[pos] = XC::elem(ru, c);
-      }
+      emit(pos, col0 + c, XC::elem(ru, c));
       ++pos;
     }
   }
   }
-  if (lane == 0) S.nnz[i] = cnt;
-  if (cnt > kCap) {
-    if (lane == 0) atomicOr(&S.flags[0], 1);
-    return;
+  return cnt;
+}
+
+// The entries past kCap of a long row -> dst[pos] (pos >= kCap), in column order.  The row
+// is loaded again one 16-byte piece per lane at a time in a rolled loop: the rare branch
+// must not add registers to the pass over X (an unrolled second walk took the fp32 form
+// from 205 to 256 + AGPRs, half its occupancy).
+template <class TX>
+__device__ void spill_walk(__amdgpu_buffer_rsrc_t rs, uint2* dst) {
+  typedef XChunk<TX> XC;
+  constexpr int E = XC::kElems;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int cnt = 0;
+  constexpr int kG = 5;                              // pieces in flight
+  static_assert(row_chunks<TX>() % kG == 0, "spill walk groups");
+#pragma unroll 1
+  for (int u0 = 0; u0 < row_chunks<TX>(); u0 += kG) {
+  u32x4 rg[kG];
+#pragma unroll
+  for (int v = 0; v < kG; ++v)
+    rg[v] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((u0 + v) * 64 + lane) * 16, 0, kAuxNT);
+#pragma unroll
+  for (int v = 0; v < kG; ++v) {
+    const int u = u0 + v;
+    const u32x4 ru = rg[v];
+    uint32_t mb = 0;
+#pragma unroll
+    for (int c = 0; c < E; ++c) mb |= uint32_t(XC::nz(ru, c)) << c;
+    const int n = __popc(mb);
+    int pos = cnt;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {                    // n <= 8
+      const uint64_t bk = __ballot((n >> k) & 1);
+      pos += __popcll(bk & lt) << k;
+      cnt += __popcll(bk) << k;
+    }
+    const int col0 = (u * 64 + lane) * E;
+    while (mb) {
+      const int c = __builtin_ctz(mb);
+      mb &= mb - 1u;
+      if (pos >= kCap) dst[pos] = make_uint2(uint32_t(col0 + c), __float_as_uint(XC::elem(ru, c)));
+      ++pos;
+    }
   }
+  }
+}
+
+// Row i of X -> its ELL list, the entries past kCap to the spill pool (+ conv1 over both).
+template <bool kConv1, class TX>
+__device__ __forceinline__ void compact_row(const SparseState& S, int64_t i, const u32x4* r,
+                                            __amdgpu_buffer_rsrc_t rs, int32_t* s_col, float* s_val,
+                                            float* __restrict__ Z1) {
+  const int lane = threadIdx.x & 63;
+  const int cnt = walk_row<TX>(r, [&](int pos, int col, float v) {
+    if (pos < kCap) {
+      s_col[pos] = col;
+      s_val[pos] = v;
+    }
+  });
+  if (lane == 0) S.nnz[i] = cnt;
+  const int nov = cnt > kCap ? cnt - kCap : 0;       // wave-uniform
+  int off = 0;
+  if (nov > 0) {
+    // a row of more words than the ELL holds (the reference caps none, getTwittergraph.py:
+    // 16-24): its tail goes to the batch's spill pool, in column order
+    int o = 0;
+    if (lane == 0) o = atomicAdd(&S.flags[1], nov);
+    o = __builtin_amdgcn_readfirstlane(o);
+    if (o < 0 || int64_t(o) + nov > S.ovf_cap) {     // pool full: the batch goes dense
+      if (lane == 0) atomicOr(&S.flags[0], 1);
+      return;
+    }
+    if (lane == 0) {
+      S.ovf_off[i] = o;
+      S.long_rows[atomicAdd(&S.flags[2], 1)] = int32_t(i);   // conv1's long-row blocks
+    }
+    uint2* dst = S.ovf + o - kCap;
+    spill_walk<TX>(rs, dst);
+    off = o;
+  }
+  const int ce = cnt < kCap ? cnt : kCap;
   __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes have landed
   __builtin_amdgcn_wave_barrier();
-  const int32_t col_l = lane < cnt ? s_col[lane] : 0;
-  const float val_l = lane < cnt ? s_val[lane] : 0.f;
-  if (lane < cnt) {
+  const int32_t col_l = lane < ce ? s_col[lane] : 0;
+  const float val_l = lane < ce ? s_val[lane] : 0.f;
+  if (lane < ce) {
     S.cols[i * kCap + lane] = col_l;
     S.vals[i * kCap + lane] = val_l;
   }
   if (kConv1) {
-    const float2 acc = conv1_row(S, cnt, col_l, val_l);
+    float2 acc = conv1_row(S, ce, col_l, val_l);
+    if (nov > 0) {   // the spilled entries, 64 at a time (this wave's own stores, read back)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      for (int k0 = 0; k0 < nov; k0 += 64) {
+        const int n = min(64, nov - k0);
+        const uint2 e = S.ovf[off + k0 + min(lane, n - 1)];
+        const float2 p = conv1_row(S, n, int32_t(e.x), __uint_as_float(e.y));
+        acc.x += p.x;
+        acc.y += p.y;
+      }
+    }
     *reinterpret_cast<float2*>(Z1 + i * (2 * H) + 2 * lane) = acc;
   }
 }
@@ -316,19 +398,19 @@ __device__ inline void compact_body(const SparseState& S, const TX* __restrict__
   const int64_t stride = int64_t(nblk) * 4;
   for (int64_t i0 = int64_t(bid) * 4 + wave; i0 < S.N; i0 += stride * kRows) {
     u32x4 r[kRows][row_chunks<TX>()];
+    __amdgpu_buffer_rsrc_t rs[kRows];
 #pragma unroll
     for (int k = 0; k < kRows; ++k) {   // all loads in flight; a row past N reads nothing
       const int64_t ik = i0 + k * stride;
-      const __amdgpu_buffer_rsrc_t rs =
-          row_rsrc(X + min<int64_t>(ik, S.N - 1) * ldx, ik < S.N ? uint32_t(S.F * sizeof(TX)) : 0u);
+      rs[k] = row_rsrc(X + min<int64_t>(ik, S.N - 1) * ldx, ik < S.N ? uint32_t(S.F * sizeof(TX)) : 0u);
 #pragma unroll
       for (int u = 0; u < row_chunks<TX>(); ++u)
-        r[k][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * 64 + lane) * 16, 0, kAuxNT);
+        r[k][u] = __builtin_amdgcn_raw_buffer_load_b128(rs[k], (u * 64 + lane) * 16, 0, kAuxNT);
     }
 #pragma unroll
     for (int k = 0; k < kRows; ++k) {
       const int64_t i = i0 + k * stride;
-      if (i < S.N) compact_row<kConv1, TX>(S, i, r[k], s_col[wave], s_val[wave], Z1);
+      if (i < S.N) compact_row<kConv1, TX>(S, i, r[k], rs[k], s_col[wave], s_val[wave], Z1);
     }
   }
 }
@@ -359,7 +441,8 @@ __global__ __launch_bounds__(kC1Threads) void k_conv1_gather(SparseState S, floa
   const int64_t i = (int64_t(blockIdx.x) * (kC1Threads / 64) + (threadIdx.x >> 6)) * kC1Rows + (lane >> 4);
   const bool live = i < S.N;
   const int64_t ic = live ? i : S.N - 1;
-  const int cnt = live ? min(S.nnz[ic], kCap) : 0;
+  const int nall = live ? S.nnz[ic] : 0;
+  const int cnt = min(nall, kCap);
   const int32_t c0 = S.cols[ic * kCap + ql], c1 = S.cols[ic * kCap + 16 + ql];
   const float v0 = S.vals[ic * kCap + ql], v1 = S.vals[ic * kCap + 16 + ql];
   // the wave's longest row bounds the loop (uniform)
@@ -388,6 +471,16 @@ __global__ __launch_bounds__(kC1Threads) void k_conv1_gather(SparseState S, floa
       a1 = f4fma(x[u], w1[u], a1);
     }
   }
+  if (nall > kCap) {   // spilled entries of a long row (rare): one at a time
+    const int64_t off = S.ovf_off[ic];
+    for (int k = 0; k < nall - kCap; ++k) {
+      const uint2 e = S.ovf[off + k];
+      const float v = __uint_as_float(e.y);
+      const float* wr = S.w1t + int64_t(min(max(int32_t(e.x), 0), int32_t(S.F - 1))) * (2 * H) + 8 * ql;
+      a0 = f4fma(v, ld4(wr), a0);
+      a1 = f4fma(v, ld4(wr + 4), a1);
+    }
+  }
   if (live) {
     st4(Z1 + i * (2 * H) + 8 * ql, a0);
     st4(Z1 + i * (2 * H) + 8 * ql + 4, a1);
@@ -404,21 +497,50 @@ __global__ __launch_bounds__(kC1Threads) void k_conv1_gather(SparseState S, floa
 #ifndef BGCN_C1_MODE
 #define BGCN_C1_MODE 2   // 0: four rows per wave (k_conv1_gather); 1 / 2: two rows, steps of 8 / 4
 #endif
+// Long rows (more than kCap non-zeros: the ELL list + the spill pool) get a block each
+// instead of a half-wave: a long row walked by one half-wave is a serial chain of gathers
+// (270 entries: ~70 us at 4 in flight), so the block's four waves take a quarter of the
+// entries each, 8 gathers in flight per wave, combined in wave order (deterministic).
+// Blocks stride over the compaction's list of long rows; with none they exit at once.
+constexpr int kLongRowBlocks = 256;
+__device__ inline void conv1_long_rows(const SparseState& S, float* __restrict__ Z1, int bid, int nblk) {
+  __shared__ float part[4][2 * H];
+  const int n_long = S.flags[2];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int q = bid; q < n_long; q += nblk) {
+    const int64_t i = S.long_rows[q];
+    const int nall = S.nnz[i];
+    const int64_t off = S.ovf_off[i];
+    const int seg = (nall + 3) / 4;
+    const int e0 = wv * seg, e1 = min(nall, e0 + seg);
+    float2 acc = make_float2(0.f, 0.f);
+    for (int k0 = e0; k0 < e1; k0 += 64) {
+      const int n = min(64, e1 - k0);
+      const int e = k0 + min(lane, n - 1);
+      // ELL entry (e < kCap) or pool entry: both loaded from clamped indices, selected after
+      const int32_t ce = S.cols[i * kCap + min(e, kCap - 1)];
+      const float ve = S.vals[i * kCap + min(e, kCap - 1)];
+      const uint2 pe = S.ovf[off + max(e - kCap, 0)];
+      const float2 p = conv1_row(S, n, e < kCap ? ce : int32_t(pe.x), e < kCap ? ve : __uint_as_float(pe.y));
+      acc.x += p.x;
+      acc.y += p.y;
+    }
+    part[wv][2 * lane] = acc.x;
+    part[wv][2 * lane + 1] = acc.y;
+    __syncthreads();
+    if (threadIdx.x < 2 * H)
+      Z1[i * (2 * H) + threadIdx.x] = (part[0][threadIdx.x] + part[1][threadIdx.x]) +
+                                     (part[2][threadIdx.x] + part[3][threadIdx.x]);
+    __syncthreads();
+  }
+}
+
+// Entries of two rows per wave (half h: row 2w + h) held by the half's lanes (cl, vl of
+// lane hl: entry hl), cnt of this half, cmax the wave-uniform bound: acc += val * W1^T[col].
 template <int kStep>
-__global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __restrict__ Z1) {
-  BT_BEGIN
-  conv1_clears(S);
-  if (!use_sparse(S)) return;
+__device__ __forceinline__ float4 conv1_half_entries(const SparseState& S, int32_t cl, float vl, int cnt,
+                                                     int cmax, float4 acc) {
   const int lane = threadIdx.x & 63, hl = lane & 31, hb = lane & 32;
-  const int64_t i = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
-  const bool live = i < S.N;
-  const int64_t ic = live ? i : S.N - 1;
-  const int cnt = live ? min(S.nnz[ic], kCap) : 0;
-  const int32_t cl = S.cols[ic * kCap + hl];
-  const float vl = S.vals[ic * kCap + hl];
-  int cmax = max(cnt, __shfl_xor(cnt, 32, 64));
-  cmax = __builtin_amdgcn_readfirstlane(cmax);
-  float4 acc = f4zero();
   for (int s0 = 0; s0 < cmax; s0 += kStep) {
     float4 w[kStep];
     float x[kStep];
@@ -434,7 +556,30 @@ __global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __res
 #pragma unroll
     for (int u = 0; u < kStep; ++u) acc = f4fma(x[u], w[u], acc);
   }
-  if (live) st4(Z1 + i * (2 * H) + 4 * hl, acc);
+  return acc;
+}
+// Blocks [0, kLongRowBlocks): the long rows (conv1_long_rows); then two rows per wave.
+template <int kStep>
+__global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __restrict__ Z1) {
+  BT_BEGIN
+  conv1_clears(S);
+  if (!use_sparse(S)) return;
+  if (blockIdx.x < kLongRowBlocks) {
+    conv1_long_rows(S, Z1, int(blockIdx.x), kLongRowBlocks);
+    return;
+  }
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int64_t i = (int64_t(blockIdx.x - kLongRowBlocks) * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool live = i < S.N;
+  const int64_t ic = live ? i : S.N - 1;
+  const int nall = live ? S.nnz[ic] : 0;
+  const int cnt = min(nall, kCap);
+  const int32_t cl = S.cols[ic * kCap + hl];
+  const float vl = S.vals[ic * kCap + hl];
+  int cmax = max(cnt, __shfl_xor(cnt, 32, 64));
+  cmax = __builtin_amdgcn_readfirstlane(cmax);
+  const float4 acc = conv1_half_entries<kStep>(S, cl, vl, cnt, cmax, f4zero());
+  if (live && nall <= kCap) st4(Z1 + i * (2 * H) + 4 * hl, acc);   // long rows: their block's
   BT_END(1);
 }
 
@@ -473,7 +618,8 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   const int d = blockIdx.y;
   const int64_t beg = S.item_beg[item], end = S.item_end[item];
   const int64_t r = S.item_root[item];
-  const int rn = S.nnz[r];
+  const int rn_all = S.nnz[r];
+  const int rn = min(rn_all, kCap);   // root slots in the ELL (the rest spilled)
   const int mh = (rn + 1) / 2;   // root slot pairs (slot 2j + h, j < mh)
   const float sc = keep.scale();
   const int64_t K2 = S.F + H;
@@ -597,6 +743,93 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
       if (ii < end) {
         Z2[ii * (2 * H) + d * H + r32] = acc0[q];
         Z2[ii * (2 * H) + d * H + 32 + r32] = acc1[q];
+      }
+    }
+  }
+  if (rn_all > kCap) {
+    // The root's spilled non-zeros (a root row of more than kCap words, rare): further
+    // [nodes x 32] x [32 x 64] products of the same form as the root slots - A the exact
+    // 0/1 keep bits, B = 2 relu(x_root,c) W2_d^T[64 + c] split three ways - 32 pool entries
+    // per round, added to the Z2 rows this thread stored above (same thread, same rows).
+    // Software-pipelined: the pool entries are loaded two rounds ahead and the W2^T rows
+    // they select one round ahead, so a round's dependent loads hide behind the previous
+    // round's tiles (under the pass over X a dependent load costs several us).
+    const int64_t off = S.ovf_off[r];
+    const int nsp = rn_all - kCap;
+    const int sq0 = threadIdx.x >> 4, sq1 = (threadIdx.x + 256) >> 4, qq = (threadIdx.x & 15) * 4;
+    auto ent_at = [&](int c0, int s_) { return S.ovf[off + min(c0 + s_, nsp - 1)]; };
+    auto w_of = [&](uint2 e) {
+      return ld4(w2t + int64_t(H + min(max(int32_t(e.x), 0), int32_t(S.F - 1))) * H + qq);
+    };
+    const int tk = min(int(threadIdx.x), kCap - 1);
+    uint2 e0 = ent_at(0, sq0), e1 = ent_at(0, sq1), rkc = ent_at(0, tk);
+    uint2 n0 = ent_at(kCap, sq0), n1 = ent_at(kCap, sq1), rkn = ent_at(kCap, tk);
+    float4 w0 = w_of(e0), w1 = w_of(e1);
+    for (int c0 = 0; c0 < nsp; c0 += kCap) {
+      const int cn = min(kCap, nsp - c0);
+      __syncthreads();   // every wave is done with Bs / rk
+      if (threadIdx.x < kCap) rk[threadIdx.x] = uint32_t(H + min(max(int32_t(rkc.x), 0), int32_t(S.F - 1)));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int s_ = j == 0 ? sq0 : sq1;
+        const uint2 ent = j == 0 ? e0 : e1;
+        const float4 w = j == 0 ? w0 : w1;
+        const float av = s_ < cn ? sc * fmaxf(__uint_as_float(ent.y), 0.f) : 0.f;
+        const float vv[4] = {av * w.x, av * w.y, av * w.z, av * w.w};
+        const int k = H + (s_ & 1) * (kCap / 2) + (s_ >> 1);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int o = (qq + u) * kC2Ld16 + k;
+          split3_bf16(vv[u], Bs[0][o], Bs[1][o], Bs[2][o]);
+        }
+      }
+      __syncthreads();
+      // the next rounds' loads, in flight during this round's tiles
+      e0 = n0; e1 = n1; rkc = rkn;
+      n0 = ent_at(c0 + 2 * kCap, sq0); n1 = ent_at(c0 + 2 * kCap, sq1); rkn = ent_at(c0 + 2 * kCap, tk);
+      w0 = w_of(e0); w1 = w_of(e1);
+      const int mc = (cn + 1) / 2;
+      for (int t = wv; t < kChunk / 32; t += 4) {
+        const int64_t i0 = beg + 32 * t;
+        if (i0 >= end) break;
+        const int64_t i = i0 + r32;
+        const uint32_t ni = uint32_t(i < end ? i : beg);
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < kCap / 2; ++j) {
+          const int sl = 2 * j + h;
+          if (j < mc && sl < cn) {
+            const uint32_t k = rk[sl];
+            m |= ((keep.get(uint32_t(d), ni, k >> 5) >> (k & 31)) & 1u) << sl;
+          }
+        }
+        f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          if (8 * tt < mc) {
+            bf16x8 ar;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ar[j] = __bf16(((m >> (2 * (8 * tt + j) + h)) & 1u) ? 1.f : 0.f);
+            const int k = H + (kCap / 2) * h + 8 * tt;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+              const int o = (32 * half + r32) * kC2Ld16 + k;
+              f32x16 c = half == 0 ? acc0 : acc1;
+              c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[2][o]), c);
+              c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[1][o]), c);
+              c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[0][o]), c);
+              if (half == 0) acc0 = c; else acc1 = c;
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int64_t ii = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+          if (ii < end) {
+            Z2[ii * (2 * H) + d * H + r32] += acc0[q];
+            Z2[ii * (2 * H) + d * H + 32 + r32] += acc1[q];
+          }
+        }
       }
     }
   }
@@ -733,12 +966,45 @@ __device__ inline void root_part_body(const SparseState& S, const float* __restr
 // No float atomics, no general sort; deterministic.  Every global load is issued
 // unconditionally (clamped index, select afterwards) so the loads of a thread overlap.
 // (bodies: kRowBlock threads; hsm / psm = the launch's dynamic shared memory)
+// Spilled entries of a group of rows, flattened over the block's threads: pre[r] = the
+// group's entries before row r (pre[nrows] = total), off[r] = row r's first pool entry.
+// f(r, entry) runs for every entry with four pool loads in flight per thread (a row's
+// entries walked by one thread were a serial chain of dependent loads: a 270-word row
+// cost the placement ~300 us).
+__device__ __forceinline__ int spill_row_of(const int* pre, int nrows, int e) {
+  int lo = 0, hi = nrows - 1;   // the last row r with pre[r] <= e (rows of no entries skipped)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pre[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+template <class Fn>
+__device__ __forceinline__ void for_spill(const SparseState& S, const int* pre, const int* off, int nrows,
+                                          Fn f) {
+  const int total = pre[nrows];
+  for (int e0 = int(threadIdx.x); e0 < total; e0 += 4 * int(blockDim.x)) {
+    int r[4];
+    uint2 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = min(e0 + u * int(blockDim.x), total - 1);
+      r[u] = spill_row_of(pre, nrows, e);
+      v[u] = S.ovf[off[r[u]] + (e - pre[r[u]])];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (e0 + u * int(blockDim.x) < total) f(r[u], v[u]);
+  }
+}
+
 __device__ inline void csc_hist_body(const SparseState& S, int bid, int32_t* hsm) {   // hsm [F]
   if (!use_sparse(S)) return;
   for (int64_t c = threadIdx.x; c < S.F; c += kRowBlock) hsm[c] = 0;
   const int64_t i = int64_t(bid) * kRowBlock + threadIdx.x;
   const int64_t ic = min<int64_t>(i, S.N - 1);
-  const int n = i < S.N ? min(S.nnz[ic], kCap) : 0;
+  const int nall = i < S.N ? S.nnz[ic] : 0;
+  const int n = min(nall, kCap);
   int32_t cl[kCap];
 #pragma unroll
   for (int q = 0; q < kCap / 4; ++q) {
@@ -749,6 +1015,30 @@ __device__ inline void csc_hist_body(const SparseState& S, int bid, int32_t* hsm
 #pragma unroll
   for (int s = 0; s < kCap; ++s)
     if (s < n) atomicAdd(&hsm[cl[s]], 1);
+  const int nsp = nall > kCap ? nall - kCap : 0;
+  if (__syncthreads_or(nsp)) {   // the block's long rows (rare): their spilled entries
+    __shared__ int pre[kRowBlock + 1], off[kRowBlock], wsum[kRowBlock / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int x = nsp;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int base = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kRowBlock / 64; ++w) {
+      base += w < wv ? wsum[w] : 0;
+      total += wsum[w];
+    }
+    pre[threadIdx.x] = base + x - nsp;
+    off[threadIdx.x] = nsp ? S.ovf_off[ic] : 0;
+    if (threadIdx.x == 0) pre[kRowBlock] = total;
+    __syncthreads();
+    for_spill(S, pre, off, kRowBlock, [&](int, uint2 v) { atomicAdd(&hsm[v.x], 1); });
+  }
   __syncthreads();
   int32_t* out = S.hist + int64_t(bid) * S.F;
   for (int64_t c = threadIdx.x; c < S.F; c += kRowBlock) out[c] = hsm[c];
@@ -886,12 +1176,23 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
     val[k] = S.vals[ic * kCap + s];
     rootbits |= uint32_t(S.root_map[ic] == int32_t(ic)) << k;
   }
+  uint32_t smask = 0u;   // bit bt: batch bt (rows 32bt .. 32bt + 31) holds a long row
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {   // ... then mask the padding slots
     const int64_t i = r0 + threadIdx.x / kCap + 8 * k;
     col[k] = (i < S.N && s < nn[k]) ? col[k] : -1;
+    smask |= (i < S.N && nn[k] > kCap) ? (1u << (k / 4)) : 0u;
   }
-  __syncthreads();
+  // the batches holding long rows place their spilled entries too (rare: those batches
+  // take the two-phase counter advance below)
+  {
+    __shared__ uint32_t smask_s;
+    if (threadIdx.x == 0) smask_s = 0u;
+    __syncthreads();
+    if (smask) atomicOr(&smask_s, smask);
+    __syncthreads();
+    smask = smask_s;
+  }
   // rows of the block in order, 32 rows (= 1024 slots, 4 per thread) per batch.  The
   // columns of one row are distinct, so an entry's rank among the batch's entries of
   // its column = the number of earlier batch rows holding that column: an OR of row
@@ -900,11 +1201,46 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
 #pragma unroll
   for (int bt = 0; bt < kRowBlock / kBatchRows; ++bt) {
     int rr[4], rank[4];
+    const bool spill = (smask >> bt) & 1u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       rr[k] = threadIdx.x / kCap + 8 * k;   // row within the batch
       const int32_t cc = col[4 * bt + k];
       if (cc >= 0) atomicOr(&rows[cc], 1u << rr[k]);
+    }
+    // spilled entries of the batch's rows (their columns are distinct from the row's ELL
+    // columns, so the same row-bit ranks hold), flattened over the block's threads
+    __shared__ int bpre[kBatchRows + 1], boff[kBatchRows];
+    __shared__ uint32_t bslot[kBatchRows];
+    if (spill) {
+      if (threadIdx.x < 64) {   // wave 0, lane t < 32: batch row t
+        const int t = threadIdx.x;
+        int nsp = 0, o = 0;
+        uint32_t sl = 0u;
+        const int64_t i = r0 + bt * kBatchRows + t;
+        if (t < kBatchRows && i < S.N) {
+          const int na = S.nnz[i];
+          if (na > kCap) {
+            nsp = na - kCap;
+            o = S.ovf_off[i];
+            sl = uint32_t(i * kCap) | kCscSpillFlag | (S.root_map[i] == int32_t(i) ? kCscRootFlag : 0u);
+          }
+        }
+        int x = nsp;
+#pragma unroll
+        for (int d = 1; d < kBatchRows; d <<= 1) {
+          const int y = __shfl_up(x, d, 64);
+          if (t >= d) x += y;
+        }
+        if (t < kBatchRows) {
+          bpre[t] = x - nsp;
+          boff[t] = o;
+          bslot[t] = sl;
+        }
+        if (t == kBatchRows - 1) bpre[kBatchRows] = x;
+      }
+      __syncthreads();
+      for_spill(S, bpre, boff, kBatchRows, [&](int r, uint2 v) { atomicOr(&rows[v.x], 1u << r); });
     }
     __syncthreads();
 #pragma unroll
@@ -919,14 +1255,32 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
         S.csc[cnt[cc] + rank[k]] = make_uint2(uint32_t(i * kCap + s) | flag, __float_as_uint(val[4 * bt + k]));
       }
     }
+    if (spill)
+      for_spill(S, bpre, boff, kBatchRows, [&](int r, uint2 v) {
+        S.csc[cnt[v.x] + __popc(rows[v.x] & ((1u << r) - 1u))] = make_uint2(bslot[r], v.y);
+      });
     __syncthreads();
+    if (!spill) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int32_t cc = col[4 * bt + k];
-      if (rank[k] == 0) {   // the batch's first entry of a column advances its counter
-        cnt[cc] += __popc(rows[cc]);
-        rows[cc] = 0u;
+      for (int k = 0; k < 4; ++k) {
+        const int32_t cc = col[4 * bt + k];
+        if (rank[k] == 0) {   // the batch's first entry of a column advances its counter
+          cnt[cc] += __popc(rows[cc]);
+          rows[cc] = 0u;
+        }
       }
+    } else {   // two phases: the counters (row bits read-only), then the clears
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (rank[k] == 0) cnt[col[4 * bt + k]] += __popc(rows[col[4 * bt + k]]);
+      for_spill(S, bpre, boff, kBatchRows, [&](int r, uint2 v) {
+        if ((rows[v.x] & ((1u << r) - 1u)) == 0u) cnt[v.x] += __popc(rows[v.x]);
+      });
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (rank[k] >= 0) rows[col[4 * bt + k]] = 0u;
+      for_spill(S, bpre, boff, kBatchRows, [&](int, uint2 v) { rows[v.x] = 0u; });
     }
     __syncthreads();
   }
@@ -947,11 +1301,21 @@ __global__ __launch_bounds__(256) void k_csc_place(SparseState S) {
 constexpr int kDw1Depth = 16;
 // Device body, 1024 threads, column block bid; smem: kDw1Smem floats.
 constexpr int kDw1Smem = 2 * 2 * H * 17;   // dW1 and the dW2 root-column partials
+// Spilled root entries (a root row of more than kCap words): their dW2 root-column
+// partial is summed over the tree's nodes directly (no ELL slot, no item partial):
+//   sum_{i in tree b} keep_d(i, 64 + c) * dZ2_d[i][o]
+__device__ __forceinline__ void tree_range(const SparseState& S, int b, int64_t& nb, int64_t& ne) {
+  const int it0 = S.tree_item0[b], it1 = S.tree_item0[b + 1];
+  nb = it1 > it0 ? S.item_beg[it0] : 0;
+  ne = it1 > it0 ? S.item_end[it1 - 1] : 0;
+}
+
 template <int kDw1Split>                       // waves per column (1 or 4)
 __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ dZ1,
                                 float* __restrict__ dw1_td, float* __restrict__ dw1_bu,
                                 const int64_t* __restrict__ batch, float* __restrict__ dw2_td,
-                                float* __restrict__ dw2_bu, float scale, int bid, float* smem) {
+                                float* __restrict__ dw2_bu, float scale, int bid, float* smem,
+                                const float* __restrict__ dZ2, const KeepSrc& keep) {
   const int kDw1Cols = int(blockDim.x >> 6) / kDw1Split;   // columns per block
   if (!use_sparse(S)) return;
   float (*t1)[17] = reinterpret_cast<float (*)[17]>(smem);
@@ -967,7 +1331,7 @@ __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ 
     for (int64_t u0 = beg + 64 * part; u0 < end; u0 += 64 * kDw1Split) {
       const int64_t u = min<int64_t>(u0 + lane, end - 1);   // clamped: duplicates, x masked
       const uint2 ent = S.csc[u];
-      const uint32_t slot = ent.x & ~kCscRootFlag;
+      const uint32_t slot = ent.x & kCscSlotMask;
       const float xv = __uint_as_float(ent.y);
       const int n = int(min<int64_t>(64, end - u0));
       const float x_l = lane < n ? xv : 0.f;
@@ -1001,6 +1365,30 @@ __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ 
         const float f = scale * fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(x_l), j)), 0.f);
         const int b = int(batch[i]);
         float2 sum = make_float2(0.f, 0.f);
+        if (__builtin_amdgcn_readlane(int32_t(ent.x), j) & int32_t(kCscSpillFlag)) {
+          int64_t nb, ne;
+          tree_range(S, b, nb, ne);
+          const uint32_t k = uint32_t(H + c);
+          for (int64_t n0 = nb; n0 < ne; n0 += 4) {   // four rows in flight, in node order
+            float2 z[4];
+            uint32_t kw[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int64_t nd = min(n0 + u, ne - 1);
+              z[u] = *reinterpret_cast<const float2*>(dZ2 + nd * (2 * H) + rd * H + ro);
+              kw[u] = keep.get(uint32_t(rd), uint32_t(nd), k >> 5);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (n0 + u < ne && ((kw[u] >> (k & 31)) & 1u)) {
+                sum.x += z[u].x;
+                sum.y += z[u].y;
+              }
+          }
+          a2.x = fmaf(f, sum.x, a2.x);
+          a2.y = fmaf(f, sum.y, a2.y);
+          continue;
+        }
         const int it0 = S.tree_item0[b], it1 = S.tree_item0[b + 1];
         for (int it = it0; it < it1; it += 4) {   // four item partials in flight, in item order
           float2 v[4];
@@ -1078,10 +1466,15 @@ __host__ __device__ inline int dw1_sliced_blocks(int64_t F, int W) {
   const int64_t groups = (F + W - 1) / W, reps = 8 / kSlices;
   return int(8 * ((groups + reps - 1) / reps));
 }
+#ifndef BGCN_SPILL_DEPTH
+#define BGCN_SPILL_DEPTH 4
+#endif
+constexpr int kSpillDepth = BGCN_SPILL_DEPTH;
 __device__ inline void dw1_sliced_body(const SparseState& S, const float* __restrict__ dZ1,
                                        float* __restrict__ dw1_td, float* __restrict__ dw1_bu,
                                        const int64_t* __restrict__ batch, float* __restrict__ dw2_td,
-                                       float* __restrict__ dw2_bu, float scale, int bid, float* smem) {
+                                       float* __restrict__ dw2_bu, float scale, int bid, float* smem,
+                                       const float* __restrict__ dZ2, const KeepSrc& keep) {
   if (!use_sparse(S)) return;
   const int W = int(blockDim.x >> 6);
   const int x = bid & 7, sl_ = x % kSlices;
@@ -1092,12 +1485,13 @@ __device__ inline void dw1_sliced_body(const SparseState& S, const float* __rest
   const int64_t F = S.F;
   const int64_t c = cg * W + wave;
   float4 a1 = f4zero(), a2 = f4zero();
+  bool spill_root = false;
   if (c < F) {
     const int64_t beg = S.col_start[c], end = S.col_end[c];
     for (int64_t u0 = beg; u0 < end; u0 += 64) {
       const int64_t u = min<int64_t>(u0 + lane, end - 1);   // clamped: duplicates, x masked
       const uint2 ent = S.csc[u];
-      const uint32_t slot = ent.x & ~kCscRootFlag;
+      const uint32_t slot = ent.x & kCscSlotMask;
       const int n = int(min<int64_t>(64, end - u0));
       const float x_l = lane < n ? __uint_as_float(ent.y) : 0.f;
       const int32_t i_l = int32_t(slot / kCap);
@@ -1123,6 +1517,10 @@ __device__ inline void dw1_sliced_body(const SparseState& S, const float* __rest
         const int32_t i = __builtin_amdgcn_readlane(i_l, j);
         const int32_t sl = int32_t(__builtin_amdgcn_readlane(int32_t(slot), j) % kCap);
         const float f = scale * fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(x_l), j)), 0.f);
+        if (__builtin_amdgcn_readlane(int32_t(ent.x), j) & int32_t(kCscSpillFlag)) {
+          spill_root = true;   // summed after the column's main pass (its registers are free then)
+          continue;
+        }
         if (g != 0) continue;
         const int b = int(batch[i]);
         float4 sum = f4zero();
@@ -1137,6 +1535,43 @@ __device__ inline void dw1_sliced_body(const SparseState& S, const float* __rest
             if (it + qq < it1) sum = f4add(sum, v[qq]);
         }
         a2 = f4fma(f, sum, a2);
+      }
+    }
+    if (spill_root) {
+      // the column's spilled root entries (a root row of more than kCap words, rare), in
+      // row order: sum_{i in tree} keep_d(i, 64 + c) * dZ2_d[i] - lane group g takes the
+      // tree's nodes g, g + 8, ..., the groups' partials combined by the fixed xor tree
+      const uint32_t k = uint32_t(H + c);
+      for (int64_t u0 = beg; u0 < end; u0 += 64) {
+        const int64_t u = min<int64_t>(u0 + lane, end - 1);
+        const uint2 ent = S.csc[u];
+        const int n = int(min<int64_t>(64, end - u0));
+        uint64_t m = __ballot(lane < n && (ent.x & kCscRootFlag) && (ent.x & kCscSpillFlag));
+        while (m) {
+          const int j = __builtin_ctzll(m);
+          m &= m - 1;
+          const int32_t i = int32_t((uint32_t(__builtin_amdgcn_readlane(int32_t(ent.x), j)) & kCscSlotMask) / kCap);
+          const float f = scale * fmaxf(__int_as_float(__builtin_amdgcn_readlane(int32_t(ent.y), j)), 0.f);
+          int64_t nb, ne;
+          tree_range(S, int(batch[i]), nb, ne);
+          float4 sum = f4zero();
+          for (int64_t n0 = nb + g; n0 < ne; n0 += kSpillDepth * kSliceGroups) {   // rows in flight
+            float4 z[kSpillDepth];
+            uint32_t kw[kSpillDepth];
+#pragma unroll
+            for (int v = 0; v < kSpillDepth; ++v) {
+              const int64_t nd = min(n0 + v * kSliceGroups, ne - 1);
+              z[v] = ld4(dZ2 + nd * (2 * H) + d * H + oo);
+              kw[v] = keep.get(uint32_t(d), uint32_t(nd), k >> 5);
+            }
+#pragma unroll
+            for (int v = 0; v < kSpillDepth; ++v)
+              if (n0 + v * kSliceGroups < ne && ((kw[v] >> (k & 31)) & 1u)) sum = f4add(sum, z[v]);
+          }
+#pragma unroll
+          for (int off = kSliceLanes; off < 64; off <<= 1) sum = f4add(sum, shfl_xor4(sum, off));
+          if (g == 0) a2 = f4fma(f, sum, a2);
+        }
       }
     }
   }
@@ -1325,9 +1760,11 @@ __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
   int b = int(blockIdx.x);
   if (b < a.n_dw1) {
     if constexpr (kDw1Split == 0)
-      dw1_sliced_body(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem);
+      dw1_sliced_body(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem,
+                      a.dZ2, a.keep);
     else
-      dw1_body<kDw1Split>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem);
+      dw1_body<kDw1Split>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem,
+                          a.dZ2, a.keep);
     BT_END(80);
     return;
   }
@@ -1414,8 +1851,12 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   t.col_total = c.take<int32_t>(size_t(F));
   t.col_start = c.take<int32_t>(size_t(F));
   t.col_end = c.take<int32_t>(size_t(F));
-  t.csc = c.take<uint2>(slots);
+  t.csc = c.take<uint2>(slots + size_t(N) * kSpillPerRow);
   t.rbits = c.take<uint32_t>(size_t(2) * N);
+  t.ovf_off = c.take<int32_t>(size_t(N));   // the per-op encoder's spill pool (a prepared
+  t.ovf_cap = N * kSpillPerRow;             // batch brings its own)
+  t.ovf = c.take<uint2>(size_t(t.ovf_cap));
+  t.long_rows = c.take<int32_t>(size_t(N));
   if (S) {
     t.mode = S->mode;
     t.flags = S->flags;
@@ -1496,6 +1937,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   S.item_beg = p.item_beg; S.item_end = p.item_end; S.item_root = p.item_root;
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
   S.csc = p.csc;
+  S.ovf_off = p.x_ovf_off; S.ovf = p.x_ovf; S.ovf_cap = p.ovf_cap; S.long_rows = p.x_long;
   S.root_map = p.node_root;
   S.bstatus = p.status;
   a.batch = bt->batch; a.rootindex = bt->rootindex;
@@ -1603,6 +2045,7 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
   S.item_beg = p.item_beg; S.item_end = p.item_end; S.item_root = p.item_root;
   S.hist = p.hist; S.col_total = p.col_total; S.col_start = p.col_start; S.col_end = p.col_end;
   S.csc = p.csc;
+  S.ovf_off = p.x_ovf_off; S.ovf = p.x_ovf; S.ovf_cap = p.ovf_cap; S.long_rows = p.x_long;
   S.root_map = p.node_root;
   S.bstatus = p.status;
   if (!(part & 1)) return mode == 1 ? BGCN_OK : sparse_csc(S, s);
@@ -1627,9 +2070,9 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
 
 int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
 #if BGCN_C1_MODE == 1
-  hipLaunchKernelGGL(k_conv1_rows2<8>, dim3(grid_for(S.N, 8)), dim3(256), 0, s, S, Z1);
+  hipLaunchKernelGGL(k_conv1_rows2<8>, dim3(kLongRowBlocks + grid_for(S.N, 8)), dim3(256), 0, s, S, Z1);
 #elif BGCN_C1_MODE == 2
-  hipLaunchKernelGGL(k_conv1_rows2<4>, dim3(grid_for(S.N, 8)), dim3(256), 0, s, S, Z1);
+  hipLaunchKernelGGL(k_conv1_rows2<4>, dim3(kLongRowBlocks + grid_for(S.N, 8)), dim3(256), 0, s, S, Z1);
 #else
   hipLaunchKernelGGL(k_conv1_gather, dim3(grid_for(S.N, (kC1Threads / 64) * kC1Rows)), dim3(kC1Threads), 0, s,
                      S, Z1);

@@ -97,12 +97,16 @@ size_t carve_prepared(Carve& c, int64_t N, int64_t B, int64_t F, int64_t Etd, in
   t.x_nnz = c.take<int32_t>(size_t(N));
   t.x_cols = c.take<int32_t>(size_t(N) * BGCN_SPARSE_CAP);
   t.x_vals = c.take<float>(size_t(N) * BGCN_SPARSE_CAP);
+  t.x_ovf_off = c.take<int32_t>(size_t(N));
+  t.x_long = c.take<int32_t>(size_t(N));
+  t.ovf_cap = N * BGCN_SPARSE_SPILL_PER_ROW;
+  t.x_ovf = c.take<uint2>(size_t(t.ovf_cap));
   const int64_t R = (N + kCscRowBlock - 1) / kCscRowBlock;
   t.hist = c.take<int32_t>(size_t(R) * size_t(F));
   t.col_total = c.take<int32_t>(size_t(F));
   t.col_start = c.take<int32_t>(size_t(F));
   t.col_end = c.take<int32_t>(size_t(F));
-  t.csc = c.take<uint2>(size_t(N) * BGCN_SPARSE_CAP);
+  t.csc = c.take<uint2>(size_t(N) * (BGCN_SPARSE_CAP + BGCN_SPARSE_SPILL_PER_ROW));
   t.td_drop = c.take<int64_t>(size_t(2 * Etd));
   t.bu_drop = c.take<int64_t>(size_t(2 * Ebu));
   t.dws_bytes = drop_ws_size(B);
@@ -127,7 +131,7 @@ static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_
   Prepared p;
   Carve c(buf, bytes);
   carve_prepared(c, N, B, F, b->td_num_edges, b->bu_num_edges, &p);
-  const int mode = (feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxFeat) ? 1 : 0;
+  const int mode = (feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxFeat || N > kSparseMaxN) ? 1 : 0;
   // one stream: the six merged launches (DropEdge, K1, the pass over X and the CSC of X
   // side by side, bgcn_sparse.hip prep_pipeline).  BGCN_PREP_MERGED=0 (read per call)
   // selects the separate launches for A/B runs: the pass over X first (beside the

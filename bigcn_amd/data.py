@@ -127,6 +127,9 @@ def graph_npz_dict(tree: dict, y: int, vocab: int = VOCAB) -> dict:
             "y": np.array(y), "cls": np.zeros((n, 1)), "tweetids": np.arange(n).astype(str)}
 
 
+SPARSE_CAP = 32   # = libbgcn's BGCN_SPARSE_CAP (ELL entries per row; the rest spill)
+
+
 # ----------------------------------------------------------------------------- dataset
 @dataclass
 class Sample:
@@ -139,6 +142,7 @@ class Sample:
     cls: Optional[torch.Tensor] = None
     tweetids: Optional[torch.Tensor] = None
     x_nnz_max: Optional[int] = None     # most non-zeros in one row of x (feature-path hint)
+    x_spill: Optional[int] = None       # sum over rows of max(nnz - BGCN_SPARSE_CAP, 0)
 
 
 def _drop(row: np.ndarray, col: np.ndarray, rate: float, rnd: random.Random):
@@ -163,9 +167,11 @@ def make_sample(d: dict, tddroprate: float = 0.0, budroprate: float = 0.0,
     if "tweetids" in d:
         tweetids = torch.tensor([int(v) for v in d["tweetids"]], dtype=torch.int64)
     x = torch.tensor(d["x"], dtype=torch.float32)
+    nnz = (x != 0).sum(1)
     return Sample(
         x=x,
-        x_nnz_max=int((x != 0).sum(1).max()) if x.numel() else 0,
+        x_nnz_max=int(nnz.max()) if x.numel() else 0,
+        x_spill=int((nnz - SPARSE_CAP).clamp_min(0).sum()) if x.numel() else 0,
         edge_index=torch.as_tensor(np.stack([row, col]), dtype=torch.int64),
         BU_edge_index=torch.as_tensor(np.stack([burow, bucol]), dtype=torch.int64),
         y=torch.tensor([int(d["y"])], dtype=torch.int64),
@@ -218,14 +224,19 @@ class Batch:
             self._x_nnz_of = self.x
         return self
 
-    # Host-side feature-path hint: the most non-zeros in one row of x.  It is bound to the
-    # x tensor it was computed for and ignored once x is replaced.
-    def set_x_nnz_max(self, n: int) -> None:
+    # Host-side feature-path hints: the most non-zeros in one row of x and the entries past
+    # the ELL cap summed over the rows (what the spill pool must hold).  They are bound to
+    # the x tensor they were computed for and ignored once x is replaced.
+    def set_x_nnz_max(self, n: int, spill: Optional[int] = None) -> None:
         self.x_nnz_max = int(n)
+        self.x_spill = None if spill is None else int(spill)
         self._x_nnz_of = self.x
 
     def x_nnz_hint(self):
         return self.__dict__.get("x_nnz_max") if self.__dict__.get("_x_nnz_of") is self.x else None
+
+    def x_spill_hint(self):
+        return self.__dict__.get("x_spill") if self.__dict__.get("_x_nnz_of") is self.x else None
 
     def keys(self):
         return [k for k in self.__dict__ if not k.startswith("_")]
@@ -257,16 +268,23 @@ def collate(samples: Sequence[Sample]) -> Batch:
     if all(s.x_nnz_max is not None for s in samples):
         # host-side hint: FusedTrainStep skips the dense fallback when every row fits the
         # sparse feature path (BGCN_FEAT_SPARSE)
-        out.set_x_nnz_max(max(s.x_nnz_max for s in samples))
+        spill = sum(s.x_spill for s in samples) if all(s.x_spill is not None for s in samples) else None
+        out.set_x_nnz_max(max(s.x_nnz_max for s in samples), spill)
     return out
 
 
 # ----------------------------------------------------------------------------- bulk synthetic batches
 def synth_batch(rng: np.random.Generator, sizes: Sequence[int], vocab: int = VOCAB,
                 num_classes: int = 4, tddroprate: float = 0.0, budroprate: float = 0.0,
-                device="cpu", root_random: bool = False, dtype=torch.float32) -> Batch:
+                device="cpu", root_random: bool = False, dtype=torch.float32,
+                long_rows: Optional[tuple] = None) -> Batch:
     """A collated batch of synthetic trees built directly (vectorised), identical in
-    layout to ``collate([make_sample(npz) ...])``.  X is materialised dense on ``device``."""
+    layout to ``collate([make_sample(npz) ...])``.  X is materialised dense on ``device``.
+
+    ``long_rows=(frac, lo, hi[, roots])``: a fraction ``frac`` of the rows draw their word
+    count uniformly from [lo, hi] instead of 1 + Poisson(11) (long posts: the reference
+    caps no row, ``getTwittergraph.py:16-24``); ``roots`` (optional) forces that many
+    tree roots among them."""
     sizes = np.asarray(sizes, dtype=np.int64)
     B = len(sizes)
     offs = np.concatenate([[0], np.cumsum(sizes)])
@@ -287,6 +305,12 @@ def synth_batch(rng: np.random.Generator, sizes: Sequence[int], vocab: int = VOC
         td_rows.append(p_s[keep_td] + offs[b]); td_cols.append(c_s[keep_td] + offs[b])
         bu_rows.append(c_s[keep_bu] + offs[b]); bu_cols.append(p_s[keep_bu] + offs[b])
     nnz = np.minimum(1 + rng.poisson(11.0, size=N), vocab)
+    if long_rows is not None:
+        frac, lo, hi = long_rows[:3]
+        pick = rng.random(N) < frac
+        if len(long_rows) > 3 and long_rows[3]:
+            pick[np.asarray(roots[:int(long_rows[3])], dtype=np.int64)] = True
+        nnz[pick] = np.minimum(rng.integers(int(lo), int(hi) + 1, size=int(pick.sum())), vocab)
     rows = np.repeat(np.arange(N, dtype=np.int64), nnz)
     # distinct ids per row: random ids, duplicates within a row collapse (set semantics);
     # the first draw of a duplicated (row, id) is kept, on the host, so x does not depend
@@ -295,6 +319,7 @@ def synth_batch(rng: np.random.Generator, sizes: Sequence[int], vocab: int = VOC
     vals = rng.integers(1, 4, size=int(nnz.sum())).astype(np.float32)
     _, first = np.unique(rows * vocab + cols, return_index=True)
     rows, cols, vals = rows[first], cols[first], vals[first]
+    row_nnz = np.bincount(rows, minlength=N)                     # after duplicate collapse
     x = torch.zeros(N, vocab, dtype=dtype, device=device)
     x.index_put_((torch.as_tensor(rows, device=device), torch.as_tensor(cols, device=device)),
                  torch.as_tensor(vals, device=device).to(dtype))
@@ -309,5 +334,6 @@ def synth_batch(rng: np.random.Generator, sizes: Sequence[int], vocab: int = VOC
     out = Batch(x=x, edge_index=ei, BU_edge_index=bei, y=y, rootindex=rootindex, batch=batch,
                 ptr=torch.as_tensor(offs, dtype=torch.int64), num_graphs=B)
     out = out.to(device)
-    out.set_x_nnz_max(int(nnz.max()) if N else 0)   # upper bound (duplicate ids collapse)
+    out.set_x_nnz_max(int(row_nnz.max()) if N else 0,
+                      int(np.maximum(row_nnz - SPARSE_CAP, 0).sum()) if N else 0)
     return out

@@ -31,13 +31,18 @@ from .optim import IMAGE_BU_W1, IMAGE_BU_W2, IMAGE_TD_W1, IMAGE_TD_W2, FusedAdam
 
 def _step_feat_mode(feat_mode: str, data) -> int:
     """C-ABI feature path of a step: "auto" becomes BGCN_FEAT_SPARSE (no dense fallback
-    launched) when the batch carries a host-side ``x_nnz_max`` within the sparse cap
-    (collate / synth_batch set it); "sparse" forces it (overflow -> check_status raises)."""
+    launched) when the batch's host-side hints say its rows fit the sparse path - every row
+    within the ELL cap, or the entries past it within the spill pool (``collate`` /
+    ``synth_batch`` set them); "sparse" forces it (a batch that does not fit -> check_status
+    raises)."""
     if feat_mode == "sparse":
         return _lib.BGCN_FEAT_SPARSE
-    if feat_mode == "auto":
+    if feat_mode == "auto" and int(data.x.size(1)) <= 5120:
         hint = data.x_nnz_hint() if hasattr(data, "x_nnz_hint") else None
-        if hint is not None and int(hint) <= _lib.BGCN_SPARSE_CAP and int(data.x.size(1)) <= 5120:
+        spill = data.x_spill_hint() if hasattr(data, "x_spill_hint") else None
+        if hint is not None and int(hint) <= _lib.BGCN_SPARSE_CAP:
+            return _lib.BGCN_FEAT_SPARSE
+        if spill is not None and int(spill) <= int(data.x.size(0)) * _lib.BGCN_SPARSE_SPILL_PER_ROW:
             return _lib.BGCN_FEAT_SPARSE
     return _FEAT_MODES[feat_mode]
 
@@ -318,9 +323,10 @@ class FusedTrainStep:
         if s & 2:
             raise IndexError("label out of range [0, num_classes)")
         if s & 4:
-            raise ValueError(f"feat_mode 'sparse': a feature row holds more than "
-                             f"{_lib.BGCN_SPARSE_CAP} non-zeros (the step's results are invalid); "
-                             f"use 'auto' or 'dense'")
+            raise ValueError(f"feat_mode 'sparse': the batch's feature rows hold more non-zeros "
+                             f"than the sparse path's ELL + spill pool ({_lib.BGCN_SPARSE_CAP} + "
+                             f"{_lib.BGCN_SPARSE_SPILL_PER_ROW} per row of the batch; the step's "
+                             f"results are invalid); use 'auto' or 'dense'")
         if s & 8:
             raise RuntimeError("libbgcn: an internal cross-workgroup hand-off timed out "
                                "(the step's results are invalid)")

@@ -209,15 +209,19 @@ typedef struct bgcn_graph_view {
   int64_t capacity; /* E + N */
 } bgcn_graph_view;
 
-/* Feature path of the fused encoder.  AUTO: X is read once and every row compacted to
- * at most BGCN_SPARSE_CAP (col, val) pairs; products with X / X[root] then skip the zero
- * entries (exact: bag-of-words rows hold ~10-20 non-zeros of 5000).  If any row holds
- * more, the batch falls back to the dense MFMA kernels on the device (no host sync).
+/* Feature path of the fused encoder.  AUTO: X is read once and every row compacted to a
+ * list of its (col, val) non-zeros: the first BGCN_SPARSE_CAP in an ELL list, the rest of
+ * a longer row spilled to a per-batch pool of BGCN_SPARSE_SPILL_PER_ROW entries per row of
+ * capacity (the words of a post are not capped, Process/getTwittergraph.py:16-24);
+ * products with X / X[root] then skip the zero entries (exact: bag-of-words rows hold
+ * ~10-20 non-zeros of 5000).  Only when a batch's spilled entries exceed the pool
+ * (more than N * (BGCN_SPARSE_CAP + BGCN_SPARSE_SPILL_PER_ROW) non-zeros in all) does the
+ * batch fall back to the dense MFMA kernels on the device (no host sync).
  * DENSE: always the dense MFMA kernels.
- * SPARSE: the AUTO path without the dense fallback - the caller guarantees rows of at
- * most BGCN_SPARSE_CAP non-zeros (e.g. known from the sparse source features); the
- * gated dense kernels are then not launched at all (shorter step).  A row with more
- * non-zeros makes the results invalid and sets bit 2 of the step's *status. */
+ * SPARSE: the AUTO path without the dense fallback - the caller guarantees the batch fits
+ * the pool (e.g. known from the sparse source features); the gated dense kernels are then
+ * not launched at all (shorter step).  A batch that does not fit makes the results
+ * invalid and sets bit 2 of the step's *status. */
 #define BGCN_FEAT_AUTO 0
 #define BGCN_FEAT_DENSE 1
 #define BGCN_FEAT_SPARSE 2
@@ -227,6 +231,7 @@ typedef struct bgcn_graph_view {
 #define BGCN_DTYPE_F32 0
 #define BGCN_DTYPE_BF16 1
 #define BGCN_SPARSE_CAP 32
+#define BGCN_SPARSE_SPILL_PER_ROW 32
 
 typedef struct bgcn_bigcn_args {
   /* batch */
@@ -245,7 +250,8 @@ typedef struct bgcn_bigcn_args {
   int training; uint64_t seed; const uint32_t* keep_words; /* NULL = generate */
   /* feature path (AUTO needs the four buffers below; they are saved for backward) */
   int feat_mode;
-  int32_t* x_flags;              /* [8] ([0] != 0: a row overflowed -> dense)  */
+  int32_t* x_flags;              /* [8] ([0] != 0: spill pool full -> dense;
+                                    [1] spill pool fill)                    */
   int32_t* x_nnz;                /* [N]                                     */
   int32_t* x_cols;               /* [N][BGCN_SPARSE_CAP]                    */
   float* x_vals;                 /* [N][BGCN_SPARSE_CAP]                    */
@@ -319,7 +325,7 @@ int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree
  * td_w1 td_b1 td_w2 td_b2 bu_w1 bu_b1 bu_w2 bu_b2 fc_w [C, 256] fc_b [C] (the
  * reference state_dict layout).  *status (optional, zeroed by the call): bit 0 = an
  * edge index outside [0, N) or a batch id outside [0, B), bit 1 = a label outside [0, C),
- * bit 2 = a feature row with more than BGCN_SPARSE_CAP non-zeros under BGCN_FEAT_SPARSE,
+ * bit 2 = a batch whose feature rows overflow the spill pool under BGCN_FEAT_SPARSE,
  * bit 3 = an internal cross-workgroup hand-off timed out (never expected).  ANY set bit
  * makes the step's results invalid: through status_flag the optimiser skips the update.
  * status_seen (optional, never cleared by the library): every step ORs its status into

@@ -108,3 +108,49 @@ def test_npz_round_trip_through_dataset(tmp_path):
     assert s.x.shape == (9, 30) and int(s.y) == 3 and int(s.rootindex) == 0
     assert torch.equal(s.BU_edge_index, s.edge_index.flip(0))
     assert len(D.BiGraphDataset(["abc"], {"abc": tree}, lower=10, data_path=str(tmp_path))) == 0
+
+
+def test_long_rows_and_spill_hints():
+    """long_rows draws long posts (the reference caps no row, getTwittergraph.py:16-24);
+    the batch carries its most non-zeros per row and the entries past the ELL cap (the
+    spill pool's fill), bound to its x; collate sums the per-sample spill."""
+    rng = np.random.default_rng(5)
+    sizes = D.synth_tree_sizes(rng, 12, 50)
+    b = D.synth_batch(rng, sizes, vocab=600, long_rows=(0.05, 40, 300, 3))
+    nnz = (b.x != 0).sum(1)
+    assert int(nnz.max()) > 40
+    assert int((nnz[b.rootindex] > 32).sum()) >= 3
+    assert b.x_nnz_hint() == int(nnz.max())
+    assert b.x_spill_hint() == int((nnz - D.SPARSE_CAP).clamp_min(0).sum())
+    b.x = b.x.clone()                                   # a replaced x drops both hints
+    assert b.x_nnz_hint() is None and b.x_spill_hint() is None
+    # per-sample hints through make_sample / collate
+    samples = []
+    for n in (5, 9):
+        x = np.zeros((n, 100), np.float32)
+        x[0, :70] = 1.0                                  # one long row per sample: 38 spilled
+        d = {"x": x, "edgeindex": np.stack([np.zeros(n - 1, np.int64), np.arange(1, n)]),
+             "y": np.int64(1), "root": x[0], "rootindex": np.int64(0)}
+        samples.append(D.make_sample(d))
+    assert samples[0].x_nnz_max == 70 and samples[0].x_spill == 38
+    c = D.collate(samples)
+    assert c.x_nnz_hint() == 70 and c.x_spill_hint() == 76
+
+
+def test_feature_path_policy_from_hints():
+    """FusedTrainStep's "auto": BGCN_FEAT_SPARSE (no dense fallback launched) when every row
+    fits the ELL or the spill fits the pool; the gated AUTO form without hints."""
+    from bigcn_amd import _lib
+    from bigcn_amd.train import _step_feat_mode
+    b = D.Batch(x=torch.zeros(10, 5000))
+    assert _step_feat_mode("auto", b) == _lib.BGCN_FEAT_AUTO          # no hints
+    b.set_x_nnz_max(20)
+    assert _step_feat_mode("auto", b) == _lib.BGCN_FEAT_SPARSE
+    b.set_x_nnz_max(300, 10 * _lib.BGCN_SPARSE_SPILL_PER_ROW)
+    assert _step_feat_mode("auto", b) == _lib.BGCN_FEAT_SPARSE
+    b.set_x_nnz_max(300, 10 * _lib.BGCN_SPARSE_SPILL_PER_ROW + 1)      # beyond the pool
+    assert _step_feat_mode("auto", b) == _lib.BGCN_FEAT_AUTO
+    b.set_x_nnz_max(300)                                                # spill unknown
+    assert _step_feat_mode("auto", b) == _lib.BGCN_FEAT_AUTO
+    assert _step_feat_mode("dense", b) == _lib.BGCN_FEAT_DENSE
+    assert _step_feat_mode("sparse", b) == _lib.BGCN_FEAT_SPARSE

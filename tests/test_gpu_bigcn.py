@@ -164,8 +164,9 @@ def test_sparse_and_dense_paths_agree_full_size():
 
 @pytest.mark.parametrize("dense_rows", [1, 200])
 def test_sparse_overflow_falls_back_to_dense(dense_rows):
-    """Rows with more than 32 non-zeros switch the batch to the dense path on the device:
-    results still match the oracle."""
+    """Dense rows (512 non-zeros): one fits the spill pool (the sparse path adds its spilled
+    terms), 200 exceed it and switch the batch to the dense path on the device; results
+    match the oracle either way."""
     from bigcn_amd.ops import keep_words, unpack_keep
     b = _synth(26, 6, 60, F=512)
     g = torch.Generator().manual_seed(3)

@@ -83,12 +83,13 @@ def _oracle_batch(b, drops, drop_seed):
     return ref
 
 
-@pytest.mark.parametrize("workload", ["twitter15", "weibo_bf16", "synth1024_bf16"])
+@pytest.mark.parametrize("workload", ["twitter15", "weibo_bf16", "synth1024_bf16", "twitter15_tail"])
 def test_full_size_step_matches_oracle(workload):
     """BASELINE configs[1] (twitter15: 128 trees x mean 256, fp32, DropEdge 0.2/0.2),
     configs[2] (weibo_bf16: 128 x mean 816, bf16 X, 2-class Net, no DropEdge) and the
-    per-GPU shape of configs[4] (synth1024_bf16: 128 x mean 1024, bf16 X, DropEdge): loss,
-    log-probs and all ten gradients of the bench's step against the fp64 oracle."""
+    per-GPU shape of configs[4] (synth1024_bf16: 128 x mean 1024, bf16 X, DropEdge), and
+    twitter15 with 1 % of the rows holding 40-300 words (the spill pool): loss, log-probs
+    and all ten gradients of the bench's step against the fp64 oracle."""
     from bigcn_amd import FusedTrainStep
     from bigcn_amd.ops import keep_words, unpack_keep
     wl = bench.WORKLOADS[workload]

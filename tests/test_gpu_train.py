@@ -406,8 +406,9 @@ def test_sparse_hint_matches_gated_fallback_path():
 
 
 def test_sparse_mode_flags_overfull_rows():
-    """feat_mode "sparse" with a row of more than 32 non-zeros: status bit 2, check_status
-    raises; a replaced x invalidates the batch's hint (auto then falls back correctly)."""
+    """feat_mode "sparse" with every row dense (768 non-zeros: far beyond the 32-entry ELL and
+    the spill pool): status bit 2, check_status raises; a replaced x invalidates the batch's
+    hint (auto then falls back correctly)."""
     from bigcn_amd import FusedTrainStep
     b = _synth(46, 8, 60, F=768)
     g = torch.Generator().manual_seed(46)
@@ -533,13 +534,15 @@ def test_train_step_more_than_four_classes():
 
 def test_inplace_x_edit_after_collate_skips_update():
     """The host nnz hint (collate / synth_batch) is bound to the x tensor object, so an
-    in-place edit that overfills a row goes unseen by the hint.  The step then flags
-    status bit 2 on the device, the fused Adam skips the update (parameters and moments
-    unchanged, no host sync) and check_status() raises."""
+    in-place edit that overfills the sparse path goes unseen by the hint.  The step then
+    flags status bit 2 on the device, the fused Adam skips the update (parameters and
+    moments unchanged, no host sync) and check_status() raises.  (One long row fits the
+    spill pool; every row at 100 words - 68 spilled per row against 32 per row of pool -
+    does not.)"""
     from bigcn_amd import FusedTrainStep
     b = _synth(47, 8, 60)
     assert b.x_nnz_hint() is not None
-    b.x[3, :40] = 1.0                                   # 40 non-zeros > the sparse cap, in place
+    b.x[:, :100] = 1.0                                  # beyond ELL + spill pool, in place
     p = O.make_params(5000, 64, 64, 4, seed=22)
     m = _model(p)
     m.train()
