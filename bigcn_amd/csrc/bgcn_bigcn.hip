@@ -821,7 +821,7 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
 // block, root partials, root columns), db1 and the gated dense dW1; joined at the end.
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
                         const Prepared* prep, bool side_busy, const HeadGradJob* head,
-                        const WeightImages* img) {
+                        const WeightImages* img, bool defer_dw1) {
   BGCN_TRY(check_args(a));
   BGCN_CHECK_ARG(a->dhead_in && a->td_dw1 && a->bu_dw1 && a->td_dw2 && a->bu_dw2 && a->td_db1 &&
                      a->bu_db1 && a->td_db2 && a->bu_db2,
@@ -916,13 +916,38 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   t.red_sparse = RedCfg{w.Sh, int64_t(H), 0, sparse ? int(grid_for(2 * H * H, 256)) : 0};
   t.db1 = ColsumJob{w.colpart, int(nblk_h), a->td_db1, a->bu_db1};
   timing_begin(5, s);
-  BGCN_TRY(bwd_tail_launch(t, s));
+  // deferred dW1 (bgcn_train_step with defer_dw1): every gradient but dW1 is final when
+  // this launch ends; bigcn_backward_dw1 runs the dW1 waves later
+  BGCN_TRY(bwd_tail_launch(t, s, defer_dw1 ? 1 : 0));
   timing_end(5, s);
   (void)side_busy;
   timing_end(9, s);   // the main stream's own chain (span class, bgcn_train_step)
   // join only what this backward forked (a next-batch preparation on the side lane is
   // waited for by the next bgcn_train_step call instead)
   if (forked) BGCN_TRY(aux_join(s, kLaneSide));
+  return BGCN_OK;
+}
+
+// The deferred dW1 of a backward that ran with defer_dw1 (same args, workspace, prepared
+// batch): the tail's dW1 waves alone (the sparse path; the dense fallback's dW1 GEMM ran
+// inside the backward).
+int bigcn_backward_dw1(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s, const Prepared* prep,
+                       const WeightImages* img) {
+  BGCN_TRY(check_args(a));
+  BGCN_CHECK_ARG(a->td_dw1 && a->bu_dw1, "null gradient pointer");
+  FusedWs w;
+  SparseState sp{};
+  const int32_t* gate = nullptr;
+  BGCN_TRY(setup(a, ws, ws_bytes, w, sp, gate, prep, img));
+  if (sp.mode == 1) return BGCN_OK;
+  BwdTailArgs t{};
+  t.S = sp;
+  t.dZ1 = w.dz1; t.dw1_td = a->td_dw1; t.dw1_bu = a->bu_dw1;
+  t.node_root = w.node_root; t.batch = a->batch; t.dw2_td = a->td_dw2; t.dw2_bu = a->bu_dw2;
+  t.keep_scale = make_keep(a).scale(); t.gate = gate;
+  timing_begin(11, s);
+  BGCN_TRY(bwd_tail_launch(t, s, 2));
+  timing_end(11, s);
   return BGCN_OK;
 }
 

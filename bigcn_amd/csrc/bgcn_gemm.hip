@@ -14,6 +14,8 @@
 // MFMA 32x32x2 f32 operand maps (cdna_hip_programming.md section 3): lane l supplies
 // A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31]; D register r of lane l is
 // D[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31].
+#include <cstdlib>
+
 #include "bgcn_internal.h"
 
 namespace bgcn {
@@ -260,6 +262,261 @@ __global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ G, in
   }
 }
 
+// ============================================================================
+// bf16 X on the bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the k-depth of the f32 MFMA per
+// instruction).  Bag-of-words X is exact in bf16; the fp32 operand (W, or dZ1) is split
+// into hi + mid + lo bf16 parts (split3_bf16: all 24 mantissa bits), so each k-step takes
+// three products (small terms first) and the result is fp32-grade - conv1's output feeds a
+// relu, where a 1e-5 relative error flips relu' for entries near zero.  Both kernels stage
+// k-contiguous bf16 rows in LDS (row stride kB16LD: 16-byte aligned ds_read_b128 per lane)
+// through registers (next tile's global loads in flight during the current tile's MFMAs).
+// Lane map of 32x32x16: lane (h = l >> 5, r = l & 31) supplies A[r][8h + j] and
+// B[8h + j][r] (j < 8); D register q is D[(q & 3) + 8 (q >> 2) + 4h][r].
+// ============================================================================
+constexpr int kB16BK = 32, kB16LD = kB16BK + 8;
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+// Y[M, Nc] = X[M, K] (bf16) . W[Nc, K]^T (fp32; rows [0, split) from W0, the rest W1).
+// Block tile 128 x 128 (4 waves as 2 x 2, wave tile 64 x 64), K % 8 == 0, ldx % 8 == 0.
+__global__ __launch_bounds__(256) void k_gemm_xwt_bf16(const bf16_t* __restrict__ X, int64_t ldx,
+                                                       const float* __restrict__ W0,
+                                                       const float* __restrict__ W1, int64_t ldw,
+                                                       int64_t split, float* __restrict__ Y, int64_t ldy,
+                                                       int64_t M, int64_t Nc, int64_t K,
+                                                       const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
+  constexpr int BM = 128, BN = 128;
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * kB16LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3][BN * kB16LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
+  const int64_t m0 = int64_t(blockIdx.x) * BM, n0 = int64_t(blockIdx.y) * BN;
+  // staging: X rows tid / 4 + 64 i, 8 k at (tid % 4) * 8; W rows tid / 8 + 32 i, 4 k at (tid % 8) * 4
+  const int xr = tid >> 2, xk = (tid & 3) * 8;
+  const int wrow = tid >> 3, wk = (tid & 7) * 4;
+  const bf16_t* xp[2];
+  bool xok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int64_t m = m0 + xr + 64 * i;
+    xok[i] = m < M;
+    xp[i] = X + (xok[i] ? m : 0) * ldx;
+  }
+  const float* wp[4];
+  bool wok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t n = n0 + wrow + 32 * i;
+    wok[i] = n < Nc;
+    const int64_t nn = wok[i] ? n : 0;
+    wp[i] = nn < split ? W0 + nn * ldw : W1 + (nn - split) * ldw;
+  }
+  u32x4v ra[2];
+  float4 rb[4];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t k = k0 + xk;
+      const bool ok = xok[i] && k < K;
+      const u32x4v v = *reinterpret_cast<const u32x4v*>(xp[i] + (ok ? k : 0));
+      ra[i] = ok ? v : u32x4v{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t k = k0 + wk;
+      const bool ok = wok[i] && k < K;
+      const float4 v = ld4(wp[i] + (ok ? k : 0));
+      rb[i] = ok ? v : f4zero();
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4v*>(&As[(xr + 64 * i) * kB16LD + xk]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v[4] = {rb[i].x, rb[i].y, rb[i].z, rb[i].w};
+      __bf16 hi[4], mi[4], lo[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split3_bf16(v[e], hi[e], mi[e], lo[e]);
+      const int o = (wrow + 32 * i) * kB16LD + wk;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        Bs[0][o + e] = hi[e];
+        Bs[1][o + e] = mi[e];
+        Bs[2][o + e] = lo[e];
+      }
+    }
+  };
+  f32x16 acc[2][2] = {};
+  const int nk = int((K + kB16BK - 1) / kB16BK);
+  gload(0);
+  sstore();
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(int64_t(kt + 1) * kB16BK);
+#pragma unroll
+    for (int s = 0; s < kB16BK / 16; ++s) {
+      const int ko = 16 * s + 8 * h;
+      bf16x8 a[2], b[3][2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+        a[mi] = *reinterpret_cast<const bf16x8*>(&As[(wr * 64 + mi * 32 + r32) * kB16LD + ko]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          b[p][ni] = *reinterpret_cast<const bf16x8*>(&Bs[p][(wc * 64 + ni * 32 + r32) * kB16LD + ko]);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          f32x16 c = acc[mi][ni];
+          c = mfma_bf16(a[mi], b[2][ni], c);
+          c = mfma_bf16(a[mi], b[1][ni], c);
+          acc[mi][ni] = mfma_bf16(a[mi], b[0][ni], c);
+        }
+    }
+    __syncthreads();
+    if (kt + 1 < nk) {
+      sstore();
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t m = m0 + wr * 64 + mi * 32 + acc_row(q, lane);
+      if (m >= M) continue;
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int64_t n = n0 + wc * 64 + ni * 32 + r32;
+        if (n < Nc) Y[m * ldy + n] = acc[mi][ni][q];
+      }
+    }
+}
+
+// Partial C_s[Mc, Nc] = G[Ks, Mc]^T (fp32, split) . X[Ks, Nc] (bf16) over the node chunk
+// of split s.  Block tile 128 (Mc) x 128 (Nc), 4 waves as 2 x 2.  Both operands are
+// k-major in memory (rows = nodes): staged transposed into k-contiguous LDS rows, two
+// nodes per 4-byte LDS write.  Nc % 8 == 0, ldx % 8 == 0, ldg % 4 == 0.
+__global__ __launch_bounds__(256) void k_gemm_tn_bf16(const float* __restrict__ G, int64_t ldg,
+                                                      const bf16_t* __restrict__ X, int64_t ldx,
+                                                      float* __restrict__ part, int64_t Mc, int64_t Nc,
+                                                      int64_t K, int64_t kchunk,
+                                                      const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
+  constexpr int BM = 128, BN = 128;
+  __shared__ __attribute__((aligned(16))) __bf16 As[3][BM * kB16LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * kB16LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
+  const int64_t n0 = int64_t(blockIdx.x) * BN, m0 = int64_t(blockIdx.y) * BM;
+  const int64_t kb = int64_t(blockIdx.z) * kchunk;
+  const int64_t ke = min<int64_t>(kb + kchunk, K);
+  float* out = part + int64_t(blockIdx.z) * Mc * Nc;
+  // staging: G nodes 2p, 2p + 1 (+16) of m quad 4q (q = tid % 32, p = tid / 32);
+  //          X nodes 2p, 2p + 1 of n octet 8o (o = tid % 16, p = tid / 16)
+  const int gq = (tid & 31) * 4, gp = (tid >> 5) * 2;
+  const int xo = (tid & 15) * 8, xp2 = (tid >> 4) * 2;
+  float4 rg[4];
+  u32x4v rx[2];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t k = k0 + gp + (i & 1) + 16 * (i >> 1);
+      const int64_t m = m0 + gq;
+      const bool ok = k < ke && m < Mc;
+      const float4 v = ld4(G + (ok ? k : 0) * ldg + (ok ? m : 0));
+      rg[i] = ok ? v : f4zero();
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t k = k0 + xp2 + i;
+      const int64_t n = n0 + xo;
+      const bool ok = k < ke && n < Nc;
+      const u32x4v v = *reinterpret_cast<const u32x4v*>(X + (ok ? k : 0) * ldx + (ok ? n : 0));
+      rx[i] = ok ? v : u32x4v{0u, 0u, 0u, 0u};
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {   // node pairs (gp, gp + 1) and (gp + 16, gp + 17)
+      const float4 u = rg[2 * pr], v = rg[2 * pr + 1];
+      const float a0[4] = {u.x, u.y, u.z, u.w}, a1[4] = {v.x, v.y, v.z, v.w};
+      const int kk = gp + 16 * pr;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        __bf16 h0, m0_, l0, h1, m1, l1;
+        split3_bf16(a0[e], h0, m0_, l0);
+        split3_bf16(a1[e], h1, m1, l1);
+        const int o = (gq + e) * kB16LD + kk;
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<bf16x2*>(&As[0][o]) = bf16x2{h0, h1};
+        *reinterpret_cast<bf16x2*>(&As[1][o]) = bf16x2{m0_, m1};
+        *reinterpret_cast<bf16x2*>(&As[2][o]) = bf16x2{l0, l1};
+      }
+    }
+    const uint32_t w0[4] = {rx[0].x, rx[0].y, rx[0].z, rx[0].w};
+    const uint32_t w1[4] = {rx[1].x, rx[1].y, rx[1].z, rx[1].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {   // n = xo + e: (X[2p][n], X[2p + 1][n]) as one 4-byte word
+      const uint32_t lo = (e & 1) ? (w0[e >> 1] >> 16) : (w0[e >> 1] & 0xffffu);
+      const uint32_t hi = (e & 1) ? (w1[e >> 1] & 0xffff0000u) : (w1[e >> 1] << 16);
+      *reinterpret_cast<uint32_t*>(&Bs[(xo + e) * kB16LD + xp2]) = lo | hi;
+    }
+  };
+  f32x16 acc[2][2] = {};
+  const int nk = int((ke - kb + kB16BK - 1) / kB16BK);
+  if (nk > 0) {
+    gload(kb);
+    sstore();
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(kb + int64_t(kt + 1) * kB16BK);
+#pragma unroll
+    for (int s = 0; s < kB16BK / 16; ++s) {
+      const int ko = 16 * s + 8 * h;
+      bf16x8 a[3][2], b[2];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+          a[p][mi] = *reinterpret_cast<const bf16x8*>(&As[p][(wr * 64 + mi * 32 + r32) * kB16LD + ko]);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        b[ni] = *reinterpret_cast<const bf16x8*>(&Bs[(wc * 64 + ni * 32 + r32) * kB16LD + ko]);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          f32x16 c = acc[mi][ni];
+          c = mfma_bf16(a[2][mi], b[ni], c);
+          c = mfma_bf16(a[1][mi], b[ni], c);
+          acc[mi][ni] = mfma_bf16(a[0][mi], b[ni], c);
+        }
+    }
+    __syncthreads();
+    if (kt + 1 < nk) {
+      sstore();
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t m = m0 + wr * 64 + mi * 32 + acc_row(q, lane);
+      if (m >= Mc) continue;
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int64_t n = n0 + wc * 64 + ni * 32 + r32;
+        if (n < Nc) out[m * Nc + n] = acc[mi][ni][q];
+      }
+    }
+}
+
 // C[m][n] = sum_s part[s][m][n] (fixed order), rows [0, split) -> C0, the rest -> C1.
 __global__ __launch_bounds__(256) void k_reduce_splits(const float* __restrict__ part, int S,
                                                        int64_t Mc, int64_t Nc, float* __restrict__ C0,
@@ -306,6 +563,16 @@ static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1
   const bool xal = (reinterpret_cast<uintptr_t>(X) & (4 * sizeof(TX) - 1)) == 0;
   bool vec = K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0 && xal && aligned16(W0) &&
              (!W1 || aligned16(W1));
+  if constexpr (sizeof(TX) == 2) {
+    // bf16 X: the bf16 MFMA with W split three ways (BGCN_GEMM_BF16=0 keeps the f32 MFMA)
+    static const bool b16 = [] { const char* e = std::getenv("BGCN_GEMM_BF16"); return !(e && atoi(e) == 0); }();
+    if (b16 && vec && K % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+      hipLaunchKernelGGL(k_gemm_xwt_bf16, dim3(grid_for(M, 128), grid_for(Nc, 128)), dim3(256), 0, stream,
+                         reinterpret_cast<const bf16_t*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K, gate);
+      BGCN_CHECK_LAUNCH();
+      return BGCN_OK;
+    }
+  }
   dim3 grid(grid_for(M, 64), grid_for(Nc, 128));
   if (vec)
     hipLaunchKernelGGL((k_gemm_xwt<true, false, TX>), grid, dim3(256), 0, stream, X, ldx, W0, W1,
@@ -418,9 +685,19 @@ static int gemm_tn_t(const float* G, int64_t ldg, const TX* X, int64_t ldx, floa
   float* part = static_cast<float*>(ws);
   const bool xal = (reinterpret_cast<uintptr_t>(X) & (4 * sizeof(TX) - 1)) == 0;
   bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) && xal;
-  dim3 grid(grid_for(Nc, 64), grid_for(Mc, 128), S);
   timing_begin(timing_cls, stream);
-  if (vec)
+  bool done = false;
+  if constexpr (sizeof(TX) == 2) {
+    static const bool b16 = [] { const char* e = std::getenv("BGCN_GEMM_BF16"); return !(e && atoi(e) == 0); }();
+    if (b16 && vec && Nc % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+      hipLaunchKernelGGL(k_gemm_tn_bf16, dim3(grid_for(Nc, 128), grid_for(Mc, 128), S), dim3(256), 0, stream, G,
+                         ldg, reinterpret_cast<const bf16_t*>(X), ldx, part, Mc, Nc, K, kchunk, gate);
+      done = true;
+    }
+  }
+  dim3 grid(grid_for(Nc, 64), grid_for(Mc, 128), S);
+  if (done) {
+  } else if (vec)
     hipLaunchKernelGGL((k_gemm_tn<true, TX>), grid, dim3(256), 0, stream, G, ldg, X, ldx, part, Mc,
                        Nc, K, kchunk, gate);
   else

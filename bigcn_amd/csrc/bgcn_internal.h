@@ -306,7 +306,11 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
 // the readout backward
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
                         const Prepared* prep = nullptr, bool side_busy = false,
-                        const HeadGradJob* head = nullptr, const WeightImages* img = nullptr);
+                        const HeadGradJob* head = nullptr, const WeightImages* img = nullptr,
+                        bool defer_dw1 = false);
+// the dW1 of a backward run with defer_dw1 (same arguments and buffers)
+int bigcn_backward_dw1(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s, const Prepared* prep,
+                       const WeightImages* img);
 
 // ---- prepared batch (bgcn_step.hip): the weight-independent state of one batch
 // (sizes shared with bgcn_sparse.h: tree work items of kChunkItems nodes, CSC row blocks)

@@ -144,6 +144,7 @@ int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s);
 // mode 1 = dense: no ELL / CSC of X)
 int prep_pipeline(const Prepared& p, const bgcn_batch* b, int64_t F, int degree_on, int mode,
                   hipStream_t s, bool x_part = true);
-int bwd_tail_launch(BwdTailArgs& a, hipStream_t s);
+// part: 0 = the whole tail; 1 = all but dW1; 2 = dW1 only (the deferred-dW1 step)
+int bwd_tail_launch(BwdTailArgs& a, hipStream_t s, int part = 0);
 
 }  // namespace bgcn

@@ -1310,7 +1310,9 @@ __device__ __forceinline__ void tree_range(const SparseState& S, int b, int64_t&
   ne = it1 > it0 ? S.item_end[it1 - 1] : 0;
 }
 
-template <int kDw1Split>                       // waves per column (1 or 4)
+// kPart: 0 = dW1 and the dW2 root columns, 1 = the dW2 root columns only (no dZ1
+// gathers, dW1 untouched: the deferred-dW1 step's tail A), 2 = dW1 only.
+template <int kDw1Split, int kPart = 0>                       // waves per column (1 or 4)
 __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ dZ1,
                                 float* __restrict__ dw1_td, float* __restrict__ dw1_bu,
                                 const int64_t* __restrict__ batch, float* __restrict__ dw2_td,
@@ -1336,7 +1338,7 @@ __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ 
       const int n = int(min<int64_t>(64, end - u0));
       const float x_l = lane < n ? xv : 0.f;
       const int32_t i_l = int32_t(slot / kCap);
-      for (int j0 = 0; j0 < n; j0 += kDw1Depth) {
+      for (int j0 = 0; j0 < (kPart == 1 ? 0 : n); j0 += kDw1Depth) {
         float2 gv[kDw1Depth];
         float x[kDw1Depth];
 #pragma unroll
@@ -1356,7 +1358,7 @@ __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ 
       // order = CSC row order) of 2 relu(x) * sum_items root_part[d][item][slot] - the
       // root entries (rare) are flagged in the CSC record, so this pass over the column
       // finds them (a separate role re-read every column and gathered node_root per entry)
-      uint64_t m = __ballot(lane < n && (ent.x & kCscRootFlag));
+      uint64_t m = kPart == 2 ? 0ull : __ballot(lane < n && (ent.x & kCscRootFlag));
       while (m) {   // in row (= tree) order
         const int j = __builtin_ctzll(m);
         m &= m - 1;
@@ -1426,9 +1428,9 @@ __device__ inline void dw1_body(const SparseState& S, const float* __restrict__ 
       acc2 += t2[ty][tx * kDw1Split + k];
     }
     float* dst = ty < H ? dw1_td + int64_t(ty) * F : dw1_bu + int64_t(ty - H) * F;
-    dst[cc] = acc;
+    if (kPart != 1) dst[cc] = acc;
     float* dst2 = ty < H ? dw2_td + int64_t(ty) * K2 : dw2_bu + int64_t(ty - H) * K2;
-    dst2[H + cc] = acc2;
+    if (kPart != 2) dst2[H + cc] = acc2;
   }
 }
 
@@ -1470,6 +1472,7 @@ __host__ __device__ inline int dw1_sliced_blocks(int64_t F, int W) {
 #define BGCN_SPILL_DEPTH 4
 #endif
 constexpr int kSpillDepth = BGCN_SPILL_DEPTH;
+template <int kPart = 0>   // 0: dW1 + the dW2 root columns, 2: dW1 only (see dw1_body)
 __device__ inline void dw1_sliced_body(const SparseState& S, const float* __restrict__ dZ1,
                                        float* __restrict__ dw1_td, float* __restrict__ dw1_bu,
                                        const int64_t* __restrict__ batch, float* __restrict__ dw2_td,
@@ -1510,7 +1513,7 @@ __device__ inline void dw1_sliced_body(const SparseState& S, const float* __rest
 #pragma unroll
         for (int v = 0; v < kSliceDepth; ++v) a1 = f4fma(xx[v], gv[v], a1);
       }
-      uint64_t m = __ballot(lane < n && (ent.x & kCscRootFlag));
+      uint64_t m = kPart == 2 ? 0ull : __ballot(lane < n && (ent.x & kCscRootFlag));
       while (m) {   // root entries, in row (= tree) order; lane group 0 holds the slice
         const int j = __builtin_ctzll(m);
         m &= m - 1;
@@ -1597,7 +1600,7 @@ __device__ inline void dw1_sliced_body(const SparseState& S, const float* __rest
     if (cc >= F) continue;
     const int o = so % H + ol;
     w1[int64_t(o) * F + cc] = t1[ol * (W + 1) + tx];
-    w2[int64_t(o) * K2 + H + cc] = t2[ol * (W + 1) + tx];
+    if (kPart != 2) w2[int64_t(o) * K2 + H + cc] = t2[ol * (W + 1) + tx];
   }
 }
 
@@ -1753,21 +1756,27 @@ constexpr int kTailSmem = cmax(cmax(kDw1Smem, kRedSmem), kColsumSmem);
 #define BGCN_TAIL_THREADS 512   // 1024-thread blocks ran one per CU: dW1 in two rounds
 #endif
 constexpr int kTailThreads = BGCN_TAIL_THREADS;   // threads per block of the tail launch
-template <int kDw1Split>   // 0: dw1_sliced_body, else dw1_body's waves per column
+// kPart (the deferred-dW1 step, bgcn_step_args.defer_dw1): 0 = every role; 1 = all but dW1
+// (the dW2 root columns by one wave per column, dw1_body<1, 1>); 2 = dW1 only
+template <int kDw1Split, int kPart = 0>   // kDw1Split 0: dw1_sliced_body, else dw1_body's waves per column
 __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[kTailSmem];
   BT_BEGIN
   int b = int(blockIdx.x);
   if (b < a.n_dw1) {
-    if constexpr (kDw1Split == 0)
-      dw1_sliced_body(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem,
-                      a.dZ2, a.keep);
+    if constexpr (kPart == 1)
+      dw1_body<1, 1>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem,
+                     a.dZ2, a.keep);
+    else if constexpr (kDw1Split == 0)
+      dw1_sliced_body<kPart>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b,
+                             smem, a.dZ2, a.keep);
     else
-      dw1_body<kDw1Split>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b, smem,
-                          a.dZ2, a.keep);
+      dw1_body<kDw1Split, kPart>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b,
+                                 smem, a.dZ2, a.keep);
     BT_END(80);
     return;
   }
+  if (kPart == 2) return;
   b -= a.n_dw1;
   if (b < a.red_dense.blocks + a.red_sparse.blocks) {
     reduce_dw2_body(a.dw2_part, a.S.F + H, a.dw2_td, a.dw2_bu, a.gate, a.red_dense, a.red_sparse, b, smem);
@@ -1791,7 +1800,7 @@ int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s) {
   return BGCN_OK;
 }
 
-int bwd_tail_launch(BwdTailArgs& a, hipStream_t s) {
+int bwd_tail_launch(BwdTailArgs& a, hipStream_t s, int part) {
   // one wave per column (with 1024-thread blocks, one per CU, four waves per column won
   // from 64k rows; with 512-thread blocks one wave wins at every size: synth1024_bf16
   // 0.839 vs 0.850-0.859 ms, weibo_bf16 0.690 vs 0.697, profiles/r02_split_ab.txt);
@@ -1803,11 +1812,29 @@ int bwd_tail_launch(BwdTailArgs& a, hipStream_t s) {
   constexpr int wpb = kTailThreads / 64;   // waves per block
   const int cols1 = split == 4 ? wpb / 4 : wpb;
   a.n_dw1 = !sparse ? 0 : split == 0 ? dw1_sliced_blocks(a.S.F, wpb) : int((a.S.F + cols1 - 1) / cols1);
+  if (part == 1) a.n_dw1 = !sparse ? 0 : int((a.S.F + wpb - 1) / wpb);   // root columns: a wave per column
   a.n_rootcols = 0;   // the dW2 root columns ride with the dW1 waves (dw1_body)
   // the reduction configurations are sized in 1024-thread blocks (4 groups of 256)
   a.red_dense.blocks *= 1024 / kTailThreads;
   a.red_sparse.blocks *= 1024 / kTailThreads;
-  const int n = a.n_dw1 + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(kTailThreads);
+  const int n = part == 2 ? a.n_dw1
+                          : a.n_dw1 + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(kTailThreads);
+  if (n == 0) return BGCN_OK;
+  if (part == 1) {
+    hipLaunchKernelGGL((k_bwd_tail<1, 1>), dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
+    BGCN_CHECK_LAUNCH();
+    return BGCN_OK;
+  }
+  if (part == 2) {
+    if (split == 4)
+      hipLaunchKernelGGL((k_bwd_tail<4, 2>), dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
+    else if (split == 1)
+      hipLaunchKernelGGL((k_bwd_tail<1, 2>), dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_bwd_tail<0, 2>), dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
+    BGCN_CHECK_LAUNCH();
+    return BGCN_OK;
+  }
   if (split == 4)
     hipLaunchKernelGGL(k_bwd_tail<4>, dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);
   else if (split == 1)

@@ -273,7 +273,52 @@ static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w
   // the side lane the dW2 chain stays on this stream, which balances the two)
   const HeadGradJob hj{w.head, w.dz, B, int(C), w.loss_row, a->grads[8], a->grads[9], a->loss,
                        a->status, a->status_flag, a->status_seen};
-  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr, &hj, img);
+  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr, &hj, img, a->defer_dw1 != 0);
+}
+
+// the encoder arguments of a step (the dW1 call re-derives them from the same inputs)
+static void step_encoder_args(const bgcn_step_args* a, const Prepared& p, const StepWs& w, bgcn_bigcn_args* e) {
+  *e = bgcn_bigcn_args{};
+  e->x = a->cur.x; e->x_dtype = a->cur.x_dtype;
+  e->ldx = a->cur.ldx; e->num_nodes = a->cur.num_nodes; e->num_graphs = a->cur.num_graphs;
+  e->in_feats = a->in_feats; e->hid = H;
+  e->batch = a->cur.batch; e->rootindex = a->cur.rootindex;
+  e->td = view_of(p.td, p.td_cap);
+  e->bu = view_of(p.bu, p.bu_cap);
+  e->td_w1 = a->params[0]; e->td_b1 = a->params[1]; e->td_w2 = a->params[2]; e->td_b2 = a->params[3];
+  e->bu_w1 = a->params[4]; e->bu_b1 = a->params[5]; e->bu_w2 = a->params[6]; e->bu_b2 = a->params[7];
+  e->training = a->training; e->seed = a->seed; e->keep_words = nullptr;
+  e->feat_mode = a->feat_mode;
+  e->x_flags = p.x_flags; e->x_nnz = p.x_nnz; e->x_cols = p.x_cols; e->x_vals = p.x_vals;
+  e->tree_ptr = p.tree_ptr; e->h1 = w.h1; e->h2 = w.h2; e->head_in = w.head; e->dhead_in = w.dhead;
+  e->td_dw1 = a->grads[0]; e->td_db1 = a->grads[1]; e->td_dw2 = a->grads[2]; e->td_db2 = a->grads[3];
+  e->bu_dw1 = a->grads[4]; e->bu_db1 = a->grads[5]; e->bu_dw2 = a->grads[6]; e->bu_db2 = a->grads[7];
+  e->save_for_backward = 1;
+}
+
+int train_step_dw1_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStream_t s) {
+  BGCN_CHECK_ARG(a, "null args");
+  BGCN_TRY(check_batch(&a->cur));
+  const int64_t N = a->cur.num_nodes, B = a->cur.num_graphs, F = a->in_feats, C = a->num_classes;
+  BGCN_CHECK_ARG(a->defer_dw1, "bgcn_train_step_dw1 follows a step run with defer_dw1 = 1");
+  BGCN_CHECK_ARG(a->grads[0] && a->grads[4], "null gradient pointer");
+  BGCN_CHECK_ARG(ws && ws_bytes >= train_step_ws_size(N, B, F, C, 0, 0), "workspace too small");
+  BGCN_CHECK_ARG(a->prepared && a->prepared_bytes >= prepared_size(N, B, F, a->cur.td_num_edges, a->cur.bu_num_edges),
+                 "prepared buffer too small");
+  StepWs w;
+  Carve c(ws, ws_bytes);
+  carve_step(c, N, B, F, C, &w);
+  Prepared p;
+  Carve cp(a->prepared, a->prepared_bytes);
+  carve_prepared(cp, N, B, F, a->cur.td_num_edges, a->cur.bu_num_edges, &p);
+  bgcn_bigcn_args e;
+  step_encoder_args(a, p, w, &e);
+  WeightImages im{};
+  if (a->images) {
+    Carve ci(a->images, bgcn_weight_images_size(F));
+    carve_images(ci, F, &im);
+  }
+  return bigcn_backward_dw1(&e, w.enc, w.enc_bytes, s, &p, a->images ? &im : nullptr);
 }
 
 }  // namespace bgcn
@@ -317,4 +362,9 @@ extern "C" int bgcn_train_step(const bgcn_step_args* args, void* workspace, size
                                bgcn_stream_t stream) {
   return bgcn::train_step_impl(args, workspace, workspace_bytes,
                                reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int bgcn_train_step_dw1(const bgcn_step_args* args, void* workspace, size_t workspace_bytes,
+                                   bgcn_stream_t stream) {
+  return bgcn::train_step_dw1_impl(args, workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream));
 }

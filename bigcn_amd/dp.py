@@ -6,7 +6,10 @@ the fused encoder on its own 128 trees; the only exchange is one all-reduce (sum
 the flat fp32 gradient bucket (1,289,476 params = 5.16 MB for the Twitter model) per
 step over RCCL (torch.distributed backend "nccl" on ROCm) / gloo on CPU.  The mean
 (÷ world) is folded into the fused Adam step (``grad_scale``), which reads the reduced
-bucket in place, so every rank applies the identical update.
+bucket in place, so every rank applies the identical update.  The fused step all-reduces
+the bucket in two parts: everything but the conv1 weight gradients while those are still
+being computed (overlap the conv1 dW with communication), then the conv1
+weights.
 """
 from __future__ import annotations
 
@@ -47,20 +50,39 @@ class GradBucket:
     gradients also tells every rank whether any rank's step was invalid (the fused Adam
     then skips the update everywhere, keeping the replicas identical)."""
 
-    def __init__(self, params: Iterable[torch.nn.Parameter], status_slot: bool = False):
+    def __init__(self, params: Iterable[torch.nn.Parameter], status_slot: bool = False,
+                 late: Iterable[torch.nn.Parameter] = ()):
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
         self.numels = [p.numel() for p in self.params]
         dev = self.params[0].device
-        # every view starts on a 16-byte boundary (the kernels' float4 paths; a Weibo head
+        # Layout: [early gradients | status slot | late gradients].  ``late`` parameters
+        # (the conv1 weights of the deferred-dW1 step) sit at the end, so the bucket
+        # all-reduces in two contiguous parts: ``flat_a`` (every other gradient and the
+        # status slot) while the late gradients are still being computed, then ``flat_b``.
+        # Every view starts on a 16-byte boundary (the kernels' float4 paths; a Weibo head
         # bias of 2 elements would otherwise misalign every parameter after it); the gaps
-        # stay zero through the all-reduce
-        offs, n = [], 0
-        for k in self.numels:
-            offs.append(n)
-            n += (k + 3) // 4 * 4
-        self._packed = all(k % 4 == 0 for k in self.numels)   # no gaps: one cat fills it
-        self.flat = torch.zeros(n + (1 if status_slot else 0), dtype=torch.float32, device=dev)
-        self.flag = self.flat[n:] if status_slot else None
+        # stay zero through the all-reduce.
+        late_ids = {id(p) for p in late}
+        order = [i for i, p in enumerate(self.params) if id(p) not in late_ids] + \
+                [i for i, p in enumerate(self.params) if id(p) in late_ids]
+        self.late = [self.params[i] for i in order if id(self.params[i]) in late_ids]
+        offs, n = [0] * len(self.params), 0
+        n_a = None
+        for i in order:
+            if n_a is None and id(self.params[i]) in late_ids:
+                n_a = n + (4 if status_slot else 0)
+                n = n_a
+            offs[i] = n
+            n += (self.numels[i] + 3) // 4 * 4
+        flag_at = n_a - 4 if (n_a is not None and status_slot) else n
+        if n_a is None:
+            n_a = n + (1 if status_slot else 0)
+        total = max(n_a, n) if self.late else n_a
+        self._packed = all(k % 4 == 0 for k in self.numels) and not self.late   # one cat fills it
+        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.flag = self.flat[flag_at:flag_at + 1] if status_slot else None
+        self.flat_a = self.flat[:n_a]        # early gradients + the status slot
+        self.flat_b = self.flat[n_a:]        # the late gradients (empty without late params)
         self._views = [self.flat[o:o + k].view_as(p) for o, k, p in zip(offs, self.numels, self.params)]
 
     def views(self) -> List[torch.Tensor]:
@@ -72,6 +94,15 @@ class GradBucket:
         """In-place SUM of the bucket over ranks (one RCCL all-reduce; no-op at world 1)."""
         if dist.is_initialized() and self.world(group) > 1:
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+
+    def allreduce_part_async(self, part: str, group=None):
+        """Start the in-place SUM of one part ("a": early gradients + status slot, "b": the
+        late gradients) and return the work handle (None at world 1 or for an empty part):
+        ``work.wait()`` orders the current stream behind the collective."""
+        t = self.flat_a if part == "a" else self.flat_b
+        if t.numel() == 0 or not (dist.is_initialized() and self.world(group) > 1):
+            return None
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
 
     def world(self, group=None) -> int:
         return dist.get_world_size(group) if dist.is_initialized() else 1

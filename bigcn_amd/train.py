@@ -17,6 +17,7 @@ exceed the device time of a 128-tree step.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -78,7 +79,10 @@ class FusedTrainStep:
         self.last_drop_seed = None
         self.opt = optimizer if optimizer is not None else bigcn_adam(model)
         self.group = group
-        self.bucket = GradBucket(self.opt.params(), status_slot=True)
+        # the conv1 weight gradients (the step's last, bgcn_train_step_dw1) at the bucket's
+        # end: with world > 1 the rest of the bucket is all-reduced while they compute
+        enc = list(model.encoder_params())
+        self.bucket = GradBucket(self.opt.params(), status_slot=True, late=[enc[0], enc[4]])
         by_id = {id(p): v for p, v in zip(self.bucket.params, self.bucket.views())}
         self.step_params = list(model.encoder_params()) + [model.fc.weight, model.fc.bias]
         missing = [i for i, p in enumerate(self.step_params) if id(p) not in by_id]
@@ -174,14 +178,17 @@ class FusedTrainStep:
         return workspace(n, self.status.device)
 
     def forward_backward(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None,
-                         next_data=None):
+                         next_data=None, defer_dw1: bool = False):
         """bgcn_train_step only (no all-reduce, no optimiser step); returns the loss.
 
         ``next_data``: the batch the next call will train on.  Its weight-independent
         preparation (K1, ELL and CSC of X) then runs inside this call on the auxiliary
         lane, overlapped with this step's latency-bound chain; the next call finds it
         ready (matched by identity - do not mutate the batch in between).  Every call
-        still does exactly one preparation's worth of work."""
+        still does exactly one preparation's worth of work.
+
+        ``defer_dw1``: return before the conv1 weight gradients are written (every other
+        gradient and the status slot are final); ``finish_dw1()`` writes them."""
         m = self.model
         F = int(data.x.size(1))
         y = _need(data.y, torch.int64, "y")
@@ -207,6 +214,7 @@ class FusedTrainStep:
         a.feat_mode = mode
         a.prepared_ready = ready
         a.prepared, a.prepared_bytes = ptr(prep), prep.numel()
+        a.defer_dw1 = 1 if defer_dw1 else 0
         self._pending = None
         nxt = None
         if next_data is not None:
@@ -237,6 +245,7 @@ class FusedTrainStep:
         # the next call (or _join_side()) has ordered a stream behind it
         self._stream = stream_handle()   # the prepared buffers belong to this stream
         self._last = (ws, N, B, F)       # the saved activations of this step (saved_activations)
+        self._dw1_pending = (ws, prep, keep, y, img) if defer_dw1 else None
         self._pending = nxt              # held before the call: a failure below may leave
         try:                             # the preparation queued on the side lane
             check(L.bgcn_train_step(ctypes.addressof(a), ptr(ws), ws.numel(), self._stream))
@@ -247,11 +256,33 @@ class FusedTrainStep:
             raise
         return loss.view(())
 
+    def finish_dw1(self) -> None:
+        """The conv1 weight gradients of a step run with ``defer_dw1`` (bgcn_train_step_dw1:
+        same arguments and buffers, on the current stream)."""
+        pend = getattr(self, "_dw1_pending", None)
+        if pend is None:
+            raise RuntimeError("no step with a deferred dW1 is pending")
+        ws = pend[0]
+        self._dw1_pending = None
+        check(_lib.lib().bgcn_train_step_dw1(ctypes.addressof(self._args), ptr(ws), ws.numel(), stream_handle()))
+
     def __call__(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None,
                  next_data=None):
-        loss = self.forward_backward(data, seed, logp, next_data)
         world = self.bucket.world(self.group)
-        self.bucket.allreduce_sum_(self.group)
+        overlap = world > 1 and os.environ.get("BGCN_DP_OVERLAP", "1") != "0"
+        if overlap:
+            # the bucket in two all-reduces: everything but the conv1 weight gradients (and
+            # the status slot) while the tail computes dW1, then dW1 (SURVEY.md 8(e))
+            loss = self.forward_backward(data, seed, logp, next_data, defer_dw1=True)
+            work_a = self.bucket.allreduce_part_async("a", self.group)
+            self.finish_dw1()
+            work_b = self.bucket.allreduce_part_async("b", self.group)
+            for w in (work_a, work_b):
+                if w is not None:
+                    w.wait()
+        else:
+            loss = self.forward_backward(data, seed, logp, next_data)
+            self.bucket.allreduce_sum_(self.group)
         # an invalid step (status bits, any rank: the flag is summed by the all-reduce)
         # updates nothing; check_status() reports why
         self.opt.step(grads=self.bucket.views(), grad_scale=1.0 / world, skip_flag=self.bucket.flag,

@@ -47,7 +47,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 4
+#define BGCN_ABI_VERSION 5
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -365,6 +365,11 @@ typedef struct bgcn_step_args {
    * derives them into the buffer. */
   void* images; int32_t images_current;
   int32_t* status_seen;          /* [1] or NULL: OR of every step's status     */
+  /* defer_dw1 = 1: the call returns with every gradient written EXCEPT the two conv1
+   * weight gradients (grads[0], grads[4]), which bgcn_train_step_dw1 writes later - so a
+   * data-parallel caller can all-reduce the rest of the bucket while dW1 computes
+   * (overlap the conv1 dW with communication). */
+  int32_t defer_dw1;
 } bgcn_step_args;
 
 /* Bytes of a weight-image buffer for in_feats = F (W1^T [F][128], W2^T [2][F+64][64]
@@ -377,6 +382,11 @@ size_t bgcn_train_step_workspace_size(int64_t num_nodes, int64_t num_graphs, int
                                       int64_t bu_num_edges);
 int bgcn_train_step(const bgcn_step_args* args, void* workspace, size_t workspace_bytes,
                     bgcn_stream_t stream);
+/* The conv1 weight gradients of a step run with defer_dw1 = 1: the same args, workspace
+ * and prepared buffer, on the same stream, before either is reused.  The reference's
+ * conv1 dW (BiGCN_Twitter.py:187 loss.backward(), the GCNConv lin weight of :22/:73). */
+int bgcn_train_step_dw1(const bgcn_step_args* args, void* workspace, size_t workspace_bytes,
+                        bgcn_stream_t stream);
 /* The saved pre-activation conv outputs of the last step run in a step workspace (the
  * fused step's form of the per-stage dumps of explain_PHEME.py:91-162): h1 = conv1 output
  * H1 (pre-relu, also the detached x2), h2 = conv2 output H2 (pre-relu), each [N, 128]

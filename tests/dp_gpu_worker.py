@@ -48,7 +48,7 @@ def main():
     for it, b in enumerate(shard_batches(rank, 3, dev)):
         step(b)
         if it == 0:
-            res["grads0"] = (step.bucket.flat[:-1] / world).cpu().numpy()
+            res["grads0"] = (torch.cat([v.reshape(-1) for v in step.bucket.views()]) / world).cpu().numpy()
     # phase 2: training mode, dropout drawn per rank, DropEdge on the device, prefetch
     m.train()
     step2 = FusedTrainStep(m, step.opt, tddroprate=0.2, budroprate=0.2, drop_seed=77 + rank)

@@ -63,6 +63,18 @@ def _worker(rank, world, port, out):
     bucket = GradBucket(params)
     views = bucket.reduce_sum()
     res = {k: (v / world).clone() for k, v in zip(p, views)}
+    # the two-part order of the fused step (everything but the conv1 weights + the status
+    # slot first, then the conv1 weights) reduces to the same bits as one all-reduce
+    split = GradBucket(params, status_slot=True, late=[params[0], params[4]])
+    for v, prm in zip(split.views(), params):
+        v.copy_(prm.grad)
+    split.flag.fill_(float(rank))
+    works = [split.allreduce_part_async("a"), split.allreduce_part_async("b")]
+    for wk in works:
+        wk.wait()
+    for k, v, ref in zip(p, split.views(), views):
+        assert torch.equal(v, ref), k
+    assert float(split.flag) == float(sum(range(world)))
     # in-place mean for torch optimisers
     bucket.allreduce_mean()
     res_mean = {k: prm.grad.clone() for k, prm in zip(p, params)}

@@ -45,15 +45,15 @@ def _concat(batches):
     return out
 
 
-def test_two_ranks_on_the_hip_step(tmp_path):
-    world = 2
+def _run_ranks(out_dir, world, overlap):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
-                   LOCAL_RANK=str(r), WORLD_SIZE=str(world), BGCN_DIST_BACKEND="gloo")
+                   LOCAL_RANK=str(r), WORLD_SIZE=str(world), BGCN_DIST_BACKEND="gloo",
+                   BGCN_DP_OVERLAP=overlap)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_gpu_worker.py"),
-                                       str(tmp_path)], env=env))
+                                       str(out_dir)], env=env))
     try:
         for p in procs:
             assert p.wait(timeout=100) == 0
@@ -61,13 +61,26 @@ def test_two_ranks_on_the_hip_step(tmp_path):
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    r0 = np.load(tmp_path / "rank0.npz")
-    r1 = np.load(tmp_path / "rank1.npz")
+    return [np.load(out_dir / f"rank{r}.npz") for r in range(world)]
+
+
+def test_two_ranks_on_the_hip_step(tmp_path):
+    """Two ranks with the overlapped two-part all-reduce (the default at world > 1: the
+    bucket minus the conv1 weight gradients reduced while bgcn_train_step_dw1 computes
+    them) and with one all-reduce after the step (BGCN_DP_OVERLAP=0): the ranks stay
+    bitwise equal, and both schedules train to bitwise-identical parameters."""
+    world = 2
+    (tmp_path / "ov").mkdir()
+    (tmp_path / "one").mkdir()
+    r0, r1 = _run_ranks(tmp_path / "ov", world, "1")
+    s0, _ = _run_ranks(tmp_path / "one", world, "0")
     params = [k for k in r0.files if k.startswith("param:")]
     assert len(params) == 10
     for k in params:
         assert np.array_equal(r0[k], r1[k]), f"ranks diverged on {k}"
+        assert np.array_equal(r0[k], s0[k]), f"overlapped and single all-reduce differ on {k}"
     assert np.array_equal(r0["grads0"], r1["grads0"])
+    assert np.array_equal(r0["grads0"], s0["grads0"])
 
     # one process on the concatenation of both shards (loss mean over 2B trees = the
     # mean of the two ranks' means): same gradients
@@ -82,11 +95,10 @@ def test_two_ranks_on_the_hip_step(tmp_path):
     step.forward_backward(full)
     torch.cuda.synchronize()
     step.check_status()
-    g = step.bucket.flat[:-1].cpu().numpy()
     off = 0
     for v in step.bucket.views():
         n = v.numel()
-        a, b = r0["grads0"][off:off + n], g[off:off + n]
+        a, b = r0["grads0"][off:off + n], v.reshape(-1).cpu().numpy()
         scale = float(np.abs(b).max())
         assert float(np.abs(a - b).max()) <= 1e-5 * max(scale, 1e-12), (tuple(v.shape), scale)
-        off += (n + 3) // 4 * 4     # views start on 16-byte boundaries (GradBucket)
+        off += n                    # grads0: the views concatenated in parameter order

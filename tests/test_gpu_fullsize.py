@@ -83,13 +83,16 @@ def _oracle_batch(b, drops, drop_seed):
     return ref
 
 
-@pytest.mark.parametrize("workload", ["twitter15", "weibo_bf16", "synth1024_bf16", "twitter15_tail"])
-def test_full_size_step_matches_oracle(workload):
+@pytest.mark.parametrize("workload,mode", [("twitter15", "auto"), ("weibo_bf16", "auto"),
+                                           ("synth1024_bf16", "auto"), ("twitter15_tail", "auto"),
+                                           ("weibo_bf16", "dense")])
+def test_full_size_step_matches_oracle(workload, mode):
     """BASELINE configs[1] (twitter15: 128 trees x mean 256, fp32, DropEdge 0.2/0.2),
     configs[2] (weibo_bf16: 128 x mean 816, bf16 X, 2-class Net, no DropEdge) and the
     per-GPU shape of configs[4] (synth1024_bf16: 128 x mean 1024, bf16 X, DropEdge), and
     twitter15 with 1 % of the rows holding 40-300 words (the spill pool): loss, log-probs
-    and all ten gradients of the bench's step against the fp64 oracle."""
+    and all ten gradients of the bench's step against the fp64 oracle.  weibo_bf16 also
+    on the dense MFMA path (feat_mode "dense": conv1 / dW1 on the bf16 MFMA)."""
     from bigcn_amd import FusedTrainStep
     from bigcn_amd.ops import keep_words, unpack_keep
     wl = bench.WORKLOADS[workload]
@@ -97,7 +100,7 @@ def test_full_size_step_matches_oracle(workload):
     pool = bench.make_pool(wl, 0, 2, DEV, drop=(0.0, 0.0))    # undropped: DropEdge on the device
     C, F = wl["classes"], wl["feats"]
     p = O.make_params(F, 64, 64, C, seed=31)
-    m = _model(p, "auto", classes=C)
+    m = _model(p, mode, classes=C)
     m.train()
     step = FusedTrainStep(m, tddroprate=drops[0], budroprate=drops[1], drop_seed=4242)
     b = pool[1]
@@ -137,7 +140,7 @@ def test_full_size_step_matches_oracle(workload):
             ties[f"{d}.{name}"] = int(flip.sum())
             assert bool((r[flip].abs() <= 1e-5 * r.abs().max()).all()), \
                 f"{d}.{name}: a relu' decision differs from the fp64 sign away from zero"
-    print(f"\n{workload} N={N}: (max-scaled, elementwise) error vs the fp64 oracle; relu' ties {ties}")
+    print(f"\n{workload} ({mode}) N={N}: (max-scaled, elementwise) error vs the fp64 oracle; relu' ties {ties}")
     for k, (e1, e2) in table.items():
         print(f"  {k:32s} {e1:.2e} {e2:.2e}")
     bad = {k: v for k, v in table.items() if v[0] > TOL or v[1] > TOL}

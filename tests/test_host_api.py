@@ -42,14 +42,25 @@ def test_fused_step_takes_the_models_degree_convention():
 
 
 def test_fused_step_bucket_carries_the_status_slot():
+    """Layout [early gradients | status slot | conv1 weight gradients]: part a (flat_a)
+    holds every gradient the deferred-dW1 step finishes first and the status slot, part b
+    (flat_b) exactly the two conv1 weight gradients."""
     from bigcn_amd import FusedTrainStep
     m = BiGCN(16, 64, 64)
     st = FusedTrainStep(m)
+    b = st.bucket
     n = sum(p.numel() for p in m.parameters())
-    assert st.bucket.flat.numel() == n + 1
-    assert st.bucket.flag.numel() == 1
-    assert st.bucket.flag.data_ptr() == st.bucket.flat.data_ptr() + 4 * n
-    assert sum(v.numel() for v in st.bucket.views()) == n
+    assert b.flag.numel() == 1
+    assert b.flat_a.numel() + b.flat_b.numel() == b.flat.numel()
+    assert b.flat_a.data_ptr() <= b.flag.data_ptr() < b.flat_a.data_ptr() + 4 * b.flat_a.numel()
+    enc = list(m.encoder_params())
+    late = {id(enc[0]), id(enc[4])}
+    lo, hi = b.flat_b.data_ptr(), b.flat_b.data_ptr() + 4 * b.flat_b.numel()
+    for p, v in zip(b.params, b.views()):
+        inside = lo <= v.data_ptr() < hi
+        assert inside == (id(p) in late), tuple(p.shape)
+    assert b.flat_b.numel() == enc[0].numel() + enc[4].numel()
+    assert sum(v.numel() for v in b.views()) == n
 
 
 def test_bucket_views_are_16_byte_aligned():
@@ -61,9 +72,8 @@ def test_bucket_views_are_16_byte_aligned():
     st = FusedTrainStep(m)
     b = st.bucket
     assert all(v.data_ptr() % 16 == 0 for v in b.views())
-    assert b.flag.data_ptr() == b.flat.data_ptr() + 4 * (b.flat.numel() - 1)
     for p in b.params:
         p.grad = torch.full_like(p, 2.0)
     views = b.reduce_sum()
     assert all(bool((v == 2.0).all()) for v in views)
-    assert float(b.flat[:-1].sum()) == 2.0 * sum(p.numel() for p in b.params)
+    assert float(b.flat.sum()) - float(b.flag.sum()) == 2.0 * sum(p.numel() for p in b.params)
