@@ -656,9 +656,11 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
 
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
   float* hs = &Hs[wv * 32 * kC2Ld];   // this wave's staged 32 x 64 H1 tile
-  for (int t = wv; t < kChunk / 32; t += 4) {
+  // the main product of tile t (32 nodes of the item): H1 tile staged through LDS, the
+  // dropout-masked relu(H1) and the root keep bits generated in registers, six-product
+  // bf16 MFMAs; the root keep masks go to S.rbits
+  auto tile = [&](int t, f32x16& acc0, f32x16& acc1) {
     const int64_t i0 = beg + 32 * t;
-    if (i0 >= end) break;
     const int64_t i = i0 + r32;
     const bool ok = i < end;
     {   // coalesced staging: 8 x 1 KiB per wave instead of 32 scattered rows per load
@@ -692,7 +694,8 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
       }
       m |= bit << (2 * j + h);
     }
-    f32x16 acc0 = {}, acc1 = {};
+    acc0 = f32x16{};
+    acc1 = f32x16{};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {   // H1 columns 32h + 8s + j
       bf16x8 ah, am, al;
@@ -737,6 +740,9 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
     m |= __shfl_xor(m, 32);
     if (h == 0 && ok) S.rbits[int64_t(d) * S.N + i] = m;
     if (t == wv) BT_MARK(2, 2);
+  };
+  auto store = [&](int t, const f32x16& acc0, const f32x16& acc1) {
+    const int64_t i0 = beg + 32 * t;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int64_t ii = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -745,15 +751,27 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
         Z2[ii * (2 * H) + d * H + 32 + r32] = acc1[q];
       }
     }
-  }
-  if (rn_all > kCap) {
+  };
+  static_assert(kChunk / 32 == 8, "two tiles per wave");
+  if (rn_all <= kCap) {
+    for (int t = wv; t < kChunk / 32; t += 4) {
+      if (beg + 32 * t >= end) break;
+      f32x16 acc0, acc1;
+      tile(t, acc0, acc1);
+      store(t, acc0, acc1);
+    }
+  } else {
     // The root's spilled non-zeros (a root row of more than kCap words, rare): further
     // [nodes x 32] x [32 x 64] products of the same form as the root slots - A the exact
     // 0/1 keep bits, B = 2 relu(x_root,c) W2_d^T[64 + c] split three ways - 32 pool entries
-    // per round, added to the Z2 rows this thread stored above (same thread, same rows).
-    // Software-pipelined: the pool entries are loaded two rounds ahead and the W2^T rows
-    // they select one round ahead, so a round's dependent loads hide behind the previous
-    // round's tiles (under the pass over X a dependent load costs several us).
+    // per round, accumulated into the wave's two tiles held in registers (no Z2 round
+    // trips), then stored.  Software-pipelined: the pool entries are loaded two rounds
+    // ahead and the W2^T rows they select one round ahead, so a round's dependent loads
+    // hide behind the previous round's products.
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (beg + 32 * (wv + 4 * j) < end) tile(wv + 4 * j, acc[j][0], acc[j][1]);
     const int64_t off = S.ovf_off[r];
     const int nsp = rn_all - kCap;
     const int sq0 = threadIdx.x >> 4, sq1 = (threadIdx.x + 256) >> 4, qq = (threadIdx.x & 15) * 4;
@@ -784,54 +802,48 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
         }
       }
       __syncthreads();
-      // the next rounds' loads, in flight during this round's tiles
+      // the next rounds' loads, in flight during this round's products
       e0 = n0; e1 = n1; rkc = rkn;
       n0 = ent_at(c0 + 2 * kCap, sq0); n1 = ent_at(c0 + 2 * kCap, sq1); rkn = ent_at(c0 + 2 * kCap, tk);
       w0 = w_of(e0); w1 = w_of(e1);
       const int mc = (cn + 1) / 2;
-      for (int t = wv; t < kChunk / 32; t += 4) {
-        const int64_t i0 = beg + 32 * t;
-        if (i0 >= end) break;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t i0 = beg + 32 * (wv + 4 * j);
+        if (i0 >= end) continue;
         const int64_t i = i0 + r32;
         const uint32_t ni = uint32_t(i < end ? i : beg);
         uint32_t m = 0;
 #pragma unroll
-        for (int j = 0; j < kCap / 2; ++j) {
-          const int sl = 2 * j + h;
-          if (j < mc && sl < cn) {
+        for (int jj = 0; jj < kCap / 2; ++jj) {
+          const int sl = 2 * jj + h;
+          if (jj < mc && sl < cn) {
             const uint32_t k = rk[sl];
             m |= ((keep.get(uint32_t(d), ni, k >> 5) >> (k & 31)) & 1u) << sl;
           }
         }
-        f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
           if (8 * tt < mc) {
             bf16x8 ar;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ar[j] = __bf16(((m >> (2 * (8 * tt + j) + h)) & 1u) ? 1.f : 0.f);
+            for (int jj = 0; jj < 8; ++jj) ar[jj] = __bf16(((m >> (2 * (8 * tt + jj) + h)) & 1u) ? 1.f : 0.f);
             const int k = H + (kCap / 2) * h + 8 * tt;
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
               const int o = (32 * half + r32) * kC2Ld16 + k;
-              f32x16 c = half == 0 ? acc0 : acc1;
+              f32x16 c = acc[j][half];
               c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[2][o]), c);
               c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[1][o]), c);
-              c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[0][o]), c);
-              if (half == 0) acc0 = c; else acc1 = c;
+              acc[j][half] = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[0][o]), c);
             }
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int64_t ii = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-          if (ii < end) {
-            Z2[ii * (2 * H) + d * H + r32] += acc0[q];
-            Z2[ii * (2 * H) + d * H + 32 + r32] += acc1[q];
           }
         }
       }
     }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (beg + 32 * (wv + 4 * j) < end) store(wv + 4 * j, acc[j][0], acc[j][1]);
   }
   BT_END(2);
 }
@@ -1183,16 +1195,78 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
     col[k] = (i < S.N && s < nn[k]) ? col[k] : -1;
     smask |= (i < S.N && nn[k] > kCap) ? (1u << (k / 4)) : 0u;
   }
-  // the batches holding long rows place their spilled entries too (rare: those batches
-  // take the two-phase counter advance below)
-  {
-    __shared__ uint32_t smask_s;
-    if (threadIdx.x == 0) smask_s = 0u;
+  // The block's long rows (rare): their spilled entries are indexed once for the whole
+  // block - rpre[t] = the block's spilled entries before row t (a block-wide scan), rslot /
+  // roff per row - and staged in LDS (up to kPlaceStage of them; beyond, read from the pool
+  // in place), so a batch's passes over them need no dependent global loads.
+  constexpr int kPlaceStage = 1024;
+  __shared__ int rpre[kRowBlock + 1], roff[kRowBlock], wsum[kRowBlock / 64];
+  __shared__ uint32_t rslot[kRowBlock];
+  __shared__ uint2 sbuf[kPlaceStage];
+  __shared__ uint32_t smask_s;
+  if (threadIdx.x == 0) smask_s = 0u;
+  __syncthreads();
+  if (smask) atomicOr(&smask_s, smask);
+  __syncthreads();
+  smask = smask_s;
+  bool staged = true;
+  if (smask) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t i = r0 + t;
+    const int na = i < S.N ? S.nnz[i] : 0;
+    const int nsp = na > kCap ? na - kCap : 0;
+    const int o = nsp ? S.ovf_off[i] : 0;
+    const uint32_t sl = nsp ? (uint32_t(i * kCap) | kCscSpillFlag | (S.root_map[i] == int32_t(i) ? kCscRootFlag : 0u))
+                            : 0u;
+    int x = nsp;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
     __syncthreads();
-    if (smask) atomicOr(&smask_s, smask);
+    int base = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kRowBlock / 64; ++w) {
+      base += w < wv ? wsum[w] : 0;
+      total += wsum[w];
+    }
+    rpre[t] = base + x - nsp;
+    roff[t] = o;
+    rslot[t] = sl;
+    if (t == 0) rpre[kRowBlock] = total;
+    staged = total <= kPlaceStage;
     __syncthreads();
-    smask = smask_s;
+    if (staged) {
+      for (int e0 = t; e0 < total; e0 += 4 * kRowBlock) {   // four pool loads in flight
+        uint2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = min(e0 + u * kRowBlock, total - 1);
+          const int r = spill_row_of(rpre, kRowBlock, e);
+          v[u] = S.ovf[roff[r] + (e - rpre[r])];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (e0 + u * kRowBlock < total) sbuf[e0 + u * kRowBlock] = v[u];
+      }
+    }
+    __syncthreads();
   }
+  // f(row within the batch, entry, block row) for every spilled entry of batch bt
+  auto batch_spill = [&](int bt, auto f) {
+    const int lo0 = bt * 32, e1 = rpre[lo0 + 32];
+    for (int e = rpre[lo0] + int(threadIdx.x); e < e1; e += int(blockDim.x)) {
+      int lo = lo0, hi = lo0 + 31;   // the last row with rpre <= e
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (rpre[mid] <= e) lo = mid; else hi = mid - 1;
+      }
+      const uint2 v = staged ? sbuf[e] : S.ovf[roff[lo] + (e - rpre[lo])];
+      f(lo - lo0, v, lo);
+    }
+  };
   // rows of the block in order, 32 rows (= 1024 slots, 4 per thread) per batch.  The
   // columns of one row are distinct, so an entry's rank among the batch's entries of
   // its column = the number of earlier batch rows holding that column: an OR of row
@@ -1210,38 +1284,7 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
     }
     // spilled entries of the batch's rows (their columns are distinct from the row's ELL
     // columns, so the same row-bit ranks hold), flattened over the block's threads
-    __shared__ int bpre[kBatchRows + 1], boff[kBatchRows];
-    __shared__ uint32_t bslot[kBatchRows];
-    if (spill) {
-      if (threadIdx.x < 64) {   // wave 0, lane t < 32: batch row t
-        const int t = threadIdx.x;
-        int nsp = 0, o = 0;
-        uint32_t sl = 0u;
-        const int64_t i = r0 + bt * kBatchRows + t;
-        if (t < kBatchRows && i < S.N) {
-          const int na = S.nnz[i];
-          if (na > kCap) {
-            nsp = na - kCap;
-            o = S.ovf_off[i];
-            sl = uint32_t(i * kCap) | kCscSpillFlag | (S.root_map[i] == int32_t(i) ? kCscRootFlag : 0u);
-          }
-        }
-        int x = nsp;
-#pragma unroll
-        for (int d = 1; d < kBatchRows; d <<= 1) {
-          const int y = __shfl_up(x, d, 64);
-          if (t >= d) x += y;
-        }
-        if (t < kBatchRows) {
-          bpre[t] = x - nsp;
-          boff[t] = o;
-          bslot[t] = sl;
-        }
-        if (t == kBatchRows - 1) bpre[kBatchRows] = x;
-      }
-      __syncthreads();
-      for_spill(S, bpre, boff, kBatchRows, [&](int r, uint2 v) { atomicOr(&rows[v.x], 1u << r); });
-    }
+    if (spill) batch_spill(bt, [&](int r, uint2 v, int) { atomicOr(&rows[v.x], 1u << r); });
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1256,8 +1299,8 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
       }
     }
     if (spill)
-      for_spill(S, bpre, boff, kBatchRows, [&](int r, uint2 v) {
-        S.csc[cnt[v.x] + __popc(rows[v.x] & ((1u << r) - 1u))] = make_uint2(bslot[r], v.y);
+      batch_spill(bt, [&](int r, uint2 v, int br) {
+        S.csc[cnt[v.x] + __popc(rows[v.x] & ((1u << r) - 1u))] = make_uint2(rslot[br], v.y);
       });
     __syncthreads();
     if (!spill) {
@@ -1273,14 +1316,14 @@ __device__ inline void csc_place_body(const SparseState& S, int bid, int32_t* ps
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (rank[k] == 0) cnt[col[4 * bt + k]] += __popc(rows[col[4 * bt + k]]);
-      for_spill(S, bpre, boff, kBatchRows, [&](int r, uint2 v) {
+      batch_spill(bt, [&](int r, uint2 v, int) {
         if ((rows[v.x] & ((1u << r) - 1u)) == 0u) cnt[v.x] += __popc(rows[v.x]);
       });
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (rank[k] >= 0) rows[col[4 * bt + k]] = 0u;
-      for_spill(S, bpre, boff, kBatchRows, [&](int, uint2 v) { rows[v.x] = 0u; });
+      batch_spill(bt, [&](int, uint2 v, int) { rows[v.x] = 0u; });
     }
     __syncthreads();
   }
