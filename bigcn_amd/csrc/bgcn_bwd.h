@@ -204,6 +204,9 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
 #ifndef BGCN_DH1_X6
 #define BGCN_DH1_X6 1   // 0: the three-product form (A/B only: not fp32-grade)
 #endif
+#ifndef BGCN_DH1_PREFETCH
+#define BGCN_DH1_PREFETCH 1   // 0: the next tile's loads issued after the tile (A/B)
+#endif
 constexpr int kDh1Rows = 64;
 constexpr int kDsLd = H + 8;   // bf16 row stride of the staged, split tiles
 constexpr int kDh1Smem = (6 * kDh1Rows * kDsLd) / 2 + 2 * H;
@@ -322,6 +325,11 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
       if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // four keep hashes in flight
     }
     __syncthreads();
+#if BGCN_DH1_PREFETCH
+    // the next tile's dZ2 rows and H1 values are in flight during this tile's products
+    // (dv / hv are consumed above: staged in LDS, folded into km and a2)
+    if (t + 1 < ntile) gload(blk0 + kDh1Rows);
+#endif
     // dH1: A = dZ2 rows (row rh*32 + r, o = 16s + 8h + j), B = W2^T (column c)
     f32x16 acc = {};
     const __bf16* ah = &Dh[(rh * 32 + r) * kDsLd + 8 * h];
@@ -373,7 +381,9 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
       }
     }
     __syncthreads();   // the staged tile is rewritten by the next tile
+#if !BGCN_DH1_PREFETCH
     if (t + 1 < ntile) gload(blk0 + kDh1Rows);
+#endif
   }
   cs += __shfl_xor(cs, 32);
   if (h == 0) red[rh][c] = cs;
