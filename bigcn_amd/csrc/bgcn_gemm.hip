@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ G, in
 // Lane map of 32x32x16: lane (h = l >> 5, r = l & 31) supplies A[r][8h + j] and
 // B[8h + j][r] (j < 8); D register q is D[(q & 3) + 8 (q >> 2) + 4h][r].
 // ============================================================================
-constexpr int kB16BK = 32, kB16LD = kB16BK + 8;
+constexpr int kB16BK = 32, kB16LD = kB16BK + 8;   // (64-wide k-tiles measured slower: 0.67 / 0.87 ms)
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
 // Y[M, Nc] = X[M, K] (bf16) . W[Nc, K]^T (fp32; rows [0, split) from W0, the rest W1).
@@ -291,60 +291,66 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_bf16(const bf16_t* __restrict_
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
   const int64_t m0 = int64_t(blockIdx.x) * BM, n0 = int64_t(blockIdx.y) * BN;
-  // staging: X rows tid / 4 + 64 i, 8 k at (tid % 4) * 8; W rows tid / 8 + 32 i, 4 k at (tid % 8) * 4
-  const int xr = tid >> 2, xk = (tid & 3) * 8;
-  const int wrow = tid >> 3, wk = (tid & 7) * 4;
-  const bf16_t* xp[2];
-  bool xok[2];
+  // staging: X rows tid / 4 + 64 i, 8 k at (tid % 4) * 8; W row tid % 128, 16 k at (tid / 128) * 16
+  // (each lane writes its row's 32 contiguous bytes per plane: two 16-byte LDS stores on
+  // consecutive rows across lanes, conflict-free; one 2-byte store per element per plane
+  // kept the waves parked at the barriers)
+  constexpr int kXR = BM * kB16BK / 8 / 256;   // 16-byte X pieces per thread
+  constexpr int kWK = kB16BK / 2;               // W elements per thread (one row, kWK consecutive k)
+  const int xr = tid / (kB16BK / 8), xk = (tid % (kB16BK / 8)) * 8;
+  const int wrow = tid & 127, wk = (tid >> 7) * kWK;
+  const bf16_t* xp[kXR];
+  bool xok[kXR];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int64_t m = m0 + xr + 64 * i;
+  for (int i = 0; i < kXR; ++i) {
+    const int64_t m = m0 + xr + (256 / (kB16BK / 8)) * i;
     xok[i] = m < M;
     xp[i] = X + (xok[i] ? m : 0) * ldx;
   }
-  const float* wp[4];
-  bool wok[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t n = n0 + wrow + 32 * i;
-    wok[i] = n < Nc;
-    const int64_t nn = wok[i] ? n : 0;
-    wp[i] = nn < split ? W0 + nn * ldw : W1 + (nn - split) * ldw;
-  }
-  u32x4v ra[2];
-  float4 rb[4];
+  const int64_t wn = n0 + wrow;
+  const bool wok = wn < Nc;
+  const float* wp = (wok ? wn : 0) < split ? W0 + (wok ? wn : 0) * ldw : W1 + ((wok ? wn : 0) - split) * ldw;
+  u32x4v ra[kXR];
+  float4 rb[kWK / 4];
   auto gload = [&](int64_t k0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kXR; ++i) {
       const int64_t k = k0 + xk;
       const bool ok = xok[i] && k < K;
       const u32x4v v = *reinterpret_cast<const u32x4v*>(xp[i] + (ok ? k : 0));
       ra[i] = ok ? v : u32x4v{0u, 0u, 0u, 0u};
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t k = k0 + wk;
-      const bool ok = wok[i] && k < K;
-      const float4 v = ld4(wp[i] + (ok ? k : 0));
+    for (int i = 0; i < kWK / 4; ++i) {
+      const int64_t k = k0 + wk + 4 * i;
+      const bool ok = wok && k < K;
+      const float4 v = ld4(wp + (ok ? k : 0));
       rb[i] = ok ? v : f4zero();
     }
   };
   auto sstore = [&]() {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4v*>(&As[(xr + 64 * i) * kB16LD + xk]) = ra[i];
+    for (int i = 0; i < kXR; ++i)
+      *reinterpret_cast<u32x4v*>(&As[(xr + (256 / (kB16BK / 8)) * i) * kB16LD + xk]) = ra[i];
+    bf16x8 hv[kWK / 8], mv[kWK / 8], lv[kWK / 8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kWK / 4; ++i) {
       const float v[4] = {rb[i].x, rb[i].y, rb[i].z, rb[i].w};
-      __bf16 hi[4], mi[4], lo[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) split3_bf16(v[e], hi[e], mi[e], lo[e]);
-      const int o = (wrow + 32 * i) * kB16LD + wk;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        Bs[0][o + e] = hi[e];
-        Bs[1][o + e] = mi[e];
-        Bs[2][o + e] = lo[e];
+        __bf16 x, y, z;
+        split3_bf16(v[e], x, y, z);
+        hv[i >> 1][(i & 1) * 4 + e] = x;
+        mv[i >> 1][(i & 1) * 4 + e] = y;
+        lv[i >> 1][(i & 1) * 4 + e] = z;
       }
+    }
+    const int o = wrow * kB16LD + wk;
+#pragma unroll
+    for (int j = 0; j < kWK / 8; ++j) {
+      *reinterpret_cast<bf16x8*>(&Bs[0][o + 8 * j]) = hv[j];
+      *reinterpret_cast<bf16x8*>(&Bs[1][o + 8 * j]) = mv[j];
+      *reinterpret_cast<bf16x8*>(&Bs[2][o + 8 * j]) = lv[j];
     }
   };
   f32x16 acc[2][2] = {};
@@ -415,55 +421,50 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(const float* __restrict__ 
   const int64_t kb = int64_t(blockIdx.z) * kchunk;
   const int64_t ke = min<int64_t>(kb + kchunk, K);
   float* out = part + int64_t(blockIdx.z) * Mc * Nc;
-  // staging: G nodes 2p, 2p + 1 (+16) of m quad 4q (q = tid % 32, p = tid / 32);
-  //          X nodes 2p, 2p + 1 of n octet 8o (o = tid % 16, p = tid / 16)
-  const int gq = (tid & 31) * 4, gp = (tid >> 5) * 2;
-  const int xo = (tid & 15) * 8, xp2 = (tid >> 4) * 2;
-  float4 rg[4];
-  u32x4v rx[2];
+  // staging, transposed into k-contiguous LDS rows: thread t takes column m = t % 128 of G
+  // and column n = t % 128 of X over the 16 nodes (t / 128) * 16 ..: lanes load consecutive
+  // columns (coalesced: 256 / 128 B per wave instruction) and each writes its row's 32
+  // contiguous bytes per plane as two 16-byte LDS stores on consecutive rows across lanes,
+  // conflict-free (two nodes per 4-byte store with lanes 8 rows apart hit 2 of 64 banks:
+  // 88 % of the LDS cycles were conflicts, profiles/r03_dense_bf16_pmc.txt)
+  constexpr int kNK = kB16BK / 2;   // nodes per thread
+  const int sc_ = tid & 127, sk = (tid >> 7) * kNK;
+  float rg[kNK];
+  uint32_t rx[kNK];
   auto gload = [&](int64_t k0) {
+    const int64_t m = m0 + sc_, n = n0 + sc_;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t k = k0 + gp + (i & 1) + 16 * (i >> 1);
-      const int64_t m = m0 + gq;
-      const bool ok = k < ke && m < Mc;
-      const float4 v = ld4(G + (ok ? k : 0) * ldg + (ok ? m : 0));
-      rg[i] = ok ? v : f4zero();
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t k = k0 + xp2 + i;
-      const int64_t n = n0 + xo;
-      const bool ok = k < ke && n < Nc;
-      const u32x4v v = *reinterpret_cast<const u32x4v*>(X + (ok ? k : 0) * ldx + (ok ? n : 0));
-      rx[i] = ok ? v : u32x4v{0u, 0u, 0u, 0u};
+    for (int u = 0; u < kNK; ++u) {
+      const int64_t k = k0 + sk + u;
+      const bool okg = k < ke && m < Mc, okx = k < ke && n < Nc;
+      const float g = G[(okg ? k : 0) * ldg + (okg ? m : 0)];
+      const uint32_t x = X[(okx ? k : 0) * ldx + (okx ? n : 0)];
+      rg[u] = okg ? g : 0.f;
+      rx[u] = okx ? x : 0u;
     }
   };
   auto sstore = [&]() {
+    bf16x8 hv[kNK / 8], mv[kNK / 8], lv[kNK / 8];
 #pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {   // node pairs (gp, gp + 1) and (gp + 16, gp + 17)
-      const float4 u = rg[2 * pr], v = rg[2 * pr + 1];
-      const float a0[4] = {u.x, u.y, u.z, u.w}, a1[4] = {v.x, v.y, v.z, v.w};
-      const int kk = gp + 16 * pr;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        __bf16 h0, m0_, l0, h1, m1, l1;
-        split3_bf16(a0[e], h0, m0_, l0);
-        split3_bf16(a1[e], h1, m1, l1);
-        const int o = (gq + e) * kB16LD + kk;
-        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<bf16x2*>(&As[0][o]) = bf16x2{h0, h1};
-        *reinterpret_cast<bf16x2*>(&As[1][o]) = bf16x2{m0_, m1};
-        *reinterpret_cast<bf16x2*>(&As[2][o]) = bf16x2{l0, l1};
-      }
+    for (int u = 0; u < kNK; ++u) {
+      __bf16 x, y, z;
+      split3_bf16(rg[u], x, y, z);
+      hv[u >> 3][u & 7] = x;
+      mv[u >> 3][u & 7] = y;
+      lv[u >> 3][u & 7] = z;
     }
-    const uint32_t w0[4] = {rx[0].x, rx[0].y, rx[0].z, rx[0].w};
-    const uint32_t w1[4] = {rx[1].x, rx[1].y, rx[1].z, rx[1].w};
+    const int o = sc_ * kB16LD + sk;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {   // n = xo + e: (X[2p][n], X[2p + 1][n]) as one 4-byte word
-      const uint32_t lo = (e & 1) ? (w0[e >> 1] >> 16) : (w0[e >> 1] & 0xffffu);
-      const uint32_t hi = (e & 1) ? (w1[e >> 1] & 0xffff0000u) : (w1[e >> 1] << 16);
-      *reinterpret_cast<uint32_t*>(&Bs[(xo + e) * kB16LD + xp2]) = lo | hi;
+    for (int j = 0; j < kNK / 8; ++j) {
+      *reinterpret_cast<bf16x8*>(&As[0][o + 8 * j]) = hv[j];
+      *reinterpret_cast<bf16x8*>(&As[1][o + 8 * j]) = mv[j];
+      *reinterpret_cast<bf16x8*>(&As[2][o + 8 * j]) = lv[j];
+      u32x4v w;
+      w.x = rx[8 * j + 0] | (rx[8 * j + 1] << 16);
+      w.y = rx[8 * j + 2] | (rx[8 * j + 3] << 16);
+      w.z = rx[8 * j + 4] | (rx[8 * j + 5] << 16);
+      w.w = rx[8 * j + 6] | (rx[8 * j + 7] << 16);
+      *reinterpret_cast<u32x4v*>(&Bs[o + 8 * j]) = w;
     }
   };
   f32x16 acc[2][2] = {};
