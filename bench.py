@@ -426,6 +426,7 @@ def main():
             loss = step(warmup + i)
             if rank == 0 and (i + 1) % max(1, steps // 4) == 0:
                 log(f"[{mode}] step {i + 1}/{steps}")
+        t_host = time.perf_counter() - t0               # host enqueue time of the K steps
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -481,7 +482,7 @@ def main():
         v = torch.tensor([report["status"], report["invalid_steps"]], dtype=torch.int64, device=dev)
         if world > 1:
             dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        return {"value": value, "dt": dt, "N_avg": N_avg, "roof": roof, "kernels": kernels,
+        return {"value": value, "dt": dt, "t_host": t_host, "N_avg": N_avg, "roof": roof, "kernels": kernels,
                 "loss": float(loss.item()), "status": int(v[0]), "invalid_steps": int(v[1])}
 
     main_res = run(args.feat_mode, args.steps, args.warmup)
@@ -523,6 +524,7 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "trees/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "host_enqueue_ms_per_step": round(main_res["t_host"] / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16 x, f32 accumulate" if wl.get("xdtype") == "bf16" else "f32",
             "data": "synthetic (reference npz/Batch layout; real Twitter15 trees absent)",

@@ -125,7 +125,7 @@ def scatter_mean(src: torch.Tensor, index: torch.Tensor, dim: int = 0,
 def root_extend(src: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor) -> torch.Tensor:
     """The Python loop of ``BiGCN_Twitter.py:46-50`` / ``:59-63``, kept as a loop."""
     out = torch.zeros(len(batch), src.size(1), dtype=src.dtype)
-    batch_size = int(max(batch)) + 1
+    batch_size = int(batch.max()) + 1                # the reference's max(batch)
     for b in range(batch_size):
         index = torch.eq(batch, b)
         out[index] = src[rootindex[b]]
@@ -189,20 +189,25 @@ def direction_forward(p: Dict[str, torch.Tensor], prefix: str, x: torch.Tensor,
     x1 = copy.copy(x.float())                                            # :28
     h = gcn_conv(x, edge_index, w1, b1, degree_on=degree_on)             # :42
     x2 = copy.copy(h)                                                    # :44  detached leaf
-    h = torch.cat((h, root_extend(x1, batch, rootindex)), 1)             # :46-51
-    if m1 is None:
-        h = F.relu(h)                                                    # :53
-    else:   # the same relu, its decision on conv1's columns injected
-        hid = m1.size(1)
-        h = torch.cat((_relu(h[:, :hid], m1), F.relu(h[:, hid:])), 1)
+    # :46-54 - cat((h, root_extend(x1))), relu, dropout - evaluated per column block:
+    # relu and the dropout are elementwise, so applying them to conv1's columns and to
+    # the root-extend columns apart is the same tensor.  The root-extend block is a
+    # constant (no parameter reaches it), so autograd's buffers stay 64 wide instead of
+    # hid + F wide (the full-size parity tests run this at N > 100k, F = 5000).
+    hid = h.size(1)
+    root = F.relu(root_extend(x1, batch, rootindex).to(h.dtype))        # :46-51, :53
+    h = F.relu(h) if m1 is None else _relu(h, m1)                        # :53 (decision injectable)
     if training:                                                         # :54
         if keep_mask is None:
-            h = F.dropout(h, training=True)
+            h = F.dropout(torch.cat((h, root), 1), training=True)
         else:
-            h = h * keep_mask.to(h.dtype) * 2.0
+            h = torch.cat((h * keep_mask[:, :hid] * 2.0, root.mul_(keep_mask[:, hid:]).mul_(2.0)), 1)
+    else:
+        h = torch.cat((h, root), 1)
+    del root
     if stages is not None:
         stages[f"{prefix}.h1"] = x2.detach().clone()
-        stages[f"{prefix}.a2"] = h.detach().clone()
+        stages[f"{prefix}.a2"] = h.detach()
     h = gcn_conv(h, edge_index, w2, b2, degree_on=degree_on)             # :56
     if stages is not None:
         stages[f"{prefix}.h2"] = h.detach().clone()

@@ -37,6 +37,7 @@ from test_gpu_train import KEYS, _model
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
+_ORACLE_CACHE = {}   # (workload, drop seed) -> (relu masks, oracle result) of the last run
 
 
 def errors(a, b):
@@ -84,8 +85,8 @@ def _oracle_batch(b, drops, drop_seed):
 
 
 @pytest.mark.parametrize("workload,mode", [("twitter15", "auto"), ("weibo_bf16", "auto"),
-                                           ("synth1024_bf16", "auto"), ("twitter15_tail", "auto"),
-                                           ("weibo_bf16", "dense")])
+                                           ("weibo_bf16", "dense"), ("synth1024_bf16", "auto"),
+                                           ("twitter15_tail", "auto")])
 def test_full_size_step_matches_oracle(workload, mode):
     """BASELINE configs[1] (twitter15: 128 trees x mean 256, fp32, DropEdge 0.2/0.2),
     configs[2] (weibo_bf16: 128 x mean 816, bf16 X, 2-class Net, no DropEdge) and the
@@ -125,7 +126,16 @@ def test_full_size_step_matches_oracle(workload, mode):
     h1, h2 = h1.cpu(), h2.cpu()
     masks = {d: (h1[:, 64 * k:64 * (k + 1)] > 0, h2[:, 64 * k:64 * (k + 1)] > 0)
              for k, d in enumerate(("TDrumorGCN", "BUrumorGCN"))}
-    rlogp, rloss, rgrads, st = _oracle(ref, p, True, mk[0], mk[1], relu_masks=masks)
+    # weibo_bf16 runs twice (sparse, dense) on the same batch, seeds and parameters: the
+    # fp64 oracle (the bulk of this test's time) is reused when the relu' decisions agree
+    key = (workload, step.last_drop_seed)
+    hit = _ORACLE_CACHE.get(key)
+    if hit is not None and all(torch.equal(a, b) for d in masks for a, b in zip(masks[d], hit[0][d])):
+        rlogp, rloss, rgrads, st = hit[1]
+    else:
+        rlogp, rloss, rgrads, st = _oracle(ref, p, True, mk[0], mk[1], relu_masks=masks)
+        _ORACLE_CACHE.clear()
+        _ORACLE_CACHE[key] = (masks, (rlogp, rloss, rgrads, st))
     del mk
     table = {k: errors(g, rgrads[k]) for k, g in zip(KEYS, grads)}
     table["logp"] = errors(logp, rlogp)
