@@ -212,9 +212,11 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
                                                        const int64_t* __restrict__ rootindex,
                                                        int64_t N, int64_t B, float* __restrict__ head,
                                                        float* __restrict__ rpart, HeadArgs hd,
-                                                       float* __restrict__ dH2, float* __restrict__ colpart2) {
+                                                       float* __restrict__ dH2, float* __restrict__ colpart2,
+                                                       uint64_t* __restrict__ sgn) {
   BT_BEGIN
   __shared__ float4 red[2][kRoSlices][16];
+  __shared__ float4 redc[2][kRoSlices][16];
   __shared__ float4 hrow[4 * H / 4];
   __shared__ int s_head;
   const bool fuse = dH2 != nullptr;
@@ -223,7 +225,7 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
   int item0 = 0, nit = 1;
   if (blk < S.max_items) {
     if (blk >= S.tree_item0[S.B]) {
-      if (fuse && threadIdx.x < 2 * H) colpart2[int64_t(blk) * (2 * H) + threadIdx.x] = 0.f;
+      if ((fuse || sgn) && threadIdx.x < 2 * H) colpart2[int64_t(blk) * (2 * H) + threadIdx.x] = 0.f;
       return;
     }
     b = S.item_tree[blk];
@@ -251,6 +253,7 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
   }
   const float* src = H2 + d * H + lane * 4;
   float4 s = f4zero();
+  float4 pc = f4zero();   // sgn: positive-H2 counts of this thread's columns
   uint64_t sg = 0;   // relu' of this thread's rows: bit 4k + c for row slice + 16k, column c
   int k = 0;
   for (int64_t i = beg + slice; i < end; i += 8 * kRoSlices, k += 8) {
@@ -258,16 +261,37 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = ld4(src + min<int64_t>(i + u * kRoSlices, end - 1) * (2 * H));
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (i + u * kRoSlices < end) {
+    for (int u = 0; u < 8; ++u) {
+      const bool ok = i + u * kRoSlices < end;
+      if (ok) {
         s = f4add(s, f4relu(v[u]));
         const uint64_t m4 = uint64_t(v[u].x > 0.f) | (uint64_t(v[u].y > 0.f) << 1) |
                             (uint64_t(v[u].z > 0.f) << 2) | (uint64_t(v[u].w > 0.f) << 3);
         sg |= m4 << (4 * (k + u));
       }
+      if (sgn) {
+        // the row's sign word (bit 16c + l = column 4l + c) from four ballots over the
+        // wave's 4 row slices x 16 lanes; lane 0 of each slice stores its row's word
+        const int sh = 16 * (slice & 3);
+        const uint64_t b0 = (__ballot(ok && v[u].x > 0.f) >> sh) & 0xffffull;
+        const uint64_t b1 = (__ballot(ok && v[u].y > 0.f) >> sh) & 0xffffull;
+        const uint64_t b2 = (__ballot(ok && v[u].z > 0.f) >> sh) & 0xffffull;
+        const uint64_t b3 = (__ballot(ok && v[u].w > 0.f) >> sh) & 0xffffull;
+        if (ok && lane == 0) sgn[(i + u * kRoSlices) * 2 + d] = b0 | (b1 << 16) | (b2 << 32) | (b3 << 48);
+        if (ok) pc = f4add(pc, make_float4(float(v[u].x > 0.f), float(v[u].y > 0.f), float(v[u].z > 0.f),
+                                           float(v[u].w > 0.f)));
+      }
+    }
   }
   red[d][slice][lane] = s;
+  if (sgn) redc[d][slice][lane] = pc;
   __syncthreads();
+  if (sgn && blk < S.max_items && slice == 0) {   // the item's counts, slices in order
+    float4 acc = redc[d][0][lane];
+#pragma unroll
+    for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, redc[d][q][lane]);
+    st4(colpart2 + int64_t(blk) * (2 * H) + d * H + lane * 4, acc);
+  }
   if (threadIdx.x >= 64 && !fuse) return;   // wave 0 finishes the item (and the tree)
   if (threadIdx.x < 64) {
     bool last = true;
@@ -599,12 +623,10 @@ size_t bigcn_ws_size(int64_t N, int64_t B, int64_t F, int64_t hid) {
 
 // TD (columns [0, H)) and BU (columns [H, 2H)) aggregations of one [N, 2H] matrix in
 // one launch; `transposed` selects A^T (backward).
-static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool transposed,
-                     int64_t N, const float* in, float* out, const float* bias_td,
-                     const float* bias_bu, int epi, FusedWs& w, hipStream_t s) {
+static SpmmBatch pair_batch(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool transposed,
+                            int64_t N, const float* in, float* out, const float* bias_td,
+                            const float* bias_bu, int epi, FusedWs& w) {
   const size_t half = w.spmm_bytes / 2 / 256 * 256;
-  BGCN_CHECK_ARG(spmm_ws_size(td.capacity, H) <= half && spmm_ws_size(bu.capacity, H) <= half,
-                 "graph capacity exceeds workspace");
   SpmmBatch sb{};
   sb.rows = N;
   sb.F = H;
@@ -618,7 +640,34 @@ static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool 
                        reinterpret_cast<float*>(reinterpret_cast<char*>(w.spmm_ws) + d * half),
                        spmm_groups(v.capacity, H), v.capacity, w.plan[d][transposed ? 1 : 0]};
   }
+  return sb;
+}
+
+static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool transposed,
+                     int64_t N, const float* in, float* out, const float* bias_td,
+                     const float* bias_bu, int epi, FusedWs& w, hipStream_t s,
+                     const SpmmSign* sign = nullptr) {
+  const size_t half = w.spmm_bytes / 2 / 256 * 256;
+  BGCN_CHECK_ARG(spmm_ws_size(td.capacity, H) <= half && spmm_ws_size(bu.capacity, H) <= half,
+                 "graph capacity exceeds workspace");
+  SpmmBatch sb = pair_batch(td, bu, transposed, N, in, out, bias_td, bias_bu, epi, w);
+  if (sign) sb.sg = *sign;
   return spmm_batch_impl(sb, 2, s);
+}
+
+// The sparse path's readout backward rides in the backward's first aggregation (dZ2 =
+// A^T dH2 from the readout's H2 sign words, SpmmSign) whenever that aggregation takes K1's
+// plans: no dH2 round trip, no k_readout_bwd launch.  The forward's readout then stores the
+// sign words (in the dH2 buffer, unused on this path) and per-item positive counts (db2 =
+// sum over items of count x dhead / tree size, the middle launch).  BGCN_READOUT_SIGN=0
+// (read per call) keeps k_readout_bwd / the fused readout.
+static bool readout_sign(const bgcn_bigcn_args* a, const SparseState& sp, FusedWs& w) {
+  if (sp.mode == 1) return false;
+  const char* e = std::getenv("BGCN_READOUT_SIGN");
+  if (e && atoi(e) == 0) return false;
+  const SpmmBatch sb = pair_batch(a->td, a->bu, true, a->num_nodes, nullptr, nullptr, nullptr, nullptr,
+                                  BGCN_EPI_NONE, w);
+  return spmm_planned(sb, 2);
 }
 
 // Workspace + sparse state of one call.  The sparse path's per-row lists and its
@@ -795,18 +844,20 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z2, a->h2, a->td_b2, a->bu_b2, BGCN_EPI_NONE, w, s));
   const HeadArgs no_head{};
   if (sparse) {
-    const bool fuse = readout_fused(sp, B, head != nullptr && head->W != nullptr,
-                                    head != nullptr && head->status != nullptr, head ? head->C : 0);
+    const bool sign = readout_sign(a, sp, w);
+    const bool fuse = !sign && readout_fused(sp, B, head != nullptr && head->W != nullptr,
+                                             head != nullptr && head->status != nullptr, head ? head->C : 0);
     HeadArgs hd = head ? *head : no_head;
     hd.publish = fuse ? 1 : 0;
+    uint64_t* sgn = sign ? reinterpret_cast<uint64_t*>(w.d2) : nullptr;
     if (hd.C <= 4)
       hipLaunchKernelGGL(k_readout_items<4>, dim3(unsigned(sp.max_items + B)), dim3(512), 0, s, sp, a->h1,
                          a->h2, a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd,
-                         fuse ? w.d2 : nullptr, w.colpart2);
+                         fuse ? w.d2 : nullptr, w.colpart2, sgn);
     else
       hipLaunchKernelGGL(k_readout_items<kMaxClasses>, dim3(unsigned(sp.max_items + B)), dim3(512), 0, s, sp,
                          a->h1, a->h2, a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd, nullptr,
-                         w.colpart2);
+                         w.colpart2, sgn);
   }
   else
     hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B)), dim3(1024), 0, s, a->h1, a->h2,
@@ -843,15 +894,18 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   const int nhead = head ? head->C + 1 : 0;
   // fused into the forward's k_readout_items (dH2 and per-item db2 partials are written;
   // the head's weight gradients move to extra blocks of the middle launch)
-  const bool rfused = readout_fused(sp, B, head != nullptr && head->head != nullptr,
-                                    head != nullptr && head->status != nullptr, head ? head->C : 0);
+  const bool sign = readout_sign(a, sp, w);
+  const bool rfused = sign || readout_fused(sp, B, head != nullptr && head->head != nullptr,
+                                            head != nullptr && head->status != nullptr, head ? head->C : 0);
   if (!rfused) {
     hipLaunchKernelGGL(k_readout_bwd, dim3(unsigned(nblk_r + nhead)), dim3(256), 0, s, a->dhead_in, a->h2,
                        a->batch, a->tree_ptr, N, B, w.d2, w.colpart2, int(nblk_r), head ? *head : no_head);
     BGCN_CHECK_LAUNCH();
   }
-  // dZ2 = A^T dH2
-  BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.d2, w.dz2, nullptr, nullptr, BGCN_EPI_NONE, w, s));
+  // dZ2 = A^T dH2 (sign: dH2 generated from the readout's H2 sign words)
+  const SpmmSign sg{reinterpret_cast<const uint64_t*>(w.d2), a->dhead_in, a->batch, a->tree_ptr, B};
+  BGCN_TRY(spmm_pair(a->td, a->bu, true, N, sign ? nullptr : w.d2, w.dz2, nullptr, nullptr, BGCN_EPI_NONE, w, s,
+                     sign ? &sg : nullptr));
   // the CSC of X, when the forward did not leave one, is built on the side lane
   bool forked = false;
   if (sparse && !have_csc) {
@@ -877,7 +931,10 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   m.W2td = a->td_w2; m.W2bu = a->bu_w2; m.dH1 = w.dh1; m.colpart = w.colpart; m.nblk_h = int(nblk_h);
   m.rows_h = w.kchunkh;
   m.db2 = ColsumJob{w.colpart2, rfused ? sp.max_items : int(nblk_r), a->td_db2, a->bu_db2};
-  if (rfused) {
+  if (sign) {   // the partials are per-item positive counts, scaled by their tree's dhead
+    m.db2_dhead = a->dhead_in;
+  }
+  if (rfused && head) {
     m.hg = *head;
     m.n_hg = nhead;
   }

@@ -22,14 +22,31 @@ struct SpmmProb {
   SpmmPlan plan;     // F = 64 only; plan.bnd == nullptr -> merge-path chunks + fixup
 };
 
+// Readout-gradient input of the planned F = 64 aggregation (the fused step's dZ2 = A^T dH2
+// with the readout backward folded in): when sgn != nullptr, problem d's input row j is
+//   dH2_d[j][c] = [H2_d[j][c] > 0] * dhead[b][hoff_d + c] / cnt_b,   b = tree of j,
+// (BiGCN_Twitter.py:57,65: relu then scatter_mean; hoff = 2H for TD, 0 for BU: the head
+// input is cat(BU, TD), :128) read from the readout's H2 sign words: sgn[j][d] bit 16k + l
+// = column 4l + k.  A tree's edges stay inside it, so row i's sum is
+//   dZ2_d[i] = (dhead[b(i)][hoff_d ..] / cnt_b(i)) * sum_j w_ij [H2_d[j] > 0].
+struct SpmmSign {
+  const uint64_t* sgn;       // [rows][2] or nullptr
+  const float* dhead;        // [B][kHeadIn]
+  const int64_t* batch;      // [rows] node -> tree
+  const int32_t* tree_ptr;   // [B + 1]
+  int64_t B;
+};
+
 struct SpmmBatch {
   SpmmProb p[2];
   int64_t rows;
   int F;
   int epi;
+  SpmmSign sg;   // sg.sgn != nullptr: readout-gradient input (planned F = 64 path only)
 };
 
 int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream);
+bool spmm_planned(const SpmmBatch& sb, int count);   // whether the launch takes K1's plans
 // the plans K1 left in a graph-pair workspace (bgcn_build_graph_pair layout)
 void graph_pair_plans(void* ws, size_t ws_bytes, int64_t Etd, int64_t Ebu, int64_t N, SpmmPlan td[2],
                       SpmmPlan bu[2]);
@@ -207,6 +224,31 @@ __device__ inline void colsum_job_block(const ColsumJob& j, int jb, float* sm) {
   if (g == 0) {
     float s = red[cl];
     for (int q = 1; q < kColsumGroups; ++q) s += red[q * cpb + cl];
+    if (c < 64) j.out_td[c] = s; else j.out_bu[c - 64] = s;
+  }
+}
+
+// The same sums with one 256-thread block per column (128 blocks): for many partials
+// (the readout's per-item db2 partials, ~N/32: 3.3k at Weibo size, where the 16-group
+// form above ran 23 us on 8 blocks at the end of the middle launch).  Lane t of the block
+// sums partials p = t, t + 256, ...; the 256 lane sums are combined by a fixed
+// butterfly in each wave and the four wave sums in wave order (deterministic).
+constexpr int kColsumColBlocks = 128;
+__device__ inline void colsum_col_block(const ColsumJob& j, int c, float* sm) {
+  float acc = 0.f;
+  int p = int(threadIdx.x);
+  for (; p + 768 < j.P; p += 1024) {   // 4 loads in flight
+    const float v0 = j.part[int64_t(p) * 128 + c], v1 = j.part[int64_t(p + 256) * 128 + c];
+    const float v2 = j.part[int64_t(p + 512) * 128 + c], v3 = j.part[int64_t(p + 768) * 128 + c];
+    acc += v0; acc += v1; acc += v2; acc += v3;
+  }
+  for (; p < j.P; p += 256) acc += j.part[int64_t(p) * 128 + c];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float s = ((sm[0] + sm[1]) + sm[2]) + sm[3];
     if (c < 64) j.out_td[c] = s; else j.out_bu[c - 64] = s;
   }
 }

@@ -120,6 +120,8 @@ struct BwdMidArgs {
   int nblk_h;                    // dH1 blocks per direction (node splits of rows_h nodes)
   int64_t rows_h;
   ColsumJob db2;
+  const float* db2_dhead = nullptr;   // non-null: db2's partials are per-item positive-H2
+                                      // counts (the readout-gradient aggregation, SpmmSign)
   HeadGradJob hg{};               // the classifier head's weight gradients (readout fused)
   int n_hg = 0;
 };

@@ -1754,9 +1754,46 @@ __global__ __launch_bounds__(256) void k_prep_f(PrepArgs a) {
 }
 
 // ---------------------------------------------------------------- merged backward launches
-// middle (256 threads): dW2 partials (dense / relu(H1) block), dW2 root partials, dH1,
-// db2 column sums;  tail (1024 threads): dW1 over the CSC, dW2 root columns, the dW2
-// partial reduction, db1 column sums.  Roles by block range, in that order.
+// middle (256 threads): dH1 (+ the relu(H1) block of dW2), db2 column sums, dW2 partials
+// (dense path), dW2 root partials, the head's weight gradients;  tail (512 threads): dW1
+// over the CSC, dW2 root columns, the dW2 partial reduction, db1 column sums.  Roles by
+// block range, in that order.
+// db2 from the readout's per-item positive-H2 counts (BwdMidArgs::db2_dhead): dH2 of a
+// row is [H2 > 0] * dhead[b] / |tree b| (BiGCN_Twitter.py:57,65), so column c of db2 =
+// sum_i dH2[i][c] = sum over items p of count[p][c] * dhead[tree(p)][hc] / |tree(p)|; one
+// block per column, the fixed order of colsum_col_block (items past tree_item0[B]: none).
+__device__ inline void db2_from_counts(const BwdMidArgs& a, int c, float* sm) {
+  const int nit = a.S.tree_item0[a.S.B];
+  const int hc = c < H ? 2 * H + c : c - H;   // head input = cat(BU, TD) (:128)
+  const float* cnt = a.db2.part;
+  float acc = 0.f;
+  for (int p0 = 0; p0 < nit; p0 += 4 * 256) {   // 4 items per thread in flight
+    int32_t b[4];
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = min(p0 + u * 256 + int(threadIdx.x), nit - 1);
+      b[u] = a.S.item_tree[p];
+      v[u] = cnt[int64_t(p) * 128 + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t bb = min<int64_t>(max<int64_t>(b[u], 0), a.S.B - 1);
+      const float n = float(max(a.tree_ptr[bb + 1] - a.tree_ptr[bb], 1));
+      const float g = a.db2_dhead[bb * kHeadIn + hc];
+      if (p0 + u * 256 + int(threadIdx.x) < nit) acc += v[u] * (g / n);
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float s = ((sm[0] + sm[1]) + sm[2]) + sm[3];
+    if (c < H) a.db2.out_td[c] = s; else a.db2.out_bu[c - H] = s;
+  }
+}
+
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int kMidSmem = cmax(cmax(cmax(kDw2Smem, kRootPartSmem), cmax(kDh1Smem, kColsumSmem)), kHeadGradSmem);
 template <class TX>
@@ -1773,6 +1810,13 @@ __global__ __launch_bounds__(256, 2) void k_bwd_mid(BwdMidArgs a) {   // LDS: tw
     return;
   }
   b -= 2 * a.nblk_h;
+  if (b < kColsumColBlocks) {   // db2 before the short roles: not the launch's last blocks
+    if (a.db2_dhead) db2_from_counts(a, b, smem);
+    else colsum_col_block(a.db2, b, smem);
+    BT_END(73);
+    return;
+  }
+  b -= kColsumColBlocks;
   if (b < a.n_dw2) {
     dw2_body<TX>(static_cast<const TX*>(a.X), a.ldx, a.S.F, a.H1, a.dZ2, a.node_root, a.S.N, a.keep,
                  a.gate, a.dw2_dense, a.dw2_sparse, a.n_dw2_dense, b, smem);
@@ -1785,13 +1829,7 @@ __global__ __launch_bounds__(256, 2) void k_bwd_mid(BwdMidArgs a) {   // LDS: tw
     BT_END(71);
     return;
   }
-  b -= a.n_root;
-  if (b < colsum_job_blocks(256)) {
-    colsum_job_block(a.db2, b, smem);
-    BT_END(73);
-    return;
-  }
-  head_grad_block(a.hg, b - colsum_job_blocks(256), smem);
+  head_grad_block(a.hg, b - a.n_root, smem);
 }
 
 constexpr int kTailSmem = cmax(cmax(kDw1Smem, kRedSmem), kColsumSmem);
@@ -1834,7 +1872,7 @@ __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
 
 int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s) {
   a.n_root = (a.S.mode != 1) ? 2 * a.S.max_items : 0;
-  const int n = a.n_dw2 + a.n_root + 2 * a.nblk_h + colsum_job_blocks(256) + a.n_hg;
+  const int n = a.n_dw2 + a.n_root + 2 * a.nblk_h + kColsumColBlocks + a.n_hg;
   if (x_dtype == BGCN_DTYPE_BF16)
     hipLaunchKernelGGL(k_bwd_mid<bf16_t>, dim3(unsigned(n)), dim3(256), 0, s, a);
   else

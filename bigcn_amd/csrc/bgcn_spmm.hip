@@ -125,6 +125,22 @@ constexpr int kRowsThreads = BGCN_ROWS_THREADS;
 constexpr int64_t kPlanMaxEntries = int64_t(1) << 30;   // capacity (E + N) up to which plans are used
 constexpr int kRowsGroups = kRowsThreads / 16;
 
+// kSign (SpmmBatch::sg): the input rows are the readout's dH2, generated from the H2 sign
+// words of the gathered rows (8 bytes per neighbour instead of a 256-byte row) and scaled
+// per output row by its tree's dhead / count (the rows of one chunk mostly share one or two
+// trees: the first and the last entry's tree scales are loaded with the entries).
+__device__ __forceinline__ float4 sign_bits(uint64_t wd, int lane) {
+  return make_float4(float((wd >> lane) & 1ull), float((wd >> (16 + lane)) & 1ull),
+                     float((wd >> (32 + lane)) & 1ull), float((wd >> (48 + lane)) & 1ull));
+}
+__device__ __forceinline__ float4 tree_scale(const SpmmSign& sg, int64_t b, int hoff, int fo) {
+  b = min<int64_t>(max<int64_t>(b, 0), sg.B - 1);   // ids out of range: status bit (K1 / head)
+  const float cnt = float(max(sg.tree_ptr[b + 1] - sg.tree_ptr[b], 1));
+  const float4 dh = ld4(sg.dhead + b * kHeadIn + hoff + fo);
+  return make_float4(dh.x / cnt, dh.y / cnt, dh.z / cnt, dh.w / cnt);
+}
+
+template <bool kSign>
 __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
   BT_BEGIN
   constexpr int LANES = 16;
@@ -132,6 +148,8 @@ __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_
   const int lane = threadIdx.x % LANES, grp = threadIdx.x / LANES;
   const int fo = lane * 4;
   const int base_lane = ((threadIdx.x & 63) / LANES) * LANES;
+  const int hoff = blockIdx.y == 0 ? kHeadIn / 2 : 0;   // kSign: TD's r1 block sits after BU's
+  const uint64_t* sgn = sb.sg.sgn + blockIdx.y;      // kSign: this problem's word of row j
   __shared__ float4 red[kRowsGroups][LANES];
   if (int64_t(blockIdx.x) < nchunk) {
     // XCD-contiguous chunk ranges: a tree's rows and the neighbours they gather stay in one
@@ -147,6 +165,27 @@ __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_
     const int64_t e1 = min<int64_t>(bd.x + LANES + lane, P.capacity - 1);
     const int32_t r0 = P.row[e0], c0 = P.col[e0], r1 = P.row[e1], c1 = P.col[e1];
     const float w0 = P.w[e0], w1 = P.w[e1];
+    // kSign: the trees of the chunk's first and last rows and their scales
+    int64_t bA = 0, bZ = 0;
+    float4 gA = f4zero(), gZ = f4zero();
+    if constexpr (kSign) {
+      const int32_t ra = __shfl(r0, base_lane, 64);
+      const int32_t rz = __shfl(n > LANES ? r1 : r0, base_lane + ((n - 1) & (LANES - 1)), 64);
+      bA = sb.sg.batch[max(ra, 0)];
+      bZ = sb.sg.batch[max(rz, 0)];
+      gA = tree_scale(sb.sg, bA, hoff, fo);
+      gZ = tree_scale(sb.sg, bZ, hoff, fo);
+    }
+    auto finish = [&](int32_t r, float4 acc) {
+      if constexpr (kSign) {
+        const int64_t b = sb.sg.batch[r];
+        const float4 gs = b == bA ? gA : (b == bZ ? gZ : tree_scale(sb.sg, b, hoff, fo));
+        st4(P.out + int64_t(r) * P.ld_out + fo,
+            make_float4(acc.x * gs.x, acc.y * gs.y, acc.z * gs.z, acc.w * gs.w));
+      } else {
+        st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+      }
+    };
     float4 acc = f4zero();
     int32_t cur = -1;
     for (int k0 = 0; k0 < n; k0 += 8) {
@@ -162,21 +201,24 @@ __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_
         const int32_t ck = __shfl(hi ? c1 : c0, src, 64);
         ww[u] = __shfl(hi ? w1 : w0, src, 64);
         rr[u] = k < n ? rk : -1;
-        v[u] = ld4(P.in + int64_t(ck) * P.ld_in + fo);   // unconditional (ck is a real row)
+        if constexpr (kSign)
+          v[u] = sign_bits(sgn[int64_t(ck) * 2], lane);    // unconditional (ck is a real row)
+        else
+          v[u] = ld4(P.in + int64_t(ck) * P.ld_in + fo);   // unconditional (ck is a real row)
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int32_t r = rr[u];
         if (r < 0) break;
         if (r != cur) {
-          if (cur >= 0) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+          if (cur >= 0) finish(cur, acc);
           cur = r;
           acc = f4zero();
         }
         acc = f4fma(ww[u], v[u], acc);
       }
     }
-    if (cur >= 0) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+    if (cur >= 0) finish(cur, acc);
     BT_END(3);
     return;
   }
@@ -185,6 +227,8 @@ __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_
   for (int j = int(blockIdx.x - nchunk); j < nl; j += nlongblk) {
     const int32_t r = P.plan.longs[j];
     const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
+    float4 gs = f4zero();
+    if constexpr (kSign) gs = tree_scale(sb.sg, sb.sg.batch[r], hoff, fo);   // under the gathers
     float4 acc = f4zero();
     int64_t e = rs + grp;
     for (; e + 7 * kRowsGroups < re; e += 8 * kRowsGroups) {
@@ -194,20 +238,32 @@ __global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_
       for (int u = 0; u < 8; ++u) {
         const int64_t eu = e + u * kRowsGroups;
         ww[u] = P.w[eu];
-        v[u] = ld4(P.in + int64_t(P.col[eu]) * P.ld_in + fo);
+        if constexpr (kSign)
+          v[u] = sign_bits(sgn[int64_t(P.col[eu]) * 2], lane);
+        else
+          v[u] = ld4(P.in + int64_t(P.col[eu]) * P.ld_in + fo);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc = f4fma(ww[u], v[u], acc);
     }
-    for (; e < re; e += kRowsGroups) acc = f4fma(P.w[e], ld4(P.in + int64_t(P.col[e]) * P.ld_in + fo), acc);
+    for (; e < re; e += kRowsGroups) {
+      if constexpr (kSign)
+        acc = f4fma(P.w[e], sign_bits(sgn[int64_t(P.col[e]) * 2], lane), acc);
+      else
+        acc = f4fma(P.w[e], ld4(P.in + int64_t(P.col[e]) * P.ld_in + fo), acc);
+    }
     red[grp][lane] = acc;
     __syncthreads();
     if (grp == 0) {
       float4 t = red[0][lane];
 #pragma unroll 8
       for (int q = 1; q < kRowsGroups; ++q) t = f4add(t, red[q][lane]);
-      const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
-      st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(t, bv, sb.epi));
+      if constexpr (kSign) {
+        st4(P.out + int64_t(r) * P.ld_out + fo, make_float4(t.x * gs.x, t.y * gs.y, t.z * gs.z, t.w * gs.w));
+      } else {
+        const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
+        st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(t, bv, sb.epi));
+      }
     }
     __syncthreads();
   }
@@ -465,6 +521,25 @@ size_t spmm_ws_size(int64_t capacity, int32_t F) {
 static bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 
+// Whether spmm_batch_impl takes K1's plans (k_spmm_rows) for these problems.  The plan pays
+// off while long rows are few and short (one block each): measured on the fused step
+// beside the next batch's preparation, Twitter15-sized batches (E + N = 55k) 0.356 vs
+// 0.362 ms per step; with 1024-thread row blocks (one per CU) Weibo-sized ones (188k)
+// lost (0.85 vs 0.77 ms), with 512-thread blocks they win too (weibo_bf16 0.698-0.700 vs
+// 0.719, synth1024_bf16 0.853 vs 0.867: profiles/r02_plan_ab.txt).  BGCN_SPMM_PLAN=0/1
+// forces either form (A/B runs; read per call: tests switch it).
+bool spmm_planned(const SpmmBatch& sb, int count) {
+  bool planned = sb.F == 64;
+  int64_t capmax = 0;
+  for (int k = 0; k < count; ++k) {
+    planned = planned && sb.p[k].plan.bnd && sb.p[k].plan.longs && sb.p[k].plan.nlong;
+    capmax = sb.p[k].capacity > capmax ? sb.p[k].capacity : capmax;
+  }
+  const char* pe = std::getenv("BGCN_SPMM_PLAN");
+  const int plan_env = pe ? atoi(pe) : -1;
+  return planned && (plan_env == 1 || (plan_env != 0 && capmax <= kPlanMaxEntries));
+}
+
 // count problems (1 or 2) described by sb.p[0..count), each with its own part buffer
 int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   const int F = sb.F;
@@ -474,7 +549,7 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   int64_t gmax = 0;
   for (int k = 0; k < count; ++k) {
     const SpmmProb& P = sb.p[k];
-    BGCN_CHECK_ARG(P.ptr && P.row && P.col && P.w && P.in && P.out && P.part, "null pointer");
+    BGCN_CHECK_ARG(P.ptr && P.row && P.col && P.w && (P.in || sb.sg.sgn) && P.out && P.part, "null pointer");
     BGCN_CHECK_ARG(P.ld_in % 4 == 0 && P.ld_out % 4 == 0 && P.ld_in >= F && P.ld_out >= F,
                    "ld must be >= F and a multiple of 4");
     BGCN_CHECK_ARG(a16(P.in) && a16(P.out) && (!P.bias || a16(P.bias)) && a16(P.part),
@@ -483,28 +558,23 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   }
   if (gmax == 0) return BGCN_OK;
   const unsigned gy = unsigned(count);
-  bool planned = F == 64;
   int64_t capmax = 0;
-  for (int k = 0; k < count; ++k) {
-    planned = planned && sb.p[k].plan.bnd && sb.p[k].plan.longs && sb.p[k].plan.nlong;
-    capmax = sb.p[k].capacity > capmax ? sb.p[k].capacity : capmax;
-  }
-  // The plan pays off while long rows are few and short (one block each): measured on the
-  // fused step beside the next batch's preparation, Twitter15-sized batches (E + N = 55k)
-  // 0.356 vs 0.362 ms per step; with 1024-thread row blocks (one per CU) Weibo-sized
-  // ones (188k) lost (0.85 vs 0.77 ms), with 512-thread blocks they win too (weibo_bf16
-  // 0.698-0.700 vs 0.719, synth1024_bf16 0.853 vs 0.867: profiles/r02_plan_ab.txt).
-  // BGCN_SPMM_PLAN=0/1 forces either form (A/B runs).
-  const char* pe = std::getenv("BGCN_SPMM_PLAN");   // read per call: tests switch it
-  const int plan_env = pe ? atoi(pe) : -1;
-  planned = planned && (plan_env == 1 || (plan_env != 0 && capmax <= kPlanMaxEntries));
+  for (int k = 0; k < count; ++k) capmax = sb.p[k].capacity > capmax ? sb.p[k].capacity : capmax;
+  const bool planned = spmm_planned(sb, count);
+  BGCN_CHECK_ARG(!sb.sg.sgn || (planned && count == 2 && sb.sg.dhead && sb.sg.batch && sb.sg.tree_ptr &&
+                                sb.sg.B > 0),
+                 "readout-gradient input needs the planned TD/BU pair");
   if (planned) {   // K1's plans: complete rows per chunk, long rows per block, no fixup
     const int64_t gplan = (capmax + kPlanGrid - 1) / kPlanGrid;   // K1's chunk grid
     const int64_t nchunk = (gplan + kRowsGroups - 1) / kRowsGroups;
     int nlongblk = int(std::min<int64_t>(256, std::max<int64_t>(1, capmax / (kPlanChunk + 1))));
     nlongblk += int((8 - (nchunk + nlongblk) % 8) % 8);   // gridDim.x % 8 == 0 (xcd_contig)
-    hipLaunchKernelGGL(k_spmm_rows, dim3(unsigned(nchunk + nlongblk), gy), dim3(kRowsThreads), 0, stream,
-                       sb, nchunk, nlongblk);
+    if (sb.sg.sgn)
+      hipLaunchKernelGGL(k_spmm_rows<true>, dim3(unsigned(nchunk + nlongblk), gy), dim3(kRowsThreads), 0, stream,
+                         sb, nchunk, nlongblk);
+    else
+      hipLaunchKernelGGL(k_spmm_rows<false>, dim3(unsigned(nchunk + nlongblk), gy), dim3(kRowsThreads), 0,
+                         stream, sb, nchunk, nlongblk);
   } else if (F == 64) {
     constexpr int L = 16;
     hipLaunchKernelGGL(k_spmm_narrow<L>, dim3(grid_for(gmax, 256 / L), gy), dim3(256), 0, stream, sb);

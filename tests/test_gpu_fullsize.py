@@ -167,6 +167,7 @@ def test_readout_handoffs_under_prefetch_load(monkeypatch):
     sets a status bit (no spin time-out, no K1 look-back time-out).  Then twenty steps with
     the fused Adam: no update skipped."""
     from bigcn_amd import FusedTrainStep
+    monkeypatch.setenv("BGCN_READOUT_SIGN", "0")   # the hand-off path (not the sign words')
     wl = bench.WORKLOADS["twitter15"]
     pool = bench.make_pool(wl, 0, 4, DEV, drop=(0.0, 0.0))
     p = O.make_params(5000, 64, 64, 4, seed=32)
@@ -208,6 +209,42 @@ def test_readout_handoffs_under_prefetch_load(monkeypatch):
     rep = step.run_report()
     assert rep == {"status": 0, "invalid_steps": 0}, rep
     assert step.opt.step_count == 20
+
+
+@pytest.mark.parametrize("workload", ["twitter15", "weibo_bf16"])
+def test_readout_sign_words_match_readout_bwd(workload, monkeypatch):
+    """The readout backward folded into dZ2's aggregation (H2 sign words + per-item
+    positive counts, BGCN_READOUT_SIGN default) against dH2 written by the readout
+    backward and aggregated as a tensor (=0), three full-size steps with the next batch
+    prepared beside them: identical loss (the forward is the same), every gradient within
+    1e-5 of its max (the sign path scales each row's neighbour sum by the tree's dhead /
+    size once instead of every neighbour's dH2 entry: fp32 rounding only)."""
+    from bigcn_amd import FusedTrainStep
+    wl = bench.WORKLOADS[workload]
+    C = wl["classes"]
+    pool = bench.make_pool(wl, 0, 2, DEV, drop=(0.0, 0.0))
+    p = O.make_params(5000, 64, 64, C, seed=34)
+    runs = {}
+    for sign in ("1", "0"):
+        monkeypatch.setenv("BGCN_READOUT_SIGN", sign)
+        m = _model(p, classes=C)
+        m.train()
+        step = FusedTrainStep(m, tddroprate=wl["drop"][0], budroprate=wl["drop"][1], drop_seed=91)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        out = []
+        with torch.cuda.stream(s):
+            for i in range(3):
+                loss = step.forward_backward(pool[i % 2], seed=700 + i, next_data=pool[(i + 1) % 2])
+                out.append((loss.clone(), [step.grads()[prm].clone() for prm in step.step_params]))
+            step.discard_prefetch()
+        torch.cuda.synchronize()
+        assert step.run_report()["status"] == 0, sign
+        runs[sign] = out
+    for i, ((l1, g1), (l0, g0)) in enumerate(zip(runs["1"], runs["0"])):
+        assert torch.equal(l1, l0), i
+        for k, a, c in zip(KEYS, g1, g0):
+            close(a, c, tol=1e-5, what=f"{workload} step {i} {k}")
 
 
 def test_run_report_counts_invalid_steps():
