@@ -1,5 +1,5 @@
 """Diagnostic: per-wave lifetimes of the training chain's kernels (chain alone, prepared
-batch reused) from a -DBGCN_BLOCK_TRACE build of libbgcn (bgcn_trace.h):
+batch reused; --in-step: with the next batch's preparation beside it) from a -DBGCN_BLOCK_TRACE build of libbgcn (bgcn_trace.h):
 
     make -C bigcn_amd/csrc OUT=../../build/variants/libbgcn_bt.so OBJDIR=../../build/obj_bt \\
          EXTRA=-DBGCN_BLOCK_TRACE
@@ -30,6 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="twitter15")
     ap.add_argument("--mhz", type=float, default=100.0)
+    ap.add_argument("--in-step", action="store_true",
+                    help="record a step with the next batch's preparation running beside it")
     args = ap.parse_args()
     import bench
     from bigcn_amd import BiGCN, FusedTrainStep, _lib
@@ -59,7 +61,11 @@ def main():
         for r in readers:
             r(None, 0, 1)           # reset + enable
         fused._pending = pend
-        fused(pool[0])
+        if args.in_step:
+            fused(pool[0], next_data=pool[1])
+            fused.discard_prefetch()
+        else:
+            fused(pool[0])
         torch.cuda.synchronize()
     recs, marks = [], []
     for r in readers:
