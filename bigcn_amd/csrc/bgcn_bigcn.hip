@@ -190,21 +190,16 @@ __global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ 
 // threads = 2 directions x 16 row slices x 16 lanes x float4, eight row loads in flight
 // per slice.  A tree of one item finishes in its block; otherwise every item stores its
 // partial (rpart[item][2H]) and the tree's last arrival (rtick[b], zeroed by the
-// prologue / conv1, re-zeroed by the last arrival) adds the partials in item order: a fixed
-// order whichever block arrives last (deterministic).  Blocks from max_items on cover
-// trees without nodes (mean 0, root row 0, head on the bias).
+// prologue / conv1) adds the partials in item order: a fixed order whichever block arrives
+// last (deterministic).  Blocks from max_items on cover trees without nodes (mean 0, root
+// row 0, head on the bias).
 //
-// dH2 != nullptr (the train step, every item block resident): the readout backward rides
-// along.  The tree's head block publishes dhead write-through and releases the tree
-// (rtick[b] = kReleased); the tree's other item blocks wait for it (one thread, a bounded
-// spin: status bit 3 instead of a hang), then every item block writes dH2 = dhead/cnt x
-// relu'(H2) for its own rows from the sign bits it kept while summing them (no H2 re-read,
-// no k_readout_bwd launch) and its db2 partial colpart2[item] (padding items write zeros).
+// sgn != nullptr (the backward's readout-gradient aggregation follows, SpmmSign): every
+// row's relu'(H2) as a sign word per direction (bit 16c + l = column 4l + c) and the item's
+// positive counts per column (cnt[item][2H], padding items zero: db2 in the middle launch).
+// The readout backward needs no hand-off inside this launch (dhead is read by later
+// launches), so item blocks never wait for each other at any batch size.
 constexpr int kRoSlices = 16;
-constexpr int kReleased = 1 << 30;
-#ifndef BGCN_SPIN_MAX
-#define BGCN_SPIN_MAX (1 << 22)
-#endif
 template <int MC>   // classes of the head held in registers (HeadRegs)
 __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseState S, const float* __restrict__ H1,
                                                        const float* __restrict__ H2,
@@ -212,20 +207,17 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
                                                        const int64_t* __restrict__ rootindex,
                                                        int64_t N, int64_t B, float* __restrict__ head,
                                                        float* __restrict__ rpart, HeadArgs hd,
-                                                       float* __restrict__ dH2, float* __restrict__ colpart2,
-                                                       uint64_t* __restrict__ sgn) {
+                                                       float* __restrict__ cnt, uint64_t* __restrict__ sgn) {
   BT_BEGIN
   __shared__ float4 red[2][kRoSlices][16];
   __shared__ float4 redc[2][kRoSlices][16];
   __shared__ float4 hrow[4 * H / 4];
-  __shared__ int s_head;
-  const bool fuse = dH2 != nullptr;
   const int blk = int(blockIdx.x);
   int64_t b, beg, end;
   int item0 = 0, nit = 1;
   if (blk < S.max_items) {
     if (blk >= S.tree_item0[S.B]) {
-      if ((fuse || sgn) && threadIdx.x < 2 * H) colpart2[int64_t(blk) * (2 * H) + threadIdx.x] = 0.f;
+      if (sgn && threadIdx.x < 2 * H) cnt[int64_t(blk) * (2 * H) + threadIdx.x] = 0.f;
       return;
     }
     b = S.item_tree[blk];
@@ -254,24 +246,17 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
   const float* src = H2 + d * H + lane * 4;
   float4 s = f4zero();
   float4 pc = f4zero();   // sgn: positive-H2 counts of this thread's columns
-  uint64_t sg = 0;   // relu' of this thread's rows: bit 4k + c for row slice + 16k, column c
-  int k = 0;
-  for (int64_t i = beg + slice; i < end; i += 8 * kRoSlices, k += 8) {
+  for (int64_t i = beg + slice; i < end; i += 8 * kRoSlices) {
     float4 v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = ld4(src + min<int64_t>(i + u * kRoSlices, end - 1) * (2 * H));
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const bool ok = i + u * kRoSlices < end;
-      if (ok) {
-        s = f4add(s, f4relu(v[u]));
-        const uint64_t m4 = uint64_t(v[u].x > 0.f) | (uint64_t(v[u].y > 0.f) << 1) |
-                            (uint64_t(v[u].z > 0.f) << 2) | (uint64_t(v[u].w > 0.f) << 3);
-        sg |= m4 << (4 * (k + u));
-      }
+      if (ok) s = f4add(s, f4relu(v[u]));
       if (sgn) {
-        // the row's sign word (bit 16c + l = column 4l + c) from four ballots over the
-        // wave's 4 row slices x 16 lanes; lane 0 of each slice stores its row's word
+        // the row's sign word from four ballots over the wave's 4 row slices x 16 lanes;
+        // lane 0 of each slice stores its row's word
         const int sh = 16 * (slice & 3);
         const uint64_t b0 = (__ballot(ok && v[u].x > 0.f) >> sh) & 0xffffull;
         const uint64_t b1 = (__ballot(ok && v[u].y > 0.f) >> sh) & 0xffffull;
@@ -290,122 +275,65 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
     float4 acc = redc[d][0][lane];
 #pragma unroll
     for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, redc[d][q][lane]);
-    st4(colpart2 + int64_t(blk) * (2 * H) + d * H + lane * 4, acc);
+    st4(cnt + int64_t(blk) * (2 * H) + d * H + lane * 4, acc);
   }
-  if (threadIdx.x >= 64 && !fuse) return;   // wave 0 finishes the item (and the tree)
-  if (threadIdx.x < 64) {
-    bool last = true;
-    float4 acc = f4zero();
+  if (threadIdx.x >= 64) return;   // wave 0 finishes the item (and the tree)
+  bool last = true;
+  float4 acc = f4zero();
+  if (threadIdx.x < 32) {
+    acc = red[dd][0][ll];
+#pragma unroll
+    for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, red[dd][q][ll]);
+  }
+  if (nit > 1) {
+    // partials go out as agent-scope atomic stores (write-through past the XCD's L2) and
+    // are read back by the last arrival with agent-scope atomic loads: no L2 write-back /
+    // invalidate (a __threadfence per block cost the launch 13.7 -> 48 us)
+    float* p = rpart + int64_t(blk) * (2 * H) + dd * H + ll * 4;
     if (threadIdx.x < 32) {
-      acc = red[dd][0][ll];
-#pragma unroll
-      for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, red[dd][q][ll]);
+      __hip_atomic_store(p + 0, acc.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 1, acc.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 2, acc.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 3, acc.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (nit > 1) {
-      // partials go out as agent-scope atomic stores (write-through past the XCD's L2) and
-      // are read back by the last arrival with agent-scope atomic loads: no L2 write-back /
-      // invalidate (a __threadfence per block cost the launch 13.7 -> 48 us)
-      float* p = rpart + int64_t(blk) * (2 * H) + dd * H + ll * 4;
-      if (threadIdx.x < 32) {
-        __hip_atomic_store(p + 0, acc.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p + 1, acc.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p + 2, acc.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p + 3, acc.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      __builtin_amdgcn_s_waitcnt(0);   // the stores are acknowledged before the ticket
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      int tk = 0;
-      if (threadIdx.x == 0)
-        tk = __hip_atomic_fetch_add(&S.rtick[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      tk = __shfl(tk, 0, 64);
-      last = tk == nit - 1;
-      if (last && threadIdx.x < 32) {
-        const float* q0 = rpart + int64_t(item0) * (2 * H) + dd * H + ll * 4;
-        for (int q = 0; q < nit; ++q) {
-          const float* pq = q0 + int64_t(q) * (2 * H);
-          const float4 v = make_float4(__hip_atomic_load(pq + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                       __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                       __hip_atomic_load(pq + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                       __hip_atomic_load(pq + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          acc = q == 0 ? v : f4add(acc, v);
-        }
-      }
-    }
-    if (threadIdx.x == 0) s_head = last ? 1 : 0;
-    if (last) {
-      const int64_t t0 = tree_ptr[b], t1 = tree_ptr[b + 1];
-      const int base = (dd == 1 ? 0 : 2 * H) + ll * 4;   // BU first (:128)
-      if (threadIdx.x < 32) {
-        const float cnt = float(t1 - t0 > 0 ? t1 - t0 : 1);
-        acc = make_float4(acc.x / cnt, acc.y / cnt, acc.z / cnt, acc.w / cnt);
-        st4(head + b * (4 * H) + base, acc);
-        hrow[base / 4] = acc;
-      } else {
-        const float4 hr = (t1 > t0 && root >= 0 && root < N) ? hroot : f4zero();
-        st4(head + b * (4 * H) + base + H, hr);
-        hrow[(base + H) / 4] = hr;
-      }
-      if (hd.W != nullptr) {
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): wave 0's hrow writes have landed
-        __builtin_amdgcn_wave_barrier();
-        head_row(hd, b, B, hrow[threadIdx.x], hreg);
-        if (fuse) {   // release the tree's other item blocks
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          __builtin_amdgcn_s_waitcnt(0);   // dhead (write-through) acknowledged first
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          if (nit > 1 && threadIdx.x == 0)
-            __hip_atomic_store(&S.rtick[b], kReleased, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);   // the stores are acknowledged before the ticket
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    int tk = 0;
+    if (threadIdx.x == 0)
+      tk = __hip_atomic_fetch_add(&S.rtick[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tk = __shfl(tk, 0, 64);
+    last = tk == nit - 1;
+    if (last && threadIdx.x < 32) {
+      const float* q0 = rpart + int64_t(item0) * (2 * H) + dd * H + ll * 4;
+      for (int q = 0; q < nit; ++q) {
+        const float* pq = q0 + int64_t(q) * (2 * H);
+        const float4 v = make_float4(__hip_atomic_load(pq + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(pq + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(pq + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        acc = q == 0 ? v : f4add(acc, v);
       }
     }
   }
-  if (!fuse) {
-    BT_END(5);
-    return;
-  }
-  __syncthreads();
-  if (blk >= S.max_items) return;   // a tree without nodes: no rows
-  if (!s_head && threadIdx.x == 0) {
-    int n = 0;
-    while (__hip_atomic_load(&S.rtick[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < kReleased) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++n > BGCN_SPIN_MAX) {   // never expected: results invalid, the update is skipped
-        if (hd.status) atomicOr(hd.status, kStatusInternal);
-        break;
-      }
+  if (last) {
+    const int64_t t0 = tree_ptr[b], t1 = tree_ptr[b + 1];
+    const int base = (dd == 1 ? 0 : 2 * H) + ll * 4;   // BU first (:128)
+    if (threadIdx.x < 32) {
+      const float n = float(t1 - t0 > 0 ? t1 - t0 : 1);
+      acc = make_float4(acc.x / n, acc.y / n, acc.z / n, acc.w / n);
+      st4(head + b * (4 * H) + base, acc);
+      hrow[base / 4] = acc;
+    } else {
+      const float4 hr = (t1 > t0 && root >= 0 && root < N) ? hroot : f4zero();
+      st4(head + b * (4 * H) + base + H, hr);
+      hrow[(base + H) / 4] = hr;
     }
-  }
-  __syncthreads();
-  // dH2 of this item's rows (the arithmetic of k_readout_bwd) and the item's db2 partial
-  const int64_t t0 = tree_ptr[b], t1 = tree_ptr[b + 1];
-  const float cnt = float(max(t1 - t0, int64_t(1)));
-  const float* dp = hd.dhead + b * kHeadIn + (d == 1 ? 0 : 2 * H) + lane * 4;
-  const float4 dh = make_float4(__hip_atomic_load(dp + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                __hip_atomic_load(dp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                __hip_atomic_load(dp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                __hip_atomic_load(dp + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  float4 cs = f4zero();
-#pragma unroll 4
-  for (int kk = 0; kk < kChunk / kRoSlices; ++kk) {
-    const int64_t i = beg + slice + int64_t(kk) * kRoSlices;
-    if (i >= end) break;
-    const uint32_t m4 = uint32_t(sg >> (4 * kk)) & 15u;
-    float4 g;
-    g.x = (m4 & 1u) ? dh.x / cnt : 0.f;
-    g.y = (m4 & 2u) ? dh.y / cnt : 0.f;
-    g.z = (m4 & 4u) ? dh.z / cnt : 0.f;
-    g.w = (m4 & 8u) ? dh.w / cnt : 0.f;
-    st4(dH2 + i * (2 * H) + d * H + lane * 4, g);
-    cs = f4add(cs, g);
-  }
-  red[d][slice][lane] = cs;
-  __syncthreads();
-  if (slice == 0) {
-    float4 acc = red[d][0][lane];
-#pragma unroll
-    for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, red[d][q][lane]);
-    st4(colpart2 + int64_t(blk) * (2 * H) + d * H + lane * 4, acc);
+    if (hd.W != nullptr) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): wave 0's hrow writes have landed
+      __builtin_amdgcn_wave_barrier();
+      head_row(hd, b, B, hrow[threadIdx.x], hreg);
+    }
   }
   BT_END(5);
 }
@@ -717,26 +645,6 @@ static bool dense_launched(const bgcn_bigcn_args* a, const SparseState& sp) {
   return sp.mode == 1 || a->feat_mode != BGCN_FEAT_SPARSE;
 }
 
-// The readout backward rides in k_readout_items (train step, sparse path) when every item
-// block can be resident at once (its waiting blocks must not hold the slots their tree's
-// head block needs) and the step has a status word (a timed-out wait must invalidate the
-// step); BGCN_READOUT_FUSED=0 (read per call) keeps k_readout_bwd.
-static bool readout_fused(const SparseState& sp, int64_t B, bool have_head, bool have_status, int C) {
-  if (sp.mode == 1 || !have_head || !have_status || C > 4) return false;   // (k_readout_items<4>)
-  const char* e = std::getenv("BGCN_READOUT_FUSED");
-  if (e && atoi(e) == 0) return false;
-  static const int64_t slots = [] {
-    int dev = 0, ncu = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k_readout_items<4>), 512, 0) !=
-            hipSuccess)
-      return int64_t(0);
-    return int64_t(ncu) * int64_t(per);
-  }();
-  return int64_t(sp.max_items) + B <= slots;
-}
-
 // Forward.  Main stream: node maps, conv1 (sparse compaction + gather, or dense MFMA),
 // propagate, conv2, propagate, readout.  When a backward follows, the CSC of X for dW1
 // is built on the auxiliary lane right after conv1's lin, overlapped with the
@@ -844,20 +752,15 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
   BGCN_TRY(spmm_pair(a->td, a->bu, false, N, w.z2, a->h2, a->td_b2, a->bu_b2, BGCN_EPI_NONE, w, s));
   const HeadArgs no_head{};
   if (sparse) {
-    const bool sign = readout_sign(a, sp, w);
-    const bool fuse = !sign && readout_fused(sp, B, head != nullptr && head->W != nullptr,
-                                             head != nullptr && head->status != nullptr, head ? head->C : 0);
-    HeadArgs hd = head ? *head : no_head;
-    hd.publish = fuse ? 1 : 0;
-    uint64_t* sgn = sign ? reinterpret_cast<uint64_t*>(w.d2) : nullptr;
+    const HeadArgs hd = head ? *head : no_head;
+    uint64_t* sgn = readout_sign(a, sp, w) ? reinterpret_cast<uint64_t*>(w.d2) : nullptr;
     if (hd.C <= 4)
       hipLaunchKernelGGL(k_readout_items<4>, dim3(unsigned(sp.max_items + B)), dim3(512), 0, s, sp, a->h1,
-                         a->h2, a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd,
-                         fuse ? w.d2 : nullptr, w.colpart2, sgn);
+                         a->h2, a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd, w.colpart2, sgn);
     else
       hipLaunchKernelGGL(k_readout_items<kMaxClasses>, dim3(unsigned(sp.max_items + B)), dim3(512), 0, s, sp,
-                         a->h1, a->h2, a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd, nullptr,
-                         w.colpart2, sgn);
+                         a->h1, a->h2, a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd, w.colpart2,
+                         sgn);
   }
   else
     hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B)), dim3(1024), 0, s, a->h1, a->h2,
@@ -887,17 +790,15 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   const bool have_csc = a->save_for_backward || prep != nullptr;
   hipStream_t x;
 
-  // readout + relu' -> dH2 (+ the head's weight gradients in extra blocks); db2 is
-  // reduced by extra blocks of k_dh1
+  // readout + relu' -> dH2: folded into the next aggregation on the sparse path (the
+  // forward's readout left the H2 sign words and per-item counts, readout_sign; the head's
+  // weight gradients then run in extra blocks of the middle launch), else k_readout_bwd
+  // (+ the head's weight gradients in its extra blocks); db2 in the middle launch
   const int64_t nblk_r = (N + kReadBwdRows - 1) / kReadBwdRows;
   const HeadGradJob no_head{};
   const int nhead = head ? head->C + 1 : 0;
-  // fused into the forward's k_readout_items (dH2 and per-item db2 partials are written;
-  // the head's weight gradients move to extra blocks of the middle launch)
   const bool sign = readout_sign(a, sp, w);
-  const bool rfused = sign || readout_fused(sp, B, head != nullptr && head->head != nullptr,
-                                            head != nullptr && head->status != nullptr, head ? head->C : 0);
-  if (!rfused) {
+  if (!sign) {
     hipLaunchKernelGGL(k_readout_bwd, dim3(unsigned(nblk_r + nhead)), dim3(256), 0, s, a->dhead_in, a->h2,
                        a->batch, a->tree_ptr, N, B, w.d2, w.colpart2, int(nblk_r), head ? *head : no_head);
     BGCN_CHECK_LAUNCH();
@@ -930,11 +831,11 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   m.n_dw2 = m.n_dw2_dense;   // the sparse relu(H1) block is formed by the dH1 blocks
   m.W2td = a->td_w2; m.W2bu = a->bu_w2; m.dH1 = w.dh1; m.colpart = w.colpart; m.nblk_h = int(nblk_h);
   m.rows_h = w.kchunkh;
-  m.db2 = ColsumJob{w.colpart2, rfused ? sp.max_items : int(nblk_r), a->td_db2, a->bu_db2};
+  m.db2 = ColsumJob{w.colpart2, sign ? sp.max_items : int(nblk_r), a->td_db2, a->bu_db2};
   if (sign) {   // the partials are per-item positive counts, scaled by their tree's dhead
     m.db2_dhead = a->dhead_in;
   }
-  if (rfused && head) {
+  if (sign && head) {   // the head's weight gradients (k_readout_bwd's extra blocks otherwise)
     m.hg = *head;
     m.n_hg = nhead;
   }

@@ -92,7 +92,6 @@ struct HeadArgs {
   int32_t* status;       // bit 1: label out of range
   const int32_t* in_status;  // OR-ed into *status once (prepared batch's K1 flags), or nullptr
   const int32_t* in_xflags;  // BGCN_FEAT_SPARSE: the compaction's overflow flag (-> bit 2)
-  int publish = 0;       // dhead stored write-through (agent-scope atomics) for other CUs
 };
 
 // One wave, row b of the head: h = head_in[b][4l .. 4l+3] held by lane l.
@@ -167,15 +166,7 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
   if (l == 0 && !yok) hd.loss_row[b] = 0.f;
   if (l == 0 && b == 0 && hd.in_status && hd.status && *hd.in_status) atomicOr(hd.status, *hd.in_status);
   if (l == 0 && b == 0 && hd.in_xflags && hd.status && *hd.in_xflags) atomicOr(hd.status, 4);
-  if (hd.publish) {   // read in the same launch by the tree's other item blocks
-    float* p = hd.dhead + b * kHeadIn + 4 * l;
-    __hip_atomic_store(p + 0, dh.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(p + 1, dh.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(p + 2, dh.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(p + 3, dh.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    st4(hd.dhead + b * kHeadIn + 4 * l, dh);
-  }
+  st4(hd.dhead + b * kHeadIn + 4 * l, dh);
 }
 __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4 h) {
   HeadRegs<kMaxClasses> r;

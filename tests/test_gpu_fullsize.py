@@ -157,45 +157,16 @@ def test_full_size_step_matches_oracle(workload, mode):
     assert not bad, f"{workload}: beyond {TOL:g}: {bad}"
 
 
-def test_readout_handoffs_under_prefetch_load(monkeypatch):
-    """The fused readout backward's cross-workgroup hand-offs (item partials to the tree's
-    last arrival, dhead from the head block to the tree's other item blocks) with the
-    next batch's paced pass over X running beside them, exactly as in the bench: twenty
-    consecutive full-size twitter15 steps with BGCN_READOUT_FUSED=1 equal the separate
-    k_readout_bwd launch (=0) bit for bit - loss and every gradient except db2, whose
-    partials are grouped by item instead of by row block (summation order) - and no step
-    sets a status bit (no spin time-out, no K1 look-back time-out).  Then twenty steps with
-    the fused Adam: no update skipped."""
+def test_steps_under_prefetch_load_stay_valid():
+    """The cross-workgroup hand-offs left in the step (the readout's item partials to the
+    tree's last arrival, K1's decoupled look-back of the next batch on the side lane) under
+    the load the bench puts beside them: twenty consecutive full-size twitter15 steps with
+    the fused Adam and the next batch's preparation beside each, no status bit set and no
+    update skipped."""
     from bigcn_amd import FusedTrainStep
-    monkeypatch.setenv("BGCN_READOUT_SIGN", "0")   # the hand-off path (not the sign words')
     wl = bench.WORKLOADS["twitter15"]
     pool = bench.make_pool(wl, 0, 4, DEV, drop=(0.0, 0.0))
     p = O.make_params(5000, 64, 64, 4, seed=32)
-    runs = {}
-    for fused in ("1", "0"):
-        monkeypatch.setenv("BGCN_READOUT_FUSED", fused)
-        m = _model(p)
-        m.train()
-        step = FusedTrainStep(m, tddroprate=0.2, budroprate=0.2, drop_seed=77)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        out = []
-        with torch.cuda.stream(s):
-            for i in range(20):
-                loss = step.forward_backward(pool[i % 4], seed=500 + i, next_data=pool[(i + 1) % 4])
-                out.append((loss.clone(), [step.grads()[prm].clone() for prm in step.step_params]))
-            step.discard_prefetch()
-        torch.cuda.synchronize()
-        assert step.run_report()["status"] == 0, fused
-        runs[fused] = out
-    for i, ((l1, g1), (l0, g0)) in enumerate(zip(runs["1"], runs["0"])):
-        assert torch.equal(l1, l0), i
-        for k, a, c in zip(KEYS, g1, g0):
-            if k.endswith("conv2.bias"):
-                close(a, c, what=f"step {i} {k}")
-            else:
-                assert torch.equal(a, c), (i, k)
-    monkeypatch.setenv("BGCN_READOUT_FUSED", "1")
     m = _model(p)
     m.train()
     step = FusedTrainStep(m, tddroprate=0.2, budroprate=0.2, drop_seed=78)

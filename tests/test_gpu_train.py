@@ -484,21 +484,21 @@ def test_dw1_column_split_matches(monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["auto", "sparse"])
-def test_fused_readout_backward_matches(monkeypatch, mode):
-    """The readout backward fused into the item readout (dH2 from the kept sign bits after
-    the tree's head releases its item blocks, per-item db2 partials, head weight gradients
-    in the middle launch) against the separate k_readout_bwd launch: loss, logp and every
-    gradient bit for bit except db2 (partials grouped by item instead of by 64 rows:
-    summation order).  Trees of up to ~1500 nodes span several items, so item blocks wait
-    for their tree's head; the status word stays clean (no spin time-out)."""
+def test_readout_sign_path_matches_readout_bwd(monkeypatch, mode):
+    """The readout backward folded into dZ2's aggregation (the readout's H2 sign words and
+    per-item positive counts, db2 and the head's weight gradients in the middle launch)
+    against the separate k_readout_bwd launch + aggregation of the dH2 tensor
+    (BGCN_READOUT_SIGN=0): loss and logp bit for bit (same forward), every gradient within
+    1e-5 of its max (each row's neighbour sum is scaled by its tree's dhead / size once
+    instead of per neighbour).  Trees of up to ~1500 nodes span several items."""
     from bigcn_amd import FusedTrainStep
     b = _synth(49, 48, 300)
     if mode == "auto":
         _unhinted(b)   # the device-gated dense fallback launched (and gated off)
     p = O.make_params(5000, 64, 64, 4, seed=33)
     res = {}
-    for fused in ("1", "0"):
-        monkeypatch.setenv("BGCN_READOUT_FUSED", fused)
+    for sign in ("1", "0"):
+        monkeypatch.setenv("BGCN_READOUT_SIGN", sign)
         m = _model(p, mode)
         m.train()
         step = FusedTrainStep(m)
@@ -506,20 +506,16 @@ def test_fused_readout_backward_matches(monkeypatch, mode):
         loss = step.forward_backward(b, seed=8, logp=logp)
         step.check_status()
         g = step.grads()
-        res[fused] = (loss.clone(), logp.clone(), {k: g[prm].clone() for k, prm in zip(KEYS, step.step_params)})
+        res[sign] = (loss.clone(), logp.clone(), {k: g[prm].clone() for k, prm in zip(KEYS, step.step_params)})
     assert torch.equal(res["1"][0], res["0"][0])
     assert torch.equal(res["1"][1], res["0"][1])
     for k in KEYS:
-        if k.endswith("conv2.bias"):
-            close(res["1"][2][k], res["0"][2][k], what=k)
-        else:
-            assert torch.equal(res["1"][2][k], res["0"][2][k]), k
+        close(res["1"][2][k], res["0"][2][k], tol=1e-5, what=k)
 
 
 def test_train_step_more_than_four_classes():
-    """C = 7: the readout holds every class's head operands (k_readout_items<16>) and the
-    readout backward stays a separate launch (the fused form is sized for <= 4 classes);
-    loss, logp and every gradient match the oracle."""
+    """C = 7: the readout holds every class's head operands (k_readout_items<16>); loss,
+    logp and every gradient match the oracle."""
     from bigcn_amd import BiGCN, FusedTrainStep
     b = _synth(50, 24, 300)
     b.y = (b.y * 7 + torch.arange(b.y.numel(), device=DEV)) % 7
