@@ -98,7 +98,7 @@ def test_fused_midsize_5000_features(training, mode):
     masks = (None, None)
     if training:
         kw = keep_words(seed, N, 5000, DEV)
-        m = unpack_keep(kw.cpu(), 64 + 5000)
+        m = unpack_keep(kw, 64 + 5000).cpu()
         masks = (m[0], m[1])
         frac = float(m.float().mean())
         assert 0.49 < frac < 0.51, frac
@@ -174,7 +174,7 @@ def test_sparse_overflow_falls_back_to_dense(dense_rows):
     b.x[rows.to(DEV)] = torch.rand(dense_rows, 512, generator=g).to(DEV)
     p = O.make_params(512, 64, 64, 4, seed=9)
     N = b.x.size(0)
-    m = unpack_keep(keep_words(7, N, 512, DEV).cpu(), 64 + 512)
+    m = unpack_keep(keep_words(7, N, 512, DEV), 64 + 512).cpu()
     logp, loss, grads, head = gpu_step(b, p, True, None, seed=7, mode="auto")
     rlogp, _, rgrads, st = _oracle(b, p, True, m[0], m[1])
     close(logp, rlogp, what="logp")

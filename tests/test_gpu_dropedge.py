@@ -105,7 +105,7 @@ def test_train_step_device_dropedge_matches_oracle(prefetch):
         bu = O.drop_edges(b.BU_edge_index.cpu().numpy(), batch, B, 0.2, step.last_drop_seed, 1)
         assert td.shape[1] < b.edge_index.size(1)
         from bigcn_amd.ops import keep_words, unpack_keep
-        mk = unpack_keep(keep_words(77, b.x.size(0), 5000, DEV).cpu(), 64 + 5000)
+        mk = unpack_keep(keep_words(77, b.x.size(0), 5000, DEV), 64 + 5000).cpu()
         ref_b = type("B", (), {})()
         ref_b.x, ref_b.batch, ref_b.rootindex, ref_b.y = b.x, b.batch, b.rootindex, b.y
         ref_b.edge_index, ref_b.BU_edge_index = torch.as_tensor(td), torch.as_tensor(bu)

@@ -119,7 +119,7 @@ def test_full_size_step_matches_oracle(workload, mode):
     assert step.run_report()["status"] == 0
     N = b.x.size(0)
     assert N > 25000, N                                                  # really full size
-    mk = unpack_keep(keep_words(12, N, F, DEV).cpu(), 64 + F)
+    mk = unpack_keep(keep_words(12, N, F, DEV), 64 + F).cpu()
     ref = _oracle_batch(b, drops, step.last_drop_seed)
     if drops[0] > 0:
         assert ref.edge_index.size(1) < b.edge_index.size(1)

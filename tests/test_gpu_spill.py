@@ -78,7 +78,7 @@ def test_long_rows_train_step_matches_oracle(mode, split, monkeypatch):
     torch.cuda.synchronize()
     step.check_status()
     N = b.x.size(0)
-    mk = unpack_keep(keep_words(seed, N, 5000, DEV).cpu(), 64 + 5000)
+    mk = unpack_keep(keep_words(seed, N, 5000, DEV), 64 + 5000).cpu()
     h1, h2 = (t.cpu() for t in step.saved_activations())
     masks = {d: (h1[:, 64 * k:64 * (k + 1)] > 0, h2[:, 64 * k:64 * (k + 1)] > 0)
              for k, d in enumerate(("TDrumorGCN", "BUrumorGCN"))}
@@ -101,7 +101,7 @@ def test_long_rows_encoder_matches_oracle(training):
     seed = 99
     masks = (None, None)
     if training:
-        mk = unpack_keep(keep_words(seed, N, 5000, DEV).cpu(), 64 + 5000)
+        mk = unpack_keep(keep_words(seed, N, 5000, DEV), 64 + 5000).cpu()
         masks = (mk[0], mk[1])
     logp, loss, grads, head = gpu_step(b, p, training, None, seed=seed, mode="auto")
     rlogp, rloss, rgrads, st = _oracle(b, p, training, *masks)
@@ -142,7 +142,7 @@ def test_spill_pool_overflow(monkeypatch):
     torch.cuda.synchronize()
     step.check_status()
     N = b.x.size(0)
-    mk = unpack_keep(keep_words(8, N, 512, DEV).cpu(), 64 + 512)
+    mk = unpack_keep(keep_words(8, N, 512, DEV), 64 + 512).cpu()
     _, rloss, rgrads, _ = _oracle(b, p, True, mk[0], mk[1])
     close(loss, rloss, what="loss")
     for k, prm in zip(KEYS, step.step_params):

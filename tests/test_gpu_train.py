@@ -54,7 +54,7 @@ def test_train_step_matches_oracle(training, mode):
     loss = step.forward_backward(b, seed=seed, logp=logp)
     masks = (None, None)
     if training:
-        mk = unpack_keep(keep_words(seed, N, 5000, DEV).cpu(), 64 + 5000)
+        mk = unpack_keep(keep_words(seed, N, 5000, DEV), 64 + 5000).cpu()
         masks = (mk[0], mk[1])
     rlogp, rloss, rgrads, _ = _oracle(b, p, training, *masks)
     close(logp, rlogp, what="logp")
@@ -254,7 +254,7 @@ def test_pheme_768_dense_features(training, mode):
     loss = step.forward_backward(b, seed=seed, logp=logp)
     masks = (None, None)
     if training:
-        mk = unpack_keep(keep_words(seed, N, 768, DEV).cpu(), 64 + 768)
+        mk = unpack_keep(keep_words(seed, N, 768, DEV), 64 + 768).cpu()
         masks = (mk[0], mk[1])
     rlogp, rloss, rgrads, _ = _oracle(b, p, training, *masks)
     close(logp, rlogp, what="logp")
@@ -288,7 +288,7 @@ def test_sparse_signed_features(training):
     loss = step.forward_backward(b, seed=seed, logp=logp)
     masks = (None, None)
     if training:
-        mk = unpack_keep(keep_words(seed, N, 2000, DEV).cpu(), 64 + 2000)
+        mk = unpack_keep(keep_words(seed, N, 2000, DEV), 64 + 2000).cpu()
         masks = (mk[0], mk[1])
     rlogp, rloss, rgrads, _ = _oracle(b, p, training, *masks)
     close(logp, rlogp, what="logp")
@@ -336,7 +336,7 @@ def test_weibo_bf16_features_match_fp32(mode):
             close(a, c, tol=1e-5, what=f"{k} bf16 vs fp32")
     b.x = xb.float()
     N = b.x.size(0)
-    mk = unpack_keep(keep_words(seed, N, 5000, DEV).cpu(), 64 + 5000)
+    mk = unpack_keep(keep_words(seed, N, 5000, DEV), 64 + 5000).cpu()
     rlogp, rloss, rgrads, _ = _oracle(b, p, True, mk[0], mk[1])
     close(p1, rlogp, what="logp")
     close(l1, rloss, what="loss")
@@ -450,7 +450,7 @@ def test_planned_and_merge_path_aggregation_match_oracle(plan, monkeypatch):
     seed = 31
     logp = torch.empty(b.num_graphs, 4, device=DEV)
     loss = step.forward_backward(b, seed=seed, logp=logp)
-    mk = unpack_keep(keep_words(seed, b.x.size(0), 512, DEV).cpu(), 64 + 512)
+    mk = unpack_keep(keep_words(seed, b.x.size(0), 512, DEV), 64 + 512).cpu()
     rlogp, rloss, rgrads, _ = _oracle(b, p, True, mk[0], mk[1])
     close(logp, rlogp, what="logp")
     close(loss, rloss, what="loss")
