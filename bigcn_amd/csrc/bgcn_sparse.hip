@@ -1512,7 +1512,7 @@ __host__ __device__ inline int dw1_sliced_blocks(int64_t F, int W) {
   return int(8 * ((groups + reps - 1) / reps));
 }
 #ifndef BGCN_SPILL_DEPTH
-#define BGCN_SPILL_DEPTH 4
+#define BGCN_SPILL_DEPTH 1
 #endif
 constexpr int kSpillDepth = BGCN_SPILL_DEPTH;
 template <int kPart = 0>   // 0: dW1 + the dW2 root columns, 2: dW1 only (see dw1_body)

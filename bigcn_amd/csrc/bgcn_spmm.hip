@@ -122,6 +122,9 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
 #define BGCN_ROWS_THREADS 512   // 1024-thread blocks ran one per CU (block trace)
 #endif
 constexpr int kRowsThreads = BGCN_ROWS_THREADS;
+#ifndef BGCN_ROWS_WPE
+#define BGCN_ROWS_WPE 1   // minimum waves per SIMD the compiler budgets registers for (A/B knob)
+#endif
 constexpr int64_t kPlanMaxEntries = int64_t(1) << 30;   // capacity (E + N) up to which plans are used
 constexpr int kRowsGroups = kRowsThreads / 16;
 
@@ -141,7 +144,7 @@ __device__ __forceinline__ float4 tree_scale(const SpmmSign& sg, int64_t b, int 
 }
 
 template <bool kSign>
-__global__ __launch_bounds__(kRowsThreads) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
+__global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BGCN_ROWS_WPE))) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
   BT_BEGIN
   constexpr int LANES = 16;
   const SpmmProb& P = sb.p[blockIdx.y];
