@@ -1511,6 +1511,9 @@ __host__ __device__ inline int dw1_sliced_blocks(int64_t F, int W) {
   const int64_t groups = (F + W - 1) / W, reps = 8 / kSlices;
   return int(8 * ((groups + reps - 1) / reps));
 }
+// rows in flight per lane group in the spilled-root sweep (rare): 1 keeps the launch at 64
+// VGPRs, 8 dW1 waves per SIMD (4: 80 VGPRs, 6 waves; twitter15 +1 %,
+// profiles/r03_tail_depth_ab.txt)
 #ifndef BGCN_SPILL_DEPTH
 #define BGCN_SPILL_DEPTH 1
 #endif
