@@ -119,6 +119,163 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const TX* __restrict__ X, int
   }
 }
 
+// The same conv2 for bf16 X on the bf16 MFMA (v_mfma_f32_32x32x16_bf16).  Block = 128 nodes
+// x the 64 outputs of direction d = blockIdx.y; wave w takes nodes [32w, 32w + 32) and both
+// 32-wide output tiles.  Lane map: lane (h = l >> 5, r = l & 31) supplies A[r][8h + j] and
+// B[8h + j][r]; D register q is D[(q & 3) + 8 (q >> 2) + 4h][r].
+//   k < 64, the H1 block: A = keep * s * relu(H1) is fp32 - each lane builds its fragments
+//     straight from global memory (8 consecutive H1 values, its keep word) and from W2's
+//     rows (8 consecutive k of output r), both split three ways: six products (mfma_x6),
+//     fp32-grade (conv2's output feeds a relu).
+//   k >= 64, the root block, in 32-wide k-tiles aligned to the keep words: A = keep * s *
+//     relu(x_root) is exact in bf16 (bag-of-words counts, s = 2), so three products against
+//     W2 split three ways.  A staged as 16-byte pieces of one node's row per lane on
+//     consecutive nodes, B as one W2 row's 8 consecutive k per lane on consecutive rows
+//     (row stride kC2fLd: conflict-free 16-byte LDS stores); the next tile's global loads
+//     are in flight during the current tile's MFMAs.
+constexpr int kC2fBK = 32, kC2fLd = kC2fBK + 8;
+__global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const bf16_t* __restrict__ X, int64_t ldx, int64_t F,
+                                                        const float* __restrict__ H1,
+                                                        const int32_t* __restrict__ node_root,
+                                                        const float* __restrict__ W2td,
+                                                        const float* __restrict__ W2bu,
+                                                        float* __restrict__ Z2, int64_t N, KeepSrc keep,
+                                                        const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
+  constexpr int BM = 128;
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * kC2fLd];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3][H * kC2fLd];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int d = blockIdx.y;
+  const float* W2 = d == 0 ? W2td : W2bu;
+  const int64_t ldw = H + F;
+  const int64_t m0 = int64_t(blockIdx.x) * BM;
+  const float sc = keep.scale();
+  f32x16 acc[2] = {};
+
+  {   // the H1 block (k < 64): fragments from global memory, six products
+    const int64_t m = m0 + 32 * wave + r32;
+    const bool mok = m < N;
+    const float* hrow = H1 + (mok ? m : 0) * (2 * H) + d * H;
+#pragma unroll
+    for (int s = 0; s < H / 16; ++s) {
+      const int k = 16 * s + 8 * h;
+      const uint32_t wd = mok ? keep.get(uint32_t(d), uint32_t(m), uint32_t(k >> 5)) : 0u;
+      const float4 x0 = ld4(hrow + k), x1 = ld4(hrow + k + 4);
+      const float xa[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      bf16x8 ah, am, al;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = ((wd >> ((k + j) & 31)) & 1u) ? sc * fmaxf(xa[j], 0.f) : 0.f;
+        __bf16 p, q, t;
+        split3_bf16(a, p, q, t);
+        ah[j] = p; am[j] = q; al[j] = t;
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float* wrow = W2 + int64_t(32 * c + r32) * ldw + k;
+        const float4 w0 = ld4(wrow), w1 = ld4(wrow + 4);
+        const float wa[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        bf16x8 bh, bm, bl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          __bf16 p, q, t;
+          split3_bf16(wa[j], p, q, t);
+          bh[j] = p; bm[j] = q; bl[j] = t;
+        }
+        acc[c] = mfma_x6(ah, am, al, bh, bm, bl, acc[c]);
+      }
+    }
+  }
+
+  // the root block: k-tiles of 32 A2 columns (64 + 32t ..), keep word 2 + t
+  const int ar = tid & (BM - 1), ak = (tid >> 7) * 16;         // A: node ar, columns ak .. ak + 15
+  const int64_t am_ = m0 + ar;
+  const bool aok = am_ < N;
+  const bf16_t* xrow = X + int64_t(aok ? node_root[am_] : 0) * ldx;
+  const int br = tid & (H - 1), bk = (tid >> 6) * 8;           // B: W2 row br, k bk .. bk + 7
+  const float* wrow = W2 + int64_t(br) * ldw + H;
+  u32x4 ra[2];
+  uint32_t rw = 0;
+  float4 rb[2];
+  auto gload = [&](int64_t c0) {   // c0: first X column of the tile
+    rw = aok ? keep.get(uint32_t(d), uint32_t(am_), uint32_t((H + c0) >> 5)) : 0u;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t c = c0 + ak + 8 * i;
+      const bool ok = aok && c < F;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(xrow + (ok ? c : 0));
+      ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t c = c0 + bk + 4 * i;
+      const bool ok = c < F;   // F % 4 == 0
+      const float4 v = ld4(wrow + (ok ? c : 0));
+      rb[i] = ok ? v : f4zero();
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {   // keep * s * relu(x): exact in bf16 (s is 1 or 2)
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t wv = ra[i][j >> 1];
+        const float x = __uint_as_float((j & 1) ? (wv & 0xffff0000u) : (wv << 16));
+        const bool kept = (rw >> (ak + 8 * i + j)) & 1u;
+        v[j] = __bf16(kept ? sc * fmaxf(x, 0.f) : 0.f);
+      }
+      *reinterpret_cast<bf16x8*>(&As[ar * kC2fLd + ak + 8 * i]) = v;
+    }
+    bf16x8 hv, mv, lv;
+    const float wv[8] = {rb[0].x, rb[0].y, rb[0].z, rb[0].w, rb[1].x, rb[1].y, rb[1].z, rb[1].w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __bf16 p, q, t;
+      split3_bf16(wv[j], p, q, t);
+      hv[j] = p; mv[j] = q; lv[j] = t;
+    }
+    const int o = br * kC2fLd + bk;
+    *reinterpret_cast<bf16x8*>(&Bs[0][o]) = hv;
+    *reinterpret_cast<bf16x8*>(&Bs[1][o]) = mv;
+    *reinterpret_cast<bf16x8*>(&Bs[2][o]) = lv;
+  };
+  const int nk = int((F + kC2fBK - 1) / kC2fBK);
+  gload(0);
+  sstore();
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(int64_t(kt + 1) * kC2fBK);
+#pragma unroll
+    for (int s = 0; s < kC2fBK / 16; ++s) {
+      const int ko = 16 * s + 8 * h;
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[(32 * wave + r32) * kC2fLd + ko]);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int o = (32 * c + r32) * kC2fLd + ko;
+        f32x16 t = acc[c];
+        t = mfma_bf16(a, *reinterpret_cast<const bf16x8*>(&Bs[2][o]), t);
+        t = mfma_bf16(a, *reinterpret_cast<const bf16x8*>(&Bs[1][o]), t);
+        acc[c] = mfma_bf16(a, *reinterpret_cast<const bf16x8*>(&Bs[0][o]), t);
+      }
+    }
+    __syncthreads();
+    if (kt + 1 < nk) {
+      sstore();
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t m = m0 + 32 * wave + acc_row(q, lane);
+    if (m >= N) continue;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) Z2[m * (2 * H) + d * H + 32 * c + r32] = acc[c][q];
+  }
+}
+
 // ---------------------------------------------------------------- readout
 // head_in[b] = [BU: mean(relu(H2_bu)) | H1_bu[root] , TD: mean(relu(H2_td)) | H1_td[root]]
 // One 1024-thread block per tree: per direction 32 row slices x 16 lanes x float4, eight
@@ -640,6 +797,14 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
   return BGCN_OK;
 }
 
+// the dense path's conv2 on the bf16 MFMA (bf16 X; BGCN_GEMM_BF16=0, read once, keeps the
+// f32 MFMA form): 16-byte X rows and W2 rows
+static bool bf16_mfma_ok(const bgcn_bigcn_args* a) {
+  static const bool b16 = [] { const char* e = std::getenv("BGCN_GEMM_BF16"); return !(e && atoi(e) == 0); }();
+  return b16 && a->in_feats % 8 == 0 && a->ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(a->x) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(a->td_w2) & 15) == 0 && (reinterpret_cast<uintptr_t>(a->bu_w2) & 15) == 0;
+}
+
 // whether the (gated) dense kernels are launched at all
 static bool dense_launched(const bgcn_bigcn_args* a, const SparseState& sp) {
   return sp.mode == 1 || a->feat_mode != BGCN_FEAT_SPARSE;
@@ -738,7 +903,12 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
   timing_begin(2, s);
   if (sparse) BGCN_TRY(sparse_conv2(sp, a->h1, a->tree_ptr, a->rootindex, w.z2, keep, s));
   if (dense_launched(a, sp)) {
-    if (a->x_dtype == BGCN_DTYPE_BF16)
+    // bf16 X: the bf16 MFMA (BGCN_GEMM_BF16=0 keeps the f32 MFMA form)
+    if (a->x_dtype == BGCN_DTYPE_BF16 && bf16_mfma_ok(a))
+      hipLaunchKernelGGL(k_conv2_fwd_bf16, dim3(grid_for(N, 128), 2), dim3(256), 0, s,
+                         static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
+                         a->bu_w2, w.z2, N, keep, gate);
+    else if (a->x_dtype == BGCN_DTYPE_BF16)
       hipLaunchKernelGGL(k_conv2_fwd<bf16_t>, dim3(grid_for(N, 64), 2), dim3(256), 0, s,
                          static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
                          a->bu_w2, w.z2, N, keep, gate);
