@@ -44,15 +44,15 @@ def _ref_graph_fns():
 
 
 def _ref_parse(lines):
-    """``getTwittergraph.main`` tree parsing (``Process/getTwittergraph.py:77-84``)."""
-    treeDic = {}
-    for line in lines:
-        line = line.rstrip()
-        eid, indexP, indexC = line.split("\t")[0], line.split("\t")[1], int(line.split("\t")[2])
-        max_degree, maxL, Vec = int(line.split("\t")[3]), int(line.split("\t")[4]), line.split("\t")[5]
-        treeDic.setdefault(eid, {})[indexC] = {"parent": indexP, "max_degree": max_degree,
-                                                 "maxL": maxL, "vec": Vec}
-    return treeDic
+    """The tree dictionary ``getTwittergraph.main`` builds from the RvNN lines
+    (``Process/getTwittergraph.py:77-84``): tree id -> {child index: {parent (str, "None"
+    for the root), max_degree, maxL, vec (the "word:count" string)}}."""
+    trees = {}
+    for raw in lines:
+        fields = raw.rstrip().split("\t")
+        node = {"parent": fields[1], "max_degree": int(fields[3]), "maxL": int(fields[4]), "vec": fields[5]}
+        trees.setdefault(fields[0], {})[int(fields[2])] = node
+    return trees
 
 
 def format_fixture():
