@@ -260,3 +260,50 @@ def test_batch_ids_out_of_range_invalidate_the_step():
     assert step.run_report()["invalid_steps"] == 1
     for k, v in m.state_dict().items():
         assert torch.equal(v, before[k]), k
+
+
+@pytest.mark.parametrize("mode", ["auto", "dense"])
+def test_ragged_trees_step_matches_oracle(mode):
+    """Edge shapes in one batch against the fp64 oracle, training mode with DropEdge drawn
+    on the device and the next batch prepared beside the step: single-node trees (no
+    edges: a row with only its self loop, a one-row item, DropEdge over an empty list),
+    two- and three-node trees, and a 4000-node tree whose root holds ~2000 children (BU
+    rows far past the plan's 16-entry chunks: the aggregation's long-row blocks, a tree of
+    many readout items).  Loss, logp and all ten gradients at the elementwise bar."""
+    from bigcn_amd import FusedTrainStep
+    from bigcn_amd.data import synth_batch
+    from bigcn_amd.ops import keep_words, unpack_keep
+    rng = np.random.default_rng(77)
+    sizes = [1, 1, 2, 3, 4000, 1, 17, 2, 64, 1, 300, 5]
+    b = synth_batch(rng, sizes, 5000, 4, device=DEV)
+    nxt = synth_batch(np.random.default_rng(78), [3, 1, 50, 2], 5000, 4, device=DEV)
+    p = O.make_params(5000, 64, 64, 4, seed=35)
+    m = _model(p, mode)
+    m.train()
+    step = FusedTrainStep(m, tddroprate=0.2, budroprate=0.2, drop_seed=4243)
+    logp = torch.empty(b.num_graphs, 4, device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        loss = step.forward_backward(b, seed=13, logp=logp, next_data=nxt)
+        grads = [step.grads()[prm].clone() for prm in step.step_params]
+        h1, h2 = (t.clone().cpu() for t in step.saved_activations())
+        step.discard_prefetch()
+    torch.cuda.synchronize()
+    step.check_status()
+    N = b.x.size(0)
+    assert N == sum(sizes)
+    mk = unpack_keep(keep_words(13, N, 5000, DEV), 64 + 5000).cpu()
+    ref = _oracle_batch(b, (0.2, 0.2), step.last_drop_seed)
+    masks = {d: (h1[:, 64 * k:64 * (k + 1)] > 0, h2[:, 64 * k:64 * (k + 1)] > 0)
+             for k, d in enumerate(("TDrumorGCN", "BUrumorGCN"))}
+    rlogp, rloss, rgrads, st = _oracle(ref, p, True, mk[0], mk[1], relu_masks=masks)
+    for k, d in enumerate(("TDrumorGCN", "BUrumorGCN")):
+        for name, mine in (("h1", h1), ("h2", h2)):
+            r = st[f"{d}.{name}"]
+            flip = (mine[:, 64 * k:64 * (k + 1)] > 0) != (r > 0)
+            assert bool((r[flip].abs() <= 1e-5 * r.abs().max()).all()), f"{d}.{name}: relu' off a tie"
+    close_elem(logp, rlogp, what="logp")
+    close_elem(loss.reshape(1), rloss.reshape(1), what="loss")
+    for k, g in zip(KEYS, grads):
+        close_elem(g, rgrads[k], what=k)
