@@ -606,6 +606,7 @@ struct FusedWs {
   float* dw2_part;                        // [2][S2][H][H+F]
   float* tn_ws; size_t tn_bytes;
   int S2; int64_t kchunk2;
+  int S2d; int64_t kchunk2d;              // the dense feature mode's dW2 node splits (more: shorter loops)
   int Sh; int64_t kchunkh;
   SpmmPlan plan[2][2];                    // [td, bu][forward, backward] (prepared batch) or null
 };
@@ -643,6 +644,15 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   t.kchunk2 = kc;
   t.S2 = int((N + kc - 1) / kc);
   if (t.S2 < 1) t.S2 = 1;
+  // dense feature mode: node splits of >= 2048 nodes, at most 32 (its dW2 blocks loop over
+  // a split's nodes: 8 splits left 400+ serial k-tiles per block at Weibo size)
+  {
+    int64_t kd = std::max<int64_t>(2048, (N + 31) / 32);
+    kd = (kd + 63) / 64 * 64;
+    t.kchunk2d = kd;
+    t.S2d = int(std::max<int64_t>(1, (N + kd - 1) / kd));
+    if (t.S2d < t.S2) { t.S2d = t.S2; t.kchunk2d = t.kchunk2; }
+  }
   // sparse path: relu(H1) block of dW2 over node splits of >= 128 nodes (partial rows of
   // 64), at most ~kDw2MaxSplits splits: every split writes a 2 x 64 x 64 partial that the
   // tail re-reads (118k nodes: 922 splits = 30 MB of partials at 128 nodes each)
@@ -653,7 +663,7 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   t.kchunkh = std::max<int64_t>(128, ((N + BGCN_DW2_MAX_SPLITS - 1) / BGCN_DW2_MAX_SPLITS + 63) / 64 * 64);
   t.Sh = int((N + t.kchunkh - 1) / t.kchunkh);
   if (t.Sh < 1) t.Sh = 1;
-  const size_t dense_part = size_t(2) * t.S2 * H * (H + F), sparse_part = size_t(2) * t.Sh * H * H;
+  const size_t dense_part = size_t(2) * std::max(t.S2, t.S2d) * H * (H + F), sparse_part = size_t(2) * t.Sh * H * H;
   t.dw2_part = c.take<float>(dense_part > sparse_part ? dense_part : sparse_part);
   t.tn_bytes = tn_ws_size(2 * H, F, N);
   t.tn_ws = c.take<float>(t.tn_bytes / sizeof(float) + 1);
@@ -797,8 +807,8 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
   return BGCN_OK;
 }
 
-// the dense path's conv2 on the bf16 MFMA (bf16 X; BGCN_GEMM_BF16=0, read once, keeps the
-// f32 MFMA form): 16-byte X rows and W2 rows
+// the dense path's conv2 and dW2 root columns on the bf16 MFMA (bf16 X; BGCN_GEMM_BF16=0,
+// read once, keeps the f32 MFMA forms): 16-byte X rows and W2 rows
 static bool bf16_mfma_ok(const bgcn_bigcn_args* a) {
   static const bool b16 = [] { const char* e = std::getenv("BGCN_GEMM_BF16"); return !(e && atoi(e) == 0); }();
   return b16 && a->in_feats % 8 == 0 && a->ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(a->x) & 15) == 0 &&
@@ -995,9 +1005,21 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   m.S = sp;
   m.X = a->x; m.ldx = a->ldx; m.H1 = a->h1; m.dZ2 = w.dz2;
   m.node_root = w.node_root; m.tree_ptr = a->tree_ptr; m.gate = gate; m.keep = keep;
-  m.dw2_dense = Dw2Cfg{w.kchunk2, w.S2, gxd, 1, H + F, w.dw2_part};
+  // the dense feature mode takes its own (larger) node-split count; auto mode's gated
+  // fallback keeps the small one (its blocks are launched every step and mostly exit)
+  const int S2 = sp.mode == 1 ? w.S2d : w.S2;
+  const int64_t kchunk2 = sp.mode == 1 ? w.kchunk2d : w.kchunk2;
+  m.dw2_dense = Dw2Cfg{kchunk2, S2, gxd, 1, H + F, w.dw2_part};
   m.dw2_sparse = Dw2Cfg{w.kchunkh, w.Sh, 1, 0, int64_t(H), w.dw2_part};
-  m.n_dw2_dense = dense_launched(a, sp) ? gxd * w.S2 * 2 : 0;
+  m.n_dw2_dense = dense_launched(a, sp) ? gxd * S2 * 2 : 0;
+  if (m.n_dw2_dense && sp.mode == 1 && a->x_dtype == BGCN_DTYPE_BF16 && bf16_mfma_ok(a)) {
+    // dense mode, bf16 X: the root columns on the bf16 MFMA (k_dw2_bf16, a launch of its
+    // own), dw2_body keeps column tile 0 (the H1 columns)
+    m.gxb = int(grid_for(F, 128));
+    m.n_dw2b = m.gxb * S2 * 2;
+    m.dw2_dense.gx = 1;
+    m.n_dw2_dense = S2 * 2;
+  }
   m.n_dw2 = m.n_dw2_dense;   // the sparse relu(H1) block is formed by the dH1 blocks
   m.W2td = a->td_w2; m.W2bu = a->bu_w2; m.dH1 = w.dh1; m.colpart = w.colpart; m.nblk_h = int(nblk_h);
   m.rows_h = w.kchunkh;
@@ -1010,6 +1032,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     m.n_hg = nhead;
   }
   timing_begin(3, s);
+  BGCN_TRY(dw2_bf16_launch(m, s));
   BGCN_TRY(bwd_mid_launch(m, a->x_dtype, s));
   timing_end(3, s);
 
@@ -1039,7 +1062,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   t.keep_scale = keep.scale(); t.dw2_part = w.dw2_part; t.gate = gate;
   t.keep = keep; t.dZ2 = w.dz2;
   // 1024-thread blocks, 4 output tiles of 64 each
-  t.red_dense = RedCfg{w.S2, H + F, 1,
+  t.red_dense = RedCfg{S2, H + F, 1,
                        dense_launched(a, sp) ? int(std::min<unsigned>(grid_for(2 * H * (H + F), 256), 256)) : 0};
   t.red_sparse = RedCfg{w.Sh, int64_t(H), 0, sparse ? int(grid_for(2 * H * H, 256)) : 0};
   t.db1 = ColsumJob{w.colpart, int(nblk_h), a->td_db1, a->bu_db1};

@@ -125,6 +125,140 @@ __device__ inline void dw2_body(const TX* __restrict__ X, int64_t ldx, int64_t F
   }
 }
 
+// The dense config's root columns (c >= 64) for bf16 X on the bf16 MFMA:
+//   part[d][s][o][64 + x] = sum_{i in split s} dZ2_d[i][o] * keep(d, i, 64 + x) * s * relu(X[root(i)][x])
+// (the H1 columns c < 64 stay with dw2_body's column tile 0).  The A2 values are exact in
+// bf16 (bag-of-words counts, s = 1 or 2) and dZ2 is split three ways: three products,
+// fp32-grade.  Block tile 64 (o) x 128 (x) over 64-node k-tiles, 4 waves as 2 x 2 (wave
+// tile 32 x 64).  Both operands are node-major in memory and staged transposed into
+// node-contiguous LDS rows, each lane writing its row's contiguous nodes as 16-byte stores
+// on consecutive rows (conflict-free); the tile's 64 x 4 keep words are hashed once (one per
+// thread) and shared through LDS.  Block id: (column tile bx, split, direction) with gxb
+// column tiles of 128.  smem: kDw2bSmem floats.
+constexpr int kDw2bBK = 64, kDw2bLd = kDw2bBK + 8;
+constexpr int kDw2bSmem = (3 * H * kDw2bLd + 128 * kDw2bLd) / 2 + kDw2bBK * 4;
+__device__ inline void dw2_bf16_body(const bf16_t* __restrict__ X, int64_t ldx, int64_t F,
+                                     const float* __restrict__ dZ2, const int32_t* __restrict__ node_root,
+                                     int64_t N, KeepSrc keep, const int32_t* __restrict__ gate,
+                                     const Dw2Cfg& cfg, int gxb, int bid, float* smem) {
+  if (!dense_active(gate)) return;
+  __bf16* As = reinterpret_cast<__bf16*>(smem);                 // [3][64 o][kDw2bLd]
+  __bf16* Bs = As + 3 * H * kDw2bLd;                            // [128 x][kDw2bLd]
+  uint32_t* kwl = reinterpret_cast<uint32_t*>(Bs + 128 * kDw2bLd);   // [64 nodes][4 words]
+  const int S = cfg.S;
+  const int bx = bid % gxb, split = (bid / gxb) % S, d = bid / (gxb * S);
+  const int64_t n0 = int64_t(bx) * 128;                         // first X column of the tile
+  const int64_t kb = int64_t(split) * cfg.kchunk, ke = min<int64_t>(kb + cfg.kchunk, N);
+  const float sc = keep.scale();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
+  constexpr int kGN = kDw2bBK / 4, kBN = kDw2bBK / 2;           // nodes per thread: dZ2 / A2
+  const int go = tid & 63, gn = (tid >> 6) * kGN;               // dZ2: column o, kGN nodes
+  const int bc = tid & 127, bn = (tid >> 7) * kBN;              // A2: column x, kBN nodes
+  const bool cok = n0 + bc < F;
+  const uint32_t w0 = uint32_t((H + n0) >> 5);                  // the tile's first keep word
+  float rg[kGN];
+  uint32_t rx[kBN / 2];   // two bf16 per word
+  uint32_t rk = 0;
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int u = 0; u < kGN; ++u) {
+      const int64_t k = k0 + gn + u;
+      const float v = dZ2[min<int64_t>(k, ke - 1) * (2 * H) + d * H + go];
+      rg[u] = k < ke ? v : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kBN; u += 2) {
+      uint32_t two = 0;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int64_t k = k0 + bn + u + t;
+        const int32_t root = node_root[min<int64_t>(k, ke - 1)];
+        const uint16_t v = X[int64_t(root < 0 ? 0 : root) * ldx + (cok ? n0 + bc : 0)];
+        two |= uint32_t((k < ke && cok) ? v : uint16_t(0)) << (16 * t);
+      }
+      rx[u >> 1] = two;
+    }
+    {
+      const int64_t k = k0 + (tid >> 2);
+      const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(k, ke - 1)), w0 + uint32_t(tid & 3));
+      rk = k < ke ? wd : 0u;
+    }
+  };
+  auto sstore = [&]() {
+    kwl[tid] = rk;
+#pragma unroll
+    for (int j = 0; j < kGN / 8; ++j) {
+      bf16x8 hv, mv, lv;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        __bf16 x, y, z;
+        split3_bf16(rg[8 * j + u], x, y, z);
+        hv[u] = x; mv[u] = y; lv[u] = z;
+      }
+      const int oa = go * kDw2bLd + gn + 8 * j;
+      *reinterpret_cast<bf16x8*>(&As[oa]) = hv;
+      *reinterpret_cast<bf16x8*>(&As[H * kDw2bLd + oa]) = mv;
+      *reinterpret_cast<bf16x8*>(&As[2 * H * kDw2bLd + oa]) = lv;
+    }
+    __syncthreads();   // kwl
+    const int wsel = bc >> 5, bit = bc & 31;
+#pragma unroll
+    for (int j = 0; j < kBN / 8; ++j) {
+      bf16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int u = 8 * j + e;
+        const bool kept = (kwl[(bn + u) * 4 + wsel] >> bit) & 1u;
+        const float x = __uint_as_float((rx[u >> 1] >> (16 * (u & 1))) << 16);
+        v[e] = __bf16(kept ? sc * fmaxf(x, 0.f) : 0.f);   // exact: s is 1 or 2
+      }
+      *reinterpret_cast<bf16x8*>(&Bs[bc * kDw2bLd + bn + 8 * j]) = v;
+    }
+  };
+  f32x16 acc[2] = {};
+  const int nk = int((ke - kb + kDw2bBK - 1) / kDw2bBK);
+  if (nk > 0) {
+    gload(kb);
+    sstore();
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(kb + int64_t(kt + 1) * kDw2bBK);
+#pragma unroll
+    for (int s = 0; s < kDw2bBK / 16; ++s) {
+      const int ko = 16 * s + 8 * h;
+      const int oa = (wr * 32 + r32) * kDw2bLd + ko;
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&As[oa]);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&As[H * kDw2bLd + oa]);
+      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(&As[2 * H * kDw2bLd + oa]);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Bs[(wc * 64 + ni * 32 + r32) * kDw2bLd + ko]);
+        f32x16 c = acc[ni];
+        c = mfma_bf16(a2, b, c);
+        c = mfma_bf16(a1, b, c);
+        acc[ni] = mfma_bf16(a0, b, c);
+      }
+    }
+    __syncthreads();
+    if (kt + 1 < nk) {
+      sstore();
+      __syncthreads();
+    }
+  }
+  float* out = cfg.part + (int64_t(d) * S + split) * (H * cfg.ldp) + H + n0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int o = wr * 32 + acc_row(q, lane);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int c = wc * 64 + ni * 32 + r32;
+      if (n0 + c < F) out[int64_t(o) * cfg.ldp + c] = acc[ni][q];
+    }
+  }
+}
+
 // dW2_d[o][c] = sum_s part[d][s][o][c] (fixed order) for c < ldp; the dense config
 // reduces all 64+F columns, the sparse config the relu(H1) block (the root columns come
 // from the root-column body).  A 256-thread group owns 64 consecutive outputs (a tile);

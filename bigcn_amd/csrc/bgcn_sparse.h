@@ -114,6 +114,7 @@ struct BwdMidArgs {
   KeepSrc keep;
   Dw2Cfg dw2_dense, dw2_sparse;  // dW2 partials: dense config blocks first
   int n_dw2_dense, n_dw2;
+  int n_dw2b = 0, gxb = 0;        // dense mode, bf16 X: the root columns' blocks (k_dw2_bf16)
   int n_root;                    // (set by launcher)
   const float *W2td, *W2bu;      // dH1
   float *dH1, *colpart;
@@ -142,6 +143,7 @@ struct BwdTailArgs {
   ColsumJob db1;
 };
 int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s);
+int dw2_bf16_launch(BwdMidArgs& a, hipStream_t s);   // dense mode, bf16 X: dW2 root columns
 // the whole weight-independent preparation of one batch on one stream (six launches;
 // mode 1 = dense: no ELL / CSC of X)
 int prep_pipeline(const Prepared& p, const bgcn_batch* b, int64_t F, int degree_on, int mode,

@@ -1873,6 +1873,22 @@ __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
 
 }  // namespace
 
+// The dense feature mode's dW2 root columns for bf16 X (dw2_bf16_body) as a launch of its
+// own: ~45 KB of LDS, three blocks per CU (inside the middle launch they ran at its two
+// per CU).
+__global__ __launch_bounds__(256) void k_dw2_bf16(BwdMidArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[kDw2bSmem];
+  dw2_bf16_body(static_cast<const bf16_t*>(a.X), a.ldx, a.S.F, a.dZ2, a.node_root, a.S.N, a.keep, a.gate,
+                a.dw2_dense, a.gxb, int(blockIdx.x), smem);
+}
+
+int dw2_bf16_launch(BwdMidArgs& a, hipStream_t s) {
+  if (a.n_dw2b <= 0) return BGCN_OK;
+  hipLaunchKernelGGL(k_dw2_bf16, dim3(unsigned(a.n_dw2b)), dim3(256), 0, s, a);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
 int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s) {
   a.n_root = (a.S.mode != 1) ? 2 * a.S.max_items : 0;
   const int n = a.n_dw2 + a.n_root + 2 * a.nblk_h + kColsumColBlocks + a.n_hg;
