@@ -167,17 +167,31 @@ __device__ inline void dw2_bf16_body(const bf16_t* __restrict__ X, int64_t ldx, 
       const float v = dZ2[min<int64_t>(k, ke - 1) * (2 * H) + d * H + go];
       rg[u] = k < ke ? v : 0.f;
     }
+    // the nodes' root rows: a 32-node run inside one tree (the common case: trees are
+    // contiguous and hundreds of nodes long) shares one root, so one X element per thread
+    const int64_t kf = min<int64_t>(k0 + bn, ke - 1), kl = min<int64_t>(k0 + bn + kBN - 1, ke - 1);
+    const int32_t rf = node_root[kf], rl = node_root[kl];
+    if (rf == rl) {   // wave-uniform (the wave's threads share bn)
+      const uint16_t v = X[int64_t(rf < 0 ? 0 : rf) * ldx + (cok ? n0 + bc : 0)];
+      const uint32_t vv = cok ? uint32_t(v) : 0u;
 #pragma unroll
-    for (int u = 0; u < kBN; u += 2) {
-      uint32_t two = 0;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int64_t k = k0 + bn + u + t;
-        const int32_t root = node_root[min<int64_t>(k, ke - 1)];
-        const uint16_t v = X[int64_t(root < 0 ? 0 : root) * ldx + (cok ? n0 + bc : 0)];
-        two |= uint32_t((k < ke && cok) ? v : uint16_t(0)) << (16 * t);
+      for (int u = 0; u < kBN; u += 2) {
+        const bool ok0 = k0 + bn + u < ke, ok1 = k0 + bn + u + 1 < ke;
+        rx[u >> 1] = (ok0 ? vv : 0u) | ((ok1 ? vv : 0u) << 16);
       }
-      rx[u >> 1] = two;
+    } else {
+#pragma unroll
+      for (int u = 0; u < kBN; u += 2) {
+        uint32_t two = 0;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int64_t k = k0 + bn + u + t;
+          const int32_t root = node_root[min<int64_t>(k, ke - 1)];
+          const uint16_t v = X[int64_t(root < 0 ? 0 : root) * ldx + (cok ? n0 + bc : 0)];
+          two |= uint32_t((k < ke && cok) ? v : uint16_t(0)) << (16 * t);
+        }
+        rx[u >> 1] = two;
+      }
     }
     {
       const int64_t k = k0 + (tid >> 2);
