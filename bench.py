@@ -552,6 +552,7 @@ def main():
             out["dropin_path"] = {
                 "value": round(dropin_res["value"], 2), "unit": "trees/s",
                 "ms_per_step": round(dropin_res["dt"] / n * 1e3, 4), "steps": n,
+                "host_enqueue_ms_per_step": round(dropin_res["t_host"] / n * 1e3, 4),
                 "what": "--path autograd: model(data) -> F.nll_loss -> loss.backward() -> optimiser "
                         "step per batch (BiGCN_Twitter.py:183-189 verbatim on the drop-in GCNConv / "
                         "scatter_mean modules), host DropEdge once per pool batch (untimed)"}

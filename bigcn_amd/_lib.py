@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_gemm_xwt", "bgcn_gemm_xw", "bgcn_gemm_tn_workspace_size", "bgcn_gemm_tn",
     "bgcn_colsum_workspace_size", "bgcn_colsum",
     "bgcn_scatter_mean_workspace_size", "bgcn_scatter_mean_fwd", "bgcn_scatter_mean_bwd",
+    "bgcn_head_forward", "bgcn_head_backward",
     "bgcn_drop_edges_workspace_size", "bgcn_drop_edges",
     "bgcn_bigcn_workspace_size", "bgcn_bigcn_forward", "bgcn_bigcn_backward",
     "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_adam_step",
@@ -148,6 +149,9 @@ _SIGS = {
                                       c_void_p]),
     "bgcn_scatter_mean_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32,
                                       c_int64, c_void_p, c_int64, c_void_p]),
+    "bgcn_head_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    "bgcn_head_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p,
+                                   c_void_p, c_void_p, c_void_p]),
     "bgcn_bigcn_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64]),
     "bgcn_bigcn_forward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
     "bgcn_bigcn_backward": (c_int, [POINTER(BiGCNArgs), c_void_p, c_size_t, c_void_p]),
@@ -200,11 +204,17 @@ def load_library(path: str = LIB_PATH):
         return lib
 
 
+_gpu_seen = False
+
+
 def lib():
-    """The library, for device work: requires a ROCm device."""
-    if not torch.cuda.is_available():
-        raise BGCNError("the bigcn_amd HIP path needs a ROCm GPU (no CPU fallback exists)")
-    return load_library()
+    """The library, for device work: requires a ROCm device (checked until one is seen)."""
+    global _gpu_seen
+    if not _gpu_seen:
+        if not torch.cuda.is_available():
+            raise BGCNError("the bigcn_amd HIP path needs a ROCm GPU (no CPU fallback exists)")
+        _gpu_seen = True
+    return _lib if _lib is not None else load_library()
 
 
 def check(rc: int) -> None:
@@ -214,7 +224,18 @@ def check(rc: int) -> None:
 
 
 def stream_handle(device=None) -> int:
+    """hipStream_t of the current torch stream (of `device`, default the current device).
+    The per-call form reads torch's raw current stream (~0.1 us; the Stream object path
+    costs ~3 us and runs several times per drop-in training step)."""
+    if device is None and _raw_stream is not None:
+        return _raw_stream(_cur_device())
     return torch.cuda.current_stream(device).cuda_stream
+
+
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_device = getattr(torch._C, "_cuda_getDevice", None)
+if _cur_device is None:
+    _raw_stream = None
 
 
 def ptr(t) -> int:

@@ -7,7 +7,8 @@ parameter layout are identical, so reference checkpoints load with ``load_state_
 
 ``BiGCN.forward`` runs the fused bidirectional encoder (:func:`bigcn_amd.ops.bigcn_encoder`:
 both directions, conv1 for TD and BU in one pass over ``x``, the root extension /
-relu / dropout generated inside the conv2 GEMM).  ``TDrumorGCN.forward`` /
+relu / dropout generated inside the conv2 GEMM) and the ``fc`` + ``log_softmax`` head
+(the K9 kernels) as one autograd node (:func:`bigcn_amd.ops.bigcn_net`).  ``TDrumorGCN.forward`` /
 ``BUrumorGCN.forward`` called on their own follow the reference op sequence with the
 drop-in :class:`GCNConv` and :func:`scatter_mean`.
 """
@@ -17,7 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from .conv import GCNConv
-from .ops import Graph, bigcn_encoder, build_graph_pair, degree_code, scatter_mean
+from .ops import Graph, bigcn_encoder, bigcn_net, build_graph_pair, degree_code, feat_path, head_fits, scatter_mean
 
 
 def _graphs(data, degree_on: str = "col"):
@@ -107,6 +108,9 @@ class BiGCN(torch.nn.Module):
         self.device = device
         self.keep_words = None  # optional injected dropout draw (tests)
         self.feat_mode = "auto"  # "auto": sparse feature path with device-side dense fallback
+        # True: fc + log_softmax run as the K9 head kernels inside the encoder's autograd
+        # node (bigcn_net) whenever fc fits them; False: torch's Linear + log_softmax
+        self.fused_head = True
 
     def _convs(self):
         return (self.TDrumorGCN.conv1, self.TDrumorGCN.conv2, self.BUrumorGCN.conv1, self.BUrumorGCN.conv2)
@@ -124,6 +128,13 @@ class BiGCN(torch.nn.Module):
         for c in self._convs():
             c.degree_on = value
 
+    def _feat(self, data):
+        # "auto" with the batch's hints (bound to x's identity and version) saying its rows
+        # fit: BGCN_FEAT_SPARSE, the dense fallback kernels are not launched at all; every
+        # other case keeps the device-gated fallback (the encoder entry points have no
+        # status word to report a batch that does not fit)
+        return feat_path("auto", data) if self.feat_mode == "auto" else self.feat_mode
+
     def encoder_params(self):
         t, b = self.TDrumorGCN, self.BUrumorGCN
         return (t.conv1.lin.weight, t.conv1.bias, t.conv2.lin.weight, t.conv2.bias,
@@ -135,9 +146,17 @@ class BiGCN(torch.nn.Module):
             seed = _draw_seed() if self.training else 0
         return bigcn_encoder(data.x, data.batch, data.rootindex, td, bu, _num_graphs(data),
                              self.encoder_params(), training=self.training, seed=seed,
-                             keep_words=self.keep_words, feat_mode=self.feat_mode)
+                             keep_words=self.keep_words, feat_mode=self._feat(data))
 
     def forward(self, data, seed=None):
+        if self.fused_head and head_fits(self.fc):
+            # :126-130 as one autograd node (encoder + the K9 fc / log_softmax kernels)
+            td, bu = _graphs(data, self.degree_on)
+            if seed is None:
+                seed = _draw_seed() if self.training else 0
+            return bigcn_net(data.x, data.batch, data.rootindex, td, bu, _num_graphs(data),
+                             self.encoder_params(), self.fc.weight, self.fc.bias, training=self.training,
+                             seed=seed, keep_words=self.keep_words, feat_mode=self._feat(data))
         x = self.encode(data, seed)            # cat(BU_x, TD_x)  (:126-128)
         x = self.fc(x)                         # :129
         return F.log_softmax(x, dim=1)         # :130

@@ -215,28 +215,34 @@ class Batch:
         return int(self.x.size(0))
 
     def to(self, device, non_blocking: bool = False):
-        hinted = self.__dict__.get("_x_nnz_of") is self.__dict__.get("x")
+        hinted = self._hint_ok()
         for k, v in list(self.__dict__.items()):
             if isinstance(v, torch.Tensor) and not k.startswith("_"):
                 self.__dict__[k] = v.to(device, non_blocking=non_blocking)
         self.__dict__.pop("_bgcn_graphs", None)
         if hinted:
-            self._x_nnz_of = self.x
+            self._x_nnz_of, self._x_nnz_ver = self.x, self.x._version
         return self
 
     # Host-side feature-path hints: the most non-zeros in one row of x and the entries past
     # the ELL cap summed over the rows (what the spill pool must hold).  They are bound to
-    # the x tensor they were computed for and ignored once x is replaced.
+    # the x tensor they were computed for (its identity and version counter) and ignored
+    # once x is replaced or modified in place.
     def set_x_nnz_max(self, n: int, spill: Optional[int] = None) -> None:
         self.x_nnz_max = int(n)
         self.x_spill = None if spill is None else int(spill)
-        self._x_nnz_of = self.x
+        self._x_nnz_of, self._x_nnz_ver = self.x, self.x._version
+
+    def _hint_ok(self) -> bool:
+        x = self.__dict__.get("x")
+        return (x is not None and self.__dict__.get("_x_nnz_of") is x
+                and self.__dict__.get("_x_nnz_ver") == x._version)
 
     def x_nnz_hint(self):
-        return self.__dict__.get("x_nnz_max") if self.__dict__.get("_x_nnz_of") is self.x else None
+        return self.__dict__.get("x_nnz_max") if self._hint_ok() else None
 
     def x_spill_hint(self):
-        return self.__dict__.get("x_spill") if self.__dict__.get("_x_nnz_of") is self.x else None
+        return self.__dict__.get("x_spill") if self._hint_ok() else None
 
     def keys(self):
         return [k for k in self.__dict__ if not k.startswith("_")]

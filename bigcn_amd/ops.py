@@ -32,19 +32,34 @@ def _dev_check(*ts):
 
 
 # ----------------------------------------------------------------------------- K1
+_GRAPH_I32 = ("t_ptr", "s_ptr", "t_row", "t_col", "s_row", "s_col")
+_GRAPH_F32 = ("t_w", "s_w")
+_SEG_ALIGN = 64   # elements: every array starts 256-byte aligned inside its buffer
+
+
 class Graph:
     """Normalised adjacency of one direction in both CSR orientations.
 
     ``t_*`` rows are targets (forward aggregation, ``out[i] = sum norm * h[src]``),
-    ``s_*`` rows are sources (the transposed product of the backward pass)."""
+    ``s_*`` rows are sources (the transposed product of the backward pass).  The arrays
+    live in two flat buffers (int32 / fp32, shared by the TD and BU graphs of a pair);
+    the per-array tensors are views made on first access - the kernels take pointers."""
 
-    __slots__ = ("num_nodes", "num_edges", "capacity", "t_ptr", "t_row", "t_col", "t_w",
-                 "s_ptr", "s_row", "s_col", "s_w", "status", "_view")
+    __slots__ = ("num_nodes", "num_edges", "capacity", "status", "_bufs", "_lay", "_views", "_ptrs")
+
+    def _array(self, name: str) -> torch.Tensor:
+        v = self._views.get(name)
+        if v is None:
+            k, off, n = self._lay[name]
+            v = self._bufs[k].narrow(0, off, n)
+            self._views[name] = v
+        return v
 
     def view(self) -> GraphView:
         v = GraphView()
-        v.t_ptr, v.t_row, v.t_col, v.t_w = ptr(self.t_ptr), ptr(self.t_row), ptr(self.t_col), ptr(self.t_w)
-        v.s_ptr, v.s_row, v.s_col, v.s_w = ptr(self.s_ptr), ptr(self.s_row), ptr(self.s_col), ptr(self.s_w)
+        q = self._ptrs
+        v.t_ptr, v.t_row, v.t_col, v.t_w = q["t_ptr"], q["t_row"], q["t_col"], q["t_w"]
+        v.s_ptr, v.s_row, v.s_col, v.s_w = q["s_ptr"], q["s_row"], q["s_col"], q["s_w"]
         v.capacity = self.capacity
         return v
 
@@ -57,23 +72,49 @@ class Graph:
             raise IndexError("edge_index contains an index out of range [0, num_nodes)")
 
 
+for _name in _GRAPH_I32 + _GRAPH_F32:
+    setattr(Graph, _name, property(lambda self, _n=_name: self._array(_n)))
+
+
+def _seg(n: int) -> int:
+    return (n + _SEG_ALIGN - 1) // _SEG_ALIGN * _SEG_ALIGN
+
+
+def _alloc_graphs(edges, N: int, dev, status=None):
+    """Graphs of E = edges[k] edges over N nodes, all arrays carved from one int32 and
+    one fp32 allocation."""
+    ni = sum(2 * _seg(N + 1) + 4 * _seg(E + N) for E in edges)
+    nf = sum(2 * _seg(E + N) for E in edges)
+    bi = torch.empty(ni, dtype=torch.int32, device=dev)
+    bf = torch.empty(nf, dtype=torch.float32, device=dev)
+    pi, pf = bi.data_ptr(), bf.data_ptr()
+    st = torch.zeros(1, dtype=torch.int32, device=dev) if status is None else status
+    out, oi, of = [], 0, 0
+    for E in edges:
+        cap = E + N
+        g = Graph()
+        g.num_nodes, g.num_edges, g.capacity, g.status = N, E, cap, st
+        g._bufs, g._views, g._lay, g._ptrs = (bi, bf), {}, {}, {}
+        for name in _GRAPH_I32:
+            n = N + 1 if name.endswith("ptr") else cap
+            g._lay[name], g._ptrs[name] = (0, oi, n), pi + 4 * oi
+            oi += _seg(n)
+        for name in _GRAPH_F32:
+            g._lay[name], g._ptrs[name] = (1, of, cap), pf + 4 * of
+            of += _seg(cap)
+        out.append(g)
+    return out
+
+
 def _alloc_graph(E: int, N: int, dev, status=None) -> Graph:
-    cap = E + N
-    g = Graph()
-    g.num_nodes, g.num_edges, g.capacity = N, E, cap
-    i32 = dict(dtype=torch.int32, device=dev)
-    f32 = dict(dtype=torch.float32, device=dev)
-    g.t_ptr, g.s_ptr = torch.empty(N + 1, **i32), torch.empty(N + 1, **i32)
-    g.t_row, g.t_col, g.t_w = torch.empty(cap, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32)
-    g.s_row, g.s_col, g.s_w = torch.empty(cap, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32)
-    g.status = torch.zeros(1, **i32) if status is None else status
-    return g
+    return _alloc_graphs((E,), N, dev, status)[0]
 
 
 def _csr_out(g: Graph) -> _lib.CsrOut:
     c = _lib.CsrOut()
-    c.t_ptr, c.t_row, c.t_col, c.t_w = ptr(g.t_ptr), ptr(g.t_row), ptr(g.t_col), ptr(g.t_w)
-    c.s_ptr, c.s_row, c.s_col, c.s_w = ptr(g.s_ptr), ptr(g.s_row), ptr(g.s_col), ptr(g.s_w)
+    q = g._ptrs
+    c.t_ptr, c.t_row, c.t_col, c.t_w = q["t_ptr"], q["t_row"], q["t_col"], q["t_w"]
+    c.s_ptr, c.s_row, c.s_col, c.s_w = q["s_ptr"], q["s_row"], q["s_col"], q["s_w"]
     return c
 
 
@@ -90,6 +131,8 @@ def degree_code(degree_on: str) -> int:
 def _check_ei(edge_index: torch.Tensor) -> torch.Tensor:
     if edge_index.dim() != 2 or edge_index.size(0) != 2:
         raise ValueError("edge_index must be [2, E]")
+    if edge_index.dtype == torch.int64 and edge_index.is_contiguous():
+        return edge_index
     return edge_index.to(torch.int64).contiguous()
 
 
@@ -101,15 +144,13 @@ def build_graph_pair(td_edge_index: torch.Tensor, bu_edge_index: torch.Tensor, n
     td_ei, bu_ei = _check_ei(td_edge_index), _check_ei(bu_edge_index)
     N = int(num_nodes)
     dev = td_ei.device
-    status = torch.zeros(1, dtype=torch.int32, device=dev)
-    td = _alloc_graph(int(td_ei.size(1)), N, dev, status)
-    bu = _alloc_graph(int(bu_ei.size(1)), N, dev, status)
+    td, bu = _alloc_graphs((int(td_ei.size(1)), int(bu_ei.size(1))), N, dev)
     L = _lib.lib()
     ws = workspace(L.bgcn_graph_pair_workspace_size(td.num_edges, bu.num_edges, N), dev)
     a, b = _csr_out(td), _csr_out(bu)
-    check(L.bgcn_build_graph_pair(ptr(td_ei), td.num_edges, ptr(bu_ei), bu.num_edges, N,
+    check(L.bgcn_build_graph_pair(td_ei.data_ptr(), td.num_edges, bu_ei.data_ptr(), bu.num_edges, N,
                                   dcode, ctypes.byref(a), ctypes.byref(b),
-                                  ptr(status), ptr(ws), ws.numel(), stream_handle()))
+                                  td.status.data_ptr(), ws.data_ptr(), ws.numel(), stream_handle()))
     if validate:
         td.check()
     return td, bu
@@ -127,8 +168,8 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, edge_weight: Optional[
     L = _lib.lib()
     ws = workspace(L.bgcn_graph_workspace_size(E, N), dev)
     check(L.bgcn_build_graph(ptr(ei), ptr(ew), E, N, dcode,
-                             ptr(g.t_ptr), ptr(g.t_row), ptr(g.t_col), ptr(g.t_w),
-                             ptr(g.s_ptr), ptr(g.s_row), ptr(g.s_col), ptr(g.s_w),
+                             *(g._ptrs[n] for n in ("t_ptr", "t_row", "t_col", "t_w",
+                                                    "s_ptr", "s_row", "s_col", "s_w")),
                              ptr(g.status), ptr(ws), ws.numel(), stream_handle()))
     if validate:
         g.check()
@@ -204,8 +245,8 @@ def spmm(g: Graph, x: torch.Tensor, bias: Optional[torch.Tensor] = None, relu: b
         raise ValueError("out must be a row-major fp32 [N, F] tensor")
     L = _lib.lib()
     ws = workspace(L.bgcn_spmm_workspace_size(g.capacity, F), x.device)
-    p = (g.s_ptr, g.s_row, g.s_col, g.s_w) if transposed else (g.t_ptr, g.t_row, g.t_col, g.t_w)
-    check(L.bgcn_spmm(ptr(p[0]), ptr(p[1]), ptr(p[2]), ptr(p[3]), N, g.capacity, ptr(x), x.stride(0),
+    p = [g._ptrs[("s_" if transposed else "t_") + n] for n in ("ptr", "row", "col", "w")]
+    check(L.bgcn_spmm(p[0], p[1], p[2], p[3], N, g.capacity, ptr(x), x.stride(0),
                       ptr(out), out.stride(0), F, ptr(bias), 1 if relu else 0, ptr(ws), ws.numel(),
                       stream_handle()))
     return out
@@ -343,6 +384,28 @@ _PARAM_ORDER = ("td_w1", "td_b1", "td_w2", "td_b2", "bu_w1", "bu_b1", "bu_w2", "
 _FEAT_MODES = {"auto": _lib.BGCN_FEAT_AUTO, "sparse": _lib.BGCN_FEAT_AUTO, "dense": _lib.BGCN_FEAT_DENSE}
 
 
+def feat_path(feat_mode: str, data) -> int:
+    """C-ABI feature path for a batch: "auto" becomes BGCN_FEAT_SPARSE (no dense fallback
+    launched) when the batch's host-side hints say its rows fit the sparse path - every row
+    within the ELL cap, or the entries past it within the spill pool (``collate`` /
+    ``synth_batch`` set them, bound to x's identity and version); "sparse" forces it (in
+    the fused step a batch that does not fit -> check_status raises)."""
+    if feat_mode == "sparse":
+        return _lib.BGCN_FEAT_SPARSE
+    if feat_mode == "auto" and int(data.x.size(1)) <= 5120:
+        hint = data.x_nnz_hint() if hasattr(data, "x_nnz_hint") else None
+        if hint is not None and int(hint) <= _lib.BGCN_SPARSE_CAP:
+            return _lib.BGCN_FEAT_SPARSE
+        spill = data.x_spill_hint() if hasattr(data, "x_spill_hint") else None
+        if spill is not None and int(spill) <= int(data.x.size(0)) * _lib.BGCN_SPARSE_SPILL_PER_ROW:
+            return _lib.BGCN_FEAT_SPARSE
+    return _FEAT_MODES[feat_mode]
+
+
+def _feat_code(feat_mode) -> int:
+    return feat_mode if isinstance(feat_mode, int) else _FEAT_MODES[feat_mode]
+
+
 def check_encoder_shapes(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, params) -> None:
     """Host-side shape contract of the fused encoder (the kernels trust it)."""
     if x.dim() != 2:
@@ -371,79 +434,140 @@ def x_dtype_code(x: torch.Tensor) -> int:
     return _lib.BGCN_DTYPE_BF16 if x.dtype == torch.bfloat16 else _lib.BGCN_DTYPE_F32
 
 
+_GRAD_ORDER = tuple(n.replace("_w", "_dw").replace("_b", "_db") for n in _PARAM_ORDER)
+
+
 def _fill_args(a: BiGCNArgs, x, batch, rootindex, td, bu, B, training, seed, keep, feat_mode, xs, params):
     N, F = x.shape
-    a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats, a.hid = ptr(x), x.stride(0), N, B, F, HID
+    a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats, a.hid = x.data_ptr(), x.stride(0), N, B, F, HID
     a.x_dtype = x_dtype_code(x)
-    a.batch, a.rootindex = ptr(batch), ptr(rootindex)
+    a.batch, a.rootindex = batch.data_ptr(), rootindex.data_ptr()
     a.td, a.bu = td.view(), bu.view()
-    for name, p in zip(_PARAM_ORDER, params):
-        setattr(a, name, ptr(p))
+    a.td_w1, a.td_b1, a.td_w2, a.td_b2, a.bu_w1, a.bu_b1, a.bu_w2, a.bu_b2 = (p.data_ptr() for p in params)
     a.training, a.seed = int(bool(training)), int(seed) & (2**64 - 1)
     a.keep_words = ptr(keep)
     a.feat_mode = feat_mode
     if xs is not None:
-        a.x_flags, a.x_nnz, a.x_cols, a.x_vals = (ptr(t) for t in xs)
+        a.x_flags, a.x_nnz, a.x_cols, a.x_vals = (t.data_ptr() for t in xs)
+
+
+def _encoder_forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training, seed, keep_words,
+                     feat_mode, params, stream):
+    """The encoder's native forward; returns (head [B, 256], tensors for backward) and
+    keeps the rest of the forward -> backward state on ``ctx`` (``_encoder_backward``)."""
+    x = features(x)
+    N, F = x.shape
+    dev = x.device
+    L = _lib.lib()
+    xs = None
+    if feat_mode != _lib.BGCN_FEAT_DENSE:
+        cap = _lib.BGCN_SPARSE_CAP
+        xs = (torch.empty(8, dtype=torch.int32, device=dev), torch.empty(N, dtype=torch.int32, device=dev),
+              torch.empty(N * cap, dtype=torch.int32, device=dev),
+              torch.empty(N * cap, dtype=torch.float32, device=dev))
+    a = BiGCNArgs()
+    _fill_args(a, x, batch, rootindex, td, bu, B, training, seed, keep_words, feat_mode, xs, params)
+    tree_ptr = torch.empty(B + 1, dtype=torch.int32, device=dev)
+    h1 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
+    h2 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
+    head = torch.empty(B, 4 * HID, dtype=torch.float32, device=dev)
+    a.tree_ptr, a.h1, a.h2, a.head_in = tree_ptr.data_ptr(), h1.data_ptr(), h2.data_ptr(), head.data_ptr()
+    a.save_for_backward = 1 if any(ctx.needs_input_grad) else 0
+    ws = workspace(L.bgcn_bigcn_workspace_size(N, B, F, HID), dev)
+    check(L.bgcn_bigcn_forward(ctypes.byref(a), ws.data_ptr(), ws.numel(), stream))
+    ctx.ws = ws if a.save_for_backward else None   # forward -> backward state (bgcn.h)
+    ctx.args = a                                   # the backward reuses the filled struct
+    ctx.graphs = (td, bu)
+    ctx.meta = (B, N, params[0].device)
+    ctx.has_keep = keep_words is not None
+    empty = x.new_empty(0)
+    # saved for autograd's version checks and lifetime (the struct holds their pointers)
+    saved = (x, batch, rootindex, keep_words if keep_words is not None else empty, tree_ptr, h1, h2,
+             *(xs if xs is not None else (empty,) * 4), *params)
+    return head, saved
+
+
+_ENC_SAVED = 11   # tensors of _encoder_forward's `saved` before the parameters
+
+
+def _encoder_backward(ctx, saved, dhead, stream):
+    """Gradients of the 8 encoder parameters (reference order) from dhead [B, 256]."""
+    params = saved[_ENC_SAVED:_ENC_SAVED + 8]
+    L = _lib.lib()
+    a = ctx.args
+    a.dhead_in = dhead.data_ptr()
+    grads = [torch.empty_like(p) for p in params]
+    for name, gt in zip(_GRAD_ORDER, grads):
+        setattr(a, name, gt.data_ptr())
+    ws = ctx.ws
+    ctx.ws = None
+    if ws is None:
+        raise RuntimeError("bigcn_encoder: backward called twice or without a saved forward")
+    check(L.bgcn_bigcn_backward(ctypes.byref(a), ws.data_ptr(), ws.numel(), stream))
+    return grads
 
 
 class _BiGCNEncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training, seed, keep_words,
                 feat_mode, *params):
-        x = features(x)
-        N, F = x.shape
-        dev = x.device
-        L = _lib.lib()
-        xs = None
-        if feat_mode != _lib.BGCN_FEAT_DENSE:
-            cap = _lib.BGCN_SPARSE_CAP
-            xs = (torch.empty(8, dtype=torch.int32, device=dev), torch.empty(N, dtype=torch.int32, device=dev),
-                  torch.empty(N * cap, dtype=torch.int32, device=dev),
-                  torch.empty(N * cap, dtype=torch.float32, device=dev))
-        a = BiGCNArgs()
-        _fill_args(a, x, batch, rootindex, td, bu, B, training, seed, keep_words, feat_mode, xs, params)
-        tree_ptr = torch.empty(B + 1, dtype=torch.int32, device=dev)
-        h1 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
-        h2 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
-        head = torch.empty(B, 4 * HID, dtype=torch.float32, device=dev)
-        a.tree_ptr, a.h1, a.h2, a.head_in = ptr(tree_ptr), ptr(h1), ptr(h2), ptr(head)
-        a.save_for_backward = 1 if any(ctx.needs_input_grad) else 0
-        ws = workspace(L.bgcn_bigcn_workspace_size(N, B, F, HID), dev)
-        check(L.bgcn_bigcn_forward(ctypes.byref(a), ptr(ws), ws.numel(), stream_handle()))
-        ctx.ws = ws if a.save_for_backward else None   # forward -> backward state (bgcn.h)
-        ctx.save_flag = a.save_for_backward
-        ctx.graphs = (td, bu)
-        ctx.meta = (B, training, seed, feat_mode)
-        empty = x.new_empty(0)
-        ctx.save_for_backward(x, batch, rootindex, keep_words if keep_words is not None else empty,
-                              tree_ptr, h1, h2, *(xs if xs is not None else (empty,) * 4), *params)
-        ctx.has_keep = keep_words is not None
+        head, saved = _encoder_forward(ctx, x, batch, rootindex, td, bu, B, training, seed, keep_words,
+                                       feat_mode, params, stream_handle())
+        ctx.save_for_backward(*saved)
         return head
 
     @staticmethod
     def backward(ctx, dhead):
-        x, batch, rootindex, keep, tree_ptr, h1, h2, xf, xn, xc, xv, *params = ctx.saved_tensors
-        td, bu = ctx.graphs
-        B, training, seed, feat_mode = ctx.meta
-        N, F = x.shape
-        dev = x.device
-        L = _lib.lib()
+        saved = ctx.saved_tensors
         dhead = dhead.contiguous().float()
-        a = BiGCNArgs()
-        xs = None if feat_mode == _lib.BGCN_FEAT_DENSE else (xf, xn, xc, xv)
-        _fill_args(a, x, batch, rootindex, td, bu, B, training, seed, keep if ctx.has_keep else None,
-                   feat_mode, xs, params)
-        a.tree_ptr, a.h1, a.h2, a.dhead_in = ptr(tree_ptr), ptr(h1), ptr(h2), ptr(dhead)
-        grads = [torch.empty_like(p) for p in params]
-        for name, gt in zip(_PARAM_ORDER, grads):
-            setattr(a, name.replace("_w", "_dw").replace("_b", "_db"), ptr(gt))
-        a.save_for_backward = ctx.save_flag
-        ws = ctx.ws
-        ctx.ws = None
-        if ws is None:
-            raise RuntimeError("bigcn_encoder: backward called twice or without a saved forward")
-        check(L.bgcn_bigcn_backward(ctypes.byref(a), ptr(ws), ws.numel(), stream_handle()))
-        return (None,) * 10 + tuple(grads)
+        return (None,) * 10 + tuple(_encoder_backward(ctx, saved, dhead, stream_handle()))
+
+
+class _BiGCNNetFn(torch.autograd.Function):
+    """encoder -> fc -> log_softmax (``BiGCN.forward``, BiGCN_Twitter.py:126-130) as one
+    autograd node: the encoder's native forward / backward plus the K9 head
+    (``bgcn_head_forward`` / ``bgcn_head_backward``) - no library GEMM, log_softmax or
+    their backward kernels, and one node for the autograd engine to run."""
+
+    @staticmethod
+    def forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training, seed, keep_words,
+                feat_mode, fc_w, fc_b, *params):
+        s = stream_handle()
+        head, saved = _encoder_forward(ctx, x, batch, rootindex, td, bu, B, training, seed, keep_words,
+                                       feat_mode, params, s)
+        C = fc_w.size(0)
+        logp = torch.empty(B, C, dtype=torch.float32, device=head.device)
+        check(_lib.lib().bgcn_head_forward(head.data_ptr(), fc_w.data_ptr(), fc_b.data_ptr(), B, C,
+                                           logp.data_ptr(), s))
+        ctx.save_for_backward(*saved, head, logp, fc_w, fc_b)
+        return logp
+
+    @staticmethod
+    def backward(ctx, dlogp):
+        saved = ctx.saved_tensors
+        head, logp, fc_w, fc_b = saved[-4:]
+        dlogp = dlogp.contiguous().float()
+        B, C = logp.shape
+        s = stream_handle()
+        dhead = torch.empty_like(head)
+        dfc_w, dfc_b = torch.empty_like(fc_w), torch.empty_like(fc_b)
+        check(_lib.lib().bgcn_head_backward(head.data_ptr(), logp.data_ptr(), dlogp.data_ptr(), fc_w.data_ptr(),
+                                            B, C, dhead.data_ptr(), dfc_w.data_ptr(), dfc_b.data_ptr(), s))
+        grads = _encoder_backward(ctx, saved, dhead, s)
+        return (None,) * 10 + (dfc_w, dfc_b) + tuple(grads)
+
+
+def _encoder_inputs(x, batch, rootindex, params, keep_words):
+    _dev_check(x, batch, rootindex, keep_words, *params)
+    for p in params:
+        if p.dtype != torch.float32 or not p.is_contiguous():
+            raise ValueError("parameters must be contiguous fp32")
+    check_encoder_shapes(x, batch, rootindex, params)
+    if batch.dtype != torch.int64 or not batch.is_contiguous():
+        batch = batch.to(torch.int64).contiguous()
+    if rootindex.dtype != torch.int64 or not rootindex.is_contiguous():
+        rootindex = rootindex.to(torch.int64).contiguous()
+    return batch, rootindex, (keep_words.contiguous() if keep_words is not None else None)
 
 
 def bigcn_encoder(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, td: Graph, bu: Graph,
@@ -455,17 +579,36 @@ def bigcn_encoder(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor,
     reference layout (``convN.lin.weight [out, in]``, ``convN.bias``).  ``keep_words``
     optionally injects the dropout draw as packed bits [2, N, ceil((64+F)/32)] int32.
     ``feat_mode``: "auto" (sparse feature path, dense MFMA fallback decided on the
-    device) or "dense" (always the dense MFMA kernels)."""
-    _dev_check(x, batch, rootindex, keep_words, *params)
-    for p in params:
-        if p.dtype != torch.float32 or not p.is_contiguous():
-            raise ValueError("parameters must be contiguous fp32")
-    check_encoder_shapes(x, batch, rootindex, params)
-    if keep_words is not None:
-        keep_words = keep_words.contiguous()
-    return _BiGCNEncoderFn.apply(x, batch.to(torch.int64).contiguous(), rootindex.to(torch.int64).contiguous(),
-                                 td, bu, int(num_graphs), bool(training), int(seed), keep_words,
-                                 _FEAT_MODES[feat_mode], *params)
+    device), "dense" (always the dense MFMA kernels) or a C-ABI code (``feat_path``:
+    BGCN_FEAT_SPARSE when the batch's hints say its rows fit)."""
+    batch, rootindex, keep_words = _encoder_inputs(x, batch, rootindex, params, keep_words)
+    return _BiGCNEncoderFn.apply(x, batch, rootindex, td, bu, int(num_graphs), bool(training), int(seed),
+                                 keep_words, _feat_code(feat_mode), *params)
+
+
+def head_fits(fc: torch.nn.Module) -> bool:
+    """Whether ``fc`` is a head the K9 kernels take: Linear(256, C <= 16) with a bias,
+    contiguous fp32 weights."""
+    w, b = getattr(fc, "weight", None), getattr(fc, "bias", None)
+    return (isinstance(fc, torch.nn.Linear) and w is not None and b is not None and w.dim() == 2
+            and w.size(1) == 4 * HID and 0 < w.size(0) <= 16 and w.dtype == torch.float32
+            and b.dtype == torch.float32 and w.is_contiguous() and b.is_contiguous())
+
+
+def bigcn_net(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, td: Graph, bu: Graph,
+              num_graphs: int, params, fc_w: torch.Tensor, fc_b: torch.Tensor, training: bool = False,
+              seed: int = 0, keep_words: Optional[torch.Tensor] = None, feat_mode: str = "auto") -> torch.Tensor:
+    """``log_softmax(fc(bigcn_encoder(...)), dim=1)`` [B, C] (``BiGCN_Twitter.py:126-130``)
+    as one autograd node: the encoder plus the K9 head kernels.  ``fc_w`` [C, 256] and
+    ``fc_b`` [C] are the ``fc`` Linear's parameters (C <= 16)."""
+    batch, rootindex, keep_words = _encoder_inputs(x, batch, rootindex, params, keep_words)
+    _dev_check(fc_w, fc_b)
+    if (fc_w.dim() != 2 or fc_w.size(1) != 4 * HID or not 0 < fc_w.size(0) <= 16 or fc_b.shape != (fc_w.size(0),)
+            or fc_w.dtype != torch.float32 or fc_b.dtype != torch.float32
+            or not fc_w.is_contiguous() or not fc_b.is_contiguous()):
+        raise ValueError("fc must be a contiguous fp32 Linear(256, C <= 16) with a bias")
+    return _BiGCNNetFn.apply(x, batch, rootindex, td, bu, int(num_graphs), bool(training), int(seed), keep_words,
+                             _feat_code(feat_mode), fc_w, fc_b, *params)
 
 
 def keep_words(seed: int, num_nodes: int, in_feats: int, device) -> torch.Tensor:

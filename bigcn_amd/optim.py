@@ -68,7 +68,6 @@ class FusedAdam:
             elif p.grad is not None:
                 p.grad.zero_()
 
-    @torch.no_grad()
     def step(self, grads: Optional[Sequence[torch.Tensor]] = None, grad_scale: float = 1.0,
              skip_flag: Optional[torch.Tensor] = None, images=None,
              skip_count: Optional[torch.Tensor] = None) -> None:
@@ -87,44 +86,45 @@ class FusedAdam:
         self.step_count += 1
         t = self.step_count
         b1, b2 = self.betas
-        gs = list(grads) if grads is not None else [p.grad for p in self.params()]
-        # the table caches pointers, so only contiguous gradients are cacheable (a
-        # non-contiguous one is copied into a fresh tensor every step)
-        cacheable = all(g is None or g.is_contiguous() for g in gs)
-        key = tuple(0 if g is None else g.data_ptr() for g in gs) if cacheable else None
-        cached = self._cache if cacheable and getattr(self, "_cache", None) and self._cache[0] == key else None
+        ps = self.params()
+        gs = list(grads) if grads is not None else [p.grad for p in ps]
+        # the tensor table (parameter / moment pointers, sizes, groups) is built once per
+        # set of present gradients; only the gradient pointers are written per step
+        # (autograd hands out fresh gradient tensors every step)
+        key = tuple(g is None for g in gs)
+        cached = self._cache if getattr(self, "_cache", None) is not None and self._cache[0] == key else None
         if cached is None:
-            # tensor table built once per distinct gradient set (the DP bucket views are
-            # persistent, so a training loop builds it once)
             a = AdamArgs()
-            keep = []
             groups = []         # param_groups index of each table entry (lr refreshed per step)
             entries = []        # params() index of each table entry
             k = 0
-            for gi, p in enumerate(self.params()):
-                gr = gs[gi]
-                if gr is None:
+            for gi, p in enumerate(ps):
+                if gs[gi] is None:
                     continue
                 entries.append(gi)
-                gr = gr.contiguous()
-                keep.append(gr)
                 m, v = self.state[p]
                 e = a.t[k]
-                e.param, e.grad, e.exp_avg, e.exp_avg_sq = ptr(p), ptr(gr), ptr(m), ptr(v)
+                e.param, e.exp_avg, e.exp_avg_sq = ptr(p), ptr(m), ptr(v)
                 e.numel = p.numel()
                 groups.append(self._group_of(p))
                 k += 1
             a.count = k
             a.beta1, a.beta2, a.eps, a.weight_decay = b1, b2, self.eps, self.weight_decay
-            cached = (key, a, keep, groups, entries)
-            self._cache = cached if cacheable else None
-        a, groups = cached[1], cached[3]
+            cached = (key, a, [a.t[k] for k in range(k)], groups, entries)   # entry proxies
+            self._cache = cached
+        keep = []   # non-contiguous gradients: contiguous copies, alive through the launch
+        a, ents, groups = cached[1], cached[2], cached[3]
         if a.count == 0:
             return
-        for k, gi in enumerate(groups):
-            a.t[k].lr = float(self.param_groups[gi]["lr"])
+        for e, gi, gj in zip(ents, cached[4], groups):
+            gr = gs[gi]
+            if not gr.is_contiguous():
+                gr = gr.contiguous()
+                keep.append(gr)
+            e.grad = gr.data_ptr()
+            e.lr = float(self.param_groups[gj]["lr"])
         if skip_flag is not None:
-            if skip_flag.dtype != torch.float32 or skip_flag.numel() != 1 or skip_flag.device != self.params()[0].device:
+            if skip_flag.dtype != torch.float32 or skip_flag.numel() != 1 or skip_flag.device != ps[0].device:
                 raise ValueError("skip_flag must be a one-element fp32 tensor on the parameters' device")
         a.skip_flag = ptr(skip_flag)
         if skip_count is not None and (skip_count.dtype != torch.int32 or skip_count.numel() != 1):
@@ -136,7 +136,6 @@ class FusedAdam:
         if images is not None:
             buf, F, roles = images
             a.images, a.images_in_feats = ptr(buf), int(F)
-            ps = self.params()
             for k, gi in enumerate(self._entries(cached)):
                 a.image_role[k] = roles.get(id(ps[gi]), 0)
         else:

@@ -26,26 +26,12 @@ from . import _lib
 from ._lib import BatchDesc, StepArgs, check, ptr, stream_handle, workspace
 from .bigcn import BiGCN, _draw_seed, _num_graphs
 from .dp import GradBucket
-from .ops import _FEAT_MODES, check_encoder_shapes, degree_code, features, x_dtype_code
+from .ops import _FEAT_MODES, check_encoder_shapes, degree_code, feat_path, features, x_dtype_code
 from .optim import IMAGE_BU_W1, IMAGE_BU_W2, IMAGE_TD_W1, IMAGE_TD_W2, FusedAdam, bigcn_adam
 
 
 def _step_feat_mode(feat_mode: str, data) -> int:
-    """C-ABI feature path of a step: "auto" becomes BGCN_FEAT_SPARSE (no dense fallback
-    launched) when the batch's host-side hints say its rows fit the sparse path - every row
-    within the ELL cap, or the entries past it within the spill pool (``collate`` /
-    ``synth_batch`` set them); "sparse" forces it (a batch that does not fit -> check_status
-    raises)."""
-    if feat_mode == "sparse":
-        return _lib.BGCN_FEAT_SPARSE
-    if feat_mode == "auto" and int(data.x.size(1)) <= 5120:
-        hint = data.x_nnz_hint() if hasattr(data, "x_nnz_hint") else None
-        spill = data.x_spill_hint() if hasattr(data, "x_spill_hint") else None
-        if hint is not None and int(hint) <= _lib.BGCN_SPARSE_CAP:
-            return _lib.BGCN_FEAT_SPARSE
-        if spill is not None and int(spill) <= int(data.x.size(0)) * _lib.BGCN_SPARSE_SPILL_PER_ROW:
-            return _lib.BGCN_FEAT_SPARSE
-    return _FEAT_MODES[feat_mode]
+    return feat_path(feat_mode, data)
 
 
 def _need(t: torch.Tensor, dtype, name: str) -> torch.Tensor:

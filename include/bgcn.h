@@ -166,6 +166,21 @@ int bgcn_scatter_mean_bwd(const float* dout, int64_t ld_dout, const int64_t* ind
                           int64_t ld_dsrc, bgcn_stream_t stream);
 
 /* --------------------------------------------------------------------------
+ * K9  the classifier head: x = self.fc(x); x = F.log_softmax(x, dim=1)
+ * Replaces: BiGCN_Twitter.py:129-130 / BiGCN_Weibo.py:87-88 (torch.nn.Linear(256, C) +
+ * log_softmax, and their autograd backward) on the per-op path.
+ * head_in [B, 256] = cat(BU_x, TD_x); fc_w [C, 256], fc_b [C] (the Linear's layout);
+ * logp [B, C]; 0 < C <= 16; head_in, fc_w and dhead_in 16-byte aligned.
+ * The backward takes any dlogp [B, C] (the gradient of whatever loss follows) and writes
+ * dhead_in [B, 256], fc_dw [C, 256], fc_db [C] (sums over the trees in index order).
+ * -------------------------------------------------------------------------- */
+int bgcn_head_forward(const float* head_in, const float* fc_w, const float* fc_b, int64_t num_graphs,
+                      int32_t num_classes, float* logp, bgcn_stream_t stream);
+int bgcn_head_backward(const float* head_in, const float* logp, const float* dlogp, const float* fc_w,
+                       int64_t num_graphs, int32_t num_classes, float* dhead_in, float* fc_dw,
+                       float* fc_db, bgcn_stream_t stream);
+
+/* --------------------------------------------------------------------------
  * DropEdge (Process/dataset.py:68-90): per tree, keep a uniform random subset of
  * exactly int(E_t * (1 - droprate)) edges (count computed in double as Python does),
  * in their original order; droprate <= 0 keeps every edge (the reference's

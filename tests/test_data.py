@@ -122,6 +122,10 @@ def test_long_rows_and_spill_hints():
     assert int((nnz[b.rootindex] > 32).sum()) >= 3
     assert b.x_nnz_hint() == int(nnz.max())
     assert b.x_spill_hint() == int((nnz - D.SPARSE_CAP).clamp_min(0).sum())
+    b.x[0, 0] += 0.0                                     # an in-place write drops both hints
+    assert b.x_nnz_hint() is None and b.x_spill_hint() is None
+    b.set_x_nnz_max(int(nnz.max()), int((nnz - D.SPARSE_CAP).clamp_min(0).sum()))
+    assert b.x_nnz_hint() == int(nnz.max())
     b.x = b.x.clone()                                   # a replaced x drops both hints
     assert b.x_nnz_hint() is None and b.x_spill_hint() is None
     # per-sample hints through make_sample / collate

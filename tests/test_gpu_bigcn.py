@@ -220,3 +220,91 @@ def test_direction_modules_generic_path():
     close(m.BUrumorGCN(b), st["BUrumorGCN.out"], what="BU")
     head = m.encode(b)
     close(head, st["head_in"], what="fused head")
+
+
+@pytest.mark.parametrize("B,C", [(1, 4), (3, 2), (128, 4), (130, 16), (300, 2)])
+def test_head_kernels_match_torch(B, C):
+    """K9 (bgcn_head_forward / _backward) against torch's Linear + log_softmax and autograd,
+    in fp64, for an arbitrary upstream gradient dlogp; elementwise bar
+    |a - b| <= 1e-5 * (|b| + rms(b))."""
+    from bigcn_amd import _lib
+    from bigcn_amd._lib import check, stream_handle
+    g = torch.Generator().manual_seed(B * 31 + C)
+    head = torch.randn(B, 256, generator=g).abs()           # relu'd readout values
+    W = torch.randn(C, 256, generator=g) * 0.06
+    bias = torch.randn(C, generator=g) * 0.1
+    dlogp = torch.randn(B, C, generator=g)
+    hd, Wd, bd = (t.double().requires_grad_(True) for t in (head, W, bias))
+    ref = F.log_softmax(F.linear(hd, Wd, bd), dim=1)
+    ref.backward(dlogp.double())
+    L = _lib.lib()
+    h, w, bb, dl = (t.to(DEV).contiguous() for t in (head, W, bias, dlogp))
+    logp = torch.empty(B, C, device=DEV)
+    dhead, dW, db = torch.empty(B, 256, device=DEV), torch.empty(C, 256, device=DEV), torch.empty(C, device=DEV)
+    s = stream_handle()
+    check(L.bgcn_head_forward(h.data_ptr(), w.data_ptr(), bb.data_ptr(), B, C, logp.data_ptr(), s))
+    check(L.bgcn_head_backward(h.data_ptr(), logp.data_ptr(), dl.data_ptr(), w.data_ptr(), B, C,
+                               dhead.data_ptr(), dW.data_ptr(), db.data_ptr(), s))
+    for a, b, what in ((logp, ref, "logp"), (dhead, hd.grad, "dhead"), (dW, Wd.grad, "dW"), (db, bd.grad, "db")):
+        a, b = a.double().cpu(), b.detach().cpu()
+        rms = float(b.pow(2).mean().sqrt())
+        bad = (a - b).abs() > 1e-5 * (b.abs() + rms)
+        assert not bad.any(), f"{what}: {int(bad.sum())} elements off, max err {float((a - b).abs().max()):.3e}"
+
+
+def test_head_rejects_bad_shapes():
+    from bigcn_amd import _lib
+    from bigcn_amd._lib import stream_handle
+    L = _lib.lib()
+    h = torch.empty(4, 256, device=DEV)
+    w = torch.empty(17, 256, device=DEV)
+    out = torch.empty(4, 17, device=DEV)
+    assert L.bgcn_head_forward(h.data_ptr(), w.data_ptr(), w.data_ptr(), 4, 17, out.data_ptr(), stream_handle()) != 0
+    assert L.bgcn_head_forward(h.data_ptr(), w.data_ptr(), 0, 4, 4, out.data_ptr(), stream_handle()) != 0
+
+
+@pytest.mark.parametrize("cls", ["BiGCN", "Net"])
+def test_model_fused_head_matches_torch_head(cls):
+    """BiGCN.forward with the K9 head in the encoder's node (fused_head, the default) against
+    the same model with torch's fc + log_softmax: same dropout seed, logp and every
+    parameter gradient (fc included) after F.nll_loss(...).backward()."""
+    import bigcn_amd
+    torch.manual_seed(3)
+    m = getattr(bigcn_amd, cls)(5000, 64, 64, DEV).to(DEV).train()
+    b = _synth(41, 9, 70)
+    if cls == "Net":
+        b.y = b.y % 2
+    out = {}
+    for fused in (True, False):
+        m.fused_head = fused
+        m.zero_grad(set_to_none=True)
+        logp = m(b, seed=1234)
+        F.nll_loss(logp, b.y).backward()
+        out[fused] = (logp.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()})
+    close(out[True][0], out[False][0], tol=1e-5, what="logp")
+    for k in out[False][1]:
+        close(out[True][1][k], out[False][1][k], tol=1e-5, what=k)
+
+
+def test_model_sparse_hint_matches_gated_auto():
+    """BiGCN.forward on a batch whose hints say its rows fit (BGCN_FEAT_SPARSE: the dense
+    fallback kernels are not launched) computes the same step, bit for bit, as with the
+    hints dropped (auto: the fallback launched and gated off on the device)."""
+    from bigcn_amd import BiGCN, _lib
+    from bigcn_amd.ops import feat_path
+    torch.manual_seed(5)
+    m = BiGCN(5000, 64, 64, DEV).to(DEV).train()
+    b = _synth(43, 7, 90)
+    assert feat_path("auto", b) == _lib.BGCN_FEAT_SPARSE
+    out = []
+    for hinted in (True, False):
+        if not hinted:
+            b._x_nnz_of = None
+            assert feat_path("auto", b) == _lib.BGCN_FEAT_AUTO
+        m.zero_grad(set_to_none=True)
+        logp = m(b, seed=99)
+        F.nll_loss(logp, b.y).backward()
+        out.append((logp.detach().clone(), [p.grad.detach().clone() for p in m.parameters()]))
+    assert torch.equal(out[0][0], out[1][0])
+    for a, c in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, c)

@@ -536,17 +536,19 @@ def test_train_step_more_than_four_classes():
     step.check_status()
 
 
-def test_inplace_x_edit_after_collate_skips_update():
-    """The host nnz hint (collate / synth_batch) is bound to the x tensor object, so an
-    in-place edit that overfills the sparse path goes unseen by the hint.  The step then
-    flags status bit 2 on the device, the fused Adam skips the update (parameters and
-    moments unchanged, no host sync) and check_status() raises.  (One long row fits the
-    spill pool; every row at 100 words - 68 spilled per row against 32 per row of pool -
-    does not.)"""
+def test_wrong_hint_skips_update():
+    """The host nnz hint (collate / synth_batch) is bound to x's identity and version
+    counter, so an in-place edit drops it.  A hint that is wrong anyway (set by hand after
+    an edit that overfills the sparse path) is caught on the device: the step flags status
+    bit 2, the fused Adam skips the update (parameters and moments unchanged, no host sync)
+    and check_status() raises.  (One long row fits the spill pool; every row at 100 words -
+    68 spilled per row against 32 per row of pool - does not.)"""
     from bigcn_amd import FusedTrainStep
     b = _synth(47, 8, 60)
     assert b.x_nnz_hint() is not None
     b.x[:, :100] = 1.0                                  # beyond ELL + spill pool, in place
+    assert b.x_nnz_hint() is None and b.x_spill_hint() is None
+    b.set_x_nnz_max(5, 0)                               # a wrong hint
     p = O.make_params(5000, 64, 64, 4, seed=22)
     m = _model(p)
     m.train()
