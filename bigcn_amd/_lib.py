@@ -32,13 +32,13 @@ BGCN_SPARSE_CAP = 32
 BGCN_SPARSE_SPILL_PER_ROW = 32   # spill pool capacity per row (rows over the ELL cap)
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1
-ABI_VERSION = 5   # BGCN_ABI_VERSION of include/bgcn.h
+ABI_VERSION = 6   # BGCN_ABI_VERSION of include/bgcn.h
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
     "bgcn_abi_version", "bgcn_last_error",
     "bgcn_graph_workspace_size", "bgcn_build_graph",
-    "bgcn_graph_pair_workspace_size", "bgcn_build_graph_pair",
+    "bgcn_graph_pair_workspace_size", "bgcn_build_graph_pair", "bgcn_graph_pair_plans",
     "bgcn_spmm_workspace_size", "bgcn_spmm",
     "bgcn_gemm_xwt", "bgcn_gemm_xw", "bgcn_gemm_tn_workspace_size", "bgcn_gemm_tn",
     "bgcn_colsum_workspace_size", "bgcn_colsum",
@@ -53,11 +53,16 @@ EXPORTED_SYMBOLS = (
 )
 
 
+class SpmmPlan(Structure):
+    """bgcn_spmm_plan (include/bgcn.h)."""
+    _fields_ = [("bnd", c_void_p), ("longs", c_void_p), ("nlong", c_void_p)]
+
+
 class GraphView(Structure):
     _fields_ = [
         ("t_ptr", c_void_p), ("t_row", c_void_p), ("t_col", c_void_p), ("t_w", c_void_p),
         ("s_ptr", c_void_p), ("s_row", c_void_p), ("s_col", c_void_p), ("s_w", c_void_p),
-        ("capacity", c_int64),
+        ("capacity", c_int64), ("plan", SpmmPlan * 2),
     ]
 
 
@@ -149,6 +154,7 @@ _SIGS = {
                                       c_void_p]),
     "bgcn_scatter_mean_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32,
                                       c_int64, c_void_p, c_int64, c_void_p]),
+    "bgcn_graph_pair_plans": (c_int, [c_void_p, c_size_t, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
     "bgcn_head_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     "bgcn_head_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p,
                                    c_void_p, c_void_p, c_void_p]),

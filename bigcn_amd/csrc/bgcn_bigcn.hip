@@ -790,7 +790,13 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
   w.spmm_bytes = ws_bytes - align_up(c.off, 256) - 256;
   w.spmm_ws = c.take<float>(1);
   for (int d = 0; d < 2; ++d)
-    for (int o = 0; o < 2; ++o) w.plan[d][o] = prep ? prep->plan[d][o] : SpmmPlan{nullptr, nullptr, nullptr};
+    for (int o = 0; o < 2; ++o) {
+      // the prepared batch's plans, else the ones the caller's graph views carry
+      // (bgcn_graph_pair_plans), else none
+      const bgcn_spmm_plan& vp = (d == 0 ? a->td : a->bu).plan[o];
+      w.plan[d][o] = prep ? prep->plan[d][o]
+                          : SpmmPlan{static_cast<const int2*>(vp.bnd), vp.longs, vp.nlong};
+    }
   if (prep) {   // the batch's weight-independent state lives in the prepared buffer
     w.node_root = prep->node_root;
     sp.item_tree = prep->item_tree; sp.tree_item0 = prep->tree_item0;

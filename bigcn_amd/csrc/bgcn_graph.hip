@@ -418,6 +418,24 @@ extern "C" int bgcn_build_graph(const int64_t* edge_index, const float* edge_wei
   return bgcn::build_graphs_impl(&a, 1, num_nodes, degree_on, reinterpret_cast<hipStream_t>(stream));
 }
 
+extern "C" int bgcn_graph_pair_plans(const void* workspace, size_t workspace_bytes, int64_t td_num_edges,
+                                     int64_t bu_num_edges, int64_t num_nodes, bgcn_spmm_plan td[2],
+                                     bgcn_spmm_plan bu[2]) {
+  if (!workspace || !td || !bu || num_nodes <= 0 || td_num_edges < 0 || bu_num_edges < 0)
+    return bgcn::fail(BGCN_EINVAL, "bad arguments");
+  const int64_t e = td_num_edges > bu_num_edges ? td_num_edges : bu_num_edges;
+  if (workspace_bytes < 2 * bgcn::align_up(bgcn::graph_ws_size(e, num_nodes), 256))
+    return bgcn::fail(BGCN_EINVAL, "workspace smaller than the build's");
+  bgcn::SpmmPlan p[2][2];
+  bgcn::graph_pair_plans(const_cast<void*>(workspace), workspace_bytes, td_num_edges, bu_num_edges, num_nodes,
+                         p[0], p[1]);
+  for (int o = 0; o < 2; ++o) {
+    td[o] = bgcn_spmm_plan{p[0][o].bnd, p[0][o].longs, p[0][o].nlong};
+    bu[o] = bgcn_spmm_plan{p[1][o].bnd, p[1][o].longs, p[1][o].nlong};
+  }
+  return BGCN_OK;
+}
+
 extern "C" size_t bgcn_graph_pair_workspace_size(int64_t td_num_edges, int64_t bu_num_edges,
                                                 int64_t num_nodes) {
   int64_t e = td_num_edges > bu_num_edges ? td_num_edges : bu_num_edges;

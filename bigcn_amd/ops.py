@@ -45,7 +45,8 @@ class Graph:
     live in two flat buffers (int32 / fp32, shared by the TD and BU graphs of a pair);
     the per-array tensors are views made on first access - the kernels take pointers."""
 
-    __slots__ = ("num_nodes", "num_edges", "capacity", "status", "_bufs", "_lay", "_views", "_ptrs")
+    __slots__ = ("num_nodes", "num_edges", "capacity", "status", "_bufs", "_lay", "_views", "_ptrs", "_plan",
+                 "_plan_ws")
 
     def _array(self, name: str) -> torch.Tensor:
         v = self._views.get(name)
@@ -61,6 +62,8 @@ class Graph:
         v.t_ptr, v.t_row, v.t_col, v.t_w = q["t_ptr"], q["t_row"], q["t_col"], q["t_w"]
         v.s_ptr, v.s_row, v.s_col, v.s_w = q["s_ptr"], q["s_row"], q["s_col"], q["s_w"]
         v.capacity = self.capacity
+        if self._plan is not None:   # the aggregation plans of bgcn_build_graph_pair
+            v.plan[0], v.plan[1] = self._plan
         return v
 
     def check(self) -> None:
@@ -95,6 +98,7 @@ def _alloc_graphs(edges, N: int, dev, status=None):
         g = Graph()
         g.num_nodes, g.num_edges, g.capacity, g.status = N, E, cap, st
         g._bufs, g._views, g._lay, g._ptrs = (bi, bf), {}, {}, {}
+        g._plan = g._plan_ws = None
         for name in _GRAPH_I32:
             n = N + 1 if name.endswith("ptr") else cap
             g._lay[name], g._ptrs[name] = (0, oi, n), pi + 4 * oi
@@ -151,6 +155,13 @@ def build_graph_pair(td_edge_index: torch.Tensor, bu_edge_index: torch.Tensor, n
     check(L.bgcn_build_graph_pair(td_ei.data_ptr(), td.num_edges, bu_ei.data_ptr(), bu.num_edges, N,
                                   dcode, ctypes.byref(a), ctypes.byref(b),
                                   td.status.data_ptr(), ws.data_ptr(), ws.numel(), stream_handle()))
+    # the build leaves both graphs' aggregation plans in its workspace: keep it with the
+    # graphs so the fused encoder takes the planned aggregation
+    pt, pb = (_lib.SpmmPlan * 2)(), (_lib.SpmmPlan * 2)()
+    check(L.bgcn_graph_pair_plans(ws.data_ptr(), ws.numel(), td.num_edges, bu.num_edges, N,
+                                  ctypes.addressof(pt), ctypes.addressof(pb)))
+    td._plan, bu._plan = (pt[0], pt[1]), (pb[0], pb[1])
+    td._plan_ws = bu._plan_ws = ws
     if validate:
         td.check()
     return td, bu

@@ -47,7 +47,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 5
+#define BGCN_ABI_VERSION 6
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -218,11 +218,30 @@ int bgcn_drop_edges(const int64_t* td_edge_index, int64_t td_num_edges, double t
  * from an injected bitmask keep_words[2][N][nw], nw = ceil((H+F)/32),
  * bit j of word w = column 32w + j; set bit = keep (x2).
  * -------------------------------------------------------------------------- */
+/* The aggregation plan of one CSR orientation (chunk bounds + the list of long rows),
+ * written by the graph builders into their workspace; all NULL = no plan. */
+typedef struct bgcn_spmm_plan {
+  const void* bnd; const int32_t* longs; const int32_t* nlong;
+} bgcn_spmm_plan;
+
 typedef struct bgcn_graph_view {
   const int32_t* t_ptr; const int32_t* t_row; const int32_t* t_col; const float* t_w;
   const int32_t* s_ptr; const int32_t* s_row; const int32_t* s_col; const float* s_w;
   int64_t capacity; /* E + N */
+  /* optional (ABI 6): the plans of the forward (by target) and backward (by source)
+   * aggregations, from bgcn_graph_pair_plans; zeros = merge-path chunks + fix-up */
+  bgcn_spmm_plan plan[2];
 } bgcn_graph_view;
+
+/* The aggregation plans a bgcn_build_graph_pair call left in its workspace (valid while
+ * that workspace is kept unmodified; same sizes as the build): plan[0] = forward
+ * aggregation (rows = targets), plan[1] = backward (rows = sources), per direction.  A
+ * bgcn_graph_view carrying them lets the fused encoder take the planned aggregation
+ * (complete rows per chunk, one launch, no fix-up) and the sign-word readout backward,
+ * as bgcn_train_step does with its prepared batch. */
+int bgcn_graph_pair_plans(const void* workspace, size_t workspace_bytes, int64_t td_num_edges,
+                          int64_t bu_num_edges, int64_t num_nodes, bgcn_spmm_plan td[2],
+                          bgcn_spmm_plan bu[2]);
 
 /* Feature path of the fused encoder.  AUTO: X is read once and every row compacted to a
  * list of its (col, val) non-zeros: the first BGCN_SPARSE_CAP in an ELL list, the rest of

@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = _lib.load_library()
     for name in _declared_functions():
         assert hasattr(lib, name), name
-    assert lib.bgcn_abi_version() == 5
+    assert lib.bgcn_abi_version() == 6
 
 
 def test_workspace_queries_without_gpu():
@@ -65,7 +65,7 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     structs = {
         "bgcn_graph_view": _lib.GraphView, "bgcn_csr_out": _lib.CsrOut,
         "bgcn_bigcn_args": _lib.BiGCNArgs, "bgcn_step_args": _lib.StepArgs,
-        "bgcn_adam_args": AdamArgs, "bgcn_batch": _lib.BatchDesc,
+        "bgcn_adam_args": AdamArgs, "bgcn_batch": _lib.BatchDesc, "bgcn_spmm_plan": _lib.SpmmPlan,
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for cname, py in structs.items():

@@ -308,3 +308,31 @@ def test_model_sparse_hint_matches_gated_auto():
     assert torch.equal(out[0][0], out[1][0])
     for a, c in zip(out[0][1], out[1][1]):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("plan", ["1", "0"])
+def test_model_train_step_matches_oracle(plan, monkeypatch):
+    """The drop-in model step (BiGCN.forward -> F.nll_loss -> backward) at F = 5000 in
+    training mode against the oracle with the in-kernel dropout draw materialised.  The
+    model's graphs come from bgcn_build_graph_pair with their aggregation plans
+    (bgcn_graph_pair_plans): plan "1" runs the planned aggregation and the sign-word readout
+    backward, "0" (BGCN_SPMM_PLAN=0) the merge-path chunks + fix-up and k_readout_bwd."""
+    from bigcn_amd import BiGCN
+    from bigcn_amd.ops import keep_words, unpack_keep
+    monkeypatch.setenv("BGCN_SPMM_PLAN", plan)
+    b = _synth(25, 12, 120, root_random=True)
+    p = O.make_params(5000, 64, 64, 4, seed=7)
+    m = BiGCN(5000, 64, 64, DEV).to(DEV)
+    m.load_state_dict({k: v.float() for k, v in p.items()})
+    m.train()
+    seed = 424242
+    logp = m(b, seed=seed)
+    loss = F.nll_loss(logp, b.y)
+    loss.backward()
+    km = unpack_keep(keep_words(seed, b.x.size(0), 5000, DEV), 64 + 5000).cpu()
+    rlogp, rloss, rgrads, _ = _oracle(b, p, True, km[0], km[1])
+    close(logp, rlogp, what="logp")
+    close(loss, rloss, what="loss")
+    grads = dict((k, q.grad) for k, q in m.named_parameters())
+    for k in p:
+        close(grads[k], rgrads[k], what=k)
