@@ -235,7 +235,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, uint
   void* base = reinterpret_cast<void*>(uint64_t(lo) | (uint64_t(hi) << 32));
   return __builtin_amdgcn_make_buffer_rsrc(base, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
-constexpr int kAuxNT = 2;   // buffer-load cache policy: non-temporal
+#ifndef BGCN_X_AUX
+#define BGCN_X_AUX 2   // A/B: the cache-policy bits of the pass over X (sc0 = 1, nt = 2, sc1 = 16)
+#endif
+constexpr int kAuxNT = BGCN_X_AUX;   // buffer-load cache policy: non-temporal
 // 16 B of an X row as one lane loads it: four fp32 or eight bf16 elements.  The zero
 // tests work on the raw bits (magnitude bits only: -0 is zero, NaN is not, as `!= 0.f`),
 // so a bf16 chunk costs the same instructions as an fp32 one for twice the elements.
