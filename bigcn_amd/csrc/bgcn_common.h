@@ -68,12 +68,14 @@ struct Carve {
 // fused step: aux_fork sets *branch to lane's stream after making it wait for the work
 // queued on `main` so far; aux_join makes `main` wait for everything queued on the lane.
 // On the legacy null stream (whose cross-stream waits synchronise the host) *branch =
-// main and the branch runs inline.  One lane is used: HIP maps streams onto a few
-// hardware queues (GPU_MAX_HW_QUEUES) and measured, only one extra stream reliably got a
-// queue of its own; the branches are ordered so that sharing it costs nothing (the
-// train step's graph build finishes on it long before the CSC of X is queued behind).
-constexpr int kAuxLanes = 1;
+// main and the branch runs inline.  The side lane carries every branch of the step; the
+// graph lane (created on first use) only the next batch's DropEdge + K1 beside its pass over
+// X (prep_pipeline).  HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES = 4):
+// the graph lane's work ends inside the pass over X, long before any collective of the step
+// is queued.
+constexpr int kAuxLanes = 2;
 constexpr int kLaneSide = 0;
+constexpr int kLaneGraph = 1;   // the next batch's DropEdge + K1 beside its pass over X
 int aux_fork(hipStream_t main, int lane, hipStream_t* branch);
 int aux_join(hipStream_t main, int lane);
 // the next-batch preparation of bgcn_train_step is not joined by its own call: its end is

@@ -44,15 +44,15 @@ struct AuxState {
 AuxState g_aux[kMaxDevices];
 std::mutex g_aux_mu;
 
-// All lanes of a device are created together, on first use.
+// Each lane of a device is created on its first use.
 AuxState* aux_state(int lane) {
   int dev = 0;
   if (lane < 0 || lane >= kAuxLanes) return nullptr;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
   AuxState& a = g_aux[dev];
-  if (!a.stream[kAuxLanes - 1]) {
-    for (int k = 0; k < kAuxLanes; ++k) {
-      if (a.stream[k]) continue;
+  if (!a.stream[lane]) {   // a lane's stream is created on its first use (an unused lane
+                           // takes no hardware queue)
+    for (int k = lane; k <= lane; ++k) {
       hipStream_t st;
       // BGCN_SIDE_CU_EVERY=k (A/B knob, read at lane creation): the lane may not use CU i
       // when i % k == k - 1, leaving those CUs to the caller's chain

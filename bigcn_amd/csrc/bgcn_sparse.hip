@@ -2050,6 +2050,9 @@ int sparse_csc(SparseState& S, hipStream_t s) {
   return BGCN_OK;
 }
 
+#ifndef BGCN_PREP_LANES_DEFAULT
+#define BGCN_PREP_LANES_DEFAULT 2   // profiles/r03_chain_experiments_late.txt
+#endif
 int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree_on, int mode,
                   hipStream_t s, bool x_part) {
   const int64_t N = bt->num_nodes, B = bt->num_graphs;
@@ -2140,13 +2143,54 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   const dim3 blk(256);
   hipLaunchKernelGGL(k_prep_a, dim3(unsigned(a.nz + a.nRP + a.nbd[0] + a.nbd[1])), blk, 0, s, a);
   BGCN_CHECK_LAUNCH();
+  const size_t hist_smem = xp ? size_t(F) * sizeof(int32_t) : 0;
+  // Two lanes (the default; BGCN_PREP_LANES=1, read once, keeps one): DropEdge select + K1
+  // run on a second lane beside the pass over X, and the CSC of X follows the pass on the
+  // side lane - the roles of each merged launch split by chain.  K1's four latency-bound
+  // launches then overlap the X window, where the chain is stalled anyway, instead of the
+  // chain's second half: twitter15 0.2691-0.2724 vs 0.2732-0.2749 ms per step over five
+  // interleaved rounds, synth1024_bf16 -0.7 %, weibo_bf16 within its noise (+0.5 %)
+  static const int lanes = [] {
+    const char* e = std::getenv("BGCN_PREP_LANES");
+    return e ? atoi(e) : BGCN_PREP_LANES_DEFAULT;
+  }();
+  if (lanes == 2 && xp) {
+    hipStream_t g = s;
+    BGCN_TRY(aux_fork(s, kLaneGraph, &g));
+    PrepArgs ag = a;           // graph chain: DropEdge select, K1 count / scan / fill / norm
+    ag.ncomp = 0; ag.R = 0; ag.nprefix = 0;
+    PrepArgs ax = a;           // X chain: tree items, the pass over X, the CSC of X
+    ax.nsel = 0; ax.nce = 0; ax.ntile = 0; ax.ne = 0; ax.nn = 0; ax.np = 0;
+    if (ag.nsel > 0) {
+      if (bt->x_dtype == BGCN_DTYPE_BF16) hipLaunchKernelGGL(k_prep_b<bf16_t>, dim3(unsigned(ag.nsel)), blk, 0, g, ag);
+      else hipLaunchKernelGGL(k_prep_b<float>, dim3(unsigned(ag.nsel)), blk, 0, g, ag);
+      BGCN_CHECK_LAUNCH();
+    }
+    if (ag.nce > 0) hipLaunchKernelGGL(k_prep_c, dim3(unsigned(2 * ag.nce)), blk, 0, g, ag);
+    if (ag.ntile > 0) hipLaunchKernelGGL(k_prep_d, dim3(unsigned(2 * ag.ntile)), blk, 0, g, ag);
+    if (ag.ne + ag.nn > 0) hipLaunchKernelGGL(k_prep_e, dim3(unsigned(2 * (ag.ne + ag.nn))), blk, 0, g, ag);
+    if (ag.ne + ag.nn + ag.np > 0)
+      hipLaunchKernelGGL(k_prep_f, dim3(unsigned(2 * (ag.ne + ag.nn + ag.np))), blk, 0, g, ag);
+    BGCN_CHECK_LAUNCH();
+    timing_begin(7, s);
+    if (bt->x_dtype == BGCN_DTYPE_BF16) hipLaunchKernelGGL(k_prep_b<bf16_t>, dim3(unsigned(1 + ax.ncomp)), blk, 0, s, ax);
+    else hipLaunchKernelGGL(k_prep_b<float>, dim3(unsigned(1 + ax.ncomp)), blk, 0, s, ax);
+    BGCN_CHECK_LAUNCH();
+    timing_end(7, s);
+    hipLaunchKernelGGL(k_prep_c, dim3(unsigned(ax.R)), blk, hist_smem, s, ax);
+    hipLaunchKernelGGL(k_prep_d, dim3(unsigned(ax.nprefix)), blk, 0, s, ax);
+    hipLaunchKernelGGL(k_prep_e, dim3(1u), blk, 0, s, ax);
+    hipLaunchKernelGGL(k_prep_f, dim3(unsigned(ax.R)), blk, 2 * hist_smem, s, ax);
+    BGCN_CHECK_LAUNCH();
+    BGCN_TRY(aux_join(s, kLaneGraph));
+    return BGCN_OK;
+  }
   timing_begin(7, s);
   const unsigned nb = unsigned(a.nsel + 1 + a.ncomp);
   if (bt->x_dtype == BGCN_DTYPE_BF16) hipLaunchKernelGGL(k_prep_b<bf16_t>, dim3(nb), blk, 0, s, a);
   else hipLaunchKernelGGL(k_prep_b<float>, dim3(nb), blk, 0, s, a);
   BGCN_CHECK_LAUNCH();
   timing_end(7, s);
-  const size_t hist_smem = xp ? size_t(F) * sizeof(int32_t) : 0;
   if (2 * a.nce + a.R > 0) {
     hipLaunchKernelGGL(k_prep_c, dim3(unsigned(2 * a.nce + a.R)), blk, hist_smem, s, a);
     BGCN_CHECK_LAUNCH();
