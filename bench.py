@@ -80,7 +80,7 @@ KERNEL_CLASSES = {
              2: "conv2 (sparse root gather)", 3: "k_bwd_mid: dW2 partials + root partials + dH1",
              5: "k_bwd_tail: dW1 over CSC(X) + dW2 root columns + reductions",
              7: "k_prep_b: paced X read + BoW compaction of the next batch beside the training chain "
-                "(+ its DropEdge select, tree items)"},
+                "(+ its tree items; its DropEdge select and K1 run on a second lane)"},
 }
 SPARSE_CAP = 32
 # rocprofv3 kernel symbol of each timed class (for the PMC traffic lookup)
@@ -89,7 +89,7 @@ ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2):
                  ("auto", 7): "bgcn::k_prep_b<float>",
                  ("dense", 0): "bgcn::k_gemm_xwt<true, false, float>", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
                  ("dense", 2): "bgcn::k_conv2_fwd<float>", ("dense", 3): "bgcn::k_dw2<float>"}
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
 
 
 def pmc_traffic(mode: str, cls: int, workload: str = "twitter15"):
@@ -266,7 +266,7 @@ def compaction_standalone(fused, b, wl, iters: int = 10):
     N = int(b.x.size(0))
     xbytes = 2 if wl.get("xdtype") == "bf16" else 4
     nbytes = N * F * xbytes + N * (SPARSE_CAP * 8.0 + 4.0)
-    out = {"kernel": "k_prep_b (X read + BoW compaction + DropEdge select + tree items), alone on the GPU",
+    out = {"kernel": "k_prep_b (X read + BoW compaction + tree items), alone on the GPU",
            "bytes_per_launch": nbytes}
     old = os.environ.get("BGCN_PREP_BLOCKS")
     try:
