@@ -19,10 +19,11 @@
  *     never allocates or frees caller memory.  Scratch comes from a caller-provided
  *     workspace whose size is returned by the matching *_workspace_size() call;
  *   - every call is asynchronous on the given stream and performs no host sync.  Global
- *     state: the thread-local error string, the opt-in kernel-timing hook, and three
- *     auxiliary HIP streams ("lanes") per device (created on first use) that the fused
- *     encoder and train step fork independent branches onto and join back into the
- *     caller's stream before returning (inline on the legacy null stream);
+ *     state: the thread-local error string, the opt-in kernel-timing hook, and two
+ *     auxiliary HIP streams ("lanes") per device (each created on first use) that the
+ *     fused encoder and train step fork independent branches onto and join back into the
+ *     caller's stream (inline on the legacy null stream); bgcn_train_step's next-batch
+ *     preparation is waited for by the next call instead (bgcn_join_side);
  *   - return value: 0 = ok, BGCN_EINVAL (-1) = invalid argument / shape,
  *     BGCN_EHIP (-2) = HIP launch error.  bgcn_last_error() gives a thread-local
  *     message.  Data-dependent errors (an edge index outside [0, N)) cannot be
