@@ -480,6 +480,11 @@ def main():
                         "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(mode, c, args.workload),
                         "kernel": KERNEL_CLASSES[mode][c], "bytes_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
+                if mode == "auto" and c == 7 and args.prefetch:
+                    roof["note"] = ("HIP events around the launch on the side lane: the bracket includes the "
+                                    "pass's dispatch delay beside the second preparation lane's launches; the "
+                                    "rocprofv3 kernel time of the same command is ~17 % shorter "
+                                    "(profiles/r03_kernel_stats.csv, BASELINE.md)")
         value = wl["trees"] * world * steps / dt
         # the step's validity (one host read after the timed region): the OR of the timed
         # steps' status words and the optimiser updates skipped as invalid, max over ranks
