@@ -298,6 +298,68 @@ def compaction_standalone(fused, b, wl, iters: int = 10):
     return out
 
 
+def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int, trees: int):
+    """SURVEY.md 8(f) row 1 / 8(d) "staging reported separately": the same training step fed
+    from the host the way the reference's loop is (BiGCN_Twitter.py:168,174-176:
+    DataLoader(..., shuffle=True, num_workers=5) -> Batch_data.to(device)) - a real
+    torch.utils.data.DataLoader with worker processes over a packed store of synthetic trees
+    of the workload's shape; workers collate each 128-tree batch into a shared page-locked
+    slot with x as the CSR of its non-zeros; one H2D copy per batch on a dedicated stream,
+    issued `depth` batches ahead; the step prepares the next batch from the compacted lists
+    (no pass over a dense x).  Timed: everything (loader, copies, steps, Adam)."""
+    from bigcn_amd import feed as FD
+    t0 = time.perf_counter()
+    store = FD.TreeStore.synthetic(trees, wl["mean"], seed=20250205 + 9, in_feats=wl["feats"],
+                                   num_classes=wl["classes"])
+    t_store = time.perf_counter() - t0
+    per_epoch = trees // wl["trees"]
+    epochs = (steps + warmup + 4) // per_epoch + 2
+    loader = FD.host_fed_loader(store, batch_size=wl["trees"], num_workers=workers, seed=7, epochs=epochs,
+                                bf16_values=wl.get("xdtype") == "bf16")
+    xdt = torch.bfloat16 if wl.get("xdtype") == "bf16" else torch.float32
+    with torch.cuda.stream(stream):
+        feeder = FD.DeviceFeeder(loader, dev, depth=3, x_dtype=xdt, timing=True)
+        it = iter(feeder)
+        cur = next(it)
+        for _ in range(warmup):
+            nxt = next(it)
+            fused(cur, next_data=nxt)
+            cur = nxt
+        torch.cuda.synchronize()
+        feeder.copy_stats(reset=True)
+        fused.run_report(reset=True)
+        nodes = 0
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            nxt = next(it)
+            fused(cur, next_data=nxt)
+            nodes += cur.num_nodes
+            cur = nxt
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        fused.discard_prefetch()
+    n, mean_bytes, copy_ms = feeder.copy_stats()
+    report = fused.run_report()
+    loader.dataset.ring.close()
+    del it, feeder, loader
+    dense_bytes = nodes / steps * wl["feats"] * (2 if xdt == torch.bfloat16 else 4)
+    return {"host_fed": {"value": round(wl["trees"] * steps / dt, 2), "unit": "trees/s",
+                         "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+                         "status": report["status"], "invalid_steps": report["invalid_steps"]},
+            "h2d_bytes_per_batch": round(mean_bytes), "h2d_ms_per_batch": round(copy_ms, 4),
+            "h2d_gbs": round(mean_bytes / (copy_ms * 1e-3) / 1e9, 2) if copy_ms > 0 else None,
+            "dense_x_bytes_per_batch": round(dense_bytes),
+            "dense_x_h2d_ms_at_measured_rate": (round(dense_bytes / (mean_bytes / copy_ms), 3)
+                                                if mean_bytes > 0 and copy_ms > 0 else None),
+            "loader": {"num_workers": workers, "batch_size": wl["trees"], "store_trees": trees,
+                       "store_build_s": round(t_store, 2), "avg_nodes_per_batch": round(nodes / steps, 1),
+                       "copy_depth": 3},
+            "what": "torch.utils.data.DataLoader (worker processes, shuffle) over a packed tree store -> "
+                    "batch packed by the worker into a shared page-locked slot (x as CSR of its non-zeros) "
+                    "-> one H2D copy per batch on a copy stream, 3 batches ahead -> FusedTrainStep with "
+                    "next-batch prefetch and device DropEdge; whole loop timed (BiGCN_Twitter.py:168,174-176)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -332,6 +394,12 @@ def main():
                          "draw is then neither repeated nor timed)")
     ap.add_argument("--compare-dropedge", type=int, default=1,
                     help="at N=1 also time the other DropEdge placement and report it beside the main line")
+    ap.add_argument("--host-fed", type=int, default=1,
+                    help="at N=1 also run the step host-fed through a DataLoader with worker processes "
+                         "(the staging object)")
+    ap.add_argument("--host-fed-workers", type=int, default=5,
+                    help="DataLoader worker processes of the host-fed run (the reference's num_workers=5)")
+    ap.add_argument("--host-fed-trees", type=int, default=2048, help="trees in the host-fed run's store")
     ap.add_argument("--dropin", type=int, default=1,
                     help="at N=1 also time the drop-in path (model(data), loss.backward(), the "
                          "optimiser: --path autograd) and report it beside the main line")
@@ -517,6 +585,11 @@ def main():
         ctx["path"] = "autograd"
         dropin_res = run(args.feat_mode, max(5, args.steps // 2), 3)
         ctx["pool"], ctx["path"] = pool, args.path
+    staging = None
+    if world == 1 and args.path == "fused" and args.host_fed and args.feat_mode == "auto":
+        # same model / optimiser / DropEdge as the headline step (its state continues)
+        staging = host_fed_bench(fused, wl, dev, stream, max(20, args.steps), min(args.warmup, 10),
+                                 args.host_fed_workers, args.host_fed_trees)
     agg = None
     if world == 1 and args.aggregation:
         agg = aggregation_bench(pool[0])
@@ -549,6 +622,9 @@ def main():
             "dropedge": ("device, re-drawn every step (timed)" if device_drop
                          else "host, applied once per pool batch at synthesis (not timed)"),
         }
+        if staging is not None:
+            staging["host_fed_over_headline"] = round(staging["host_fed"]["value"] / value, 4)
+            out["staging"] = staging
         if agg is not None:
             out["aggregation_5000"] = agg
         if comp is not None:

@@ -32,7 +32,8 @@ BGCN_SPARSE_CAP = 32
 BGCN_SPARSE_SPILL_PER_ROW = 32   # spill pool capacity per row (rows over the ELL cap)
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1
-ABI_VERSION = 6   # BGCN_ABI_VERSION of include/bgcn.h
+ABI_VERSION = 7   # BGCN_ABI_VERSION of include/bgcn.h
+BGCN_STATUS_CROSS_TREE = 16
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
@@ -47,7 +48,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_drop_edges_workspace_size", "bgcn_drop_edges",
     "bgcn_bigcn_workspace_size", "bgcn_bigcn_forward", "bgcn_bigcn_backward",
     "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_adam_step",
-    "bgcn_prepare_workspace_size", "bgcn_prepare_batch",
+    "bgcn_prepare_workspace_size", "bgcn_prepare_batch", "bgcn_csr_to_dense",
     "bgcn_train_step_workspace_size", "bgcn_train_step", "bgcn_train_step_dw1", "bgcn_join_side",
     "bgcn_weight_images_size", "bgcn_train_step_saved",
 )
@@ -62,7 +63,7 @@ class GraphView(Structure):
     _fields_ = [
         ("t_ptr", c_void_p), ("t_row", c_void_p), ("t_col", c_void_p), ("t_w", c_void_p),
         ("s_ptr", c_void_p), ("s_row", c_void_p), ("s_col", c_void_p), ("s_w", c_void_p),
-        ("capacity", c_int64), ("plan", SpmmPlan * 2),
+        ("capacity", c_int64), ("plan", SpmmPlan * 2), ("tree_status", c_void_p),
     ]
 
 
@@ -103,6 +104,7 @@ class BatchDesc(Structure):
         ("bu_edge_index", c_void_p), ("bu_num_edges", c_int64),
         ("td_droprate", c_double), ("bu_droprate", c_double), ("drop_seed", c_uint64),
         ("x_dtype", c_int32),
+        ("x_row_ptr", c_void_p), ("x_col", c_void_p), ("x_val", c_void_p),
     ]
 
 
@@ -132,8 +134,8 @@ _SIGS = {
                                  c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_graph_pair_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
     "bgcn_build_graph_pair": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int,
-                                      POINTER(CsrOut), POINTER(CsrOut), c_void_p, c_void_p, c_size_t,
-                                      c_void_p]),
+                                      POINTER(CsrOut), POINTER(CsrOut), c_void_p, c_void_p, c_void_p,
+                                      c_size_t, c_void_p]),
     "bgcn_spmm_workspace_size": (c_size_t, [c_int64, c_int32]),
     "bgcn_spmm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                           c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int, c_void_p,
@@ -171,6 +173,8 @@ _SIGS = {
     "bgcn_prepare_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64, c_int64]),
     "bgcn_prepare_batch": (c_int, [POINTER(BatchDesc), c_int64, c_int32, c_int32, c_void_p, c_size_t,
                                    c_void_p]),
+    "bgcn_csr_to_dense": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32,
+                                  c_void_p, c_void_p]),
     "bgcn_train_step_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64, c_int64, c_int64]),
     "bgcn_train_step": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_train_step_dw1": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),

@@ -27,7 +27,11 @@ def _graphs(data, degree_on: str = "col"):
     if cache is not None and cache[0] == degree_on:
         return cache[1], cache[2]
     n = data.x.size(0)
-    td, bu = build_graph_pair(data.edge_index, data.BU_edge_index, n, degree_on=degree_on)
+    # with the batch vector K1 also checks that every edge stays inside its tree (the
+    # encoder's fast readout backward relies on knowing it)
+    batch = getattr(data, "batch", None)
+    td, bu = build_graph_pair(data.edge_index, data.BU_edge_index, n, degree_on=degree_on,
+                              batch=batch if batch is not None and batch.numel() == n else None)
     try:
         data._bgcn_graphs = (degree_on, td, bu)
     except AttributeError:

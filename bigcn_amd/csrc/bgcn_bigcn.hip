@@ -609,6 +609,9 @@ struct FusedWs {
   int S2d; int64_t kchunk2d;              // the dense feature mode's dW2 node splits (more: shorter loops)
   int Sh; int64_t kchunkh;
   SpmmPlan plan[2][2];                    // [td, bu][forward, backward] (prepared batch) or null
+  // [td, bu] status words of graph builds that checked tree-locality (the prepared batch's,
+  // or bgcn_graph_view.tree_status); either null: the sign-word readout backward is off
+  const int32_t* tree_status[2];
 };
 
 int dw2_splits(int64_t N, int64_t F) {
@@ -679,13 +682,16 @@ size_t fused_ws_fixed(int64_t N, int64_t B, int64_t F) {
   return c.off;
 }
 
-int check_args(const bgcn_bigcn_args* a) {
+// prepared: the batch comes prepared (bgcn_train_step); under BGCN_FEAT_SPARSE its x is then
+// never read and may be NULL (host-fed compacted features)
+int check_args(const bgcn_bigcn_args* a, bool prepared = false) {
+  const bool need_x = !(prepared && a->feat_mode == BGCN_FEAT_SPARSE);
   BGCN_CHECK_ARG(a, "null args");
   BGCN_CHECK_ARG(a->hid == H, "fused path requires hid == out == 64");
   BGCN_CHECK_ARG(a->num_nodes > 0 && a->num_graphs > 0 && a->in_feats > 0, "bad sizes");
   BGCN_CHECK_ARG(a->in_feats % 4 == 0 && a->ldx % 4 == 0 && a->ldx >= a->in_feats,
                  "in_feats and ldx must be multiples of 4");
-  BGCN_CHECK_ARG(a->x && a->batch && a->rootindex && a->tree_ptr && a->h1 && a->h2,
+  BGCN_CHECK_ARG((a->x || !need_x) && a->batch && a->rootindex && a->tree_ptr && a->h1 && a->h2,
                  "null pointer");
   BGCN_CHECK_ARG(a->x_dtype == BGCN_DTYPE_F32 || a->x_dtype == BGCN_DTYPE_BF16, "bad x_dtype");
   BGCN_CHECK_ARG((reinterpret_cast<uintptr_t>(a->x) & 15) == 0, "x must be 16-byte aligned");
@@ -758,6 +764,10 @@ static int spmm_pair(const bgcn_graph_view& td, const bgcn_graph_view& bu, bool 
 // (read per call) keeps k_readout_bwd / the fused readout.
 static bool readout_sign(const bgcn_bigcn_args* a, const SparseState& sp, FusedWs& w) {
   if (sp.mode == 1) return false;
+  // the graphs' builds must have checked tree-locality (a cross-tree edge then switches the
+  // aggregation to per-neighbour tree scales on the device); unchecked graphs keep
+  // k_readout_bwd, which handles any edge set
+  if (!w.tree_status[0] || !w.tree_status[1]) return false;
   const char* e = std::getenv("BGCN_READOUT_SIGN");
   if (e && atoi(e) == 0) return false;
   const SpmmBatch sb = pair_batch(a->td, a->bu, true, a->num_nodes, nullptr, nullptr, nullptr, nullptr,
@@ -797,6 +807,8 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
       w.plan[d][o] = prep ? prep->plan[d][o]
                           : SpmmPlan{static_cast<const int2*>(vp.bnd), vp.longs, vp.nlong};
     }
+  w.tree_status[0] = prep ? prep->status : a->td.tree_status;
+  w.tree_status[1] = prep ? prep->status : a->bu.tree_status;
   if (prep) {   // the batch's weight-independent state lives in the prepared buffer
     w.node_root = prep->node_root;
     sp.item_tree = prep->item_tree; sp.tree_item0 = prep->tree_item0;
@@ -839,7 +851,7 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
 int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
                        int graph_lane, const HeadArgs* head, const Prepared* prep,
                        const WeightImages* img, bool img_current) {
-  BGCN_TRY(check_args(a));
+  BGCN_TRY(check_args(a, prep != nullptr));
   BGCN_CHECK_ARG(a->head_in && a->td_w1 && a->bu_w1 && a->td_w2 && a->bu_w2, "null pointer");
   const int64_t N = a->num_nodes, F = a->in_feats;
   FusedWs w;
@@ -962,7 +974,7 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
                         const Prepared* prep, bool side_busy, const HeadGradJob* head,
                         const WeightImages* img, bool defer_dw1) {
-  BGCN_TRY(check_args(a));
+  BGCN_TRY(check_args(a, prep != nullptr));
   BGCN_CHECK_ARG(a->dhead_in && a->td_dw1 && a->bu_dw1 && a->td_dw2 && a->bu_dw2 && a->td_db1 &&
                      a->bu_db1 && a->td_db2 && a->bu_db2,
                  "null gradient pointer");
@@ -990,7 +1002,8 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     BGCN_CHECK_LAUNCH();
   }
   // dZ2 = A^T dH2 (sign: dH2 generated from the readout's H2 sign words)
-  const SpmmSign sg{reinterpret_cast<const uint64_t*>(w.d2), a->dhead_in, a->batch, a->tree_ptr, B};
+  const SpmmSign sg{reinterpret_cast<const uint64_t*>(w.d2), a->dhead_in, a->batch, a->tree_ptr, B,
+                    {w.tree_status[0], w.tree_status[1]}};
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, sign ? nullptr : w.d2, w.dz2, nullptr, nullptr, BGCN_EPI_NONE, w, s,
                      sign ? &sg : nullptr));
   // the CSC of X, when the forward did not leave one, is built on the side lane
@@ -1090,7 +1103,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
 // inside the backward).
 int bigcn_backward_dw1(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s, const Prepared* prep,
                        const WeightImages* img) {
-  BGCN_TRY(check_args(a));
+  BGCN_TRY(check_args(a, prep != nullptr));
   BGCN_CHECK_ARG(a->td_dw1 && a->bu_dw1, "null gradient pointer");
   FusedWs w;
   SparseState sp{};

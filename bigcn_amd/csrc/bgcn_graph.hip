@@ -295,7 +295,7 @@ size_t graph_ws_size(int64_t E, int64_t N) {
 }
 
 int graph_batch_setup(const GraphArgs* ga, int count, int64_t N, int degree_on, GraphBatch* out,
-                      size_t zero_bytes[kMaxGraphs]) {
+                      size_t zero_bytes[kMaxGraphs], const int64_t* batch) {
   BGCN_CHECK_ARG(count >= 1 && count <= kMaxGraphs, "1 or 2 graphs per call");
   BGCN_CHECK_ARG(N > 0 && N < (int64_t(1) << 31) - 1, "num_nodes out of range");
   BGCN_CHECK_ARG(degree_on == BGCN_DEGREE_ON_COL || degree_on == BGCN_DEGREE_ON_ROW,
@@ -303,6 +303,7 @@ int graph_batch_setup(const GraphArgs* ga, int count, int64_t N, int degree_on, 
   GraphBatch gb{};
   gb.N = N;
   gb.degree_on = degree_on;
+  gb.batch = batch;
   for (int k = 0; k < count; ++k) {
     const GraphArgs& a = ga[k];
     BGCN_CHECK_ARG(a.E >= 0 && a.E + N < (int64_t(1) << 31), "num_edges out of range");
@@ -322,7 +323,8 @@ int graph_batch_setup(const GraphArgs* ga, int count, int64_t N, int degree_on, 
   return BGCN_OK;
 }
 
-int build_graphs_impl(const GraphArgs* ga, int count, int64_t N, int degree_on, hipStream_t s) {
+int build_graphs_impl(const GraphArgs* ga, int count, int64_t N, int degree_on, hipStream_t s,
+                      const int64_t* batch) {
   BGCN_CHECK_ARG(count >= 1 && count <= kMaxGraphs, "1 or 2 graphs per call");
   BGCN_CHECK_ARG(N > 0 && N < (int64_t(1) << 31) - 1, "num_nodes out of range");
   BGCN_CHECK_ARG(degree_on == BGCN_DEGREE_ON_COL || degree_on == BGCN_DEGREE_ON_ROW,
@@ -330,6 +332,7 @@ int build_graphs_impl(const GraphArgs* ga, int count, int64_t N, int degree_on, 
   GraphBatch gb{};
   gb.N = N;
   gb.degree_on = degree_on;
+  gb.batch = batch;
   int64_t Emax = 0;
   for (int k = 0; k < count; ++k) {
     const GraphArgs& a = ga[k];
@@ -415,7 +418,7 @@ extern "C" int bgcn_build_graph(const int64_t* edge_index, const float* edge_wei
                                 bgcn_stream_t stream) {
   bgcn::GraphArgs a{edge_index, edge_weight, num_edges, t_ptr, t_row, t_col, t_w,
                     s_ptr, s_row, s_col, s_w, status, workspace, workspace_bytes};
-  return bgcn::build_graphs_impl(&a, 1, num_nodes, degree_on, reinterpret_cast<hipStream_t>(stream));
+  return bgcn::build_graphs_impl(&a, 1, num_nodes, degree_on, reinterpret_cast<hipStream_t>(stream), nullptr);
 }
 
 extern "C" int bgcn_graph_pair_plans(const void* workspace, size_t workspace_bytes, int64_t td_num_edges,
@@ -458,8 +461,8 @@ void graph_pair_args(const int64_t* td_ei, int64_t Etd, const int64_t* bu_ei, in
 extern "C" int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_num_edges,
                                      const int64_t* bu_edge_index, int64_t bu_num_edges,
                                      int64_t num_nodes, int degree_on, const bgcn_csr_out* td,
-                                     const bgcn_csr_out* bu, int32_t* status, void* workspace,
-                                     size_t workspace_bytes, bgcn_stream_t stream) {
+                                     const bgcn_csr_out* bu, const int64_t* batch, int32_t* status,
+                                     void* workspace, size_t workspace_bytes, bgcn_stream_t stream) {
   using bgcn::GraphArgs;
   if (!td || !bu) return bgcn::fail(BGCN_EINVAL, "null csr descriptor");
   const size_t half = workspace_bytes / 2 / 256 * 256;
@@ -469,5 +472,5 @@ extern "C" int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_nu
        td->s_row, td->s_col, td->s_w, status, ws, half},
       {bu_edge_index, nullptr, bu_num_edges, bu->t_ptr, bu->t_row, bu->t_col, bu->t_w, bu->s_ptr,
        bu->s_row, bu->s_col, bu->s_w, status, ws ? ws + half : nullptr, half}};
-  return bgcn::build_graphs_impl(a, 2, num_nodes, degree_on, reinterpret_cast<hipStream_t>(stream));
+  return bgcn::build_graphs_impl(a, 2, num_nodes, degree_on, reinterpret_cast<hipStream_t>(stream), batch);
 }

@@ -49,6 +49,7 @@ struct GraphBatch {
   GraphIO g[kMaxGraphs];
   int64_t N;
   int degree_on;
+  const int64_t* batch;   // optional [N] tree ids: an edge across trees sets BGCN_STATUS_CROSS_TREE
 };
 
 __device__ __forceinline__ bool edge_kept(const int64_t* ei, int64_t E, int64_t N, int64_t e,
@@ -107,6 +108,9 @@ __device__ inline void graph_count_body(const GraphBatch& gb, const GraphIO& G, 
       kept = true;
       ksrc = src;
       kdst = dst;
+      // a propagation tree's edges stay inside it (PyG collation); the fused readout
+      // backward needs to know when they do not (bgcn.h BGCN_STATUS_CROSS_TREE)
+      if (gb.batch && G.status && gb.batch[src] != gb.batch[dst]) atomicOr(G.status, BGCN_STATUS_CROSS_TREE);
       int64_t psrc = -1, pdst = -1;
       if (e > 0) {
         bool pv;
@@ -416,7 +420,7 @@ struct GraphArgs {
 // the GraphBatch of 1-2 graphs without launching anything; zero_bytes[k]: the prefix of
 // graph k's workspace (at gb.g[k].cnt_t) that must be zero before the count step
 int graph_batch_setup(const GraphArgs* ga, int count, int64_t N, int degree_on, GraphBatch* out,
-                      size_t zero_bytes[kMaxGraphs]);
+                      size_t zero_bytes[kMaxGraphs], const int64_t* batch = nullptr);
 // GraphArgs of bgcn_build_graph_pair's layout (two workspace halves)
 void graph_pair_args(const int64_t* td_ei, int64_t Etd, const int64_t* bu_ei, int64_t Ebu,
                      const bgcn_csr_out* td, const bgcn_csr_out* bu, int32_t* status, void* workspace,

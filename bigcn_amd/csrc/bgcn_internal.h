@@ -35,6 +35,9 @@ struct SpmmSign {
   const int64_t* batch;      // [rows] node -> tree
   const int32_t* tree_ptr;   // [B + 1]
   int64_t B;
+  // per problem (TD, BU): the graph build's status word; BGCN_STATUS_CROSS_TREE set = some
+  // neighbour lies in another tree, so each gathered row takes its own tree's scale
+  const int32_t* tree_status[2];
 };
 
 struct SpmmBatch {
@@ -164,7 +167,9 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
     }
   }
   if (l == 0 && !yok) hd.loss_row[b] = 0.f;
-  if (l == 0 && b == 0 && hd.in_status && hd.status && *hd.in_status) atomicOr(hd.status, *hd.in_status);
+  // the prepared batch's K1 flags: bits 0-3 (BGCN_STATUS_CROSS_TREE is information, the
+  // readout backward handles such edges)
+  if (l == 0 && b == 0 && hd.in_status && hd.status && (*hd.in_status & 15)) atomicOr(hd.status, *hd.in_status & 15);
   if (l == 0 && b == 0 && hd.in_xflags && hd.status && *hd.in_xflags) atomicOr(hd.status, 4);
   st4(hd.dhead + b * kHeadIn + 4 * l, dh);
 }

@@ -84,7 +84,7 @@ struct Prepared;
 // part 1: node maps, tree items, the ELL of X (the pass over X); part 2: the CSC of X
 int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
                    const int64_t* batch, const int64_t* rootindex, const void* X, int xdt, int64_t ldx,
-                   hipStream_t s, int part = 3);
+                   hipStream_t s, int part = 3, const bgcn_batch* csr = nullptr);
 int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s);
 int sparse_compact_conv1(SparseState& S, const void* X, int xdt, int64_t ldx, float* Z1,
                          hipStream_t s);

@@ -415,6 +415,88 @@ __device__ inline void compact_body(const SparseState& S, const TX* __restrict__
   }
 }
 
+// The host-fed input form (bgcn_batch.x_row_ptr / x_col / x_val): the rows arrive already
+// compacted, in ascending column order, so the ELL list, the spill pool and the long-row
+// list are filled from them with the contents compact_row writes from the dense row (the
+// step computes the same bits either way).  One 32-lane half-wave per row (a BoW row holds
+// ~12 entries), grid-stride; reads nnz x 8 bytes instead of N x F x 4.
+__device__ inline void csr_ell_body(const SparseState& S, const int32_t* __restrict__ rp,
+                                    const int32_t* __restrict__ rc, const float* __restrict__ rv, int bid,
+                                    int nblk) {
+  if (S.mode == 1) return;
+  const int lane = threadIdx.x & 31;
+  const int64_t nhalf = int64_t(nblk) * (blockDim.x / 32);
+  for (int64_t i = (int64_t(bid) * blockDim.x + threadIdx.x) / 32; i < S.N; i += nhalf) {
+    const int32_t b = rp[i], cnt = rp[i + 1] - b;      // half-wave uniform
+    const int ce = cnt < kCap ? cnt : kCap;
+    if (lane < ce) {
+      S.cols[i * kCap + lane] = rc[b + lane];
+      S.vals[i * kCap + lane] = rv[b + lane];
+    }
+    if (lane == 0) S.nnz[i] = cnt;
+    if (cnt > kCap) {   // a long row: its tail to the spill pool, as compact_row does
+      const int nov = cnt - kCap;
+      int o = 0;
+      if (lane == 0) o = atomicAdd(&S.flags[1], nov);
+      o = __shfl(o, 0, 32);
+      if (o < 0 || int64_t(o) + nov > S.ovf_cap) {     // pool full: results invalid (status bit 2)
+        if (lane == 0) atomicOr(&S.flags[0], 1);
+        continue;
+      }
+      if (lane == 0) {
+        S.ovf_off[i] = o;
+        S.long_rows[atomicAdd(&S.flags[2], 1)] = int32_t(i);
+      }
+      for (int k = lane; k < nov; k += 32)
+        S.ovf[o + k] = make_uint2(uint32_t(rc[b + kCap + k]), __float_as_uint(rv[b + kCap + k]));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_csr_ell(SparseState S, const int32_t* __restrict__ rp,
+                                                 const int32_t* __restrict__ rc, const float* __restrict__ rv) {
+  csr_ell_body(S, rp, rc, rv, int(blockIdx.x), int(gridDim.x));
+}
+
+// bgcn_csr_to_dense: one wave per row, the row assembled in LDS (zeros, then the row's
+// entries) and written with 16-byte stores - every output element written once, in order.
+template <class TX>
+__global__ __launch_bounds__(128) void k_csr_dense(const int32_t* __restrict__ rp, const int32_t* __restrict__ rc,
+                                                   const float* __restrict__ rv, int64_t N, int64_t F,
+                                                   TX* __restrict__ X, int64_t ldx, int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) float rowbuf[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t Fp = (F + 3) / 4 * 4;
+  float* row = rowbuf + wave * Fp;
+  const int nw = int(blockDim.x) >> 6;
+  for (int64_t i = int64_t(blockIdx.x) * nw + wave; i < N; i += int64_t(gridDim.x) * nw) {
+    for (int64_t c = lane; c < Fp; c += 64) row[c] = 0.f;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int32_t b = rp[i], e = rp[i + 1];
+    for (int32_t k = b + lane; k < e; k += 64) {
+      const int32_t c = rc[k];
+      if (c >= 0 && c < F) row[c] = rv[k];
+      else if (status) atomicOr(status, 1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    TX* out = X + i * ldx;
+    if constexpr (sizeof(TX) == 4) {
+      for (int64_t c = int64_t(lane) * 4; c < F; c += 256)
+        *reinterpret_cast<float4*>(out + c) = *reinterpret_cast<const float4*>(row + c);
+    } else {   // round to nearest even (the host-fed values of a bf16 batch are bf16-exact)
+      for (int64_t c = lane; c < F; c += 64) {
+        const uint32_t u = __float_as_uint(row[c]);
+        out[c] = TX((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 template <bool kConv1, class TX>
 __global__ __launch_bounds__(256) void k_compact_conv1(SparseState S, const TX* __restrict__ X,
                                                        int64_t ldx, float* __restrict__ Z1) {
@@ -1669,6 +1751,8 @@ struct PrepArgs {
   int32_t *node_root, *tree_ptr, *status;
   const void* X;
   int64_t ldx;
+  const int32_t *xr_ptr, *xr_col;   // host-fed compacted features (X == nullptr), else null
+  const float* xr_val;
   int64_t* eptr;
   uint64_t seed;
   uint4* zero[2];
@@ -1713,7 +1797,8 @@ __global__ __launch_bounds__(256) void k_prep_b(PrepArgs a) {
     items_body(a.S, a.tree_ptr, a.rootindex);
     return;
   }
-  compact_body<false, TX>(a.S, static_cast<const TX*>(a.X), a.ldx, nullptr, b - 1, a.ncomp);
+  if (a.xr_ptr) csr_ell_body(a.S, a.xr_ptr, a.xr_col, a.xr_val, b - 1, a.ncomp);
+  else compact_body<false, TX>(a.S, static_cast<const TX*>(a.X), a.ldx, nullptr, b - 1, a.ncomp);
 }
 
 __global__ __launch_bounds__(256) void k_prep_c(PrepArgs a) {
@@ -2073,6 +2158,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   a.batch = bt->batch; a.rootindex = bt->rootindex;
   a.node_root = p.node_root; a.tree_ptr = p.tree_ptr; a.status = p.status;
   a.X = bt->x; a.ldx = bt->ldx;
+  if (!bt->x) { a.xr_ptr = bt->x_row_ptr; a.xr_col = bt->x_col; a.xr_val = bt->x_val; }
   // DropEdge (dataset.py:68-90) in the masked form: dropped edges become self loops, which
   // K1 removes - the graphs of the compacted lists, no kept count on the host
   const int64_t Etd = bt->td_num_edges, Ebu = bt->bu_num_edges;
@@ -2093,7 +2179,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   GraphArgs ga[2];
   graph_pair_args(td, Etd, bu, Ebu, &p.td, &p.bu, p.status, p.gws, p.gws_bytes, ga);
   size_t zb[2] = {0, 0};
-  BGCN_TRY(graph_batch_setup(ga, 2, N, degree_on, &a.gb, zb));
+  BGCN_TRY(graph_batch_setup(ga, 2, N, degree_on, &a.gb, zb, bt->batch));
   for (int k = 0; k < 2; ++k) {
     a.zero[k] = reinterpret_cast<uint4*>(a.gb.g[k].cnt_t);
     a.nzero[k] = int(zb[k] / 16);
@@ -2132,6 +2218,8 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
     const char* e = std::getenv("BGCN_PREP_BLOCKS");
     if (e) cap = atoi(e);
     if (cap > 0) a.ncomp = std::min(a.ncomp, cap);
+    // host-fed compacted rows: 8 rows per block over every row, nothing to pace (nnz x 8 B)
+    if (a.xr_ptr && xp) a.ncomp = int(grid_for(N, 8));
   }
   a.nce = graph_edge_blocks(Emax);
   a.R = xp ? int((N + kRowBlock - 1) / kRowBlock) : 0;
@@ -2206,7 +2294,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
 
 int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
                    const int64_t* batch, const int64_t* rootindex, const void* X, int xdt, int64_t ldx,
-                   hipStream_t s, int part) {
+                   hipStream_t s, int part, const bgcn_batch* csr) {
   SparseState S{};
   S.mode = mode;
   S.N = N; S.F = F; S.B = B;
@@ -2228,7 +2316,9 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
   BGCN_TRY(sparse_items(S, p.tree_ptr, rootindex, s));
   timing_begin(7, s);
   const dim3 grid(grid_for(N, xdt == BGCN_DTYPE_BF16 ? 8 : 4));
-  if (xdt == BGCN_DTYPE_BF16)
+  if (!X && csr)
+    hipLaunchKernelGGL(k_csr_ell, dim3(grid_for(N, 8)), dim3(256), 0, s, S, csr->x_row_ptr, csr->x_col, csr->x_val);
+  else if (xdt == BGCN_DTYPE_BF16)
     hipLaunchKernelGGL((k_compact_conv1<false, bf16_t>), grid, dim3(256), 0, s, S,
                        static_cast<const bf16_t*>(X), ldx, nullptr);
   else
@@ -2263,3 +2353,26 @@ extern "C" size_t bgcn_weight_images_size(int64_t in_feats) {
 }
 
 BT_READER(sparse)
+
+extern "C" int bgcn_csr_to_dense(const int32_t* x_row_ptr, const int32_t* x_col, const float* x_val,
+                                 int64_t num_nodes, int64_t in_feats, void* x, int64_t ldx, int32_t x_dtype,
+                                 int32_t* status, bgcn_stream_t stream) {
+  using namespace bgcn;
+  BGCN_CHECK_ARG(num_nodes > 0 && in_feats > 0 && in_feats % 4 == 0 && ldx >= in_feats && ldx % 4 == 0,
+                 "bad sizes (in_feats and ldx: multiples of 4)");
+  BGCN_CHECK_ARG(x_row_ptr && x_col && x_val && x, "null pointer");
+  BGCN_CHECK_ARG((reinterpret_cast<uintptr_t>(x) & 15) == 0, "x must be 16-byte aligned");
+  BGCN_CHECK_ARG(x_dtype == BGCN_DTYPE_F32 || x_dtype == BGCN_DTYPE_BF16, "bad x_dtype");
+  BGCN_CHECK_ARG(in_feats <= 8192, "in_feats > 8192 (the row is assembled in LDS)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t smem = size_t(2) * size_t((in_feats + 3) / 4 * 4) * sizeof(float);   // two waves' rows
+  const dim3 grid(unsigned(std::min<int64_t>((num_nodes + 1) / 2, 8192)));
+  if (x_dtype == BGCN_DTYPE_BF16)
+    hipLaunchKernelGGL(k_csr_dense<bf16_t>, grid, dim3(128), smem, s, x_row_ptr, x_col, x_val, num_nodes, in_feats,
+                       static_cast<bf16_t*>(x), ldx, status);
+  else
+    hipLaunchKernelGGL(k_csr_dense<float>, grid, dim3(128), smem, s, x_row_ptr, x_col, x_val, num_nodes, in_feats,
+                       static_cast<float*>(x), ldx, status);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}

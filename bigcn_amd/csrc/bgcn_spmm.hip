@@ -171,6 +171,9 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
     // kSign: the trees of the chunk's first and last rows and their scales
     int64_t bA = 0, bZ = 0;
     float4 gA = f4zero(), gZ = f4zero();
+    // kSign with an edge across trees (the graph build's BGCN_STATUS_CROSS_TREE, never set
+    // by PyG collation): every gathered row is scaled by its own tree, the output row not
+    const bool xt = kSign && (*sb.sg.tree_status[blockIdx.y] & BGCN_STATUS_CROSS_TREE) != 0;
     if constexpr (kSign) {
       const int32_t ra = __shfl(r0, base_lane, 64);
       const int32_t rz = __shfl(n > LANES ? r1 : r0, base_lane + ((n - 1) & (LANES - 1)), 64);
@@ -181,6 +184,10 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
     }
     auto finish = [&](int32_t r, float4 acc) {
       if constexpr (kSign) {
+        if (xt) {
+          st4(P.out + int64_t(r) * P.ld_out + fo, acc);
+          return;
+        }
         const int64_t b = sb.sg.batch[r];
         const float4 gs = b == bA ? gA : (b == bZ ? gZ : tree_scale(sb.sg, b, hoff, fo));
         st4(P.out + int64_t(r) * P.ld_out + fo,
@@ -204,9 +211,10 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
         const int32_t ck = __shfl(hi ? c1 : c0, src, 64);
         ww[u] = __shfl(hi ? w1 : w0, src, 64);
         rr[u] = k < n ? rk : -1;
-        if constexpr (kSign)
+        if constexpr (kSign) {
           v[u] = sign_bits(sgn[int64_t(ck) * 2], lane);    // unconditional (ck is a real row)
-        else
+          if (xt) v[u] = f4mul(v[u], tree_scale(sb.sg, sb.sg.batch[ck], hoff, fo));
+        } else
           v[u] = ld4(P.in + int64_t(ck) * P.ld_in + fo);   // unconditional (ck is a real row)
       }
 #pragma unroll
@@ -231,7 +239,8 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
     const int32_t r = P.plan.longs[j];
     const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
     float4 gs = f4zero();
-    if constexpr (kSign) gs = tree_scale(sb.sg, sb.sg.batch[r], hoff, fo);   // under the gathers
+    const bool xt = kSign && (*sb.sg.tree_status[blockIdx.y] & BGCN_STATUS_CROSS_TREE) != 0;
+    if constexpr (kSign) gs = xt ? make_float4(1.f, 1.f, 1.f, 1.f) : tree_scale(sb.sg, sb.sg.batch[r], hoff, fo);
     float4 acc = f4zero();
     int64_t e = rs + grp;
     for (; e + 7 * kRowsGroups < re; e += 8 * kRowsGroups) {
@@ -241,18 +250,21 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
       for (int u = 0; u < 8; ++u) {
         const int64_t eu = e + u * kRowsGroups;
         ww[u] = P.w[eu];
-        if constexpr (kSign)
+        if constexpr (kSign) {
           v[u] = sign_bits(sgn[int64_t(P.col[eu]) * 2], lane);
-        else
+          if (xt) v[u] = f4mul(v[u], tree_scale(sb.sg, sb.sg.batch[P.col[eu]], hoff, fo));
+        } else
           v[u] = ld4(P.in + int64_t(P.col[eu]) * P.ld_in + fo);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc = f4fma(ww[u], v[u], acc);
     }
     for (; e < re; e += kRowsGroups) {
-      if constexpr (kSign)
-        acc = f4fma(P.w[e], sign_bits(sgn[int64_t(P.col[e]) * 2], lane), acc);
-      else
+      if constexpr (kSign) {
+        float4 v = sign_bits(sgn[int64_t(P.col[e]) * 2], lane);
+        if (xt) v = f4mul(v, tree_scale(sb.sg, sb.sg.batch[P.col[e]], hoff, fo));
+        acc = f4fma(P.w[e], v, acc);
+      } else
         acc = f4fma(P.w[e], ld4(P.in + int64_t(P.col[e]) * P.ld_in + fo), acc);
     }
     red[grp][lane] = acc;
@@ -565,7 +577,7 @@ int spmm_batch_impl(SpmmBatch& sb, int count, hipStream_t stream) {
   for (int k = 0; k < count; ++k) capmax = sb.p[k].capacity > capmax ? sb.p[k].capacity : capmax;
   const bool planned = spmm_planned(sb, count);
   BGCN_CHECK_ARG(!sb.sg.sgn || (planned && count == 2 && sb.sg.dhead && sb.sg.batch && sb.sg.tree_ptr &&
-                                sb.sg.B > 0),
+                                sb.sg.B > 0 && sb.sg.tree_status[0] && sb.sg.tree_status[1]),
                  "readout-gradient input needs the planned TD/BU pair");
   if (planned) {   // K1's plans: complete rows per chunk, long rows per block, no fixup
     const int64_t gplan = (capmax + kPlanGrid - 1) / kPlanGrid;   // K1's chunk grid

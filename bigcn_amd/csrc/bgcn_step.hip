@@ -62,12 +62,24 @@ int check_batch(const bgcn_batch* b) {
   BGCN_CHECK_ARG(b, "null batch");
   BGCN_CHECK_ARG(b->num_nodes > 0 && b->num_graphs > 0, "bad sizes");
   BGCN_CHECK_ARG(b->td_num_edges >= 0 && b->bu_num_edges >= 0, "bad edge counts");
-  BGCN_CHECK_ARG(b->x && b->batch && b->rootindex, "null pointer");
+  BGCN_CHECK_ARG(b->batch && b->rootindex, "null pointer");
+  // features: the dense x, or (x == NULL) the host-fed CSR of its non-zeros
+  BGCN_CHECK_ARG(b->x || (b->x_row_ptr && b->x_col && b->x_val), "null x (and no compacted features)");
   BGCN_CHECK_ARG((b->td_num_edges == 0 || b->td_edge_index) && (b->bu_num_edges == 0 || b->bu_edge_index),
                  "null edge_index");
   BGCN_CHECK_ARG(b->td_droprate < 1.0 && b->bu_droprate < 1.0, "droprate must be < 1");
   BGCN_CHECK_ARG(b->x_dtype == BGCN_DTYPE_F32 || b->x_dtype == BGCN_DTYPE_BF16, "bad x_dtype");
   BGCN_CHECK_ARG((reinterpret_cast<uintptr_t>(b->x) & 15) == 0, "x must be 16-byte aligned");
+  return BGCN_OK;
+}
+
+// a batch whose features arrive compacted (bgcn_batch.x_row_ptr) has no dense x: only the
+// sparse feature path (BGCN_FEAT_SPARSE, no dense fallback kernels) can train on it
+int check_feat_input(const bgcn_batch* b, int feat_mode, int64_t F) {
+  if (b->x) return BGCN_OK;
+  BGCN_CHECK_ARG(feat_mode == BGCN_FEAT_SPARSE, "compacted features (x == NULL) need feat_mode BGCN_FEAT_SPARSE");
+  BGCN_CHECK_ARG(F <= kSparseMaxFeat && b->num_nodes <= kSparseMaxN,
+                 "compacted features: in_feats / num_nodes beyond the sparse path (expand with bgcn_csr_to_dense)");
   return BGCN_OK;
 }
 
@@ -131,6 +143,7 @@ static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_
   Prepared p;
   Carve c(buf, bytes);
   carve_prepared(c, N, B, F, b->td_num_edges, b->bu_num_edges, &p);
+  BGCN_TRY(check_feat_input(b, feat_mode, F));
   const int mode = (feat_mode == BGCN_FEAT_DENSE || F > kSparseMaxFeat || N > kSparseMaxN) ? 1 : 0;
   // one stream: the six merged launches (DropEdge, K1, the pass over X and the CSC of X
   // side by side, bgcn_sparse.hip prep_pipeline).  BGCN_PREP_MERGED=0 (read per call)
@@ -146,7 +159,7 @@ static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_
   BGCN_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int32_t), gs));
   const bool x_first = s == gs;
   if (x_first)
-    BGCN_TRY(sparse_prepare(p, N, B, F, mode, b->batch, b->rootindex, b->x, b->x_dtype, b->ldx, s, 1));
+    BGCN_TRY(sparse_prepare(p, N, B, F, mode, b->batch, b->rootindex, b->x, b->x_dtype, b->ldx, s, 1, b));
   const int64_t* td = b->td_edge_index;
   const int64_t* bu = b->bu_edge_index;
   if (b->td_droprate > 0.0 || b->bu_droprate > 0.0) {
@@ -159,10 +172,10 @@ static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_
     if (bu) bu = p.bu_drop;
   }
   BGCN_TRY(bgcn_build_graph_pair(td, b->td_num_edges, bu, b->bu_num_edges, N, degree_on, &p.td,
-                                 &p.bu, p.status, p.gws, p.gws_bytes,
+                                 &p.bu, b->batch, p.status, p.gws, p.gws_bytes,
                                  reinterpret_cast<bgcn_stream_t>(gs)));
   BGCN_TRY(sparse_prepare(p, N, B, F, mode, b->batch, b->rootindex, b->x, b->x_dtype, b->ldx, s,
-                          x_first ? 2 : 3));
+                          x_first ? 2 : 3, b));
   if (out) *out = p;
   return BGCN_OK;
 }
@@ -181,6 +194,7 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
   BGCN_TRY(check_batch(&a->cur));
   const int64_t N = a->cur.num_nodes, B = a->cur.num_graphs, F = a->in_feats, C = a->num_classes;
   BGCN_CHECK_ARG(F > 0, "bad sizes");
+  BGCN_TRY(check_feat_input(&a->cur, a->feat_mode, F));
   BGCN_CHECK_ARG(C >= 1 && C <= kMaxClasses, "num_classes must be in [1, 16]");
   BGCN_CHECK_ARG(a->y && a->loss, "null pointer");
   for (int k = 0; k < BGCN_STEP_PARAMS; ++k)
@@ -189,6 +203,7 @@ int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStrea
   BGCN_CHECK_ARG(a->prepared, "a prepared buffer is required (bgcn_prepare_workspace_size)");
   if (a->next) {
     BGCN_TRY(check_batch(a->next));
+    BGCN_TRY(check_feat_input(a->next, a->feat_mode, F));
     BGCN_CHECK_ARG(a->next_prepared && a->next_prepared != a->prepared,
                    "next_prepared must be a separate buffer");
   }

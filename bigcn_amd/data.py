@@ -183,7 +183,15 @@ def make_sample(d: dict, tddroprate: float = 0.0, budroprate: float = 0.0,
 
 class BiGraphDataset(torch.utils.data.Dataset):
     """``Process/dataset.py:45-99`` over ``<data_path>/<eid>.npz`` (size filter ``lower=2``,
-    ``upper=100000`` against ``treeDic``).  npz files are read with ``allow_pickle=False``."""
+    ``upper=100000`` against ``treeDic``).  npz files are read with ``allow_pickle=False``.
+
+    An item is ``(sample, root tweet id)`` as the reference returns ``(Data(...),
+    data['tweetids'][rootindex])`` (``dataset.py:94-99``); a DataLoader with
+    ``collate_fn=collate_pairs`` then yields ``(Batch, [root tweet ids])`` like the loop at
+    ``BiGCN_Twitter.py:174`` unpacks (``for Batch_data, tweetid in train_loader``).  The
+    root tweet id is None for npz files without ``tweetids`` (the Twitter/Weibo
+    preprocessors write none, ``getTwittergraph.py:128``).  The host-fed fast path
+    (compacted features, one buffer per batch) is :mod:`bigcn_amd.feed`."""
 
     def __init__(self, fold_x, treeDic=None, lower=2, upper=100000, tddroprate=0.0, budroprate=0.0,
                  data_path=os.path.join("..", "..", "data", "Weibograph")):
@@ -200,7 +208,10 @@ class BiGraphDataset(torch.utils.data.Dataset):
         eid = self.fold_x[index]
         with np.load(os.path.join(self.data_path, eid + ".npz"), allow_pickle=False) as f:
             d = {k: f[k] for k in f.files}
-        return make_sample(d, self.tddroprate, self.budroprate)
+        root_tid = None
+        if "tweetids" in d:
+            root_tid = d["tweetids"][int(d["rootindex"])]
+        return make_sample(d, self.tddroprate, self.budroprate), root_tid
 
 
 # ----------------------------------------------------------------------------- batch
@@ -277,6 +288,13 @@ def collate(samples: Sequence[Sample]) -> Batch:
         spill = sum(s.x_spill for s in samples) if all(s.x_spill is not None for s in samples) else None
         out.set_x_nnz_max(max(s.x_nnz_max for s in samples), spill)
     return out
+
+
+def collate_pairs(items):
+    """collate_fn for :class:`BiGraphDataset` items ``(sample, root tweet id)``: PyG's
+    ``Collater`` on tuples - ``(Batch, list of root tweet ids)``."""
+    samples, tids = zip(*items)
+    return collate(samples), list(tids)
 
 
 # ----------------------------------------------------------------------------- bulk synthetic batches

@@ -46,7 +46,7 @@ class Graph:
     the per-array tensors are views made on first access - the kernels take pointers."""
 
     __slots__ = ("num_nodes", "num_edges", "capacity", "status", "_bufs", "_lay", "_views", "_ptrs", "_plan",
-                 "_plan_ws")
+                 "_plan_ws", "_tree_checked")
 
     def _array(self, name: str) -> torch.Tensor:
         v = self._views.get(name)
@@ -64,6 +64,8 @@ class Graph:
         v.capacity = self.capacity
         if self._plan is not None:   # the aggregation plans of bgcn_build_graph_pair
             v.plan[0], v.plan[1] = self._plan
+        if self._tree_checked:       # built with the batch vector: status carries BGCN_STATUS_CROSS_TREE
+            v.tree_status = self.status.data_ptr()
         return v
 
     def check(self) -> None:
@@ -71,7 +73,7 @@ class Graph:
         s = int(self.status.item())
         if s & 8:
             raise RuntimeError("libbgcn: an internal cross-workgroup hand-off timed out")
-        if s != 0:
+        if s & ~_lib.BGCN_STATUS_CROSS_TREE:   # (an edge across trees is legal, only noted)
             raise IndexError("edge_index contains an index out of range [0, num_nodes)")
 
 
@@ -99,6 +101,7 @@ def _alloc_graphs(edges, N: int, dev, status=None):
         g.num_nodes, g.num_edges, g.capacity, g.status = N, E, cap, st
         g._bufs, g._views, g._lay, g._ptrs = (bi, bf), {}, {}, {}
         g._plan = g._plan_ws = None
+        g._tree_checked = False
         for name in _GRAPH_I32:
             n = N + 1 if name.endswith("ptr") else cap
             g._lay[name], g._ptrs[name] = (0, oi, n), pi + 4 * oi
@@ -141,11 +144,20 @@ def _check_ei(edge_index: torch.Tensor) -> torch.Tensor:
 
 
 def build_graph_pair(td_edge_index: torch.Tensor, bu_edge_index: torch.Tensor, num_nodes: int,
-                     degree_on: str = "col", validate: bool = False):
+                     degree_on: str = "col", validate: bool = False, batch: Optional[torch.Tensor] = None):
     """TD and BU graphs of one batch in one launch sequence (the fused step's K1).  The
     build's workspace (≈3.5 MB at Twitter size, about the graphs' own size) stays with the
-    two graphs: it holds their aggregation plans (``bgcn_graph_pair_plans``)."""
-    _dev_check(td_edge_index, bu_edge_index)
+    two graphs: it holds their aggregation plans (``bgcn_graph_pair_plans``).
+
+    ``batch`` (the collated batch vector, optional): the build also notes on the device
+    whether an edge joins two trees.  Only graphs built with it let the fused encoder take
+    its sign-word readout backward (which handles such edges by per-neighbour scales);
+    without it the encoder keeps the general readout backward."""
+    _dev_check(td_edge_index, bu_edge_index, batch)
+    if batch is not None:
+        if batch.numel() != int(num_nodes):
+            raise ValueError("batch must have one entry per node")
+        batch = batch.to(torch.int64).contiguous()
     dcode = degree_code(degree_on)
     td_ei, bu_ei = _check_ei(td_edge_index), _check_ei(bu_edge_index)
     N = int(num_nodes)
@@ -155,8 +167,9 @@ def build_graph_pair(td_edge_index: torch.Tensor, bu_edge_index: torch.Tensor, n
     ws = workspace(L.bgcn_graph_pair_workspace_size(td.num_edges, bu.num_edges, N), dev)
     a, b = _csr_out(td), _csr_out(bu)
     check(L.bgcn_build_graph_pair(td_ei.data_ptr(), td.num_edges, bu_ei.data_ptr(), bu.num_edges, N,
-                                  dcode, ctypes.byref(a), ctypes.byref(b),
+                                  dcode, ctypes.byref(a), ctypes.byref(b), ptr(batch),
                                   td.status.data_ptr(), ws.data_ptr(), ws.numel(), stream_handle()))
+    td._tree_checked = bu._tree_checked = batch is not None
     # the build leaves both graphs' aggregation plans in its workspace: keep it with the
     # graphs so the fused encoder takes the planned aggregation
     pt, pb = (_lib.SpmmPlan * 2)(), (_lib.SpmmPlan * 2)()
@@ -600,12 +613,19 @@ def bigcn_encoder(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor,
 
 
 def head_fits(fc: torch.nn.Module) -> bool:
-    """Whether ``fc`` is a head the K9 kernels take: Linear(256, C <= 16) with a bias,
-    contiguous fp32 weights."""
+    """Whether ``fc`` is a head the K9 kernels take in place of ``fc(...)``: exactly a
+    ``torch.nn.Linear(256, C <= 16)`` (not a subclass with its own forward) with a bias,
+    no forward hooks (their side effects would be skipped), contiguous fp32 weights on
+    16-byte boundaries (``bgcn_head_forward``'s alignment contract).  Anything else runs
+    through ``fc`` itself and torch's log_softmax."""
     w, b = getattr(fc, "weight", None), getattr(fc, "bias", None)
-    return (isinstance(fc, torch.nn.Linear) and w is not None and b is not None and w.dim() == 2
+    return (type(fc) is torch.nn.Linear and w is not None and b is not None and w.dim() == 2
+            and not fc._forward_hooks and not fc._forward_pre_hooks
+            and not torch.nn.modules.module._global_forward_hooks
+            and not torch.nn.modules.module._global_forward_pre_hooks
             and w.size(1) == 4 * HID and 0 < w.size(0) <= 16 and w.dtype == torch.float32
-            and b.dtype == torch.float32 and w.is_contiguous() and b.is_contiguous())
+            and b.dtype == torch.float32 and w.is_contiguous() and b.is_contiguous()
+            and w.data_ptr() % 16 == 0 and b.data_ptr() % 4 == 0)
 
 
 def bigcn_net(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, td: Graph, bu: Graph,

@@ -49,6 +49,7 @@ class FusedAdam:
         self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
         self.step_count = 0
         self.state = {}
+        self._cache = None
         n = sum(len(g["params"]) for g in self.param_groups)
         if n > MAX_TENSORS:
             raise ValueError(f"FusedAdam handles at most {MAX_TENSORS} tensors")
@@ -89,9 +90,19 @@ class FusedAdam:
         ps = self.params()
         gs = list(grads) if grads is not None else [p.grad for p in ps]
         # the tensor table (parameter / moment pointers, sizes, groups) is built once per
-        # set of present gradients; only the gradient pointers are written per step
-        # (autograd hands out fresh gradient tensors every step)
-        key = tuple(g is None for g in gs)
+        # set of present gradients and parameter / moment storage; only the gradient
+        # pointers are written per step (autograd hands out fresh gradient tensors every
+        # step).  The key holds every pointer the table captures, so reassigning p.data,
+        # swapping a parameter in param_groups or replacing a moment rebuilds it.
+        if len(ps) > MAX_TENSORS:
+            raise ValueError(f"FusedAdam handles at most {MAX_TENSORS} tensors")
+        for p in ps:
+            if p not in self.state:   # a parameter added to param_groups after construction
+                self.state[p] = (torch.zeros_like(p), torch.zeros_like(p))
+        key = (tuple(g is None for g in gs),
+               tuple((p.data_ptr(), p.numel(), self.state[p][0].data_ptr(), self.state[p][1].data_ptr())
+                     for p in ps),
+               tuple(len(g["params"]) for g in self.param_groups))
         cached = self._cache if getattr(self, "_cache", None) is not None and self._cache[0] == key else None
         if cached is None:
             a = AdamArgs()

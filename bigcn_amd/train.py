@@ -26,11 +26,32 @@ from . import _lib
 from ._lib import BatchDesc, StepArgs, check, ptr, stream_handle, workspace
 from .bigcn import BiGCN, _draw_seed, _num_graphs
 from .dp import GradBucket
-from .ops import _FEAT_MODES, check_encoder_shapes, degree_code, feat_path, features, x_dtype_code
+from .feed import PackedBatch
+from .ops import HID, _FEAT_MODES, check_encoder_shapes, degree_code, feat_path, features, x_dtype_code
 from .optim import IMAGE_BU_W1, IMAGE_BU_W2, IMAGE_TD_W1, IMAGE_TD_W2, FusedAdam, bigcn_adam
 
 
+def _compacted(data) -> bool:
+    """A host-fed batch whose features stay compacted (x never materialised): every
+    PackedBatch whose rows fit the sparse path; one that overflows the spill pool is
+    trained from its dense x (expanded on the device) like any collated batch."""
+    return isinstance(data, PackedBatch) and data.fits_sparse
+
+
+def _in_feats(data) -> int:
+    return int(data.in_feats) if isinstance(data, PackedBatch) else int(data.x.size(1))
+
+
+def _device(data):
+    return data.device if isinstance(data, PackedBatch) else data.x.device
+
+
 def _step_feat_mode(feat_mode: str, data) -> int:
+    if _compacted(data):
+        if feat_mode == "dense":
+            raise ValueError("feat_mode 'dense' needs the dense x; this batch's features are compacted "
+                             "(read batch.x to expand them)")
+        return _lib.BGCN_FEAT_SPARSE
     return feat_path(feat_mode, data)
 
 
@@ -98,6 +119,7 @@ class FusedTrainStep:
         self.status_seen = torch.zeros(1, dtype=torch.int32, device=model.fc.weight.device)
         self.skipped = torch.zeros(1, dtype=torch.int32, device=model.fc.weight.device)
         self._pending = None       # (batch, prepared buffer, feat_mode, tensors) from next_data
+        self._dw1_pending = None   # buffers of a defer_dw1 step until finish_dw1()
         self._stream = None
         self._next_desc = None
         # Weight images (W1^T, W2^T, the bf16 splits of W2[:, :64]) in a persistent buffer:
@@ -138,6 +160,16 @@ class FusedTrainStep:
 
     def _desc(self, data):
         """bgcn_batch of a collated batch (+ the tensors it points into, kept alive)."""
+        if _compacted(data):
+            F = _in_feats(data)
+            want = [(HID, F), (HID,), (HID, HID + F), (HID,)] * 2
+            for p, shp in zip(self.step_params[:8], want):
+                if tuple(p.shape) != shp:
+                    raise ValueError(f"parameter of shape {tuple(p.shape)}, expected {shp} for in_feats={F}")
+            d = BatchDesc()
+            data.fill_desc(d)
+            self._drop_fields(d)
+            return d, (data,)
         x = features(data.x)                         # fp32, or bf16 kept as is
         check_encoder_shapes(x, data.batch, data.rootindex, self.step_params[:8])
         if data.rootindex.numel() != _num_graphs(data) or data.y.numel() != _num_graphs(data):
@@ -152,11 +184,14 @@ class FusedTrainStep:
         d.batch, d.rootindex = ptr(batch), ptr(root)
         d.td_edge_index, d.td_num_edges = ptr(td_ei), td_ei.size(1)
         d.bu_edge_index, d.bu_num_edges = ptr(bu_ei), bu_ei.size(1)
+        self._drop_fields(d)
+        return d, (x, td_ei, bu_ei, batch, root)
+
+    def _drop_fields(self, d) -> None:
         if self.model.training and (self.tddroprate > 0 or self.budroprate > 0):
             d.td_droprate, d.bu_droprate = self.tddroprate, self.budroprate
             d.drop_seed = (self._drop_seed + self._drop_count) & (2**64 - 1)
             self._drop_count += 1
-        return d, (x, td_ei, bu_ei, batch, root)
 
     def _prep_buffer(self, d, F):
         L = _lib.lib()
@@ -175,8 +210,13 @@ class FusedTrainStep:
 
         ``defer_dw1``: return before the conv1 weight gradients are written (every other
         gradient and the status slot are final); ``finish_dw1()`` writes them."""
+        if self._dw1_pending is not None:
+            # the previous step's conv1 weight gradients are not written yet: a new step
+            # would reuse its workspace and the bucket would keep stale dW1 values
+            raise RuntimeError("a step run with defer_dw1=True is pending: call finish_dw1() first")
         m = self.model
-        F = int(data.x.size(1))
+        F = _in_feats(data)
+        dev = _device(data)
         y = _need(data.y, torch.int64, "y")
         if seed is None:
             seed = _draw_seed() if m.training else 0
@@ -214,7 +254,7 @@ class FusedTrainStep:
             a.next = None
             a.next_prepared, a.next_prepared_bytes = 0, 0
         self.last_drop_seed = int(a.cur.drop_seed) if a.cur.td_droprate > 0 or a.cur.bu_droprate > 0 else None
-        loss = torch.empty(1, dtype=torch.float32, device=data.x.device)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
         a.loss, a.logp, a.status = ptr(loss), ptr(logp), ptr(self.status)
         a.status_flag = ptr(self.bucket.flag)
         a.status_seen = ptr(self.status_seen)
@@ -224,7 +264,7 @@ class FusedTrainStep:
         L = _lib.lib()
         N, B = d.num_nodes, d.num_graphs
         ws = workspace(L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
-                                                        d.bu_num_edges), data.x.device)
+                                                        d.bu_num_edges), dev)
         # every branch the step forks joins back into the caller's stream inside the call
         # (the workspace can return to the allocator afterwards), except the next batch's
         # preparation, which outlives the call: its buffer is held in self._pending until
@@ -236,6 +276,7 @@ class FusedTrainStep:
         try:                             # the preparation queued on the side lane
             check(L.bgcn_train_step(ctypes.addressof(a), ptr(ws), ws.numel(), self._stream))
         except Exception:
+            self._dw1_pending = None     # the failed step wrote no gradients to finish
             if nxt is not None:
                 self._join_side()        # nothing may still write the buffer once it is freed
                 self._pending = None

@@ -48,7 +48,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 6
+#define BGCN_ABI_VERSION 7
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -89,7 +89,14 @@ int bgcn_build_graph(const int64_t* edge_index, const float* edge_weight, int64_
                      bgcn_stream_t stream);
 
 /* Both directions of one batch in one launch sequence (the fused step's TD graph of
- * edge_index and BU graph of BU_edge_index; dataset.py:80-90).  No edge weights. */
+ * edge_index and BU graph of BU_edge_index; dataset.py:80-90).  No edge weights.
+ * batch (optional, ABI 7): the [N] tree id per node of the collated batch; with it every
+ * edge whose ends lie in different trees sets BGCN_STATUS_CROSS_TREE in *status.  PyG
+ * collation never makes such an edge, and the fused encoder's fast readout backward
+ * (tree-scaled sign-word aggregation) needs to know that; the status word then travels
+ * with the graphs (bgcn_graph_view.tree_status) and a set bit switches that aggregation to
+ * per-neighbour tree scales (same result as k_readout_bwd + the plain aggregation). */
+#define BGCN_STATUS_CROSS_TREE 16
 typedef struct bgcn_csr_out {
   int32_t* t_ptr; int32_t* t_row; int32_t* t_col; float* t_w;
   int32_t* s_ptr; int32_t* s_row; int32_t* s_col; float* s_w;
@@ -98,8 +105,8 @@ size_t bgcn_graph_pair_workspace_size(int64_t td_num_edges, int64_t bu_num_edges
 int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_num_edges,
                           const int64_t* bu_edge_index, int64_t bu_num_edges, int64_t num_nodes,
                           int degree_on, const bgcn_csr_out* td, const bgcn_csr_out* bu,
-                          int32_t* status, void* workspace, size_t workspace_bytes,
-                          bgcn_stream_t stream);
+                          const int64_t* batch, int32_t* status, void* workspace,
+                          size_t workspace_bytes, bgcn_stream_t stream);
 
 /* --------------------------------------------------------------------------
  * K3/K4  MessagePassing.propagate(aggr='add') with message norm * x_j, + bias.
@@ -232,6 +239,11 @@ typedef struct bgcn_graph_view {
   /* optional (ABI 6): the plans of the forward (by target) and backward (by source)
    * aggregations, from bgcn_graph_pair_plans; zeros = merge-path chunks + fix-up */
   bgcn_spmm_plan plan[2];
+  /* optional (ABI 7): the status word of a bgcn_build_graph_pair call made WITH its batch
+   * argument (BGCN_STATUS_CROSS_TREE tells whether an edge crosses trees).  The fused
+   * encoder takes its sign-word readout backward only when both views carry it (or the
+   * batch was prepared by bgcn_prepare_batch); NULL keeps k_readout_bwd. */
+  const int32_t* tree_status;
 } bgcn_graph_view;
 
 /* The aggregation plans a bgcn_build_graph_pair call left in its workspace (valid while
@@ -341,7 +353,28 @@ typedef struct bgcn_batch {
   double td_droprate, bu_droprate;
   uint64_t drop_seed;
   int32_t x_dtype;               /* BGCN_DTYPE_F32 (0) / BGCN_DTYPE_BF16      */
+  /* Compacted node features (ABI 7; the host-fed input path): with x == NULL the features
+   * arrive as the CSR of their non-zeros, the form DataLoader workers emit from the
+   * per-tree npz rows (Process/dataset.py:94 x, getTwittergraph.py:67-72 word counts)
+   * so that a batch crosses PCIe as ~4 MB instead of N x 20 KB:
+   *   x_row_ptr [N + 1]  entries of node i are [x_row_ptr[i], x_row_ptr[i + 1])
+   *   x_col [nnz]        column ids in [0, in_feats), strictly ascending within a row
+   *   x_val [nnz]        the non-zero values (fp32; zeros must be left out)
+   * Preparation then fills the ELL / spill pool / CSC of X from these lists instead of
+   * reading X (identical contents, so a step computes the same bits as from the dense x),
+   * and the step must run BGCN_FEAT_SPARSE: the caller has checked that the batch fits the
+   * pool (sum over rows of max(nnz - BGCN_SPARSE_CAP, 0) <= N * BGCN_SPARSE_SPILL_PER_ROW;
+   * otherwise expand it with bgcn_csr_to_dense and pass the dense x).  ldx = in_feats. */
+  const int32_t* x_row_ptr; const int32_t* x_col; const float* x_val;
 } bgcn_batch;
+
+/* Expand a CSR of node features (bgcn_batch.x_row_ptr / x_col / x_val) into the dense
+ * [N, ldx] matrix x of x_dtype (the reference's data.x layout, Process/dataset.py:94):
+ * zeros everywhere else.  The host-fed path's fallback for a batch whose rows overflow the
+ * sparse path's pool.  Column ids outside [0, F) set *status bit 0 and are skipped. */
+int bgcn_csr_to_dense(const int32_t* x_row_ptr, const int32_t* x_col, const float* x_val, int64_t num_nodes,
+                      int64_t in_feats, void* x, int64_t ldx, int32_t x_dtype, int32_t* status,
+                      bgcn_stream_t stream);
 
 size_t bgcn_prepare_workspace_size(int64_t num_nodes, int64_t num_graphs, int64_t in_feats,
                                    int64_t td_num_edges, int64_t bu_num_edges);

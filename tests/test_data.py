@@ -104,9 +104,14 @@ def test_npz_round_trip_through_dataset(tmp_path):
     tree = D.parse_rvnn(D.tree_to_rvnn_lines("abc", par, D.synth_bow(rng, 9, vocab=30)))["abc"]
     np.savez(tmp_path / "abc.npz", **D.graph_npz_dict(tree, 3, vocab=30))
     ds = D.BiGraphDataset(["abc"], {"abc": tree}, data_path=str(tmp_path))
-    s = ds[0]
+    s, tid = ds[0]                                       # (Data, root tweet id): dataset.py:94-99
     assert s.x.shape == (9, 30) and int(s.y) == 3 and int(s.rootindex) == 0
     assert torch.equal(s.BU_edge_index, s.edge_index.flip(0))
+    assert tid == "0"                                    # tweetids[rootindex] (graph_npz_dict: ids 0..n-1)
+    # the DataLoader form of BiGCN_Twitter.py:168,174: (Batch, [root tweet ids])
+    loader = torch.utils.data.DataLoader(ds, batch_size=2, collate_fn=D.collate_pairs)
+    b, tids = next(iter(loader))
+    assert tids == ["0"] and b.num_graphs == 1 and torch.equal(b.x, s.x)
     assert len(D.BiGraphDataset(["abc"], {"abc": tree}, lower=10, data_path=str(tmp_path))) == 0
 
 

@@ -1,0 +1,178 @@
+"""CPU tests of the host-fed input path (bigcn_amd.feed): the packed store and the
+one-buffer batches against the reference-format path (per-tree npz -> BiGraphDataset item
+-> PyG-style collate, Process/dataset.py:64-99), DropEdge counts, the DataLoader with
+worker processes, and the store's .npy persistence."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from bigcn_amd import data as D
+from bigcn_amd import feed as FD
+
+
+def _npz_trees(tmp_path, count=6, vocab=64, seed=3):
+    """Reference-format npz files (getTwittergraph.py:128 keys) of random trees, some with a
+    non-zero rootindex and a long row."""
+    rng = np.random.default_rng(seed)
+    eids = []
+    for t in range(count):
+        n = int(rng.integers(1, 12))
+        par = D.synth_parents(rng, n)
+        bow = D.synth_bow(rng, n, vocab=vocab, mean_extra=4.0)
+        if t == 2 and n > 1:
+            bow[1] = (np.arange(40), np.full(40, 2.0))       # a row over the ELL cap
+        lines = D.tree_to_rvnn_lines(f"e{t}", par, bow, root_pos=(n - 1 if t % 2 else 0))
+        tree = D.parse_rvnn(lines)[f"e{t}"]
+        d = D.graph_npz_dict(tree, int(rng.integers(0, 4)), vocab=vocab)
+        d["tweetids"] = np.array([str(1000 * t + k) for k in range(n)])
+        np.savez(tmp_path / f"e{t}.npz", **d)
+        eids.append(f"e{t}")
+    return eids
+
+
+def _csr_dense(hb, N, F):
+    rp, col, val = hb.section("x_row_ptr"), hb.section("x_col"), hb.section("x_val")
+    x = np.zeros((N, F), np.float32)
+    for i in range(N):
+        x[i, col[rp[i]:rp[i + 1]]] = val[rp[i]:rp[i + 1]]
+        assert np.all(np.diff(col[rp[i]:rp[i + 1]]) > 0)         # ascending, no duplicates
+        assert np.all(val[rp[i]:rp[i + 1]] != 0)                 # non-zeros only
+    return x
+
+
+def test_pack_matches_reference_collation(tmp_path):
+    eids = _npz_trees(tmp_path)
+    store = FD.TreeStore.from_npz_dir(str(tmp_path), eids, in_feats=64)
+    ds = D.BiGraphDataset(eids, None, data_path=str(tmp_path))
+    order = [4, 0, 2, 5, 1]
+    ref = D.collate([ds[i][0] for i in order])
+    hb = FD.pack_batch(store, order)
+    m = hb.meta
+    N = ref.x.size(0)
+    assert (m["N"], m["B"], m["in_feats"]) == (N, len(order), 64)
+    assert np.array_equal(_csr_dense(hb, N, 64), ref.x.numpy())
+    assert m["nnz"] == int((ref.x != 0).sum())
+    assert m["nnz_max"] == int((ref.x != 0).sum(1).max())
+    assert m["spill"] == int(((ref.x != 0).sum(1) - D.SPARSE_CAP).clamp_min(0).sum()) > 0
+    for name in ("edge_index", "BU_edge_index"):
+        assert np.array_equal(hb.section(name).reshape(2, -1), getattr(ref, name).numpy()), name
+    for name in ("batch", "rootindex", "y", "ptr"):
+        assert np.array_equal(hb.section(name), getattr(ref, name).numpy()), name
+    # root tweet ids: the reference's second item element (dataset.py:99), as int
+    assert [str(v) for v in hb.root_tweetids] == [ds[i][1] for i in order]
+    # the collated buffer: 256-byte aligned sections, the sizes the layout says
+    for name, (off, _) in m["layout"].items():
+        assert off % 256 == 0, name
+    assert hb.buf.numel() == m["bytes"]
+
+
+def test_store_save_load_mmap(tmp_path):
+    store = FD.TreeStore.synthetic(40, 30, seed=7, in_feats=300)
+    path = store.save(str(tmp_path / "store"))
+    back = FD.TreeStore.load(path, mmap=True)
+    assert isinstance(back.cols, np.memmap) and back.eids == store.eids and back.in_feats == 300
+    a = FD.pack_batch(store, [3, 9, 1])
+    b = FD.pack_batch(back, [3, 9, 1])
+    assert a.meta == b.meta
+    for name in a.meta["layout"]:
+        assert np.array_equal(a.section(name), b.section(name)), name
+    # every tree's edges: n - 1 (parent, child) pairs sorted by (parent, child), local ids
+    for t in range(len(store)):
+        e = store.edges[:, store.tree_edge[t]:store.tree_edge[t + 1]]
+        n = int(store.tree_node[t + 1] - store.tree_node[t])
+        assert e.shape[1] == n - 1
+        assert np.array_equal(np.lexsort((e[1], e[0])), np.arange(e.shape[1]))
+        assert sorted(e[1].tolist()) == sorted(set(range(n)) - {int(store.rootindex[t])})
+
+
+def test_synthetic_store_dense_equals_packed():
+    store = FD.TreeStore.synthetic(25, 20, seed=2, in_feats=128, root_random=True)
+    trees = list(range(0, 25, 2))
+    hb = FD.pack_batch(store, trees)
+    assert np.array_equal(_csr_dense(hb, hb.meta["N"], 128), store.dense_x(trees))
+    assert not np.array_equal(hb.section("rootindex"), hb.section("ptr")[:-1])   # roots moved
+
+
+@pytest.mark.parametrize("rate", [0.2, 0.5])
+def test_host_dropedge_counts(rate):
+    """dataset.py:68-90: per tree exactly int(E_t * (1 - rate)) edges kept, in edge order,
+    TD and BU drawn independently, BU from the undropped TD list."""
+    store = FD.TreeStore.synthetic(30, 25, seed=11, in_feats=64)
+    trees = list(range(30))
+    full = FD.pack_batch(store, trees)
+    hb = FD.pack_batch(store, trees, rate, rate, rng=np.random.default_rng(0))
+    E_t = (store.tree_edge[1:] - store.tree_edge[:-1])[trees]
+    fe = full.section("edge_index").reshape(2, -1)
+    for name in ("edge_index", "BU_edge_index"):
+        e = hb.section(name).reshape(2, -1)
+        src = e[0] if name == "edge_index" else e[1]              # the parent side
+        bt = full.section("batch")[src]
+        assert np.array_equal(np.bincount(bt, minlength=30), (E_t * (1 - rate)).astype(np.int64))
+        # a subsequence of the full list, in order
+        ref = fe if name == "edge_index" else fe[::-1]
+        key_full = ref[0] * 10**6 + ref[1]
+        key = e[0] * 10**6 + e[1]
+        pos = np.searchsorted(key_full, key) if np.all(np.diff(key_full) > 0) else None
+        if pos is not None:
+            assert np.all(np.diff(pos) > 0)
+    assert not np.array_equal(hb.section("edge_index").reshape(2, -1),
+                              hb.section("BU_edge_index").reshape(2, -1)[::-1])
+
+
+def test_dataloader_with_workers(tmp_path):
+    """The loader of the host-fed bench: batch_size trees per item, worker processes, one
+    shared-memory buffer per batch (the reference's DataLoader(..., num_workers=5))."""
+    store = FD.TreeStore.synthetic(50, 20, seed=5, in_feats=200)
+    path = store.save(str(tmp_path / "s"))
+    ds = FD.PackedTreeDataset(path)
+    loader = torch.utils.data.DataLoader(ds, batch_size=8, shuffle=True, num_workers=2,
+                                         collate_fn=FD.host_collate, drop_last=True,
+                                         generator=torch.Generator().manual_seed(0))
+    seen = []
+    for hb in loader:
+        assert isinstance(hb, FD.HostBatch) and hb.meta["B"] == 8
+        ptr = hb.section("ptr")
+        seen.append(int(ptr[-1]))
+        assert hb.meta["N"] == int(ptr[-1])
+        assert np.array_equal(hb.section("batch"), np.repeat(np.arange(8), np.diff(ptr)))
+    assert len(seen) == 6 and sum(seen) <= int(store.tree_node[-1])
+
+
+def test_bf16_values_round():
+    store = FD.TreeStore.synthetic(5, 10, seed=1, in_feats=64)
+    store.vals = store.vals * np.float32(1.0 + 2.0 ** -10)    # not bf16-exact
+    hb = FD.pack_batch(store, [0, 1], bf16_values=True)
+    v = torch.from_numpy(hb.section("x_val").copy())
+    assert torch.equal(v, v.to(torch.bfloat16).float())
+
+
+class _DoneEvent:
+    def synchronize(self):
+        pass
+
+
+def test_slot_ring_loader_packs_in_place(tmp_path):
+    """host_fed_loader: workers pack each batch straight into a shared slot; only (slot,
+    sequence, sizes) cross the worker queue; a slot is reused only after its batch's copy
+    (emulated here: the feeder records a completed event per slot)."""
+    store = FD.TreeStore.synthetic(60, 15, seed=8, in_feats=100)
+    path = store.save(str(tmp_path / "s"))
+    loader = FD.host_fed_loader(path, batch_size=4, num_workers=2, shuffle=False, prefetch_factor=2)
+    ring = loader.dataset.ring
+    assert ring.nslots == 8 and ring.slot_bytes >= FD.pack_batch(store, range(56, 60)).meta["bytes"]
+    for epoch in range(2):   # > nslots batches per epoch: every slot is reused
+        for k, hb in enumerate(loader):
+            assert hb.buf is None and hb.slot == hb.seq % ring.nslots and hb.seq == 15 * epoch + k
+            ref = FD.pack_batch(store, range(4 * k, 4 * k + 4))
+            assert hb.meta == ref.meta
+            view = FD.HostBatch(ring.slot(hb.slot)[:hb.meta["bytes"]], hb.meta, hb.root_tweetids)
+            for name in ref.meta["layout"]:
+                assert np.array_equal(view.section(name), ref.section(name)), name
+            ring.events[hb.slot], ring.seqs[hb.slot] = _DoneEvent(), hb.seq
+    # a feeder that never copies a batch out: the sampler refuses to overwrite it
+    ring.seqs = [-1] * ring.nslots
+    with pytest.raises(RuntimeError, match="slot ring too small"):
+        for hb in loader:
+            pass

@@ -336,3 +336,50 @@ def test_model_train_step_matches_oracle(plan, monkeypatch):
     grads = dict((k, q.grad) for k, q in m.named_parameters())
     for k in p:
         close(grads[k], rgrads[k], what=k)
+
+
+@pytest.mark.parametrize("fused_step", [False, True])
+def test_edge_across_trees(fused_step):
+    """An edge joining two trees (never made by PyG collation, but legal for GCNConv +
+    scatter_mean): K1 built with the batch vector flags BGCN_STATUS_CROSS_TREE and the
+    sign-word readout backward then scales every gathered row by its own tree - gradients
+    match the oracle and the general readout backward (graphs built without the check)."""
+    from bigcn_amd import _lib
+    from bigcn_amd.ops import bigcn_encoder, build_graph_pair
+    b = _synth(77, 6, 20, droprates=(0.0, 0.0))
+    N = b.x.size(0)
+    u, v = int(b.ptr[0]) + 1, int(b.ptr[2]) + 2          # tree 0 -> tree 2
+    extra = torch.tensor([[u], [v]], device=DEV)
+    b.edge_index = torch.cat([b.edge_index, extra], 1)
+    b.BU_edge_index = torch.cat([b.BU_edge_index, extra.flip(0)], 1)
+    p = O.make_params(5000, 64, 64, 4, seed=31)
+    _, rloss, rgrads, _ = _oracle(b, p, False)
+    if fused_step:
+        from bigcn_amd import FusedTrainStep
+        from test_gpu_train import _model
+        m = _model(p)
+        m.eval()
+        st = FusedTrainStep(m)
+        loss = st.forward_backward(b, seed=0)
+        torch.cuda.synchronize()
+        st.check_status()
+        close(loss, rloss, what="loss")
+        for k, prm in zip(ENC_KEYS + ["fc.weight", "fc.bias"], st.step_params):
+            close(st.grads()[prm], rgrads[k], what=k)
+        return
+    got = {}
+    for checked in (True, False):
+        td, bu = build_graph_pair(b.edge_index, b.BU_edge_index, N, batch=b.batch if checked else None)
+        q = {k: v.float().to(DEV).contiguous().requires_grad_(True) for k, v in p.items()}
+        head = bigcn_encoder(b.x, b.batch, b.rootindex, td, bu, b.num_graphs, [q[k] for k in ENC_KEYS])
+        loss = F.nll_loss(F.log_softmax(F.linear(head, q["fc.weight"], q["fc.bias"]), 1), b.y)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert (int(td.status.item()) & _lib.BGCN_STATUS_CROSS_TREE) == (_lib.BGCN_STATUS_CROSS_TREE if checked else 0)
+        td.check()
+        close(loss, rloss, what="loss")
+        for k in ENC_KEYS:
+            close(q[k].grad, rgrads[k], what=k)
+        got[checked] = [q[k].grad.clone() for k in ENC_KEYS]
+    for a, c in zip(got[True], got[False]):   # per-neighbour scales = the general readout backward
+        assert torch.allclose(a, c, rtol=1e-5, atol=1e-7 * float(c.abs().max()))
