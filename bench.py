@@ -285,7 +285,9 @@ def compaction_standalone(fused, b, wl, iters: int = 10):
                                                 buf.numel(), stream_handle()))
             torch.cuda.synchronize()
             ops.set_kernel_timing(False)
-            ms, n = ops.kernel_timing(7)
+            ms, n = ops.kernel_span(7)        # the kernel's own device-side span
+            if n == 0:
+                ms, n = ops.kernel_timing(7)
             avg = ms / max(n, 1)
             gbs = nbytes / (avg * 1e-3) / 1e9
             out[name] = {"avg_ms": round(avg, 4), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
@@ -329,14 +331,31 @@ def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int
         feeder.copy_stats(reset=True)
         fused.run_report(reset=True)
         nodes = 0
+        t_next = t_call = 0.0
         t0 = time.perf_counter()
         for _ in range(steps):
+            ta = time.perf_counter()
             nxt = next(it)
+            tb = time.perf_counter()
             fused(cur, next_data=nxt)
+            t_call += time.perf_counter() - tb
+            t_next += tb - ta
             nodes += cur.num_nodes
             cur = nxt
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        fused.discard_prefetch()
+        # the same compacted batches resident on the device (no loader, no copies): the
+        # device-side rate of the compacted-input step
+        pool = [next(it) for _ in range(4)]
+        for k in range(6):
+            fused(pool[k % 4], next_data=pool[(k + 1) % 4])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for k in range(steps):
+            fused(pool[k % 4], next_data=pool[(k + 1) % 4])
+        torch.cuda.synchronize()
+        dt_res = time.perf_counter() - t1
         fused.discard_prefetch()
     n, mean_bytes, copy_ms = feeder.copy_stats()
     report = fused.run_report()
@@ -345,7 +364,13 @@ def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int
     dense_bytes = nodes / steps * wl["feats"] * (2 if xdt == torch.bfloat16 else 4)
     return {"host_fed": {"value": round(wl["trees"] * steps / dt, 2), "unit": "trees/s",
                          "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
-                         "status": report["status"], "invalid_steps": report["invalid_steps"]},
+                         "status": report["status"], "invalid_steps": report["invalid_steps"],
+                         "host_ms_per_step_in_loader": round(t_next / steps * 1e3, 4),
+                         "host_ms_per_step_in_step_call": round(t_call / steps * 1e3, 4)},
+            "compacted_resident": {"value": round(wl["trees"] * steps / dt_res, 2), "unit": "trees/s",
+                                   "ms_per_step": round(dt_res / steps * 1e3, 4),
+                                   "what": "4 compacted batches resident in HBM, cycled (no loader, no H2D): "
+                                           "the step without the pass over a dense x"},
             "h2d_bytes_per_batch": round(mean_bytes), "h2d_ms_per_batch": round(copy_ms, 4),
             "h2d_gbs": round(mean_bytes / (copy_ms * 1e-3) / 1e9, 2) if copy_ms > 0 else None,
             "dense_x_bytes_per_batch": round(dense_bytes),
@@ -504,10 +529,12 @@ def main():
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        kern = {}
+        kern, span = {}, None
         if timing and dominant:
             ops.set_kernel_timing(False)
             kern[dominant[0]] = ops.kernel_timing(dominant[0])
+            if dominant[0] == 7:   # the pass over X stamps its own device-side span
+                span = ops.kernel_span(7)
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -543,16 +570,24 @@ def main():
                         "traffic": pmc_traffic(mode, c, args.workload), "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
             else:
+                event_ms = avg_ms
+                timer = "HIP events on the launch stream"
+                if c == 7 and span is not None and span[1] > 0:
+                    # device-side span: first block start -> last block end on the constant
+                    # wall clock, the duration rocprofv3 reports for the dispatch
+                    avg_ms = span[0] / span[1]
+                    timer = "device wall-clock span (first block start to last block end, in-kernel stamps)"
                 ach = work / (avg_ms * 1e-3) / 1e9
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(mode, c, args.workload),
                         "kernel": KERNEL_CLASSES[mode][c], "bytes_per_launch": work,
-                        "avg_ms": round(avg_ms, 4)}
+                        "avg_ms": round(avg_ms, 4), "timer": timer, "event_avg_ms": round(event_ms, 4),
+                        "frac_by_event_bracket": round(work / (event_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
                 if mode == "auto" and c == 7 and args.prefetch:
-                    roof["note"] = ("HIP events around the launch on the side lane: the bracket includes the "
-                                    "pass's dispatch delay beside the second preparation lane's launches; the "
-                                    "rocprofv3 kernel time of the same command is ~17 % shorter "
-                                    "(profiles/r03_kernel_stats.csv, BASELINE.md)")
+                    roof["note"] = ("frac uses the kernel's own span (comparable with the rocprofv3 kernel "
+                                    "average under profiles/); the HIP-event bracket on the side lane also "
+                                    "holds the pass's dispatch delay behind the second preparation lane "
+                                    "(frac_by_event_bracket)")
         value = wl["trees"] * world * steps / dt
         # the step's validity (one host read after the timed region): the OR of the timed
         # steps' status words and the optimiser updates skipped as invalid, max over ranks
@@ -585,11 +620,6 @@ def main():
         ctx["path"] = "autograd"
         dropin_res = run(args.feat_mode, max(5, args.steps // 2), 3)
         ctx["pool"], ctx["path"] = pool, args.path
-    staging = None
-    if world == 1 and args.path == "fused" and args.host_fed and args.feat_mode == "auto":
-        # same model / optimiser / DropEdge as the headline step (its state continues)
-        staging = host_fed_bench(fused, wl, dev, stream, max(20, args.steps), min(args.warmup, 10),
-                                 args.host_fed_workers, args.host_fed_trees)
     agg = None
     if world == 1 and args.aggregation:
         agg = aggregation_bench(pool[0])
@@ -597,6 +627,11 @@ def main():
     if world == 1 and args.path == "fused" and args.feat_mode == "auto":
         with torch.cuda.stream(stream):
             comp = compaction_standalone(fused, pool[0], wl)
+    staging = None
+    if world == 1 and args.path == "fused" and args.host_fed and args.feat_mode == "auto":
+        # same model / optimiser / DropEdge as the headline step (its state continues)
+        staging = host_fed_bench(fused, wl, dev, stream, max(20, args.steps), min(args.warmup, 10),
+                                 args.host_fed_workers, args.host_fed_trees)
     if rank == 0:
         value, dt, N_avg = main_res["value"], main_res["dt"], main_res["N_avg"]
         roof, kernels, final_loss = main_res["roof"], main_res["kernels"], main_res["loss"]

@@ -38,7 +38,8 @@ BGCN_STATUS_CROSS_TREE = 16
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
     "bgcn_abi_version", "bgcn_last_error",
-    "bgcn_graph_workspace_size", "bgcn_build_graph",
+    "bgcn_graph_workspace_size", "bgcn_build_graph", "bgcn_graph_dinv",
+    "bgcn_edge_weight_grad_workspace_size", "bgcn_edge_weight_grad",
     "bgcn_graph_pair_workspace_size", "bgcn_build_graph_pair", "bgcn_graph_pair_plans",
     "bgcn_spmm_workspace_size", "bgcn_spmm",
     "bgcn_gemm_xwt", "bgcn_gemm_xw", "bgcn_gemm_tn_workspace_size", "bgcn_gemm_tn",
@@ -47,7 +48,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_head_forward", "bgcn_head_backward",
     "bgcn_drop_edges_workspace_size", "bgcn_drop_edges",
     "bgcn_bigcn_workspace_size", "bgcn_bigcn_forward", "bgcn_bigcn_backward",
-    "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_adam_step",
+    "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_kernel_span", "bgcn_adam_step",
     "bgcn_prepare_workspace_size", "bgcn_prepare_batch", "bgcn_csr_to_dense",
     "bgcn_train_step_workspace_size", "bgcn_train_step", "bgcn_train_step_dw1", "bgcn_join_side",
     "bgcn_weight_images_size", "bgcn_train_step_saved",
@@ -133,6 +134,10 @@ _SIGS = {
                                  c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_graph_pair_workspace_size": (c_size_t, [c_int64, c_int64, c_int64]),
+    "bgcn_graph_dinv": (c_int, [c_void_p, c_size_t, c_int64, c_int64, POINTER(c_void_p)]),
+    "bgcn_edge_weight_grad_workspace_size": (c_size_t, [c_int64]),
+    "bgcn_edge_weight_grad": (c_int, [c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_build_graph_pair": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int,
                                       POINTER(CsrOut), POINTER(CsrOut), c_void_p, c_void_p, c_void_p,
                                       c_size_t, c_void_p]),
@@ -183,6 +188,7 @@ _SIGS = {
                                       POINTER(c_void_p), POINTER(c_void_p)]),
     "bgcn_set_kernel_timing": (c_int, [c_int]),
     "bgcn_kernel_timing": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),
+    "bgcn_kernel_span": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),
 }
 
 _lock = threading.Lock()

@@ -87,6 +87,11 @@ int aux_prep_wait(hipStream_t main);
 // kernel timing hook (bench.py): record HIP events around a launch of a class
 void timing_begin(int cls, hipStream_t s);
 void timing_end(int cls, hipStream_t s);
+// the span record of the next launch of a stamped class (nullptr: not timed): blocks
+// b < kSpanStarts store their start time at [b], every block atomicMax's its end time into
+// [kSpanStarts + b % kSpanEnds] (distinct addresses: no contention) - span_stamp_*
+constexpr int kSpanStarts = 64, kSpanEnds = 8192, kSpanRecord = kSpanStarts + kSpanEnds;
+uint64_t* span_slot(int cls);
 
 constexpr int kWave = 64;
 // status word bits: 1 bad edge index, 2 bad label, 4 over-full feature row (sparse

@@ -257,6 +257,74 @@ __global__ void k_normalize(GraphBatch gb) {
   G.s_w[p] = (G.dinv[G.s_row[p]] * G.s_w[p]) * G.dinv[G.s_col[p]];
 }
 
+// ---- gcn_norm backward: the gradient w.r.t. edge_weight (EBGCN learns its edge weights,
+// model/Twitter/EBGCN.py:101-102 sigmoid -> GCNConv(..., edge_weight) at :84,178).
+// With g_e = <dout[dst_e], h[src_e]> (dL/dnorm_e), norm_e = dis[src] w_e dis[dst] and
+// dis = deg^-1/2 (deg[k] = the weights summed at k's target - or source - side, its loop
+// included):
+//   S[k]         = sum_{e: src=k} g_e norm_e + sum_{e: dst=k} g_e norm_e
+//                = <dout[k], (A h)[k]> + <h[k], (A^T dout)[k]>     (row dots, no gathers)
+//   dL/ddeg[k]   = -1/2 dis[k]^2 S[k]          (0 where dis = 0: the masked inf)
+//   dL/dw_e      = g_e dis[src] dis[dst] + dL/ddeg[key_e]            (key = dst, or src)
+//   an input self loop (its weight is the node's loop weight, add_remaining_self_loops):
+//   dL/dw_e      = <dout[k], h[k]> dis[k]^2 + dL/ddeg[k]
+// One 16-lane group per node / per edge, float4 over the (padded) feature width.
+struct EwArgs {
+  const int64_t* ei;
+  int64_t E, N;
+  int degree_on;
+  const float *dinv, *h, *agg, *dout, *dz;
+  int64_t ld;
+  int F4;
+  float *dldeg, *lgrad, *dw;
+};
+
+__device__ __forceinline__ float dot4(float4 a, float4 b) {
+  return fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
+}
+__device__ __forceinline__ float sum16(float v) {
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m, 16);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_ew_nodes(EwArgs a) {
+  const int64_t k = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 16;
+  const int l = threadIdx.x & 15;
+  if (k >= a.N) return;   // group-uniform
+  float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (int c = 4 * l; c < a.F4; c += 64) {
+    const float4 d = ld4(a.dout + k * a.ld + c), h = ld4(a.h + k * a.ld + c);
+    s1 += dot4(d, ld4(a.agg + k * a.ld + c));
+    s2 += dot4(h, ld4(a.dz + k * a.ld + c));
+    s3 += dot4(d, h);
+  }
+  s1 = sum16(s1); s2 = sum16(s2); s3 = sum16(s3);
+  if (l == 0) {
+    const float dis = a.dinv[k];
+    const float dld = dis > 0.f ? -0.5f * dis * dis * (s1 + s2) : 0.f;
+    a.dldeg[k] = dld;
+    a.lgrad[k] = s3 * dis * dis + dld;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ew_edges(EwArgs a) {
+  const int64_t e = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 16;
+  const int l = threadIdx.x & 15;
+  if (e >= a.E) return;   // group-uniform
+  const int64_t src = a.ei[e], dst = a.ei[a.E + e];
+  const bool valid = src >= 0 && src < a.N && dst >= 0 && dst < a.N;
+  if (!valid || src == dst) {
+    if (l == 0) a.dw[e] = valid ? a.lgrad[src] : 0.f;   // an input loop: the loop weight's gradient
+    return;
+  }
+  float s = 0.f;
+  for (int c = 4 * l; c < a.F4; c += 64) s += dot4(ld4(a.dout + dst * a.ld + c), ld4(a.h + src * a.ld + c));
+  s = sum16(s);
+  if (l == 0)
+    a.dw[e] = s * a.dinv[src] * a.dinv[dst] + a.dldeg[a.degree_on == BGCN_DEGREE_ON_COL ? dst : src];
+}
+
 }  // namespace
 
 size_t graph_carve(Carve& c, int64_t E, int64_t N, GraphIO* G, size_t* zero_bytes) {
@@ -473,4 +541,44 @@ extern "C" int bgcn_build_graph_pair(const int64_t* td_edge_index, int64_t td_nu
       {bu_edge_index, nullptr, bu_num_edges, bu->t_ptr, bu->t_row, bu->t_col, bu->t_w, bu->s_ptr,
        bu->s_row, bu->s_col, bu->s_w, status, ws ? ws + half : nullptr, half}};
   return bgcn::build_graphs_impl(a, 2, num_nodes, degree_on, reinterpret_cast<hipStream_t>(stream), batch);
+}
+
+extern "C" int bgcn_graph_dinv(const void* workspace, size_t workspace_bytes, int64_t num_edges, int64_t num_nodes,
+                               const float** dinv) {
+  if (!workspace || !dinv || num_nodes <= 0 || num_edges < 0) return bgcn::fail(BGCN_EINVAL, "bad arguments");
+  if (workspace_bytes < bgcn::graph_ws_size(num_edges, num_nodes))
+    return bgcn::fail(BGCN_EINVAL, "workspace smaller than the build's");
+  bgcn::Carve c(const_cast<void*>(workspace), workspace_bytes);
+  bgcn::GraphIO G{};
+  bgcn::graph_carve(c, num_edges, num_nodes, &G, nullptr);
+  *dinv = G.dinv;
+  return BGCN_OK;
+}
+
+extern "C" size_t bgcn_edge_weight_grad_workspace_size(int64_t num_nodes) {
+  return num_nodes > 0 ? 2 * bgcn::align_up(size_t(num_nodes) * sizeof(float), 256) + 256 : 0;
+}
+
+extern "C" int bgcn_edge_weight_grad(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int degree_on,
+                                     const float* dinv, const float* h, const float* agg, const float* dout,
+                                     const float* dz, int64_t ld, int32_t F, float* d_edge_weight, void* workspace,
+                                     size_t workspace_bytes, bgcn_stream_t stream) {
+  using namespace bgcn;
+  BGCN_CHECK_ARG(num_nodes > 0 && num_edges >= 0 && F > 0 && F % 4 == 0 && ld >= F && ld % 4 == 0,
+                 "bad sizes (F and ld: multiples of 4)");
+  BGCN_CHECK_ARG(degree_on == BGCN_DEGREE_ON_COL || degree_on == BGCN_DEGREE_ON_ROW, "bad degree_on");
+  BGCN_CHECK_ARG(dinv && h && agg && dout && dz && (num_edges == 0 || (edge_index && d_edge_weight)), "null pointer");
+  BGCN_CHECK_ARG(workspace && workspace_bytes >= bgcn_edge_weight_grad_workspace_size(num_nodes),
+                 "workspace too small");
+  Carve c(workspace, workspace_bytes);
+  EwArgs a{edge_index, num_edges, num_nodes, degree_on, dinv, h, agg, dout, dz, ld, int(F),
+           c.take<float>(size_t(num_nodes)), c.take<float>(size_t(num_nodes)), d_edge_weight};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_ew_nodes, dim3(grid_for(num_nodes * 16, 256)), dim3(256), 0, s, a);
+  BGCN_CHECK_LAUNCH();
+  if (num_edges > 0) {
+    hipLaunchKernelGGL(k_ew_edges, dim3(grid_for(num_edges * 16, 256)), dim3(256), 0, s, a);
+    BGCN_CHECK_LAUNCH();
+  }
+  return BGCN_OK;
 }

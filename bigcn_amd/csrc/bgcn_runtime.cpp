@@ -32,6 +32,18 @@ struct TimingState {
 TimingState g_tm;
 std::mutex g_tm_mu;
 
+// Device-side spans (span_slot): one record per launch of a stamped kernel - the start
+// times of its first kSpanStarts blocks and the end time of every block (slot b mod
+// kSpanEnds), on the device's constant wall clock, written without contended atomics; the
+// host takes min(start) and max(end).  Zeroed when timing is enabled.
+constexpr int kSpanCap = 256;   // launches per timing session
+struct SpanState {
+  uint64_t* dev = nullptr;
+  int next = 0;
+  std::vector<int> slots[kTimingClasses];
+};
+SpanState g_span;
+
 // auxiliary streams ("lanes") + fork/join events per device (created on first use)
 constexpr int kMaxDevices = 64;
 struct AuxState {
@@ -112,6 +124,15 @@ void timing_begin(int cls, hipStream_t s) {
   if (!e) return;
   (void)hipEventRecord(e, s);
   g_tm.open[cls] = e;
+}
+
+uint64_t* span_slot(int cls) {
+  if (!g_tm.enabled || cls < 0 || cls >= kTimingClasses || !((g_tm.mask >> cls) & 1u)) return nullptr;
+  std::lock_guard<std::mutex> lk(g_tm_mu);
+  if (!g_span.dev || g_span.next >= kSpanCap) return nullptr;
+  const int i = g_span.next++;
+  g_span.slots[cls].push_back(i);
+  return g_span.dev + size_t(kSpanRecord) * i;
 }
 
 void timing_end(int cls, hipStream_t s) {
@@ -210,6 +231,17 @@ extern "C" int bgcn_set_kernel_timing(int enable) {
     if (t.open[c]) (void)hipEventSynchronize(t.open[c]), t.free_events.push_back(t.open[c]);
     t.open[c] = nullptr;
   }
+  // the span array: (re)filled with {~0, 0} pairs when timing is enabled, synchronously
+  // (outside any timed region); disabling keeps the recorded spans for bgcn_kernel_span
+  auto& sp = bgcn::g_span;
+  if (t.enabled) {
+    for (auto& v : sp.slots) v.clear();
+    sp.next = 0;
+    const size_t bytes = sizeof(uint64_t) * size_t(bgcn::kSpanRecord) * bgcn::kSpanCap;
+    if (!sp.dev && hipMalloc(reinterpret_cast<void**>(&sp.dev), bytes) != hipSuccess) sp.dev = nullptr;
+    if (sp.dev && (hipMemset(sp.dev, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+      return bgcn::fail(BGCN_EHIP, "span array init failed");
+  }
   // pre-create events so that the timed loop only records (hipEventCreate is not free)
   while (t.enabled && t.free_events.size() < 1024) {
     hipEvent_t e = nullptr;
@@ -238,5 +270,37 @@ extern "C" int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* la
   v.clear();
   if (total_ms) *total_ms = float(t.total_ms[kernel_class]);
   if (launches) *launches = t.count[kernel_class];
+  return BGCN_OK;
+}
+
+// Synchronises (hipDeviceSynchronize, then one copy of the used pairs).
+extern "C" int bgcn_kernel_span(int kernel_class, float* total_ms, int64_t* launches) {
+  std::lock_guard<std::mutex> lk(bgcn::g_tm_mu);
+  if (kernel_class < 0 || kernel_class >= bgcn::kTimingClasses) return bgcn::fail(BGCN_EINVAL, "bad kernel class");
+  auto& sp = bgcn::g_span;
+  double ms = 0.0;
+  int64_t n = 0;
+  if (sp.dev && !sp.slots[kernel_class].empty()) {
+    BGCN_CHECK_HIP(hipDeviceSynchronize());
+    std::vector<uint64_t> h(size_t(bgcn::kSpanRecord) * size_t(sp.next));
+    BGCN_CHECK_HIP(hipMemcpy(h.data(), sp.dev, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    int dev = 0, khz = 0;
+    BGCN_CHECK_HIP(hipGetDevice(&dev));
+    BGCN_CHECK_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    if (khz <= 0) return bgcn::fail(BGCN_EHIP, "no wall clock rate");
+    for (int i : sp.slots[kernel_class]) {
+      const uint64_t* r = h.data() + size_t(bgcn::kSpanRecord) * i;
+      uint64_t a = ~uint64_t(0), b = 0;
+      for (int k = 0; k < bgcn::kSpanStarts; ++k)
+        if (r[k]) a = r[k] < a ? r[k] : a;
+      for (int k = bgcn::kSpanStarts; k < bgcn::kSpanRecord; ++k) b = r[k] > b ? r[k] : b;
+      if (b >= a && a != ~uint64_t(0)) {
+        ms += double(b - a) / double(khz);
+        ++n;
+      }
+    }
+  }
+  if (total_ms) *total_ms = float(ms);
+  if (launches) *launches = n;
   return BGCN_OK;
 }

@@ -1753,6 +1753,7 @@ struct PrepArgs {
   int64_t ldx;
   const int32_t *xr_ptr, *xr_col;   // host-fed compacted features (X == nullptr), else null
   const float* xr_val;
+  uint64_t* span;                   // device span stamps of the launch (timing class 7) or null
   int64_t* eptr;
   uint64_t seed;
   uint4* zero[2];
@@ -1784,7 +1785,7 @@ __global__ __launch_bounds__(256) void k_prep_a(PrepArgs a) {
 }
 
 template <class TX>
-__global__ __launch_bounds__(256) void k_prep_b(PrepArgs a) {
+__device__ inline void prep_b_body(const PrepArgs& a) {
   int b = int(blockIdx.x);
   if (b < a.nsel) {   // (tree, list) blocks first: they finish beside the pass over X
     const int d = b / int(a.S.B);
@@ -1799,6 +1800,21 @@ __global__ __launch_bounds__(256) void k_prep_b(PrepArgs a) {
   }
   if (a.xr_ptr) csr_ell_body(a.S, a.xr_ptr, a.xr_col, a.xr_val, b - 1, a.ncomp);
   else compact_body<false, TX>(a.S, static_cast<const TX*>(a.X), a.ldx, nullptr, b - 1, a.ncomp);
+}
+
+// a.span (the kernel-timing hook, class 7): every block min's its start and max's its end
+// into the launch's wall-clock pair - the kernel's own span, as rocprofv3 reports it
+template <class TX>
+__global__ __launch_bounds__(256) void k_prep_b(PrepArgs a) {
+  if (a.span && threadIdx.x == 0 && blockIdx.x < kSpanStarts)
+    a.span[blockIdx.x] = uint64_t(wall_clock64());
+  prep_b_body<TX>(a);
+  if (a.span) {
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomicMax(reinterpret_cast<unsigned long long*>(a.span) + kSpanStarts + blockIdx.x % kSpanEnds,
+                static_cast<unsigned long long>(wall_clock64()));
+  }
 }
 
 __global__ __launch_bounds__(256) void k_prep_c(PrepArgs a) {
@@ -2261,6 +2277,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
       hipLaunchKernelGGL(k_prep_f, dim3(unsigned(2 * (ag.ne + ag.nn + ag.np))), blk, 0, g, ag);
     BGCN_CHECK_LAUNCH();
     timing_begin(7, s);
+    ax.span = span_slot(7);
     if (bt->x_dtype == BGCN_DTYPE_BF16) hipLaunchKernelGGL(k_prep_b<bf16_t>, dim3(unsigned(1 + ax.ncomp)), blk, 0, s, ax);
     else hipLaunchKernelGGL(k_prep_b<float>, dim3(unsigned(1 + ax.ncomp)), blk, 0, s, ax);
     BGCN_CHECK_LAUNCH();
@@ -2274,6 +2291,7 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
     return BGCN_OK;
   }
   timing_begin(7, s);
+  a.span = span_slot(7);
   const unsigned nb = unsigned(a.nsel + 1 + a.ncomp);
   if (bt->x_dtype == BGCN_DTYPE_BF16) hipLaunchKernelGGL(k_prep_b<bf16_t>, dim3(nb), blk, 0, s, a);
   else hipLaunchKernelGGL(k_prep_b<float>, dim3(nb), blk, 0, s, a);

@@ -197,9 +197,18 @@ def build_graph(edge_index: torch.Tensor, num_nodes: int, edge_weight: Optional[
                              *(g._ptrs[n] for n in ("t_ptr", "t_row", "t_col", "t_w",
                                                     "s_ptr", "s_row", "s_col", "s_w")),
                              ptr(g.status), ptr(ws), ws.numel(), stream_handle()))
+    g._plan_ws = ws   # the build's workspace: D^-1/2 (bgcn_graph_dinv) for the edge-weight gradient
     if validate:
         g.check()
     return g
+
+
+def _graph_dinv(g: Graph) -> int:
+    """Device pointer of the D^-1/2 vector a single-graph build left in its workspace."""
+    out = ctypes.c_void_p()
+    ws = g._plan_ws
+    check(_lib.lib().bgcn_graph_dinv(ws.data_ptr(), ws.numel(), g.num_edges, g.num_nodes, ctypes.byref(out)))
+    return int(out.value)
 
 
 def drop_edges(td_edge_index: Optional[torch.Tensor], bu_edge_index: Optional[torch.Tensor],
@@ -297,10 +306,10 @@ def _linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 
 class _GCNConvFn(torch.autograd.Function):
-    """PyG-2.x GCNConv: out = A_hat (x W^T) + b."""
+    """PyG-2.x GCNConv: out = A_hat (x W^T) + b, A_hat = gcn_norm(edge_index, edge_weight)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, g: Graph):
+    def forward(ctx, x, weight, bias, g: Graph, edge_index=None, edge_weight=None, degree_on="col"):
         x = x.contiguous().float()
         weight = weight.contiguous()
         z = _pad4(_linear(x, weight))
@@ -308,20 +317,35 @@ class _GCNConvFn(torch.autograd.Function):
         b = None if bias is None else _pad4(bias.view(1, -1)).view(-1)
         out = spmm(g, z, b)[:, :O]
         ctx.g = g
-        ctx.save_for_backward(x, weight)
+        ctx.degree_on = degree_on
+        ew_grad = edge_weight is not None and ctx.needs_input_grad[5]
+        # the edge-weight gradient needs h = x W^T (padded) and the edge list
+        ctx.save_for_backward(x, weight, z if ew_grad else None, edge_index if ew_grad else None)
         ctx.has_bias = bias is not None
         return out.contiguous()
 
     @staticmethod
     def backward(ctx, dout):
-        x, weight = ctx.saved_tensors
+        x, weight, z, ei = ctx.saved_tensors
         g: Graph = ctx.g
         L = _lib.lib()
         N, K = x.shape
         O = weight.size(0)
         d = _pad4(dout.float())
-        dz = spmm(g, d, transposed=True)[:, :O].contiguous()   # A_hat^T dout
-        dx = dw = db = None
+        dzp = spmm(g, d, transposed=True)                       # A_hat^T dout (padded width)
+        dz = dzp[:, :O].contiguous()
+        dx = dw = db = dew = None
+        if len(ctx.needs_input_grad) > 5 and ctx.needs_input_grad[5] and z is not None:
+            # gcn_norm's backward (EBGCN.py:84,178 learn edge_weight): row dots of
+            # (dout, A_hat h) and (h, A_hat^T dout), then one dot per edge
+            agg = spmm(g, z)                                     # A_hat h, no bias
+            E = int(ei.size(1))
+            dew = torch.empty(E, dtype=torch.float32, device=x.device)
+            ws = workspace(L.bgcn_edge_weight_grad_workspace_size(N), x.device)
+            F4 = int(z.size(1))
+            check(L.bgcn_edge_weight_grad(ptr(ei), E, N, degree_code(ctx.degree_on), _graph_dinv(g), ptr(z),
+                                          ptr(agg), ptr(d), ptr(dzp), F4, F4, ptr(dew), ptr(ws), ws.numel(),
+                                          stream_handle()))
         if ctx.needs_input_grad[0]:
             dx = torch.empty(N, K, dtype=torch.float32, device=x.device)
             check(L.bgcn_gemm_xw(ptr(dz), dz.stride(0), ptr(weight), weight.stride(0), ptr(dx), K,
@@ -337,18 +361,23 @@ class _GCNConvFn(torch.autograd.Function):
             ws = workspace(L.bgcn_colsum_workspace_size(N, O), x.device)
             check(L.bgcn_colsum(ptr(dd), dd.stride(0), N, O, ptr(db), ptr(ws), ws.numel(),
                                 stream_handle()))
-        return dx, dw, db, None
+        return (dx, dw, db, None, None, dew, None)[:len(ctx.needs_input_grad)]
 
 
 def gcn_conv(x: torch.Tensor, edge_index_or_graph, weight: torch.Tensor,
              bias: Optional[torch.Tensor] = None, edge_weight: Optional[torch.Tensor] = None,
              degree_on: str = "col") -> torch.Tensor:
-    _dev_check(x, weight, bias)
-    if edge_weight is not None and edge_weight.requires_grad and torch.is_grad_enabled():
-        # EBGCN (EBGCN.py:84,178) learns edge weights; that gradient is not on this path
-        raise NotImplementedError("gcn_conv: gradients w.r.t. edge_weight are not supported; "
-                                  "pass edge_weight.detach()")
+    _dev_check(x, weight, bias, edge_weight)
     g = edge_index_or_graph
+    if edge_weight is not None and edge_weight.requires_grad and torch.is_grad_enabled():
+        # EBGCN (EBGCN.py:101-102 -> :84,178) learns its edge weights: gcn_norm's backward
+        if isinstance(g, Graph):
+            raise ValueError("gcn_conv: a learned edge_weight needs edge_index (the graph is built from it)")
+        ei = _check_ei(g)
+        if edge_weight.dim() != 1 or edge_weight.numel() != ei.size(1):
+            raise ValueError("edge_weight must be [E]")
+        g = build_graph(ei, x.size(0), edge_weight.detach(), degree_on)
+        return _GCNConvFn.apply(x, weight, bias, g, ei, edge_weight, degree_on)
     if not isinstance(g, Graph):
         g = build_graph(g, x.size(0), edge_weight, degree_on)
     return _GCNConvFn.apply(x, weight, bias, g)
@@ -684,4 +713,13 @@ def kernel_timing(kernel_class: int):
     ms = ctypes.c_float(0.0)
     n = ctypes.c_int64(0)
     check(_lib.lib().bgcn_kernel_timing(kernel_class, ctypes.byref(ms), ctypes.byref(n)))
+    return float(ms.value), int(n.value)
+
+
+def kernel_span(kernel_class: int):
+    """(total_ms, launches) of a stamped kernel class's device-side spans since
+    set_kernel_timing(True) (the kernel's own first-block-start to last-block-end; syncs)."""
+    ms = ctypes.c_float(0.0)
+    n = ctypes.c_int64(0)
+    check(_lib.lib().bgcn_kernel_span(kernel_class, ctypes.byref(ms), ctypes.byref(n)))
     return float(ms.value), int(n.value)

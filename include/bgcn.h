@@ -88,6 +88,28 @@ int bgcn_build_graph(const int64_t* edge_index, const float* edge_weight, int64_
                      int32_t* status, void* workspace, size_t workspace_bytes,
                      bgcn_stream_t stream);
 
+/* The D^-1/2 vector (dinv[N], fp32: deg^-1/2 with inf -> 0, the degree including the self
+ * loop) a bgcn_build_graph call left in its workspace (valid while that workspace is kept
+ * unmodified; same sizes as the build).  Input of bgcn_edge_weight_grad. */
+int bgcn_graph_dinv(const void* workspace, size_t workspace_bytes, int64_t num_edges, int64_t num_nodes,
+                    const float** dinv);
+
+/* gcn_norm backward: dL/d edge_weight of GCNConv(x, edge_index, edge_weight) - EBGCN learns
+ * its edge weights (model/Twitter/EBGCN.py:101-102 edge_pred = sigmoid(fc(...)), passed as
+ * GCNConv(..., edge_weight=edge_pred) at :84,178).  Inputs, all [N, ld] fp32 rows of width F
+ * (a multiple of 4; pad with zero columns): h = x W^T (the propagate input), agg = A_hat h
+ * (the propagate output without the bias), dout = dL/d out, dz = A_hat^T dout; dinv from
+ * bgcn_graph_dinv of the graph built from the same edge_index / edge_weight / degree_on.
+ * Writes d_edge_weight[E] in edge order: through norm_e = dinv[src] w_e dinv[dst] and through
+ * the degree of each node (PyG >= 1.6: target side, 'row': source side); an input self loop
+ * receives its node's loop-weight gradient (add_remaining_self_loops); an edge with an index
+ * outside [0, N) gets 0.  Deterministic (no float atomics). */
+size_t bgcn_edge_weight_grad_workspace_size(int64_t num_nodes);
+int bgcn_edge_weight_grad(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int degree_on,
+                          const float* dinv, const float* h, const float* agg, const float* dout,
+                          const float* dz, int64_t ld, int32_t F, float* d_edge_weight, void* workspace,
+                          size_t workspace_bytes, bgcn_stream_t stream);
+
 /* Both directions of one batch in one launch sequence (the fused step's TD graph of
  * edge_index and BU graph of BU_edge_index; dataset.py:80-90).  No edge weights.
  * batch (optional, ABI 7): the [N] tree id per node of the collated batch; with it every
@@ -528,6 +550,12 @@ int bgcn_keep_words(uint64_t seed, int64_t num_nodes, int32_t num_words, uint32_
  * auxiliary lane, 9 the caller stream's own chain up to the final join, 10 the whole call. */
 int bgcn_set_kernel_timing(int enable);
 int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* launches);
+/* The same classes' device-side spans, for the kernels that stamp themselves (class 7, the
+ * batch preparation's pass over X - or over the compacted rows - k_prep_b): per launch, the
+ * first block's start to the last block's end on the device's constant wall clock
+ * (hipDeviceAttributeWallClockRate), i.e. the kernel's own duration as rocprofv3 reports
+ * it, without the dispatch delay an event bracket on a busy lane includes.  Synchronises. */
+int bgcn_kernel_span(int kernel_class, float* total_ms, int64_t* launches);
 
 #ifdef __cplusplus
 }

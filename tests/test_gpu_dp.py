@@ -102,3 +102,15 @@ def test_two_ranks_on_the_hip_step(tmp_path):
         scale = float(np.abs(b).max())
         assert float(np.abs(a - b).max()) <= 1e-5 * max(scale, 1e-12), (tuple(v.shape), scale)
         off += n                    # grads0: the views concatenated in parameter order
+
+
+def test_rccl_deferred_dw1_one_rank():
+    """The RCCL (`nccl` backend) path of the overlapped two-part all-reduce, on a one-rank
+    group in a fresh process (the box has one GPU; RCCL refuses two ranks on one device)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+               LOCAL_RANK="0", WORLD_SIZE="1")
+    env.pop("BGCN_DIST_BACKEND", None)
+    r = subprocess.run([sys.executable, os.path.join(HERE, "nccl_gpu_worker.py")], env=env,
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "rccl ok" in r.stdout

@@ -372,6 +372,63 @@ def test_gcnconv_edge_weight_fwd_bwd(degree_on):
     close(xd.grad, x.grad, what="dx")
     close(conv.lin.weight.grad, w.grad, what="dW")
     close(conv.bias.grad, b.grad, what="db")
-    # a learnable edge weight (EBGCN's edge inference) is refused, not silently detached
-    with pytest.raises(NotImplementedError):
-        conv(xd, ei.to(DEV), ew.float().to(DEV).requires_grad_(True))
+
+
+def close_elem(a, b, what="", rtol=1e-4, floor=1e-3):
+    """Elementwise: |a - b| <= rtol * (|b| + floor * max|b|) (fp32 kernels vs fp64 oracle)."""
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    assert a.shape == b.shape, what
+    bound = rtol * (b.abs() + floor * float(b.abs().max()))
+    bad = (a - b).abs() > bound
+    assert not bool(bad.any()), f"{what}: {int(bad.sum())} of {b.numel()} off, worst {float(((a - b).abs() / bound).max()):.2f}x"
+
+
+@pytest.mark.parametrize("degree_on", ["col", "row"])
+def test_gcnconv_learned_edge_weight(degree_on):
+    """EBGCN's call form with a LEARNED edge weight: edge_pred = sigmoid(fc(sim)) (EBGCN.py:
+    101-102) passed as GCNConv(x, edge_index, edge_weight=edge_pred) (:84,178).  The gradient
+    flows through gcn_norm (the per-edge norm and every node's degree) into the weight and on
+    into fc - all against O.gcn_conv autograd (fp64), elementwise 1e-4, on a star-heavy
+    forest with an input self loop (its weight becomes the node's loop weight)."""
+    from bigcn_amd import GCNConv
+    rng = np.random.default_rng(13)
+    ei, N = rand_forest(rng, [40, 2, 130, 7], star=True)
+    ei = torch.cat([ei, torch.tensor([[5], [5]])], 1)                  # an input self loop
+    E = ei.size(1)
+    torch.manual_seed(2)
+    conv = GCNConv(96, 64, degree_on=degree_on).to(DEV)
+    with torch.no_grad():
+        conv.bias.uniform_(-0.1, 0.1)
+    fc = torch.nn.Linear(8, 1).double()
+    sim = torch.randn(E, 8, dtype=torch.float64)
+    x = torch.randn(N, 96, dtype=torch.float64, requires_grad=True)
+    w = conv.lin.weight.detach().double().cpu().requires_grad_(True)
+    b = conv.bias.detach().double().cpu().requires_grad_(True)
+    ew = torch.sigmoid(fc(sim)).view(-1)
+    ew.retain_grad()
+    ref = O.gcn_conv(x, ei, w, b, edge_weight=ew, degree_on=degree_on)
+    gout = torch.randn_like(ref)
+    ref.backward(gout)
+    fcd = torch.nn.Linear(8, 1).to(DEV)
+    with torch.no_grad():
+        fcd.weight.copy_(fc.weight.float())
+        fcd.bias.copy_(fc.bias.float())
+    xd = x.detach().float().to(DEV).requires_grad_(True)
+    ewd = torch.sigmoid(fcd(sim.float().to(DEV))).view(-1)
+    ewd.retain_grad()
+    out = conv(xd, ei.to(DEV), ewd)
+    out.backward(gout.float().to(DEV))
+    close(out, ref, what="out")
+    # dL/dw_e = g_e dis[s] dis[d] + dL/ddeg[key]: the two terms nearly cancel on some edges,
+    # so the elementwise floor is 1e-2 of the largest gradient (still 1e-6 of it absolute)
+    close_elem(ewd.grad, ew.grad, what="d edge_weight", floor=1e-2)
+    close_elem(xd.grad, x.grad, what="dx")
+    close_elem(conv.lin.weight.grad, w.grad, what="dW")
+    close_elem(conv.bias.grad, b.grad, what="db")
+    close_elem(fcd.weight.grad, fc.weight.grad, what="d fc.weight (through the edge weights)")
+    # a prebuilt graph has its weights baked in: a learned weight needs the edge list
+    from bigcn_amd.ops import build_graph, gcn_conv
+    g = build_graph(ei.to(DEV), N, ewd.detach())
+    with pytest.raises(ValueError):
+        gcn_conv(xd, g, conv.lin.weight, conv.bias, ewd)
