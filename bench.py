@@ -65,6 +65,14 @@ WORKLOADS = {
     # HBM-roofline stress shape); per GPU one step = 128 such trees (weak scaling), the
     # training-run defaults of the Twitter script (DropEdge 0.2/0.2, 4 classes).
     # configs[3] (100k trees of mean 256) has the per-GPU step shape of "twitter15".
+    # PHEME (BiGCN_Twitter.py:138-140,177-182: BiGCN(768, 64, 64), x = the tweets' 768-dim
+    # BERT CLS embeddings): dense features, so the dense MFMA path; thread sizes from the
+    # reference's own data/PHEME/*.json (1,982 threads: mean 10.5 posts, max 109)
+    "pheme768": dict(trees=128, mean=10.5, sigma=0.8, feats=768, classes=4, drop=(0.2, 0.2), dense_x=True,
+                     feat_mode="dense",
+                     desc="PHEME-shaped synthetic: 128 threads/GPU, LogNormal(0.8) sizes mean 10.5 (the "
+                          "reference's data/PHEME/*.json), 768-dim dense N(0,1) features (BERT CLS), "
+                          "DropEdge 0.2/0.2 re-drawn every step, dropout 0.5, fp32, dense MFMA path"),
     "synth1024_bf16": dict(trees=128, mean=1024, sigma=0.8, feats=5000, classes=4, drop=(0.2, 0.2),
                            xdtype="bf16",
                            desc="synthetic stress: 128 trees/GPU, LogNormal(0.8) sizes mean 1024 "
@@ -145,8 +153,12 @@ def make_pool(wl, rank, pool, device, drop=None):
         rng = np.random.default_rng(20250205 + 1 + 1000 * rank + i)
         sizes = synth_tree_sizes(rng, wl["trees"], wl["mean"], wl["sigma"])
         xdt = torch.bfloat16 if wl.get("xdtype") == "bf16" else torch.float32
-        out.append(synth_batch(rng, sizes, wl["feats"], wl["classes"], *drop, device=device, dtype=xdt,
-                               long_rows=wl.get("long_rows")))
+        b = synth_batch(rng, sizes, wl["feats"], wl["classes"], *drop, device=device, dtype=xdt,
+                        long_rows=wl.get("long_rows"))
+        if wl.get("dense_x"):   # dense embeddings (PHEME's BERT CLS rows): no sparse hints
+            g = torch.Generator(device=device).manual_seed(20250205 + i)
+            b.x = torch.randn(b.x.shape, generator=g, device=device, dtype=xdt)
+        out.append(b)
     return out
 
 
@@ -441,6 +453,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     wl = WORKLOADS[args.workload]
+    if wl.get("feat_mode") and args.feat_mode == "auto":
+        args.feat_mode = wl["feat_mode"]         # dense-feature workloads run the dense path
     if args.scaling == "strong":   # the workload's global batch split over the ranks
         wl = dict(wl, trees=max(1, wl["trees"] // world))
     torch.manual_seed(1234 + rank)

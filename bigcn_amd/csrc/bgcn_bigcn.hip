@@ -1039,7 +1039,13 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     m.dw2_dense.gx = 1;
     m.n_dw2_dense = S2 * 2;
   }
-  m.n_dw2 = m.n_dw2_dense;   // the sparse relu(H1) block is formed by the dH1 blocks
+  // dense mode, fp32 X: the dW2 blocks as their own launch (k_dw2_f32: their register
+  // budget, not the middle launch's); the middle launch then runs dH1, db2 and the head
+  const bool dw2_own = m.n_dw2_dense && sp.mode == 1 && a->x_dtype == BGCN_DTYPE_F32;
+  if (dw2_own) {
+    m.n_dw2f = m.n_dw2_dense;
+  }
+  m.n_dw2 = dw2_own ? 0 : m.n_dw2_dense;   // the sparse relu(H1) block is formed by the dH1 blocks
   m.W2td = a->td_w2; m.W2bu = a->bu_w2; m.dH1 = w.dh1; m.colpart = w.colpart; m.nblk_h = int(nblk_h);
   m.rows_h = w.kchunkh;
   m.db2 = ColsumJob{w.colpart2, sign ? sp.max_items : int(nblk_r), a->td_db2, a->bu_db2};
@@ -1051,9 +1057,11 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     m.n_hg = nhead;
   }
   timing_begin(3, s);
+  BGCN_TRY(dw2_f32_launch(m, s));
+  if (dw2_own) timing_end(3, s);   // class 3 = the dW2 GEMM alone in this form
   BGCN_TRY(dw2_bf16_launch(m, s));
   BGCN_TRY(bwd_mid_launch(m, a->x_dtype, s));
-  timing_end(3, s);
+  if (!dw2_own) timing_end(3, s);
 
   // dZ1 = A^T dH1
   BGCN_TRY(spmm_pair(a->td, a->bu, true, N, w.dh1, w.dz1, nullptr, nullptr, BGCN_EPI_NONE, w, s));

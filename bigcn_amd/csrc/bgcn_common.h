@@ -245,6 +245,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, uint
   void* base = reinterpret_cast<void*>(uint64_t(lo) | (uint64_t(hi) << 32));
   return __builtin_amdgcn_make_buffer_rsrc(base, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
+__device__ __forceinline__ void st4_chain(float* base, int64_t off, float4 v) {
+#if BGCN_WT_OUT
+  u32x4 d;
+  d.x = __float_as_uint(v.x); d.y = __float_as_uint(v.y); d.z = __float_as_uint(v.z); d.w = __float_as_uint(v.w);
+  __builtin_amdgcn_raw_buffer_store_b128(d, row_rsrc(base, 0xfffffff0u), uint32_t(off * 4), 0, 16);   // sc1
+#else
+  st4(base + off, v);
+#endif
+}
+// The chain's [N, 128] activations (Z1, H1, dZ2, dZ1, ...) are read by the NEXT launch only:
+// stored write-through (sc1), the producer's kernel boundary has no dirty lines left to write
+// back (MI355X_MICROARCH.md price table, "boundary": + B / 6 TB/s for B dirty bytes, ~2.5 us
+// per 15 MB matrix).  base: wave-uniform; off: elements (32-bit byte offsets).
+#ifndef BGCN_WT_OUT
+#define BGCN_WT_OUT 0   // A/B r04: chain alone 148-151 vs 147-154 us, step within noise
+#endif
+__device__ __forceinline__ void st4_chain(float* base, int64_t off, float4 v);
 #ifndef BGCN_X_AUX
 #define BGCN_X_AUX 2   // A/B: the cache-policy bits of the pass over X (sc0 = 1, nt = 2, sc1 = 16)
 #endif

@@ -564,8 +564,8 @@ __global__ __launch_bounds__(kC1Threads) void k_conv1_gather(SparseState S, floa
     }
   }
   if (live) {
-    st4(Z1 + i * (2 * H) + 8 * ql, a0);
-    st4(Z1 + i * (2 * H) + 8 * ql + 4, a1);
+    st4_chain(Z1, i * (2 * H) + 8 * ql, a0);
+    st4_chain(Z1, i * (2 * H) + 8 * ql + 4, a1);
   }
   BT_END(1);
 }
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __res
   int cmax = max(cnt, __shfl_xor(cnt, 32, 64));
   cmax = __builtin_amdgcn_readfirstlane(cmax);
   const float4 acc = conv1_half_entries<kStep>(S, cl, vl, cnt, cmax, f4zero());
-  if (live && nall <= kCap) st4(Z1 + i * (2 * H) + 4 * hl, acc);   // long rows: their block's
+  if (live && nall <= kCap) st4_chain(Z1, i * (2 * H) + 4 * hl, acc);   // long rows: their block's
   BT_END(1);
 }
 
@@ -1986,6 +1986,22 @@ __global__ __launch_bounds__(256) void k_dw2_bf16(BwdMidArgs a) {
 int dw2_bf16_launch(BwdMidArgs& a, hipStream_t s) {
   if (a.n_dw2b <= 0) return BGCN_OK;
   hipLaunchKernelGGL(k_dw2_bf16, dim3(unsigned(a.n_dw2b)), dim3(256), 0, s, a);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
+
+// The dense feature mode's dW2 (fp32 X; dw2_body, f32 MFMA) as a launch of its own: inside
+// the middle launch it ran at that launch's register budget (210 VGPRs since the fused
+// dH1 + relu(H1)-dW2 role of round 3: two waves per SIMD) - 76.5 -> 64 TF/s.
+__global__ __launch_bounds__(256) void k_dw2_f32(BwdMidArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[kDw2Smem];
+  dw2_body<float>(static_cast<const float*>(a.X), a.ldx, a.S.F, a.H1, a.dZ2, a.node_root, a.S.N, a.keep,
+                  a.gate, a.dw2_dense, a.dw2_sparse, a.n_dw2_dense, int(blockIdx.x), smem);
+}
+
+int dw2_f32_launch(BwdMidArgs& a, hipStream_t s) {
+  if (a.n_dw2f <= 0) return BGCN_OK;
+  hipLaunchKernelGGL(k_dw2_f32, dim3(unsigned(a.n_dw2f)), dim3(256), 0, s, a);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
       if (r != cur) {
         if (cur >= 0) {
           // `cur` ended inside this chunk (a later entry belongs to another row)
-          if (!cur_head) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+          if (!cur_head) st4_chain(P.out, int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
           else st4(P.part + (g * 2 + 0) * (LANES * 4) + fo, acc);
         }
         cur_head = cur < 0 && r == prev_row;
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void k_spmm_narrow(SpmmBatch sb) {
   }
   if (cur >= 0) {
     const bool ends = next_row != cur;
-    if (!cur_head && ends) st4(P.out + int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+    if (!cur_head && ends) st4_chain(P.out, int64_t(cur) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
     else if (cur_head) st4(P.part + (g * 2 + 0) * (LANES * 4) + fo, acc);  // head (may also extend past p1)
     else st4(P.part + (g * 2 + 1) * (LANES * 4) + fo, acc);               // tail
   }
@@ -143,6 +143,9 @@ __device__ __forceinline__ float4 tree_scale(const SpmmSign& sg, int64_t b, int 
   return make_float4(dh.x / cnt, dh.y / cnt, dh.z / cnt, dh.w / cnt);
 }
 
+#ifndef BGCN_SIGN_XT
+#define BGCN_SIGN_XT 1   // A/B only: 0 drops the cross-tree check (wrong for edges across trees)
+#endif
 template <bool kSign>
 __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BGCN_ROWS_WPE))) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
   BT_BEGIN
@@ -173,34 +176,38 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
     float4 gA = f4zero(), gZ = f4zero();
     // kSign with an edge across trees (the graph build's BGCN_STATUS_CROSS_TREE, never set
     // by PyG collation): every gathered row is scaled by its own tree, the output row not
-    const bool xt = kSign && (*sb.sg.tree_status[blockIdx.y] & BGCN_STATUS_CROSS_TREE) != 0;
+    const bool xt = kSign && BGCN_SIGN_XT && (*sb.sg.tree_status[blockIdx.y] & BGCN_STATUS_CROSS_TREE) != 0;
+    // kSign: the tree of each entry's row, loaded with the entries (a row's tree is then at
+    // hand when the row finishes - no dependent load per row)
+    int64_t bb0 = 0, bb1 = 0;
     if constexpr (kSign) {
-      const int32_t ra = __shfl(r0, base_lane, 64);
-      const int32_t rz = __shfl(n > LANES ? r1 : r0, base_lane + ((n - 1) & (LANES - 1)), 64);
-      bA = sb.sg.batch[max(ra, 0)];
-      bZ = sb.sg.batch[max(rz, 0)];
+      bb0 = sb.sg.batch[max(r0, 0)];
+      bb1 = sb.sg.batch[max(r1, 0)];
+      bA = __shfl(bb0, base_lane, 64);
+      bZ = __shfl(n > LANES ? bb1 : bb0, base_lane + ((n - 1) & (LANES - 1)), 64);
       gA = tree_scale(sb.sg, bA, hoff, fo);
       gZ = tree_scale(sb.sg, bZ, hoff, fo);
     }
-    auto finish = [&](int32_t r, float4 acc) {
+    auto finish = [&](int32_t r, float4 acc, int64_t b) {
       if constexpr (kSign) {
         if (xt) {
-          st4(P.out + int64_t(r) * P.ld_out + fo, acc);
+          st4_chain(P.out, int64_t(r) * P.ld_out + fo, acc);
           return;
         }
-        const int64_t b = sb.sg.batch[r];
         const float4 gs = b == bA ? gA : (b == bZ ? gZ : tree_scale(sb.sg, b, hoff, fo));
-        st4(P.out + int64_t(r) * P.ld_out + fo,
+        st4_chain(P.out, int64_t(r) * P.ld_out + fo,
             make_float4(acc.x * gs.x, acc.y * gs.y, acc.z * gs.z, acc.w * gs.w));
       } else {
-        st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+        st4_chain(P.out, int64_t(r) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
       }
     };
     float4 acc = f4zero();
     int32_t cur = -1;
+    int64_t curb = 0;
     for (int k0 = 0; k0 < n; k0 += 8) {
       float4 v[8];
       int32_t rr[8];
+      int64_t bk[8];
       float ww[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -210,6 +217,8 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
         const int32_t rk = __shfl(hi ? r1 : r0, src, 64);
         const int32_t ck = __shfl(hi ? c1 : c0, src, 64);
         ww[u] = __shfl(hi ? w1 : w0, src, 64);
+        if constexpr (kSign) bk[u] = __shfl(hi ? bb1 : bb0, src, 64);
+        else bk[u] = 0;
         rr[u] = k < n ? rk : -1;
         if constexpr (kSign) {
           v[u] = sign_bits(sgn[int64_t(ck) * 2], lane);    // unconditional (ck is a real row)
@@ -222,14 +231,15 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
         const int32_t r = rr[u];
         if (r < 0) break;
         if (r != cur) {
-          if (cur >= 0) finish(cur, acc);
+          if (cur >= 0) finish(cur, acc, curb);
           cur = r;
+          curb = bk[u];
           acc = f4zero();
         }
         acc = f4fma(ww[u], v[u], acc);
       }
     }
-    if (cur >= 0) finish(cur, acc);
+    if (cur >= 0) finish(cur, acc, curb);
     BT_END(3);
     return;
   }
@@ -239,7 +249,7 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
     const int32_t r = P.plan.longs[j];
     const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
     float4 gs = f4zero();
-    const bool xt = kSign && (*sb.sg.tree_status[blockIdx.y] & BGCN_STATUS_CROSS_TREE) != 0;
+    const bool xt = kSign && BGCN_SIGN_XT && (*sb.sg.tree_status[blockIdx.y] & BGCN_STATUS_CROSS_TREE) != 0;
     if constexpr (kSign) gs = xt ? make_float4(1.f, 1.f, 1.f, 1.f) : tree_scale(sb.sg, sb.sg.batch[r], hoff, fo);
     float4 acc = f4zero();
     int64_t e = rs + grp;
@@ -274,10 +284,10 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
 #pragma unroll 8
       for (int q = 1; q < kRowsGroups; ++q) t = f4add(t, red[q][lane]);
       if constexpr (kSign) {
-        st4(P.out + int64_t(r) * P.ld_out + fo, make_float4(t.x * gs.x, t.y * gs.y, t.z * gs.z, t.w * gs.w));
+        st4_chain(P.out, int64_t(r) * P.ld_out + fo, make_float4(t.x * gs.x, t.y * gs.y, t.z * gs.z, t.w * gs.w));
       } else {
         const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
-        st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(t, bv, sb.epi));
+        st4_chain(P.out, int64_t(r) * P.ld_out + fo, epilogue(t, bv, sb.epi));
       }
     }
     __syncthreads();
@@ -323,7 +333,7 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
 #pragma unroll
           for (int j = 1; j < kSmall; ++j)
             if (j < m) acc = f4add(acc, v[j]);
-          st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+          st4_chain(P.out, int64_t(r) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
         } else {
           mine = r;
         }
@@ -356,7 +366,7 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
       float4 sum = red[0][threadIdx.x];
 #pragma unroll
       for (int q = 1; q < SG; ++q) sum = f4add(sum, red[q][threadIdx.x]);
-      st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(sum, bv, sb.epi));
+      st4_chain(P.out, int64_t(r) * P.ld_out + fo, epilogue(sum, bv, sb.epi));
     }
     __syncthreads();
   }
@@ -520,7 +530,7 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_wide(SpmmBatch sb) {
     for (int u = 0; u < 4; ++u) acc = f4add(acc, v[u]);
   }
   for (; q <= g1; ++q) acc = f4add(acc, ld4(P.part + (q * 2 + 0) * int64_t(F) + fo));
-  st4(P.out + int64_t(r) * P.ld_out + fo, epilogue(acc, P.bias ? ld4(P.bias + fo) : f4zero(), sb.epi));
+  st4_chain(P.out, int64_t(r) * P.ld_out + fo, epilogue(acc, P.bias ? ld4(P.bias + fo) : f4zero(), sb.epi));
 }
 
 }  // namespace

@@ -23,7 +23,9 @@ and 0 in another; that one flip moves dW1 by ~1e-4 of its max (Weibo size: the
 reference's OWN fp32 path differs from fp64 by 3.2e-4 on TD conv1's weight through a
 single tie, tools/prec_probe.py).  The oracle therefore takes the kernel's relu'
 decisions (``relu_masks``, from the step's saved H1 / H2), and the test asserts that
-every decision differing from the fp64 sign is a tie (|h| <= 1e-5 max|h|).  The saved H1 /
+every decision differing from the fp64 sign is a tie (|h| <= 1e-6 max|h|, TIE_WINDOW) and
+that there are at most TIE_FLIPS of them per tensor.  The error tables are written to
+gpurun_out/parity/ (profiles/r04_parity_*.json).  The saved H1 /
 H2 themselves are compared with the oracle's stages at the same tolerances.
 """
 import numpy as np
@@ -37,6 +39,22 @@ from test_gpu_train import KEYS, _model
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
+TIE_WINDOW = 1e-6    # |h| / max|h| of an entry whose relu' decision may differ from fp64's
+TIE_FLIPS = 16       # differing relu' decisions allowed per [N, 64] tensor
+
+
+def _dump_table(name, N, table, ties, depth):
+    """The error table of a full-size test (max-scaled and elementwise, per tensor), the
+    relu' ties and their depth, under gpurun_out/parity/ (copied to profiles/ per round)."""
+    import json
+    import os
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, name + ".json"), "w") as f:
+        json.dump({"N": N, "tol": TOL, "tie_window": TIE_WINDOW,
+                   "errors": {k: {"max_scaled": v[0], "elementwise": v[1], "margin_x": TOL / max(v[0], v[1], 1e-300)}
+                              for k, v in table.items()},
+                   "relu_ties": ties, "tie_depth": depth}, f, indent=1)
 _ORACLE_CACHE = {}   # (workload, drop seed) -> (relu masks, oracle result) of the last run
 
 
@@ -140,7 +158,7 @@ def test_full_size_step_matches_oracle(workload, mode):
     table = {k: errors(g, rgrads[k]) for k, g in zip(KEYS, grads)}
     table["logp"] = errors(logp, rlogp)
     table["loss"] = errors(loss, rloss)
-    ties = {}
+    ties, tie_depth = {}, {}
     for k, d in enumerate(("TDrumorGCN", "BUrumorGCN")):
         for name, mine in (("h1", h1), ("h2", h2)):
             r = st[f"{d}.{name}"]
@@ -148,11 +166,16 @@ def test_full_size_step_matches_oracle(workload, mode):
             table[f"{d}.{name} (saved)"] = errors(got, r)
             flip = (got > 0) != (r > 0)
             ties[f"{d}.{name}"] = int(flip.sum())
-            assert bool((r[flip].abs() <= 1e-5 * r.abs().max()).all()), \
-                f"{d}.{name}: a relu' decision differs from the fp64 sign away from zero"
+            depth = float(r[flip].abs().max() / r.abs().max()) if bool(flip.any()) else 0.0
+            tie_depth[f"{d}.{name}"] = depth
+            # a differing relu' decision must be a tie: within fp32 rounding of zero (1e-6 of
+            # the tensor's largest magnitude), and rare (at most TIE_FLIPS of ~2-8M entries)
+            assert depth <= TIE_WINDOW, f"{d}.{name}: a relu' decision differs from the fp64 sign at {depth:.2e} of max|h|"
+            assert ties[f"{d}.{name}"] <= TIE_FLIPS, f"{d}.{name}: {ties[f'{d}.{name}']} relu' decisions differ"
     print(f"\n{workload} ({mode}) N={N}: (max-scaled, elementwise) error vs the fp64 oracle; relu' ties {ties}")
     for k, (e1, e2) in table.items():
         print(f"  {k:32s} {e1:.2e} {e2:.2e}")
+    _dump_table(f"{workload}_{mode}", N, table, ties, tie_depth)
     bad = {k: v for k, v in table.items() if v[0] > TOL or v[1] > TOL}
     assert not bad, f"{workload}: beyond {TOL:g}: {bad}"
 
