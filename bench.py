@@ -93,21 +93,27 @@ KERNEL_CLASSES = {
 SPARSE_CAP = 32
 # rocprofv3 kernel symbol of each timed class (for the PMC traffic lookup)
 ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2): "bgcn::k_conv2_sparse",
-                 ("auto", 3): "bgcn::k_bwd_mid<float>", ("auto", 5): "bgcn::k_bwd_tail<1>",
+                 ("auto", 3): "bgcn::k_bwd_mid<float>", ("auto", 5): "bgcn::k_bwd_tail<0, 0>",
                  ("auto", 7): "bgcn::k_prep_b<float>",
                  ("dense", 0): "bgcn::k_gemm_xwt<true, false, float>", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
-                 ("dense", 2): "bgcn::k_conv2_fwd<float>", ("dense", 3): "bgcn::k_dw2<float>"}
-PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
+                 ("dense", 2): "bgcn::k_conv2_fwd<float>", ("dense", 3): "bgcn::k_dw2_f32"}
 
 
-def pmc_traffic(mode: str, cls: int, workload: str = "twitter15"):
+def pmc_file(workload: str) -> str:
+    """The committed PMC passes of a workload's bench command (tools/profile_round.sh)."""
+    return os.path.join(ROOT, "profiles", f"r04_pmc_traffic_{workload}.json")
+
+
+def pmc_traffic(mode: str, cls: int, workload: str = "twitter15", xbf16: bool = False):
     """HBM bytes per launch of a kernel class from the committed PMC passes
-    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, same bench workload), or None."""
-    if mode != "auto" or workload != "twitter15":   # the committed passes ran the default bench
-        return None
+    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, the same workload's bench), or None."""
     name = ROCPROF_NAMES.get((mode, cls))
+    if name is None:
+        return None
+    if xbf16:   # the bf16-X instantiation of the templated kernels
+        name = name.replace("<float>", "<unsigned short>")
     try:
-        with open(PMC_FILE) as f:
+        with open(pmc_file(workload)) as f:
             k = json.load(f)["kernels"].get(name)
     except (OSError, ValueError):
         return None
@@ -581,7 +587,7 @@ def main():
                 ach = work / (avg_ms * 1e-3) / 1e12
                 roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
-                        "traffic": pmc_traffic(mode, c, args.workload), "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
+                        "traffic": pmc_traffic(mode, c, args.workload, wl.get("xdtype") == "bf16"), "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
             else:
                 event_ms = avg_ms
@@ -593,7 +599,7 @@ def main():
                     timer = "device wall-clock span (first block start to last block end, in-kernel stamps)"
                 ach = work / (avg_ms * 1e-3) / 1e9
                 roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(mode, c, args.workload),
+                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(mode, c, args.workload, wl.get("xdtype") == "bf16"),
                         "kernel": KERNEL_CLASSES[mode][c], "bytes_per_launch": work,
                         "avg_ms": round(avg_ms, 4), "timer": timer, "event_avg_ms": round(event_ms, 4),
                         "frac_by_event_bracket": round(work / (event_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}

@@ -352,6 +352,9 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
 #ifndef BGCN_DH1_X6
 #define BGCN_DH1_X6 1   // 0: the three-product form (A/B only: not fp32-grade)
 #endif
+#ifndef BGCN_DW2P_X6
+#define BGCN_DW2P_X6 1   // the relu(H1) block of dW2 in the six-product form (0: three products)
+#endif
 #ifndef BGCN_DH1_PREFETCH
 #define BGCN_DH1_PREFETCH 1   // 0: the next tile's loads issued after the tile (A/B)
 #endif
@@ -459,16 +462,27 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
     // this tile's per-lane operands: a2 = keep * s * relu(H1) split (dW2's B fragments in
     // accumulator row order), bit q of km = kept and H1 > 0 (dH1)
     bf16x8 a2h[2], a2l[2];
+#if BGCN_DW2P_X6
+    bf16x8 a2m[2];
+#endif
     uint32_t km = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int64_t i = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
       const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(i, N - 1)), uint32_t(c >> 5));
       const bool kept = ((wd >> (c & 31)) & 1u) && i < N;
+#if BGCN_DW2P_X6
+      __bf16 x, y, z;
+      split3_bf16(kept ? sc * fmaxf(hv[q], 0.f) : 0.f, x, y, z);
+      a2h[q >> 3][q & 7] = x;
+      a2m[q >> 3][q & 7] = y;
+      a2l[q >> 3][q & 7] = z;
+#else
       __bf16 x, y;
       split_bf16(kept ? sc * fmaxf(hv[q], 0.f) : 0.f, x, y);
       a2h[q >> 3][q & 7] = x;
       a2l[q >> 3][q & 7] = y;
+#endif
       km |= uint32_t(kept && hv[q] > 0.f) << q;
       if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // four keep hashes in flight
     }
@@ -514,6 +528,24 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
       // dW2: A = dZ2^T (o = r / 32 + r, rows in the a2 fragments' order), B = a2
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+#if BGCN_DW2P_X6
+        // the fp32-grade six-product form (both operands split three ways, ~2^-24 relative):
+        // the three-product form's ~1e-5 left the relu(H1) block of dW2 only 4-8x under
+        // the 1e-4 bar at full size (profiles/r04_parity_*.json)
+        bf16x8 z0h, z0m, z0l, z1h, z1m, z1l;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = rh * 32 + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+          z0h[j] = Dh[k * kDsLd + r];
+          z0m[j] = Dm[k * kDsLd + r];
+          z0l[j] = Dl[k * kDsLd + r];
+          z1h[j] = Dh[k * kDsLd + 32 + r];
+          z1m[j] = Dm[k * kDsLd + 32 + r];
+          z1l[j] = Dl[k * kDsLd + 32 + r];
+        }
+        pw0 = mfma_x6(z0h, z0m, z0l, a2h[s], a2m[s], a2l[s], pw0);
+        pw1 = mfma_x6(z1h, z1m, z1l, a2h[s], a2m[s], a2l[s], pw1);
+#else
         bf16x8 z0h, z0l, z1h, z1l;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -525,6 +557,7 @@ __device__ inline void dh1_body(const float* __restrict__ dZ2, const float* __re
         }
         pw0 = mfma_x3(z0h, z0l, a2h[s], a2l[s], pw0);
         pw1 = mfma_x3(z1h, z1l, a2h[s], a2l[s], pw1);
+#endif
         __builtin_amdgcn_sched_barrier(0);
       }
     }

@@ -1,30 +1,33 @@
 #!/bin/bash
-# Evidence for profiles/: default bench line, rocprofv3 kernel stats of the same
-# workload, separate FETCH_SIZE / WRITE_SIZE PMC passes (MI355X_MICROARCH.md recipe),
-# a device-side step timeline (tools/trace_probe.py) and the 5000-wide aggregation
-# probe's kernel stats + PMC traffic.  Run on the GPU box:
-#   gpurun -- 'bash tools/profile_round.sh gpurun_out/prof_r02'
+# Evidence for profiles/ (round 4): per workload the bench line, rocprofv3 kernel stats of
+# the same command, separate FETCH_SIZE / WRITE_SIZE PMC passes (MI355X_MICROARCH.md recipe;
+# tools/pmc_traffic.py applies the gfx950 corrections) -> pmc_traffic_<workload>.json (what
+# bench.py's roofline.traffic reads from profiles/r04_pmc_traffic_<workload>.json), the
+# device-side step timelines and the 5000-wide aggregation probe with its PMC traffic.
+#   gpurun -- 'bash tools/profile_round.sh gpurun_out/prof_r04 twitter15 weibo_bf16 synth1024_bf16'
 set -eo pipefail
-OUT=${1:-gpurun_out/prof}
+OUT=${1:-gpurun_out/prof}; shift
+WLS=${@:-twitter15}
 mkdir -p "$OUT"
 ROOT=$(pwd)
-LIGHT="--no-cpu-baseline --compare-dense 0 --compare-dropedge 0 --aggregation 0"
-timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.log"
+LIGHT="--no-cpu-baseline --compare-dense 0 --compare-dropedge 0 --aggregation 0 --dropin 0 --host-fed 0"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- \
-  python bench.py $LIGHT > "$OUT/bench_under_rocprof.json" 2> "$OUT/stats.log"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -- \
-  python bench.py $LIGHT --steps 5 --warmup 2 > /dev/null 2> "$OUT/fetch.log"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -- \
-  python bench.py $LIGHT --steps 5 --warmup 2 > /dev/null 2> "$OUT/write.log"
-python tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" --out "$OUT/pmc_traffic.json" > "$OUT/pmc_traffic.txt"
+for w in $WLS; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_$w" -o run -- \
+    python bench.py --workload $w $LIGHT > "$OUT/bench_under_rocprof_$w.json" 2> "$OUT/stats_$w.log"
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$w" -- \
+    python bench.py --workload $w $LIGHT --steps 5 --warmup 2 > /dev/null 2> "$OUT/fetch_$w.log"
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$w" -- \
+    python bench.py --workload $w $LIGHT --steps 5 --warmup 2 > /dev/null 2> "$OUT/write_$w.log"
+  python tools/pmc_traffic.py "$OUT/fetch_$w" "$OUT/write_$w" --out "$OUT/pmc_traffic_$w.json" > "$OUT/pmc_traffic_$w.txt"
+  echo "$w done"
+done
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/timeline" -o run -- \
   python tools/trace_probe.py --mode both > "$OUT/timeline.log" 2>&1
 python tools/step_timeline.py "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 8 > "$OUT/timeline_step.txt"
 python tools/step_timeline.py "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 20 > "$OUT/timeline_chain_alone.txt"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/agg" -o run -- \
   python tools/agg_probe.py > "$OUT/agg_probe.txt" 2> "$OUT/agg.log"
-# HBM traffic of the 5000-wide aggregation (k_spmm_slice + fixup), TD and BU graphs apart
 for g in td bu; do
   timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/agg_fetch_$g" -- \
     python tools/agg_probe.py --graphs $g --no-streams --iters 5 > /dev/null 2>> "$OUT/agg.log"
