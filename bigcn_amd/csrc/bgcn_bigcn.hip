@@ -134,7 +134,8 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const TX* __restrict__ X, int
 //     (row stride kC2fLd: conflict-free 16-byte LDS stores); the next tile's global loads
 //     are in flight during the current tile's MFMAs.
 constexpr int kC2fBK = 32, kC2fLd = kC2fBK + 8;
-__global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const bf16_t* __restrict__ X, int64_t ldx, int64_t F,
+template <class TX>
+__global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const TX* __restrict__ X, int64_t ldx, int64_t F,
                                                         const float* __restrict__ H1,
                                                         const int32_t* __restrict__ node_root,
                                                         const float* __restrict__ W2td,
@@ -142,8 +143,8 @@ __global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const bf16_t* __restrict
                                                         float* __restrict__ Z2, int64_t N, KeepSrc keep,
                                                         const int32_t* __restrict__ gate) {
   if (gate_closed(gate)) return;
-  constexpr int BM = 128;
-  __shared__ __attribute__((aligned(16))) __bf16 As[BM * kC2fLd];
+  constexpr int BM = 128, PX = sizeof(TX) == 2 ? 1 : 3;   // A planes: bf16 X exact, fp32 X split
+  __shared__ __attribute__((aligned(16))) __bf16 As[PX][BM * kC2fLd];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3][H * kC2fLd];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31;
@@ -193,17 +194,19 @@ __global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const bf16_t* __restrict
   const int ar = tid & (BM - 1), ak = (tid >> 7) * 16;         // A: node ar, columns ak .. ak + 15
   const int64_t am_ = m0 + ar;
   const bool aok = am_ < N;
-  const bf16_t* xrow = X + int64_t(aok ? node_root[am_] : 0) * ldx;
+  const TX* xrow = X + int64_t(aok ? node_root[am_] : 0) * ldx;
   const int br = tid & (H - 1), bk = (tid >> 6) * 8;           // B: W2 row br, k bk .. bk + 7
   const float* wrow = W2 + int64_t(br) * ldw + H;
-  u32x4 ra[2];
+  constexpr int kRA = 2 * sizeof(TX) / 2;   // 16-byte X pieces per thread (16 columns)
+  constexpr int kPE = 8 / (sizeof(TX) / 2); // X elements per piece
+  u32x4 ra[kRA];
   uint32_t rw = 0;
   float4 rb[2];
   auto gload = [&](int64_t c0) {   // c0: first X column of the tile
     rw = aok ? keep.get(uint32_t(d), uint32_t(am_), uint32_t((H + c0) >> 5)) : 0u;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t c = c0 + ak + 8 * i;
+    for (int i = 0; i < kRA; ++i) {
+      const int64_t c = c0 + ak + kPE * i;
       const bool ok = aok && c < F;
       const u32x4 v = *reinterpret_cast<const u32x4*>(xrow + (ok ? c : 0));
       ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
@@ -218,16 +221,32 @@ __global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const bf16_t* __restrict
   };
   auto sstore = [&]() {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {   // keep * s * relu(x): exact in bf16 (s is 1 or 2)
-      bf16x8 v;
+    for (int i = 0; i < 2; ++i) {   // keep * s * relu(x): exact in bf16 for bf16 X (s is 1 or 2)
+      bf16x8 v, vm, vl;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const uint32_t wv = ra[i][j >> 1];
-        const float x = __uint_as_float((j & 1) ? (wv & 0xffff0000u) : (wv << 16));
+        float x;
+        if constexpr (PX == 1) {
+          const uint32_t wv = ra[i][j >> 1];
+          x = __uint_as_float((j & 1) ? (wv & 0xffff0000u) : (wv << 16));
+        } else {
+          x = __uint_as_float(ra[2 * i + (j >> 2)][j & 3]);
+        }
         const bool kept = (rw >> (ak + 8 * i + j)) & 1u;
-        v[j] = __bf16(kept ? sc * fmaxf(x, 0.f) : 0.f);
+        const float a = kept ? sc * fmaxf(x, 0.f) : 0.f;
+        if constexpr (PX == 1) {
+          v[j] = __bf16(a);
+        } else {
+          __bf16 p, q, t;
+          split3_bf16(a, p, q, t);
+          v[j] = p; vm[j] = q; vl[j] = t;
+        }
       }
-      *reinterpret_cast<bf16x8*>(&As[ar * kC2fLd + ak + 8 * i]) = v;
+      *reinterpret_cast<bf16x8*>(&As[0][ar * kC2fLd + ak + 8 * i]) = v;
+      if constexpr (PX == 3) {
+        *reinterpret_cast<bf16x8*>(&As[PX - 2][ar * kC2fLd + ak + 8 * i]) = vm;
+        *reinterpret_cast<bf16x8*>(&As[PX - 1][ar * kC2fLd + ak + 8 * i]) = vl;
+      }
     }
     bf16x8 hv, mv, lv;
     const float wv[8] = {rb[0].x, rb[0].y, rb[0].z, rb[0].w, rb[1].x, rb[1].y, rb[1].z, rb[1].w};
@@ -251,14 +270,23 @@ __global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const bf16_t* __restrict
 #pragma unroll
     for (int s = 0; s < kC2fBK / 16; ++s) {
       const int ko = 16 * s + 8 * h;
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[(32 * wave + r32) * kC2fLd + ko]);
+      bf16x8 a[PX];
+#pragma unroll
+      for (int p = 0; p < PX; ++p) a[p] = *reinterpret_cast<const bf16x8*>(&As[p][(32 * wave + r32) * kC2fLd + ko]);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int o = (32 * c + r32) * kC2fLd + ko;
-        f32x16 t = acc[c];
-        t = mfma_bf16(a, *reinterpret_cast<const bf16x8*>(&Bs[2][o]), t);
-        t = mfma_bf16(a, *reinterpret_cast<const bf16x8*>(&Bs[1][o]), t);
-        acc[c] = mfma_bf16(a, *reinterpret_cast<const bf16x8*>(&Bs[0][o]), t);
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&Bs[0][o]);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&Bs[1][o]);
+        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(&Bs[2][o]);
+        if constexpr (PX == 1) {
+          f32x16 t = acc[c];
+          t = mfma_bf16(a[0], b2, t);
+          t = mfma_bf16(a[0], b1, t);
+          acc[c] = mfma_bf16(a[0], b0, t);
+        } else {
+          acc[c] = mfma_x6(a[0], a[PX - 2], a[PX - 1], b0, b1, b2, acc[c]);
+        }
       }
     }
     __syncthreads();
@@ -825,11 +853,13 @@ static int setup(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, FusedWs& w
   return BGCN_OK;
 }
 
-// the dense path's conv2 and dW2 root columns on the bf16 MFMA (bf16 X; BGCN_GEMM_BF16=0,
-// read once, keeps the f32 MFMA forms): 16-byte X rows and W2 rows
+// the dense path's conv2 and dW2 root columns on the bf16 MFMA: bf16 X exact (BGCN_GEMM_BF16=0,
+// read once, keeps the f32 MFMA forms), fp32 X split three ways, six products
+// (BGCN_GEMM_X6=0, read once, keeps the f32 MFMA forms); 16-byte X rows and W2 rows
 static bool bf16_mfma_ok(const bgcn_bigcn_args* a) {
   static const bool b16 = [] { const char* e = std::getenv("BGCN_GEMM_BF16"); return !(e && atoi(e) == 0); }();
-  return b16 && a->in_feats % 8 == 0 && a->ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(a->x) & 15) == 0 &&
+  static const bool x6 = [] { const char* e = std::getenv("BGCN_GEMM_X6"); return !(e && atoi(e) == 0); }();
+  return (a->x_dtype == BGCN_DTYPE_BF16 ? b16 : x6) && a->in_feats % 8 == 0 && a->ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(a->x) & 15) == 0 &&
          (reinterpret_cast<uintptr_t>(a->td_w2) & 15) == 0 && (reinterpret_cast<uintptr_t>(a->bu_w2) & 15) == 0;
 }
 
@@ -933,8 +963,12 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
   if (dense_launched(a, sp)) {
     // bf16 X: the bf16 MFMA (BGCN_GEMM_BF16=0 keeps the f32 MFMA form)
     if (a->x_dtype == BGCN_DTYPE_BF16 && bf16_mfma_ok(a))
-      hipLaunchKernelGGL(k_conv2_fwd_bf16, dim3(grid_for(N, 128), 2), dim3(256), 0, s,
+      hipLaunchKernelGGL(k_conv2_fwd_bf16<bf16_t>, dim3(grid_for(N, 128), 2), dim3(256), 0, s,
                          static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
+                         a->bu_w2, w.z2, N, keep, gate);
+    else if (a->x_dtype == BGCN_DTYPE_F32 && bf16_mfma_ok(a))
+      hipLaunchKernelGGL(k_conv2_fwd_bf16<float>, dim3(grid_for(N, 128), 2), dim3(256), 0, s,
+                         static_cast<const float*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
                          a->bu_w2, w.z2, N, keep, gate);
     else if (a->x_dtype == BGCN_DTYPE_BF16)
       hipLaunchKernelGGL(k_conv2_fwd<bf16_t>, dim3(grid_for(N, 64), 2), dim3(256), 0, s,
@@ -1031,7 +1065,10 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   m.dw2_dense = Dw2Cfg{kchunk2, S2, gxd, 1, H + F, w.dw2_part};
   m.dw2_sparse = Dw2Cfg{w.kchunkh, w.Sh, 1, 0, int64_t(H), w.dw2_part};
   m.n_dw2_dense = dense_launched(a, sp) ? gxd * S2 * 2 : 0;
-  if (m.n_dw2_dense && sp.mode == 1 && a->x_dtype == BGCN_DTYPE_BF16 && bf16_mfma_ok(a)) {
+  // (fp32 X: the six-product form of k_dw2_bf16 measured 394 + 126 us against the f32
+  // MFMA launch's 469 at the bench workload, so fp32 keeps k_dw2_f32)
+  const bool dw2b = m.n_dw2_dense && sp.mode == 1 && a->x_dtype == BGCN_DTYPE_BF16 && bf16_mfma_ok(a);
+  if (dw2b) {
     // dense mode, bf16 X: the root columns on the bf16 MFMA (k_dw2_bf16, a launch of its
     // own), dw2_body keeps column tile 0 (the H1 columns)
     m.gxb = int(grid_for(F, 128));
@@ -1041,7 +1078,7 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   }
   // dense mode, fp32 X: the dW2 blocks as their own launch (k_dw2_f32: their register
   // budget, not the middle launch's); the middle launch then runs dH1, db2 and the head
-  const bool dw2_own = m.n_dw2_dense && sp.mode == 1 && a->x_dtype == BGCN_DTYPE_F32;
+  const bool dw2_own = m.n_dw2_dense && sp.mode == 1 && a->x_dtype == BGCN_DTYPE_F32 && !dw2b;
   if (dw2_own) {
     m.n_dw2f = m.n_dw2_dense;
   }

@@ -276,30 +276,86 @@ __global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ G, in
 constexpr int kB16BK = 32, kB16LD = kB16BK + 8;   // (64-wide k-tiles measured slower: 0.67 / 0.87 ms)
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
-// Y[M, Nc] = X[M, K] (bf16) . W[Nc, K]^T (fp32; rows [0, split) from W0, the rest W1).
-// Block tile 128 x 128 (4 waves as 2 x 2, wave tile 64 x 64), K % 8 == 0, ldx % 8 == 0.
-__global__ __launch_bounds__(256) void k_gemm_xwt_bf16(const bf16_t* __restrict__ X, int64_t ldx,
+// X's bf16 planes: bf16 X is exact (one plane, three products per k-step); fp32 X is split
+// three ways like the fp32 operand (three planes, mfma_x6: six products, fp32-grade) - the
+// f32-input MFMA issues at 1/16 of the bf16 rate, so six bf16 products are still ~2.7x
+// its throughput (BGCN_GEMM_X6=0, read once, keeps the f32 MFMA kernels for fp32 X)
+template <class TX> struct XPlanes { static constexpr int P = sizeof(TX) == 2 ? 1 : 3; };
+// the split planes of 8 consecutive X elements (16 B bf16 / 32 B fp32 in registers)
+template <class TX> struct XPiece;
+template <> struct XPiece<bf16_t> {
+  u32x4v v;
+  __device__ __forceinline__ void load(const bf16_t* p, bool ok) {
+    const u32x4v t = *reinterpret_cast<const u32x4v*>(p);
+    v = ok ? t : u32x4v{0u, 0u, 0u, 0u};
+  }
+  __device__ __forceinline__ void store(__bf16* const* planes, int o) const {
+    *reinterpret_cast<u32x4v*>(planes[0] + o) = v;
+  }
+};
+template <> struct XPiece<float> {
+  float4 v[2];
+  __device__ __forceinline__ void load(const float* p, bool ok) {
+    const float4 a = ld4(p), b = ld4(p + 4);
+    v[0] = ok ? a : f4zero();
+    v[1] = ok ? b : f4zero();
+  }
+  __device__ __forceinline__ void store(__bf16* const* planes, int o) const {
+    bf16x8 h, m, l;
+    const float e[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __bf16 x, y, z;
+      split3_bf16(e[j], x, y, z);
+      h[j] = x; m[j] = y; l[j] = z;
+    }
+    *reinterpret_cast<bf16x8*>(planes[0] + o) = h;
+    *reinterpret_cast<bf16x8*>(planes[1] + o) = m;
+    *reinterpret_cast<bf16x8*>(planes[2] + o) = l;
+  }
+};
+// acc += a.b with a in PA planes and b in PB (one exact operand: three products; both split
+// three ways: six, mfma_x6)
+template <int PA, int PB>
+__device__ __forceinline__ f32x16 mfma_planes(const bf16x8 (&a)[PA], const bf16x8 (&b)[PB], f32x16 c) {
+  if constexpr (PA == 1) {
+    c = mfma_bf16(a[0], b[2], c);
+    c = mfma_bf16(a[0], b[1], c);
+    return mfma_bf16(a[0], b[0], c);
+  } else if constexpr (PB == 1) {
+    c = mfma_bf16(a[2], b[0], c);
+    c = mfma_bf16(a[1], b[0], c);
+    return mfma_bf16(a[0], b[0], c);
+  } else {
+    return mfma_x6(a[0], a[1], a[2], b[0], b[1], b[2], c);
+  }
+}
+
+// Y[M, Nc] = X[M, K] (bf16 or fp32) . W[Nc, K]^T (fp32; rows [0, split) from W0, the rest
+// W1).  Block tile 128 x 128 (4 waves as 2 x 2, wave tile 64 x 64), K % 8 == 0, ldx % 8 == 0.
+template <class TX>
+__global__ __launch_bounds__(256) void k_gemm_xwt_bf16(const TX* __restrict__ X, int64_t ldx,
                                                        const float* __restrict__ W0,
                                                        const float* __restrict__ W1, int64_t ldw,
                                                        int64_t split, float* __restrict__ Y, int64_t ldy,
                                                        int64_t M, int64_t Nc, int64_t K,
                                                        const int32_t* __restrict__ gate) {
   if (gate_closed(gate)) return;
-  constexpr int BM = 128, BN = 128;
-  __shared__ __attribute__((aligned(16))) __bf16 As[BM * kB16LD];
+  constexpr int BM = 128, BN = 128, PX = XPlanes<TX>::P;
+  __shared__ __attribute__((aligned(16))) __bf16 As[PX][BM * kB16LD];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3][BN * kB16LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
   const int64_t m0 = int64_t(blockIdx.x) * BM, n0 = int64_t(blockIdx.y) * BN;
   // staging: X rows tid / 4 + 64 i, 8 k at (tid % 4) * 8; W row tid % 128, 16 k at (tid / 128) * 16
-  // (each lane writes its row's 32 contiguous bytes per plane: two 16-byte LDS stores on
+  // (each lane writes its row's contiguous k-range per plane as 16-byte LDS stores on
   // consecutive rows across lanes, conflict-free; one 2-byte store per element per plane
   // kept the waves parked at the barriers)
-  constexpr int kXR = BM * kB16BK / 8 / 256;   // 16-byte X pieces per thread
+  constexpr int kXR = BM * kB16BK / 8 / 256;   // 8-element X pieces per thread
   constexpr int kWK = kB16BK / 2;               // W elements per thread (one row, kWK consecutive k)
   const int xr = tid / (kB16BK / 8), xk = (tid % (kB16BK / 8)) * 8;
   const int wrow = tid & 127, wk = (tid >> 7) * kWK;
-  const bf16_t* xp[kXR];
+  const TX* xp[kXR];
   bool xok[kXR];
 #pragma unroll
   for (int i = 0; i < kXR; ++i) {
@@ -310,15 +366,17 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_bf16(const bf16_t* __restrict_
   const int64_t wn = n0 + wrow;
   const bool wok = wn < Nc;
   const float* wp = (wok ? wn : 0) < split ? W0 + (wok ? wn : 0) * ldw : W1 + ((wok ? wn : 0) - split) * ldw;
-  u32x4v ra[kXR];
+  XPiece<TX> ra[kXR];
   float4 rb[kWK / 4];
+  __bf16* aplanes[PX];
+#pragma unroll
+  for (int p = 0; p < PX; ++p) aplanes[p] = As[p];
   auto gload = [&](int64_t k0) {
 #pragma unroll
     for (int i = 0; i < kXR; ++i) {
       const int64_t k = k0 + xk;
       const bool ok = xok[i] && k < K;
-      const u32x4v v = *reinterpret_cast<const u32x4v*>(xp[i] + (ok ? k : 0));
-      ra[i] = ok ? v : u32x4v{0u, 0u, 0u, 0u};
+      ra[i].load(xp[i] + (ok ? k : 0), ok);
     }
 #pragma unroll
     for (int i = 0; i < kWK / 4; ++i) {
@@ -330,8 +388,7 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_bf16(const bf16_t* __restrict_
   };
   auto sstore = [&]() {
 #pragma unroll
-    for (int i = 0; i < kXR; ++i)
-      *reinterpret_cast<u32x4v*>(&As[(xr + (256 / (kB16BK / 8)) * i) * kB16LD + xk]) = ra[i];
+    for (int i = 0; i < kXR; ++i) ra[i].store(aplanes, (xr + (256 / (kB16BK / 8)) * i) * kB16LD + xk);
     bf16x8 hv[kWK / 8], mv[kWK / 8], lv[kWK / 8];
 #pragma unroll
     for (int i = 0; i < kWK / 4; ++i) {
@@ -363,24 +420,21 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_bf16(const bf16_t* __restrict_
 #pragma unroll
     for (int s = 0; s < kB16BK / 16; ++s) {
       const int ko = 16 * s + 8 * h;
-      bf16x8 a[2], b[3][2];
+      bf16x8 a[2][PX], b[2][3];
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
-        a[mi] = *reinterpret_cast<const bf16x8*>(&As[(wr * 64 + mi * 32 + r32) * kB16LD + ko]);
+#pragma unroll
+        for (int p = 0; p < PX; ++p)
+          a[mi][p] = *reinterpret_cast<const bf16x8*>(&As[p][(wr * 64 + mi * 32 + r32) * kB16LD + ko]);
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
-          b[p][ni] = *reinterpret_cast<const bf16x8*>(&Bs[p][(wc * 64 + ni * 32 + r32) * kB16LD + ko]);
+          b[ni][p] = *reinterpret_cast<const bf16x8*>(&Bs[p][(wc * 64 + ni * 32 + r32) * kB16LD + ko]);
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          f32x16 c = acc[mi][ni];
-          c = mfma_bf16(a[mi], b[2][ni], c);
-          c = mfma_bf16(a[mi], b[1][ni], c);
-          acc[mi][ni] = mfma_bf16(a[mi], b[0][ni], c);
-        }
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mfma_planes<PX, 3>(a[mi], b[ni], acc[mi][ni]);
     }
     __syncthreads();
     if (kt + 1 < nk) {
@@ -402,19 +456,20 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_bf16(const bf16_t* __restrict_
     }
 }
 
-// Partial C_s[Mc, Nc] = G[Ks, Mc]^T (fp32, split) . X[Ks, Nc] (bf16) over the node chunk
-// of split s.  Block tile 128 (Mc) x 128 (Nc), 4 waves as 2 x 2.  Both operands are
-// k-major in memory (rows = nodes): staged transposed into k-contiguous LDS rows, two
-// nodes per 4-byte LDS write.  Nc % 8 == 0, ldx % 8 == 0, ldg % 4 == 0.
+// Partial C_s[Mc, Nc] = G[Ks, Mc]^T (fp32, split) . X[Ks, Nc] (bf16 or fp32, XPlanes) over
+// the node chunk of split s.  Block tile 128 (Mc) x 128 (Nc), 4 waves as 2 x 2.  Both
+// operands are k-major in memory (rows = nodes): staged transposed into k-contiguous LDS
+// rows.  Nc % 8 == 0, ldx % 8 == 0, ldg % 4 == 0.
+template <class TX>
 __global__ __launch_bounds__(256) void k_gemm_tn_bf16(const float* __restrict__ G, int64_t ldg,
-                                                      const bf16_t* __restrict__ X, int64_t ldx,
+                                                      const TX* __restrict__ X, int64_t ldx,
                                                       float* __restrict__ part, int64_t Mc, int64_t Nc,
                                                       int64_t K, int64_t kchunk,
                                                       const int32_t* __restrict__ gate) {
   if (gate_closed(gate)) return;
-  constexpr int BM = 128, BN = 128;
+  constexpr int BM = 128, BN = 128, PX = XPlanes<TX>::P;
   __shared__ __attribute__((aligned(16))) __bf16 As[3][BM * kB16LD];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * kB16LD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[PX][BN * kB16LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
   const int64_t n0 = int64_t(blockIdx.x) * BN, m0 = int64_t(blockIdx.y) * BM;
@@ -423,14 +478,14 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(const float* __restrict__ 
   float* out = part + int64_t(blockIdx.z) * Mc * Nc;
   // staging, transposed into k-contiguous LDS rows: thread t takes column m = t % 128 of G
   // and column n = t % 128 of X over the 16 nodes (t / 128) * 16 ..: lanes load consecutive
-  // columns (coalesced: 256 / 128 B per wave instruction) and each writes its row's 32
-  // contiguous bytes per plane as two 16-byte LDS stores on consecutive rows across lanes,
-  // conflict-free (two nodes per 4-byte store with lanes 8 rows apart hit 2 of 64 banks:
-  // 88 % of the LDS cycles were conflicts, profiles/r03_dense_bf16_pmc.txt)
+  // columns (coalesced) and each writes its row's 32 contiguous bytes per plane as two
+  // 16-byte LDS stores on consecutive rows across lanes, conflict-free (two nodes per 4-byte
+  // store with lanes 8 rows apart hit 2 of 64 banks: 88 % of the LDS cycles were conflicts,
+  // profiles/r03_dense_bf16_pmc.txt)
   constexpr int kNK = kB16BK / 2;   // nodes per thread
   const int sc_ = tid & 127, sk = (tid >> 7) * kNK;
   float rg[kNK];
-  uint32_t rx[kNK];
+  float rx[kNK];
   auto gload = [&](int64_t k0) {
     const int64_t m = m0 + sc_, n = n0 + sc_;
 #pragma unroll
@@ -438,17 +493,17 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(const float* __restrict__ 
       const int64_t k = k0 + sk + u;
       const bool okg = k < ke && m < Mc, okx = k < ke && n < Nc;
       const float g = G[(okg ? k : 0) * ldg + (okg ? m : 0)];
-      const uint32_t x = X[(okx ? k : 0) * ldx + (okx ? n : 0)];
+      const float x = xs(X + (okx ? k : 0) * ldx + (okx ? n : 0));
       rg[u] = okg ? g : 0.f;
-      rx[u] = okx ? x : 0u;
+      rx[u] = okx ? x : 0.f;
     }
   };
-  auto sstore = [&]() {
+  auto split_store = [&](const float (&r)[kNK], __bf16* p0, __bf16* p1, __bf16* p2) {
     bf16x8 hv[kNK / 8], mv[kNK / 8], lv[kNK / 8];
 #pragma unroll
     for (int u = 0; u < kNK; ++u) {
       __bf16 x, y, z;
-      split3_bf16(rg[u], x, y, z);
+      split3_bf16(r[u], x, y, z);
       hv[u >> 3][u & 7] = x;
       mv[u >> 3][u & 7] = y;
       lv[u >> 3][u & 7] = z;
@@ -456,16 +511,17 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(const float* __restrict__ 
     const int o = sc_ * kB16LD + sk;
 #pragma unroll
     for (int j = 0; j < kNK / 8; ++j) {
-      *reinterpret_cast<bf16x8*>(&As[0][o + 8 * j]) = hv[j];
-      *reinterpret_cast<bf16x8*>(&As[1][o + 8 * j]) = mv[j];
-      *reinterpret_cast<bf16x8*>(&As[2][o + 8 * j]) = lv[j];
-      u32x4v w;
-      w.x = rx[8 * j + 0] | (rx[8 * j + 1] << 16);
-      w.y = rx[8 * j + 2] | (rx[8 * j + 3] << 16);
-      w.z = rx[8 * j + 4] | (rx[8 * j + 5] << 16);
-      w.w = rx[8 * j + 6] | (rx[8 * j + 7] << 16);
-      *reinterpret_cast<u32x4v*>(&Bs[o + 8 * j]) = w;
+      *reinterpret_cast<bf16x8*>(p0 + o + 8 * j) = hv[j];
+      if (p1) *reinterpret_cast<bf16x8*>(p1 + o + 8 * j) = mv[j];
+      if (p2) *reinterpret_cast<bf16x8*>(p2 + o + 8 * j) = lv[j];
     }
+  };
+  auto sstore = [&]() {
+    split_store(rg, As[0], As[1], As[2]);
+    if constexpr (PX == 1)   // bf16 X: exact, one plane (the conversion back is exact)
+      split_store(rx, Bs[0], nullptr, nullptr);
+    else
+      split_store(rx, Bs[0], Bs[PX > 1 ? 1 : 0], Bs[PX > 2 ? 2 : 0]);
   };
   f32x16 acc[2][2] = {};
   const int nk = int((ke - kb + kB16BK - 1) / kB16BK);
@@ -479,24 +535,21 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(const float* __restrict__ 
 #pragma unroll
     for (int s = 0; s < kB16BK / 16; ++s) {
       const int ko = 16 * s + 8 * h;
-      bf16x8 a[3][2], b[2];
+      bf16x8 a[2][3], b[2][PX];
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
-          a[p][mi] = *reinterpret_cast<const bf16x8*>(&As[p][(wr * 64 + mi * 32 + r32) * kB16LD + ko]);
+          a[mi][p] = *reinterpret_cast<const bf16x8*>(&As[p][(wr * 64 + mi * 32 + r32) * kB16LD + ko]);
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-        b[ni] = *reinterpret_cast<const bf16x8*>(&Bs[(wc * 64 + ni * 32 + r32) * kB16LD + ko]);
+      for (int p = 0; p < PX; ++p)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          b[ni][p] = *reinterpret_cast<const bf16x8*>(&Bs[p][(wc * 64 + ni * 32 + r32) * kB16LD + ko]);
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          f32x16 c = acc[mi][ni];
-          c = mfma_bf16(a[2][mi], b[ni], c);
-          c = mfma_bf16(a[1][mi], b[ni], c);
-          acc[mi][ni] = mfma_bf16(a[0][mi], b[ni], c);
-        }
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mfma_planes<3, PX>(a[mi], b[ni], acc[mi][ni]);
     }
     __syncthreads();
     if (kt + 1 < nk) {
@@ -515,6 +568,147 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(const float* __restrict__ 
         const int64_t n = n0 + wc * 64 + ni * 32 + r32;
         if (n < Nc) out[m * Nc + n] = acc[mi][ni][q];
       }
+    }
+}
+
+// conv1 for fp32 X on the bf16 MFMA in the six-product form, with X read straight into
+// the A fragments.  Each X element feeds exactly one wave (a wave owns 32 rows and all 128
+// output columns of its block), so X never passes through LDS: lane (h, r) loads pieces i
+// = 0..7 of row r of each 64-wide k-tile, floats 8i + 4h .. + 3 (one instruction moves 32
+// contiguous bytes of each of 32 rows; consecutive instructions finish each 128-byte line),
+// and splits them three ways in registers; k is permuted consistently on both operands
+// (k-step s takes pieces 2s and 2s + 1; W's LDS rows hold the same k in that order), so
+// the MFMA's sum is unchanged.  W (the 2.5 MB shared operand, L2-resident) is
+// split once per block and k-tile into LDS planes (double buffer, one barrier per k-tile).
+// X tiles are prefetched two k-tiles ahead (the tile about to be used is split into its
+// bf16 fragments first, which frees its registers for the load two tiles on).  Block: 4
+// waves = 128 rows x 128 columns; Nc % 128 == 0, K % 4 == 0, ldx % 4 == 0, 16-byte rows.
+constexpr int kX6KT = 64, kX6LD = kX6KT + 8;   // k-tile, LDS row stride (144 B: conflict-free b128)
+__global__ __launch_bounds__(256) void k_gemm_xwt_x6(const float* __restrict__ X, int64_t ldx,
+                                                     const float* __restrict__ W0, const float* __restrict__ W1,
+                                                     int64_t ldw, int64_t split, float* __restrict__ Y, int64_t ldy,
+                                                     int64_t M, int64_t K, const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
+  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][3][128 * kX6LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int64_t n0 = int64_t(blockIdx.y) * 128;
+  const int64_t row = int64_t(blockIdx.x) * 128 + wave * 32 + r32;
+  const bool rok = row < M;
+  // range-checked buffer loads (rows past M read zeros; one 32-bit offset register per
+  // operand, the tile offset in an SGPR, the piece in the immediate): the host checks that
+  // M * ldx * 4 and the W rows fit 32-bit offsets
+  const __amdgpu_buffer_rsrc_t xr = row_rsrc(X, uint32_t(M * ldx * 4));
+  const uint32_t xo = rok ? uint32_t((row * ldx + 4 * h) * 4) : 0xfffffff0u;
+  const int wcol = tid & 127, wkh = (tid >> 7) * 32;           // W staging: column, k-half
+  const int64_t wn0 = n0 + (wcol & ~63);                        // the wave's 64 columns: one of W0 / W1
+  const __amdgpu_buffer_rsrc_t wrs = row_rsrc(wn0 < split ? W0 + wn0 * ldw : W1 + (wn0 - split) * ldw,
+                                              uint32_t(64 * ldw * 4));
+  const uint32_t wo = uint32_t(((wcol & 63) * ldw + wkh) * 4);
+  const int nk = int((K + kX6KT - 1) / kX6KT);
+
+  float4 xa[2][8];    // X tiles in flight (ring of two)
+  float4 wr[8];       // the next W tile
+  bf16x8 af[4][3];    // the current X tile's fragments: k-step x plane
+  f32x16 acc[4] = {};
+  auto ld = [](__amdgpu_buffer_rsrc_t r, uint32_t vo, int so) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+  };
+  // (the k tail - the next row's data - is masked where the tile is consumed, so that no
+  // instruction touches a load's registers before its phase)
+  auto xload = [&](float4 (&d)[8], int kt) {   // piece i: k = 8i + 4h .. + 3 of the tile
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = ld(xr, xo + 32 * i, kt * kX6KT * 4);
+  };
+  auto wload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wr[i] = ld(wrs, wo + 16 * i, kt * kX6KT * 4);
+  };
+  // LDS position of tile k inside its 16-group: 8 ((k >> 2) & 1) + 4 (k >> 3) + (k & 3), so
+  // that lane h's b128 at 16 s + 8 h holds k = 16 s + 4 h + (0..3) and 16 s + 8 + 4 h + (0..3),
+  // the k of its two X pieces 2s and 2s + 1
+  auto wstore = [&](int kt) {
+    const int buf = kt & 1;
+    const int64_t k0 = int64_t(kt) * kX6KT + wkh;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // 8 positions per 16-byte store: group j >> 1, half j & 1
+      bf16x8 p0, p1, p2;
+      const int g = j >> 1, hh = j & 1;   // positions 8 hh .. : k = 16 g + 4 hh + (0..3), 16 g + 8 + 4 hh + ..
+      const float4 w0 = k0 + 16 * g + 4 * hh < K ? wr[4 * g + hh] : f4zero();
+      const float4 w1 = k0 + 16 * g + 8 + 4 * hh < K ? wr[4 * g + 2 + hh] : f4zero();
+      const float v[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 a, b, c;
+        split3_bf16(v[e], a, b, c);
+        p0[e] = a; p1[e] = b; p2[e] = c;
+      }
+      const int o = wcol * kX6LD + wkh + 8 * j;
+      *reinterpret_cast<bf16x8*>(&Ws[buf][0][o]) = p0;
+      *reinterpret_cast<bf16x8*>(&Ws[buf][1][o]) = p1;
+      *reinterpret_cast<bf16x8*>(&Ws[buf][2][o]) = p2;
+    }
+  };
+  auto xsplit = [&](const float4 (&d)[8], int kt) {   // k-step s = pieces 2s, 2s + 1
+    const int64_t k0 = int64_t(kt) * kX6KT + 4 * h;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const float4 x0 = k0 + 16 * st < K ? d[2 * st] : f4zero();
+      const float4 x1 = k0 + 16 * st + 8 < K ? d[2 * st + 1] : f4zero();
+      const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 a, b, c;
+        split3_bf16(v[e], a, b, c);
+        af[st][0][e] = a; af[st][1][e] = b; af[st][2][e] = c;
+      }
+    }
+  };
+  auto mma = [&](int buf) {
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int o = (32 * ni + r32) * kX6LD + 16 * st + 8 * h;
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&Ws[buf][0][o]);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&Ws[buf][1][o]);
+        const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(&Ws[buf][2][o]);
+        acc[ni] = mfma_x6(af[st][0], af[st][1], af[st][2], b0, b1, b2, acc[ni]);
+      }
+    }
+  };
+  // one k-tile: split the current X tile, reuse its registers for the tile two on, MFMAs on
+  // the W planes of this tile, then stage the next W tile into the other buffer
+  // (no conditional loads in the loop: a load under a branch is waited for at the join, which
+  // serialised every tile; tiles past K load zeros through the masks, and the tile count is
+  // rounded up to even for the two-tile ring)
+  // (scheduling barriers keep the phases in this order: the compiler otherwise hoists the W
+  // split above the MFMAs and waits for its L2 loads right after issuing them)
+  auto step = [&](float4 (&cur)[8], int kt) {
+    wload(kt + 1);
+    xsplit(cur, kt);
+    xload(cur, kt + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(kt & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    wstore(kt + 1);
+    __syncthreads();
+  };
+  wload(0);
+  wstore(0);
+  xload(xa[0], 0);
+  xload(xa[1], 1);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(xa[0], kt);
+    step(xa[1], kt + 1);
+  }
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t m = int64_t(blockIdx.x) * 128 + wave * 32 + acc_row(q, lane);
+      if (m < M) Y[m * ldy + n0 + 32 * ni + r32] = acc[ni][q];
     }
 }
 
@@ -551,6 +745,18 @@ size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K) {
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// whether X of this type takes the bf16 MFMA kernels: bf16 X (BGCN_GEMM_BF16=0 keeps the
+// f32 MFMA) and fp32 X in the six-product form (BGCN_GEMM_X6=0 keeps the f32 MFMA); both
+// read once
+template <class TX>
+static bool bf16_mfma_for() {
+  static const bool on = [] {
+    const char* e = std::getenv(sizeof(TX) == 2 ? "BGCN_GEMM_BF16" : "BGCN_GEMM_X6");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 template <class TX>
 static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
                       int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
@@ -564,15 +770,21 @@ static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1
   const bool xal = (reinterpret_cast<uintptr_t>(X) & (4 * sizeof(TX) - 1)) == 0;
   bool vec = K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0 && xal && aligned16(W0) &&
              (!W1 || aligned16(W1));
-  if constexpr (sizeof(TX) == 2) {
-    // bf16 X: the bf16 MFMA with W split three ways (BGCN_GEMM_BF16=0 keeps the f32 MFMA)
-    static const bool b16 = [] { const char* e = std::getenv("BGCN_GEMM_BF16"); return !(e && atoi(e) == 0); }();
-    if (b16 && vec && K % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
-      hipLaunchKernelGGL(k_gemm_xwt_bf16, dim3(grid_for(M, 128), grid_for(Nc, 128)), dim3(256), 0, stream,
-                         reinterpret_cast<const bf16_t*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K, gate);
-      BGCN_CHECK_LAUNCH();
-      return BGCN_OK;
-    }
+  // fp32 X: the six-product kernel with X straight into the A fragments
+  if (sizeof(TX) == 4 && bf16_mfma_for<TX>() && vec && Nc % 128 == 0 && split % 64 == 0 &&
+      (reinterpret_cast<uintptr_t>(X) & 15) == 0 && M * ldx * 4 < (int64_t(1) << 32) - 16 &&
+      64 * ldw * 4 < (int64_t(1) << 32)) {
+    hipLaunchKernelGGL(k_gemm_xwt_x6, dim3(grid_for(M, 128), unsigned(Nc / 128)), dim3(256), 0, stream,
+                       reinterpret_cast<const float*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, K, gate);
+    BGCN_CHECK_LAUNCH();
+    return BGCN_OK;
+  }
+  // the bf16 MFMA with W split three ways (bf16 X exact, fp32 X split too: XPlanes)
+  if (bf16_mfma_for<TX>() && vec && K % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+    hipLaunchKernelGGL(k_gemm_xwt_bf16<TX>, dim3(grid_for(M, 128), grid_for(Nc, 128)), dim3(256), 0, stream,
+                       X, ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K, gate);
+    BGCN_CHECK_LAUNCH();
+    return BGCN_OK;
   }
   dim3 grid(grid_for(M, 64), grid_for(Nc, 128));
   if (vec)
@@ -688,13 +900,13 @@ static int gemm_tn_t(const float* G, int64_t ldg, const TX* X, int64_t ldx, floa
   bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) && xal;
   timing_begin(timing_cls, stream);
   bool done = false;
-  if constexpr (sizeof(TX) == 2) {
-    static const bool b16 = [] { const char* e = std::getenv("BGCN_GEMM_BF16"); return !(e && atoi(e) == 0); }();
-    if (b16 && vec && Nc % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
-      hipLaunchKernelGGL(k_gemm_tn_bf16, dim3(grid_for(Nc, 128), grid_for(Mc, 128), S), dim3(256), 0, stream, G,
-                         ldg, reinterpret_cast<const bf16_t*>(X), ldx, part, Mc, Nc, K, kchunk, gate);
-      done = true;
-    }
+  // bf16 X: the bf16 MFMA with G split three ways.  fp32 X keeps the f32 MFMA: the
+  // six-product forms measured 385 us (k_gemm_tn_bf16<float>) and 489 us (X read straight
+  // into the B fragments) against its 377 us at the bench workload
+  if (sizeof(TX) == 2 && bf16_mfma_for<TX>() && vec && Nc % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+    hipLaunchKernelGGL(k_gemm_tn_bf16<TX>, dim3(grid_for(Nc, 128), grid_for(Mc, 128), S), dim3(256), 0, stream, G,
+                       ldg, X, ldx, part, Mc, Nc, K, kchunk, gate);
+    done = true;
   }
   dim3 grid(grid_for(Nc, 64), grid_for(Mc, 128), S);
   if (done) {

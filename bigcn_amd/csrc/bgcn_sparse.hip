@@ -415,143 +415,6 @@ __device__ inline void compact_body(const SparseState& S, const TX* __restrict__
   }
 }
 
-// The pass over X in address order (BGCN_COMPACT_GROUP, contiguous X): a block of four
-// waves takes a group of R consecutive rows (~80 KB: 4 fp32 / 8 bf16 rows of 5000) as ONE
-// contiguous range, and every wave instruction loads 1 KB of it in address order (the four
-// waves sweep 4 KB at a time) - the access pattern that moves a plain copy at 6.3-6.5 TB/s
-// (tools/copy_probe.hip) against 4.7-4.9 TB/s for one 20 KB row per wave.  The compaction
-// then spans the group: each 16-byte piece's non-zero count goes to LDS, a block scan over
-// the pieces in address order gives every piece its rank inside its row, and each lane
-// writes its own non-zeros (ELL slot or spill pool) from the registers that still hold them.
-// Same ELL / spill / long-row contents as compact_body.
-constexpr int kGroupPer = 10;                     // 16-byte pieces per thread per group
-constexpr int kGroupPieceCap = kGroupPer * 256;   // ~40 KB per group (fp32 2 / bf16 4 rows of 5000)
-constexpr int kGroupRowCap = 64;
-template <class TX>
-__host__ __device__ inline int group_rows(int64_t F) {
-  const int64_t C = F * int64_t(sizeof(TX)) / 16;
-  const int64_t r = C > 0 ? kGroupPieceCap / C : 1;
-  return int(r < 1 ? 1 : (r > kGroupRowCap ? kGroupRowCap : r));
-}
-struct GroupLds {
-  uint8_t cnt[kGroupPieceCap];
-  uint16_t off[kGroupPieceCap + 1];
-  int32_t wsum[4];
-  int32_t rowspill[kGroupRowCap];
-};
-// one group's compaction from its pieces r[] (loaded by the caller)
-template <class TX>
-__device__ __forceinline__ void compact_group(const SparseState& S, const u32x4 (&r)[kGroupPer], int64_t row0,
-                                              int nrow, int C, GroupLds& L) {
-  typedef XChunk<TX> XC;
-  constexpr int E = XC::kElems;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  uint32_t mk[kGroupPer];
-#pragma unroll
-  for (int k = 0; k < kGroupPer; ++k) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int c = 0; c < E; ++c) m |= uint32_t(XC::nz(r[k], c)) << c;
-    mk[k] = m;
-    L.cnt[tid + 256 * k] = uint8_t(__popc(m));
-  }
-  __syncthreads();
-  // exclusive scan of the piece counts in address order: thread t owns [kGroupPer t, + kGroupPer)
-  int cs[kGroupPer], tot = 0;
-#pragma unroll
-  for (int j = 0; j < kGroupPer; ++j) { cs[j] = L.cnt[kGroupPer * tid + j]; tot += cs[j]; }
-  int inc = tot;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += v;
-  }
-  if (lane == 63) L.wsum[wv] = inc;
-  __syncthreads();
-  int run = inc - tot;
-  for (int w = 0; w < wv; ++w) run += L.wsum[w];
-#pragma unroll
-  for (int j = 0; j < kGroupPer; ++j) { L.off[kGroupPer * tid + j] = uint16_t(run); run += cs[j]; }
-  if (tid == 255) L.off[kGroupPieceCap] = uint16_t(run);
-  __syncthreads();
-  // per row: count, and a spill range for a row over the ELL cap
-  if (tid < nrow) {
-    const int cnt = int(L.off[(tid + 1) * C]) - int(L.off[tid * C]);
-    const int64_t i = row0 + tid;
-    S.nnz[i] = cnt;
-    int o = -1;
-    if (cnt > kCap) {   // a long post (getTwittergraph.py:16-24 caps none): its tail to the pool
-      const int nov = cnt - kCap;
-      o = atomicAdd(&S.flags[1], nov);
-      if (o < 0 || int64_t(o) + nov > S.ovf_cap) {   // pool full: the batch goes dense
-        atomicOr(&S.flags[0], 1);
-        o = -1;
-      } else {
-        S.ovf_off[i] = o;
-        S.long_rows[atomicAdd(&S.flags[2], 1)] = int32_t(i);
-      }
-    }
-    L.rowspill[tid] = o;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kGroupPer; ++k) {
-    uint32_t m = mk[k];
-    if (!m) continue;
-    const int p = tid + 256 * k;
-    const int rr = p / C;
-    int pos = int(L.off[p]) - int(L.off[rr * C]);
-    const int64_t i = row0 + rr;
-    const int col0 = (p - rr * C) * E;
-    while (m) {
-      const int c = __builtin_ctz(m);
-      m &= m - 1u;
-      const float v = XC::elem(r[k], c);
-      if (pos < kCap) {
-        S.cols[i * kCap + pos] = col0 + c;
-        S.vals[i * kCap + pos] = v;
-      } else if (L.rowspill[rr] >= 0) {
-        S.ovf[L.rowspill[rr] + pos - kCap] = make_uint2(uint32_t(col0 + c), __float_as_uint(v));
-      }
-      ++pos;
-    }
-  }
-  __syncthreads();   // the next group rewrites the LDS tables
-}
-
-template <class TX>
-__device__ inline void group_load(const SparseState& S, const TX* __restrict__ X, int64_t g, int R, int C,
-                                  u32x4 (&r)[kGroupPer]) {
-  const int64_t row0 = g * R;
-  const int nrow = int(max<int64_t>(min<int64_t>(R, S.N - row0), 0));
-  const __amdgpu_buffer_rsrc_t rs = row_rsrc(X + min<int64_t>(row0, S.N - 1) * S.F, uint32_t(nrow * C) * 16u);
-#pragma unroll
-  for (int k = 0; k < kGroupPer; ++k)   // past the group (or the batch): 0 (range check)
-    r[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int(threadIdx.x) + 256 * k) * 16, 0, kAuxNT);
-}
-
-// groups g = bid, bid + nblk, ...: the next group's loads are issued before this one's
-// compaction (two register sets), so the block always has ~40 KB of X in flight
-template <class TX>
-__device__ inline void compact_group_body(const SparseState& S, const TX* __restrict__ X, int bid, int nblk) {
-  __shared__ GroupLds L;
-  if (S.mode == 1) return;
-  const int C = int(S.F * int64_t(sizeof(TX)) / 16);       // pieces per row
-  const int R = group_rows<TX>(S.F);
-  const int64_t G = (S.N + R - 1) / R;
-  u32x4 ra[kGroupPer], rb[kGroupPer];
-  int64_t g = bid;
-  if (g < G) group_load<TX>(S, X, g, R, C, ra);
-  for (; g < G; g += 2 * int64_t(nblk)) {
-    const int64_t g1 = g + nblk;
-    if (g1 < G) group_load<TX>(S, X, g1, R, C, rb);
-    compact_group<TX>(S, ra, g * R, int(min<int64_t>(R, S.N - g * R)), C, L);
-    if (g1 >= G) break;
-    if (g1 + nblk < G) group_load<TX>(S, X, g1 + nblk, R, C, ra);
-    compact_group<TX>(S, rb, g1 * R, int(min<int64_t>(R, S.N - g1 * R)), C, L);
-  }
-}
-
 // The host-fed input form (bgcn_batch.x_row_ptr / x_col / x_val): the rows arrive already
 // compacted, in ascending column order, so the ELL list, the spill pool and the long-row
 // list are filled from them with the contents compact_row writes from the dense row (the
@@ -1894,7 +1757,6 @@ struct PrepArgs {
   const int32_t *xr_ptr, *xr_col;   // host-fed compacted features (X == nullptr), else null
   const float* xr_val;
   uint64_t* span;                   // device span stamps of the launch (timing class 7) or null
-  int xgroup;                       // the pass over X by row groups in address order (compact_group_body)
   int64_t* eptr;
   uint64_t seed;
   uint4* zero[2];
@@ -1940,7 +1802,6 @@ __device__ inline void prep_b_body(const PrepArgs& a) {
     return;
   }
   if (a.xr_ptr) csr_ell_body(a.S, a.xr_ptr, a.xr_col, a.xr_val, b - 1, a.ncomp);
-  else if (a.xgroup) compact_group_body<TX>(a.S, static_cast<const TX*>(a.X), b - 1, a.ncomp);
   else compact_body<false, TX>(a.S, static_cast<const TX*>(a.X), a.ldx, nullptr, b - 1, a.ncomp);
 }
 
@@ -2309,9 +2170,6 @@ int sparse_csc(SparseState& S, hipStream_t s) {
   return BGCN_OK;
 }
 
-#ifndef BGCN_COMPACT_GROUP
-#define BGCN_COMPACT_GROUP 0   // 1: the pass over X by row groups in address order (measured slower)
-#endif
 #ifndef BGCN_PREP_LANES_DEFAULT
 #define BGCN_PREP_LANES_DEFAULT 2   // profiles/r03_chain_experiments_late.txt
 #endif
@@ -2391,13 +2249,6 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
     }();
     const bool bf = bt->x_dtype == BGCN_DTYPE_BF16;
     a.ncomp = xp ? int(grid_for(N, bf ? 8 : 4)) : 0;
-    // contiguous rows of whole 16-byte pieces: the pass by row groups in address order
-    static const int grp = [] { const char* e = std::getenv("BGCN_COMPACT_GROUP"); return e ? atoi(e) : BGCN_COMPACT_GROUP; }();
-    const size_t esz = bf ? 2 : 4;
-    a.xgroup = (grp && bt->x && bt->ldx == F && (F * esz) % 16 == 0) ? 1 : 0;
-    if (a.xgroup && xp)
-      a.ncomp = int((N + (bf ? group_rows<bf16_t>(F) : group_rows<float>(F)) - 1) /
-                    (bf ? group_rows<bf16_t>(F) : group_rows<float>(F)));
     int cap = bf ? (compact_by_prefix<bf16_t>() ? ncu : 0) : ncu + ncu / 2;
     const char* e = std::getenv("BGCN_PREP_BLOCKS");
     if (e) cap = atoi(e);

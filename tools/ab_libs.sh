@@ -5,7 +5,7 @@
 #   bash tools/ab_libs.sh base build/variants/libbgcn_c128.so ...   ("base" = in-tree lib)
 set -eo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-L="--no-cpu-baseline --compare-dense 0 --aggregation 0 --compare-dropedge 0 --dropin 0 --host-fed 0 --steps 200 --warmup 10"
+L="--no-cpu-baseline --compare-dense 0 --aggregation 0 --compare-dropedge 0 --dropin 0 --host-fed 0 --steps 200 --warmup 10 $BENCH_ARGS"
 for v in "$@"; do
   tag=$(basename "$v" .so)
   if [ "$v" = base ]; then unset BGCN_LIB; else export BGCN_LIB=$(pwd)/$v; fi
