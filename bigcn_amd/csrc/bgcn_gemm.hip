@@ -712,6 +712,143 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_x6(const float* __restrict__ X
     }
 }
 
+// The same conv1 with the split work spread between the MFMAs (one wave per SIMD hides up
+// to ~5 single-issue instructions per 32-cycle MFMA gap: MI355X_MICROARCH.md), so the tile
+// is MFMA-paced instead of MFMA phase + split phase.  A tile's 16 MFMA groups (k-step st x
+// column tile ni, six products each) carry, in order: the split of the tile's own X piece 3
+// (groups 0-3, while st = 0 runs), then the next tile's X pieces 0, 1, 2 into the fragment
+// slots st = 0, 1, 2 free by then (groups 4-15), and the next tile's W split into the other
+// LDS buffer (groups 4-11).  X tiles ride a ring of three register slots (the load of tile
+// kt + 3 is issued as soon as tile kt's raw piece 3 is split), the next W tile is loaded at
+// group 11 and written one tile later.  One barrier per k-tile.
+__global__ __launch_bounds__(256) void k_gemm_xwt_x6p(const float* __restrict__ X, int64_t ldx,
+                                                      const float* __restrict__ W0, const float* __restrict__ W1,
+                                                      int64_t ldw, int64_t split, float* __restrict__ Y, int64_t ldy,
+                                                      int64_t M, int64_t K, const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
+  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][3][128 * kX6LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int64_t n0 = int64_t(blockIdx.y) * 128;
+  const int64_t row = int64_t(blockIdx.x) * 128 + wave * 32 + r32;
+  const bool rok = row < M;
+  const __amdgpu_buffer_rsrc_t xr = row_rsrc(X, uint32_t(M * ldx * 4));
+  const uint32_t xo = rok ? uint32_t((row * ldx + 4 * h) * 4) : 0xfffffff0u;
+  const int wcol = tid & 127, wkh = (tid >> 7) * 32;
+  const int64_t wn0 = n0 + (wcol & ~63);
+  const __amdgpu_buffer_rsrc_t wrs = row_rsrc(wn0 < split ? W0 + wn0 * ldw : W1 + (wn0 - split) * ldw,
+                                              uint32_t(64 * ldw * 4));
+  const uint32_t wo = uint32_t(((wcol & 63) * ldw + wkh) * 4);
+  const int nk = int((K + kX6KT - 1) / kX6KT);
+
+  float4 x0[8], x1[8], x2[8];   // X tile ring
+  float4 wr[8];                  // the next W tile (raw)
+  bf16x8 af[4][3];               // fragments by k-step (rolling: see above)
+  f32x16 acc[4] = {};
+  auto ld = [](__amdgpu_buffer_rsrc_t r, uint32_t vo, int so) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+  };
+  auto xload = [&](float4 (&d)[8], int kt) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = ld(xr, xo + 32 * i, kt * kX6KT * 4);
+  };
+  auto wload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wr[i] = ld(wrs, wo + 16 * i, kt * kX6KT * 4);
+  };
+  // two elements (e, e + 1) of X piece st of tile kt into fragment slot st
+  auto xpart = [&](const float4 (&d)[8], int kt, int st, int e) {
+    const int64_t k = int64_t(kt) * kX6KT + 4 * h + 16 * st + (e < 4 ? 0 : 8);
+    const float4 q = k < K ? d[2 * st + (e >> 2)] : f4zero();
+    const float v0 = (e & 3) == 0 ? q.x : q.z, v1 = (e & 3) == 0 ? q.y : q.w;
+    __bf16 a, b, c;
+    split3_bf16(v0, a, b, c);
+    af[st][0][e] = a; af[st][1][e] = b; af[st][2][e] = c;
+    split3_bf16(v1, a, b, c);
+    af[st][0][e + 1] = a; af[st][1][e + 1] = b; af[st][2][e + 1] = c;
+  };
+  // W chunk j (8 LDS positions of the 16-group permutation) of tile kt into buffer kt & 1
+  auto wchunk = [&](int kt, int j) {
+    const int buf = kt & 1;
+    const int64_t k0 = int64_t(kt) * kX6KT + wkh;
+    const int g = j >> 1, hh = j & 1;
+    const float4 w0 = k0 + 16 * g + 4 * hh < K ? wr[4 * g + hh] : f4zero();
+    const float4 w1 = k0 + 16 * g + 8 + 4 * hh < K ? wr[4 * g + 2 + hh] : f4zero();
+    const float v[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    bf16x8 p0, p1, p2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 a, b, c;
+      split3_bf16(v[e], a, b, c);
+      p0[e] = a; p1[e] = b; p2[e] = c;
+    }
+    const int o = wcol * kX6LD + wkh + 8 * j;
+    *reinterpret_cast<bf16x8*>(&Ws[buf][0][o]) = p0;
+    *reinterpret_cast<bf16x8*>(&Ws[buf][1][o]) = p1;
+    *reinterpret_cast<bf16x8*>(&Ws[buf][2][o]) = p2;
+  };
+  auto mg = [&](int buf, int st, int ni) {
+    const int o = (32 * ni + r32) * kX6LD + 16 * st + 8 * h;
+    const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&Ws[buf][0][o]);
+    const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&Ws[buf][1][o]);
+    const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(&Ws[buf][2][o]);
+    acc[ni] = mfma_x6(af[st][0], af[st][1], af[st][2], b0, b1, b2, acc[ni]);
+  };
+  // tile kt: A = X(kt) (piece 3 still raw), B = X(kt + 1), C = X(kt + 2) (in flight)
+  auto tile = [&](int kt, float4 (&A)[8], float4 (&B)[8]) {
+    const int buf = kt & 1;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      mg(buf, 0, ni);
+      xpart(A, kt, 3, 2 * ni);
+    }
+    xload(A, kt + 3);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      mg(buf, 1, ni);
+      xpart(B, kt + 1, 0, 2 * ni);
+      if (ni & 1) wchunk(kt + 1, ni >> 1);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      mg(buf, 2, ni);
+      xpart(B, kt + 1, 1, 2 * ni);
+      if (ni & 1) wchunk(kt + 1, 2 + (ni >> 1));
+    }
+    wload(kt + 2);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      mg(buf, 3, ni);
+      xpart(B, kt + 1, 2, 2 * ni);
+    }
+    __syncthreads();
+  };
+  wload(0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wchunk(0, j);
+  xload(x0, 0);
+  xload(x1, 1);
+  xload(x2, 2);
+  wload(1);
+#pragma unroll
+  for (int st = 0; st < 3; ++st)
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) xpart(x0, 0, st, e);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 3) {
+    tile(kt, x0, x1);
+    tile(kt + 1, x1, x2);
+    tile(kt + 2, x2, x0);
+  }
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t m = int64_t(blockIdx.x) * 128 + wave * 32 + acc_row(q, lane);
+      if (m < M) Y[m * ldy + n0 + 32 * ni + r32] = acc[ni][q];
+    }
+}
+
 // C[m][n] = sum_s part[s][m][n] (fixed order), rows [0, split) -> C0, the rest -> C1.
 __global__ __launch_bounds__(256) void k_reduce_splits(const float* __restrict__ part, int S,
                                                        int64_t Mc, int64_t Nc, float* __restrict__ C0,
@@ -774,8 +911,13 @@ static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1
   if (sizeof(TX) == 4 && bf16_mfma_for<TX>() && vec && Nc % 128 == 0 && split % 64 == 0 &&
       (reinterpret_cast<uintptr_t>(X) & 15) == 0 && M * ldx * 4 < (int64_t(1) << 32) - 16 &&
       64 * ldw * 4 < (int64_t(1) << 32)) {
-    hipLaunchKernelGGL(k_gemm_xwt_x6, dim3(grid_for(M, 128), unsigned(Nc / 128)), dim3(256), 0, stream,
-                       reinterpret_cast<const float*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, K, gate);
+    static const int pipe = [] { const char* e = std::getenv("BGCN_X6_PIPE"); return e ? atoi(e) : 1; }();
+    if (pipe)
+      hipLaunchKernelGGL(k_gemm_xwt_x6p, dim3(grid_for(M, 128), unsigned(Nc / 128)), dim3(256), 0, stream,
+                         reinterpret_cast<const float*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, K, gate);
+    else
+      hipLaunchKernelGGL(k_gemm_xwt_x6, dim3(grid_for(M, 128), unsigned(Nc / 128)), dim3(256), 0, stream,
+                         reinterpret_cast<const float*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, K, gate);
     BGCN_CHECK_LAUNCH();
     return BGCN_OK;
   }
