@@ -849,6 +849,137 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_x6p(const float* __restrict__ 
     }
 }
 
+// dW1 for fp32 X in the six-product form, pipelined like k_gemm_xwt_x6p with the roles
+// turned: the partial C_s[128, Nc] = G[Ks, 128]^T . X[Ks, Nc] over node split s.  Wave w
+// owns X columns n0 + 32w + r (lane r) and all 128 rows m; lane (h, r) loads X[node][col]
+// for the 32 nodes [32h, 32h + 32) of each 64-node tile (dword loads: a wave instruction
+// covers two node rows' 128 contiguous bytes), k-step st taking nodes 32h + 8st + (0..7);
+// G (dZ1) is staged per tile into LDS planes [m][node] (float4 loads of 4 columns x 8
+// nodes per thread, split, one 16-byte store per column and plane).  The split work rides
+// between the MFMAs as in the conv1 kernel; X tiles on a ring of two register slots.
+// Mc == 128.
+__global__ __launch_bounds__(256) void k_gemm_tn_x6p(const float* __restrict__ G, int64_t ldg,
+                                                     const float* __restrict__ X, int64_t ldx,
+                                                     float* __restrict__ part, int64_t Nc, int64_t K,
+                                                     int64_t kchunk, const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[2][3][128 * kX6LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+  const int64_t col = int64_t(blockIdx.x) * 128 + 32 * wave + r32;
+  const bool cok = col < Nc;
+  const int64_t kb = int64_t(blockIdx.z) * kchunk, ke = min<int64_t>(kb + kchunk, K);
+  float* out = part + int64_t(blockIdx.z) * 128 * Nc;
+  const __amdgpu_buffer_rsrc_t xr = row_rsrc(X, uint32_t(K * ldx * 4));
+  const uint32_t xo = cok ? uint32_t((col + 32 * h * ldx) * 4) : 0xfffffff0u;
+  const int gm4 = (tid & 31) * 4, gnb = (tid >> 5) * 8;
+  const __amdgpu_buffer_rsrc_t grs = row_rsrc(G, uint32_t(K * ldg * 4));
+  const uint32_t go = uint32_t((gm4 + gnb * ldg) * 4);
+  const int nk = int((ke - kb + kX6KT - 1) / kX6KT);
+
+  float x0[32], x1[32];           // X tile ring (two slots: 32 dword loads per tile, and
+                                  // vmcnt counts at most 63 loads in flight)
+  float4 gv[8];                   // the next G tile (raw)
+  bf16x8 bf[4][3];                // B fragments by k-step (rolling)
+  f32x16 acc[4] = {};
+  auto xload = [&](float (&d)[32], int kt) {
+    const int64_t node = kb + int64_t(kt) * kX6KT;
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      d[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xo, int((node + j) * ldx * 4), 0));
+  };
+  auto gload = [&](int kt) {
+    const int64_t node = kb + int64_t(kt) * kX6KT;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(grs, go, int((node + j) * ldg * 4), 0);
+      gv[j] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+  };
+  // two elements (e, e + 1) of X k-step st of tile kt into fragment slot st
+  auto xpart = [&](const float (&d)[32], int kt, int st, int e) {
+    const int64_t node = kb + int64_t(kt) * kX6KT + 32 * h + 8 * st + e;
+    const float v0 = node < ke ? d[8 * st + e] : 0.f, v1 = node + 1 < ke ? d[8 * st + e + 1] : 0.f;
+    __bf16 a, b, c;
+    split3_bf16(v0, a, b, c);
+    bf[st][0][e] = a; bf[st][1][e] = b; bf[st][2][e] = c;
+    split3_bf16(v1, a, b, c);
+    bf[st][0][e + 1] = a; bf[st][1][e + 1] = b; bf[st][2][e + 1] = c;
+  };
+  // G column gm4 + c of tile kt: its 8 nodes as one 16-byte store per plane, buffer kt & 1
+  auto gchunk = [&](int kt, int c) {
+    const int buf = kt & 1;
+    const int64_t node = kb + int64_t(kt) * kX6KT + gnb;
+    bf16x8 p0, p1, p2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float4 q = gv[e];
+      const float v = node + e < ke ? (c == 0 ? q.x : c == 1 ? q.y : c == 2 ? q.z : q.w) : 0.f;
+      __bf16 a, b, cc;
+      split3_bf16(v, a, b, cc);
+      p0[e] = a; p1[e] = b; p2[e] = cc;
+    }
+    const int o = (gm4 + c) * kX6LD + gnb;
+    *reinterpret_cast<bf16x8*>(&Gs[buf][0][o]) = p0;
+    *reinterpret_cast<bf16x8*>(&Gs[buf][1][o]) = p1;
+    *reinterpret_cast<bf16x8*>(&Gs[buf][2][o]) = p2;
+  };
+  auto mg = [&](int buf, int st, int mi) {
+    const int o = (32 * mi + r32) * kX6LD + 32 * h + 8 * st;
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&Gs[buf][0][o]);
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&Gs[buf][1][o]);
+    const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(&Gs[buf][2][o]);
+    acc[mi] = mfma_x6(a0, a1, a2, bf[st][0], bf[st][1], bf[st][2], acc[mi]);
+  };
+  auto tile = [&](int kt, float (&A)[32], float (&B)[32]) {
+    const int buf = kt & 1;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      mg(buf, 0, mi);
+      xpart(A, kt, 3, 2 * mi);
+    }
+    xload(A, kt + 2);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      mg(buf, 1, mi);
+      xpart(B, kt + 1, 0, 2 * mi);
+      if (mi & 1) gchunk(kt + 1, mi >> 1);
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      mg(buf, 2, mi);
+      xpart(B, kt + 1, 1, 2 * mi);
+      if (mi & 1) gchunk(kt + 1, 2 + (mi >> 1));
+    }
+    gload(kt + 2);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      mg(buf, 3, mi);
+      xpart(B, kt + 1, 2, 2 * mi);
+    }
+    __syncthreads();
+  };
+  gload(0);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) gchunk(0, c);
+  xload(x0, 0);
+  xload(x1, 1);
+  gload(1);
+#pragma unroll
+  for (int st = 0; st < 3; ++st)
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) xpart(x0, 0, st, e);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    tile(kt, x0, x1);
+    tile(kt + 1, x1, x0);
+  }
+  if (!cok) return;   // (the output column is the lane's own)
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) out[int64_t(32 * mi + acc_row(q, lane)) * Nc + col] = acc[mi][q];
+}
+
 // C[m][n] = sum_s part[s][m][n] (fixed order), rows [0, split) -> C0, the rest -> C1.
 __global__ __launch_bounds__(256) void k_reduce_splits(const float* __restrict__ part, int S,
                                                        int64_t Mc, int64_t Nc, float* __restrict__ C0,
@@ -911,7 +1042,7 @@ static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1
   if (sizeof(TX) == 4 && bf16_mfma_for<TX>() && vec && Nc % 128 == 0 && split % 64 == 0 &&
       (reinterpret_cast<uintptr_t>(X) & 15) == 0 && M * ldx * 4 < (int64_t(1) << 32) - 16 &&
       64 * ldw * 4 < (int64_t(1) << 32)) {
-    static const int pipe = [] { const char* e = std::getenv("BGCN_X6_PIPE"); return e ? atoi(e) : 1; }();
+    static const int pipe = [] { const char* e = std::getenv("BGCN_X6_PIPE"); return e ? atoi(e) : 0; }();
     if (pipe)
       hipLaunchKernelGGL(k_gemm_xwt_x6p, dim3(grid_for(M, 128), unsigned(Nc / 128)), dim3(256), 0, stream,
                          reinterpret_cast<const float*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, K, gate);
@@ -1042,10 +1173,21 @@ static int gemm_tn_t(const float* G, int64_t ldg, const TX* X, int64_t ldx, floa
   bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) && xal;
   timing_begin(timing_cls, stream);
   bool done = false;
-  // bf16 X: the bf16 MFMA with G split three ways.  fp32 X keeps the f32 MFMA: the
-  // six-product forms measured 385 us (k_gemm_tn_bf16<float>) and 489 us (X read straight
-  // into the B fragments) against its 377 us at the bench workload
-  if (sizeof(TX) == 2 && bf16_mfma_for<TX>() && vec && Nc % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+  static const int tn_pipe = [] { const char* e = std::getenv("BGCN_TN_PIPE"); return e ? atoi(e) : 0; }();
+  if (sizeof(TX) == 4 && tn_pipe && bf16_mfma_for<TX>() && Mc == 128 && (K + 256) * ldx * 4 < (int64_t(1) << 31) &&
+      (K + 256) * ldg * 4 < (int64_t(1) << 31)) {
+    // fp32 X: the pipelined six-product kernel, about one block per CU over the column
+    // tiles x node splits (within the workspace's split count)
+    const int64_t tiles = (Nc + 127) / 128;
+    int64_t s6 = std::max<int64_t>(1, std::min<int64_t>(S, (256 + tiles - 1) / tiles));
+    int64_t kc = (K + s6 - 1) / s6;
+    kc = (kc + kX6KT - 1) / kX6KT * kX6KT;
+    s6 = (K + kc - 1) / kc;
+    hipLaunchKernelGGL(k_gemm_tn_x6p, dim3(unsigned(tiles), 1, unsigned(s6)), dim3(256), 0, stream, G, ldg,
+                       reinterpret_cast<const float*>(X), ldx, part, Nc, K, kc, gate);
+    S = int(s6);
+    done = true;
+  } else if (sizeof(TX) == 2 && bf16_mfma_for<TX>() && vec && Nc % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
     hipLaunchKernelGGL(k_gemm_tn_bf16<TX>, dim3(grid_for(Nc, 128), grid_for(Mc, 128), S), dim3(256), 0, stream, G,
                        ldg, X, ldx, part, Mc, Nc, K, kchunk, gate);
     done = true;
