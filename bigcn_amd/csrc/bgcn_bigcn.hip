@@ -633,7 +633,6 @@ struct FusedWs {
   float* spmm_ws; size_t spmm_bytes;
   float* dw2_part;                        // [2][S2][H][H+F]
   float* tn_ws; size_t tn_bytes;
-  uint16_t* w1img;                        // the dense conv1's W1 split images (fp32 X, gemm_xwt_x)
   int S2; int64_t kchunk2;
   int S2d; int64_t kchunk2d;              // the dense feature mode's dW2 node splits (more: shorter loops)
   int Sh; int64_t kchunkh;
@@ -699,7 +698,6 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   t.dw2_part = c.take<float>(dense_part > sparse_part ? dense_part : sparse_part);
   t.tn_bytes = tn_ws_size(2 * H, F, N);
   t.tn_ws = c.take<float>(t.tn_bytes / sizeof(float) + 1);
-  t.w1img = c.take<uint16_t>(size_t(w_img_elems(F, 2 * H)));
   if (w) *w = t;
   return c.off;
 }
@@ -909,7 +907,7 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
     }
     if (dense_launched(a, sp))
       BGCN_TRY(gemm_xwt_x(a->x, a->x_dtype, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H,
-                          F, s, gate, w.w1img));
+                          F, s, gate));
     if (graph_lane >= 0) BGCN_TRY(aux_join(s, graph_lane));   // K1 of a just-prepared batch
     return forward_tail(a, w, sp, keep, gate, s, head, false);
   }
@@ -935,7 +933,7 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
   if (dense_launched(a, sp)) {
     timing_begin(sparse ? 4 : 0, s);
     BGCN_TRY(gemm_xwt_x(a->x, a->x_dtype, a->ldx, a->td_w1, a->bu_w1, F, H, w.z1, 2 * H, N, 2 * H, F,
-                        s, gate, w.w1img));
+                        s, gate));
     timing_end(sparse ? 4 : 0, s);
   }
   // the graphs (built on graph_lane by bgcn_train_step) and the items are needed from

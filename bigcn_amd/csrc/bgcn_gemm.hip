@@ -849,284 +849,6 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_x6p(const float* __restrict__ 
     }
 }
 
-// W split once per call (k_w_split_x6) into the k-tile images the conv1 kernel stages:
-// img[((t * 3 + p) * 128 + c) * 64 + q] = plane p of W row c at tile t, LDS position q (the
-// 16-group permutation of k_gemm_xwt_x6p's wstore; zeros past K).  Every block then copies
-// its W tile (12 16-byte loads per thread) instead of splitting 2.5 MB of W again: the split
-// was half of the conv1 kernel's VALU instructions (6.4 per MFMA, over the ~5 an MFMA gap
-// hides at one wave per SIMD: profiles/r04_dense_pmc.txt).
-__global__ __launch_bounds__(256) void k_w_split_x6(const float* __restrict__ W0, const float* __restrict__ W1,
-                                                    int64_t ldw, int64_t split, int64_t K, int nk,
-                                                    uint16_t* __restrict__ img, const int32_t* __restrict__ gate) {
-  if (gate_closed(gate)) return;
-  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;   // (tile, column, chunk of 8)
-  if (idx >= int64_t(nk) * 128 * 8) return;
-  const int j = int(idx & 7), c = int((idx >> 3) & 127), t = int(idx >> 10);
-  const float* row = c < split ? W0 + int64_t(c) * ldw : W1 + (int64_t(c) - split) * ldw;
-  const int g = j >> 1, hh = j & 1;
-  bf16x8 p0, p1, p2;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int64_t k = int64_t(t) * kX6KT + 16 * g + (e < 4 ? 0 : 8) + 4 * hh + (e & 3);
-    const float v = k < K ? row[k] : 0.f;
-    __bf16 a, b, cc;
-    split3_bf16(v, a, b, cc);
-    p0[e] = a; p1[e] = b; p2[e] = cc;
-  }
-  const int64_t o = (int64_t(t) * 3 * 128 + c) * 64 + 8 * j;
-  *reinterpret_cast<bf16x8*>(img + o) = p0;
-  *reinterpret_cast<bf16x8*>(img + o + 128 * 64) = p1;
-  *reinterpret_cast<bf16x8*>(img + o + 2 * 128 * 64) = p2;
-}
-
-// k_gemm_xwt_x6p with W from the pre-split image (staging = copies, no split) and X on a
-// ring of two register slots (a k-tile now outlasts the HBM latency).
-__global__ __launch_bounds__(256) void k_gemm_xwt_x6q(const float* __restrict__ X, int64_t ldx,
-                                                      const uint16_t* __restrict__ img, float* __restrict__ Y,
-                                                      int64_t ldy, int64_t M, int64_t K,
-                                                      const int32_t* __restrict__ gate) {
-  if (gate_closed(gate)) return;
-  __shared__ __attribute__((aligned(16))) __bf16 Ws[2][3][128 * kX6LD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
-  const int64_t row = int64_t(blockIdx.x) * 128 + wave * 32 + r32;
-  const bool rok = row < M;
-  const __amdgpu_buffer_rsrc_t xr = row_rsrc(X, uint32_t(M * ldx * 4));
-  const uint32_t xo = rok ? uint32_t((row * ldx + 4 * h) * 4) : 0xfffffff0u;
-  const int wcol = tid & 127, wkh = (tid >> 7) * 32;
-  const int nk = int((K + kX6KT - 1) / kX6KT);
-  // the image of column block blockIdx.y (Nc / 128 blocks of 128 columns, tiles in order)
-  const uint16_t* wimg = img + int64_t(blockIdx.y) * nk * 3 * 128 * 64;
-  const __amdgpu_buffer_rsrc_t wrs = row_rsrc(wimg, uint32_t(int64_t(nk) * 3 * 128 * 64 * 2));
-  const uint32_t wo = uint32_t((wcol * 64 + wkh) * 2);
-
-  float4 x0[8], x1[8];           // X tile ring
-  u32x4 wr[12];                  // the next W tile: plane p, chunk j -> wr[4p + j]
-  bf16x8 af[4][3];               // fragments by k-step (rolling, as in k_gemm_xwt_x6p)
-  f32x16 acc[4] = {};
-  auto ld = [](__amdgpu_buffer_rsrc_t r, uint32_t vo, int so) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0);
-    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
-  };
-  auto xload = [&](float4 (&d)[8], int kt) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) d[i] = ld(xr, xo + 32 * i, kt * kX6KT * 4);
-  };
-  auto wload = [&](int kt) {   // tiles past the image read zeros (range check)
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        wr[4 * p + j] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wo + (p * 128 * 64 + 8 * j) * 2,
-                                                              kt * 3 * 128 * 64 * 2, 0);
-  };
-  auto wchunk = [&](int kt, int j) {
-    const int buf = kt & 1;
-    const int o = wcol * kX6LD + wkh + 8 * j;
-#pragma unroll
-    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(&Ws[buf][p][o]) = wr[4 * p + j];
-  };
-  auto xpart = [&](const float4 (&d)[8], int kt, int st, int e) {
-    const int64_t k = int64_t(kt) * kX6KT + 4 * h + 16 * st + (e < 4 ? 0 : 8);
-    const float4 q = k < K ? d[2 * st + (e >> 2)] : f4zero();
-    const float v0 = (e & 3) == 0 ? q.x : q.z, v1 = (e & 3) == 0 ? q.y : q.w;
-    __bf16 a, b, c;
-    split3_bf16(v0, a, b, c);
-    af[st][0][e] = a; af[st][1][e] = b; af[st][2][e] = c;
-    split3_bf16(v1, a, b, c);
-    af[st][0][e + 1] = a; af[st][1][e + 1] = b; af[st][2][e + 1] = c;
-  };
-  auto mg = [&](int buf, int st, int ni) {
-    const int o = (32 * ni + r32) * kX6LD + 16 * st + 8 * h;
-    const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&Ws[buf][0][o]);
-    const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&Ws[buf][1][o]);
-    const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(&Ws[buf][2][o]);
-    acc[ni] = mfma_x6(af[st][0], af[st][1], af[st][2], b0, b1, b2, acc[ni]);
-  };
-  // tile kt: A = X(kt) (piece 3 still raw), B = X(kt + 1)
-  auto tile = [&](int kt, float4 (&A)[8], float4 (&B)[8]) {
-    const int buf = kt & 1;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      mg(buf, 0, ni);
-      xpart(A, kt, 3, 2 * ni);
-    }
-    xload(A, kt + 2);
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      mg(buf, 1, ni);
-      xpart(B, kt + 1, 0, 2 * ni);
-      if (ni & 1) wchunk(kt + 1, ni >> 1);
-    }
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      mg(buf, 2, ni);
-      xpart(B, kt + 1, 1, 2 * ni);
-      if (ni & 1) wchunk(kt + 1, 2 + (ni >> 1));
-    }
-    wload(kt + 2);
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      mg(buf, 3, ni);
-      xpart(B, kt + 1, 2, 2 * ni);
-    }
-    __syncthreads();
-  };
-  wload(0);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) wchunk(0, j);
-  xload(x0, 0);
-  xload(x1, 1);
-  wload(1);
-#pragma unroll
-  for (int st = 0; st < 3; ++st)
-#pragma unroll
-    for (int e = 0; e < 8; e += 2) xpart(x0, 0, st, e);
-  __syncthreads();
-  for (int kt = 0; kt < nk; kt += 2) {
-    tile(kt, x0, x1);
-    tile(kt + 1, x1, x0);
-  }
-  const int64_t n0 = int64_t(blockIdx.y) * 128;
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int64_t m = int64_t(blockIdx.x) * 128 + wave * 32 + acc_row(q, lane);
-      if (m < M) Y[m * ldy + n0 + 32 * ni + r32] = acc[ni][q];
-    }
-}
-
-// dW1 for fp32 X in the six-product form, pipelined like k_gemm_xwt_x6p with the roles
-// turned: the partial C_s[128, Nc] = G[Ks, 128]^T . X[Ks, Nc] over node split s.  Wave w
-// owns X columns n0 + 32w + r (lane r) and all 128 rows m; lane (h, r) loads X[node][col]
-// for the 32 nodes [32h, 32h + 32) of each 64-node tile (dword loads: a wave instruction
-// covers two node rows' 128 contiguous bytes), k-step st taking nodes 32h + 8st + (0..7);
-// G (dZ1) is staged per tile into LDS planes [m][node] (float4 loads of 4 columns x 8
-// nodes per thread, split, one 16-byte store per column and plane).  The split work rides
-// between the MFMAs as in the conv1 kernel; X tiles on a ring of two register slots.
-// Mc == 128.
-__global__ __launch_bounds__(256) void k_gemm_tn_x6p(const float* __restrict__ G, int64_t ldg,
-                                                     const float* __restrict__ X, int64_t ldx,
-                                                     float* __restrict__ part, int64_t Nc, int64_t K,
-                                                     int64_t kchunk, const int32_t* __restrict__ gate) {
-  if (gate_closed(gate)) return;
-  __shared__ __attribute__((aligned(16))) __bf16 Gs[2][3][128 * kX6LD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
-  const int64_t col = int64_t(blockIdx.x) * 128 + 32 * wave + r32;
-  const bool cok = col < Nc;
-  const int64_t kb = int64_t(blockIdx.z) * kchunk, ke = min<int64_t>(kb + kchunk, K);
-  float* out = part + int64_t(blockIdx.z) * 128 * Nc;
-  const __amdgpu_buffer_rsrc_t xr = row_rsrc(X, uint32_t(K * ldx * 4));
-  const uint32_t xo = cok ? uint32_t((col + 32 * h * ldx) * 4) : 0xfffffff0u;
-  const int gm4 = (tid & 31) * 4, gnb = (tid >> 5) * 8;
-  const __amdgpu_buffer_rsrc_t grs = row_rsrc(G, uint32_t(K * ldg * 4));
-  const uint32_t go = uint32_t((gm4 + gnb * ldg) * 4);
-  const int nk = int((ke - kb + kX6KT - 1) / kX6KT);
-
-  float x0[32], x1[32];           // X tile ring (two slots: 32 dword loads per tile, and
-                                  // vmcnt counts at most 63 loads in flight)
-  float4 gv[8];                   // the next G tile (raw)
-  bf16x8 bf[4][3];                // B fragments by k-step (rolling)
-  f32x16 acc[4] = {};
-  auto xload = [&](float (&d)[32], int kt) {
-    const int64_t node = kb + int64_t(kt) * kX6KT;
-#pragma unroll
-    for (int j = 0; j < 32; ++j)
-      d[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xo, int((node + j) * ldx * 4), 0));
-  };
-  auto gload = [&](int kt) {
-    const int64_t node = kb + int64_t(kt) * kX6KT;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(grs, go, int((node + j) * ldg * 4), 0);
-      gv[j] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
-    }
-  };
-  // two elements (e, e + 1) of X k-step st of tile kt into fragment slot st
-  auto xpart = [&](const float (&d)[32], int kt, int st, int e) {
-    const int64_t node = kb + int64_t(kt) * kX6KT + 32 * h + 8 * st + e;
-    const float v0 = node < ke ? d[8 * st + e] : 0.f, v1 = node + 1 < ke ? d[8 * st + e + 1] : 0.f;
-    __bf16 a, b, c;
-    split3_bf16(v0, a, b, c);
-    bf[st][0][e] = a; bf[st][1][e] = b; bf[st][2][e] = c;
-    split3_bf16(v1, a, b, c);
-    bf[st][0][e + 1] = a; bf[st][1][e + 1] = b; bf[st][2][e + 1] = c;
-  };
-  // G column gm4 + c of tile kt: its 8 nodes as one 16-byte store per plane, buffer kt & 1
-  auto gchunk = [&](int kt, int c) {
-    const int buf = kt & 1;
-    const int64_t node = kb + int64_t(kt) * kX6KT + gnb;
-    bf16x8 p0, p1, p2;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float4 q = gv[e];
-      const float v = node + e < ke ? (c == 0 ? q.x : c == 1 ? q.y : c == 2 ? q.z : q.w) : 0.f;
-      __bf16 a, b, cc;
-      split3_bf16(v, a, b, cc);
-      p0[e] = a; p1[e] = b; p2[e] = cc;
-    }
-    const int o = (gm4 + c) * kX6LD + gnb;
-    *reinterpret_cast<bf16x8*>(&Gs[buf][0][o]) = p0;
-    *reinterpret_cast<bf16x8*>(&Gs[buf][1][o]) = p1;
-    *reinterpret_cast<bf16x8*>(&Gs[buf][2][o]) = p2;
-  };
-  auto mg = [&](int buf, int st, int mi) {
-    const int o = (32 * mi + r32) * kX6LD + 32 * h + 8 * st;
-    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&Gs[buf][0][o]);
-    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&Gs[buf][1][o]);
-    const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(&Gs[buf][2][o]);
-    acc[mi] = mfma_x6(a0, a1, a2, bf[st][0], bf[st][1], bf[st][2], acc[mi]);
-  };
-  auto tile = [&](int kt, float (&A)[32], float (&B)[32]) {
-    const int buf = kt & 1;
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      mg(buf, 0, mi);
-      xpart(A, kt, 3, 2 * mi);
-    }
-    xload(A, kt + 2);
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      mg(buf, 1, mi);
-      xpart(B, kt + 1, 0, 2 * mi);
-      if (mi & 1) gchunk(kt + 1, mi >> 1);
-    }
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      mg(buf, 2, mi);
-      xpart(B, kt + 1, 1, 2 * mi);
-      if (mi & 1) gchunk(kt + 1, 2 + (mi >> 1));
-    }
-    gload(kt + 2);
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      mg(buf, 3, mi);
-      xpart(B, kt + 1, 2, 2 * mi);
-    }
-    __syncthreads();
-  };
-  gload(0);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) gchunk(0, c);
-  xload(x0, 0);
-  xload(x1, 1);
-  gload(1);
-#pragma unroll
-  for (int st = 0; st < 3; ++st)
-#pragma unroll
-    for (int e = 0; e < 8; e += 2) xpart(x0, 0, st, e);
-  __syncthreads();
-  for (int kt = 0; kt < nk; kt += 2) {
-    tile(kt, x0, x1);
-    tile(kt + 1, x1, x0);
-  }
-  if (!cok) return;   // (the output column is the lane's own)
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) out[int64_t(32 * mi + acc_row(q, lane)) * Nc + col] = acc[mi][q];
-}
-
 // C[m][n] = sum_s part[s][m][n] (fixed order), rows [0, split) -> C0, the rest -> C1.
 __global__ __launch_bounds__(256) void k_reduce_splits(const float* __restrict__ part, int S,
                                                        int64_t Mc, int64_t Nc, float* __restrict__ C0,
@@ -1175,7 +897,7 @@ static bool bf16_mfma_for() {
 template <class TX>
 static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
                       int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
-                      hipStream_t stream, const int32_t* gate, uint16_t* wimg = nullptr) {
+                      hipStream_t stream, const int32_t* gate) {
   BGCN_CHECK_ARG(X && W0 && Y, "null pointer");
   BGCN_CHECK_ARG(M >= 0 && Nc > 0 && K > 0, "bad shape");
   BGCN_CHECK_ARG(ldx >= K && ldw >= K && ldy >= Nc, "bad leading dimension");
@@ -1190,21 +912,7 @@ static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1
       (reinterpret_cast<uintptr_t>(X) & 15) == 0 && M * ldx * 4 < (int64_t(1) << 32) - 16 &&
       64 * ldw * 4 < (int64_t(1) << 32)) {
     static const int pipe = [] { const char* e = std::getenv("BGCN_X6_PIPE"); return e ? atoi(e) : 1; }();
-    const int nk = int((K + kX6KT - 1) / kX6KT);
-    if (pipe == 2 && wimg && int64_t(nk) * 3 * 128 * 64 * 2 < (int64_t(1) << 32)) {
-      // W split once into the tile images, then the copy-staged kernel
-      const int64_t nw = int64_t(nk) * 128 * 8;
-      for (int64_t cb = 0; cb < Nc / 128; ++cb) {   // rows r0 + c: W0 below `split`, W1 above
-        const int64_t r0 = cb * 128;
-        const int64_t sp = std::max<int64_t>(0, std::min<int64_t>(128, split - r0));
-        hipLaunchKernelGGL(k_w_split_x6, dim3(grid_for(nw, 256)), dim3(256), 0, stream, W0 + r0 * ldw,
-                           W1 ? W1 + (r0 + sp - split) * ldw : nullptr, ldw, sp, K, nk,
-                           wimg + cb * int64_t(nk) * 3 * 128 * 64, gate);
-        BGCN_CHECK_LAUNCH();
-      }
-      hipLaunchKernelGGL(k_gemm_xwt_x6q, dim3(grid_for(M, 128), unsigned(Nc / 128)), dim3(256), 0, stream,
-                         reinterpret_cast<const float*>(X), ldx, wimg, Y, ldy, M, K, gate);
-    } else if (pipe)
+    if (pipe)
       hipLaunchKernelGGL(k_gemm_xwt_x6p, dim3(grid_for(M, 128), unsigned(Nc / 128)), dim3(256), 0, stream,
                          reinterpret_cast<const float*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, K, gate);
     else
@@ -1239,12 +947,12 @@ int gemm_xwt_impl(const float* X, int64_t ldx, const float* W0, const float* W1,
 
 int gemm_xwt_x(const void* X, int xdt, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
                int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
-               hipStream_t stream, const int32_t* gate, uint16_t* wimg) {
+               hipStream_t stream, const int32_t* gate) {
   if (xdt == BGCN_DTYPE_BF16)
     return gemm_xwt_t(static_cast<const bf16_t*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K,
                       stream, gate);
   return gemm_xwt_t(static_cast<const float*>(X), ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K,
-                    stream, gate, wimg);
+                    stream, gate);
 }
 
 int gemm_xw_impl(const float* X, int64_t ldx, const float* W, int64_t ldw, float* Y, int64_t ldy,
@@ -1334,21 +1042,11 @@ static int gemm_tn_t(const float* G, int64_t ldg, const TX* X, int64_t ldx, floa
   bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) && xal;
   timing_begin(timing_cls, stream);
   bool done = false;
-  static const int tn_pipe = [] { const char* e = std::getenv("BGCN_TN_PIPE"); return e ? atoi(e) : 0; }();
-  if (sizeof(TX) == 4 && tn_pipe && bf16_mfma_for<TX>() && Mc == 128 && (K + 256) * ldx * 4 < (int64_t(1) << 31) &&
-      (K + 256) * ldg * 4 < (int64_t(1) << 31)) {
-    // fp32 X: the pipelined six-product kernel, about one block per CU over the column
-    // tiles x node splits (within the workspace's split count)
-    const int64_t tiles = (Nc + 127) / 128;
-    int64_t s6 = std::max<int64_t>(1, std::min<int64_t>(S, (256 + tiles - 1) / tiles));
-    int64_t kc = (K + s6 - 1) / s6;
-    kc = (kc + kX6KT - 1) / kX6KT * kX6KT;
-    s6 = (K + kc - 1) / kc;
-    hipLaunchKernelGGL(k_gemm_tn_x6p, dim3(unsigned(tiles), 1, unsigned(s6)), dim3(256), 0, stream, G, ldg,
-                       reinterpret_cast<const float*>(X), ldx, part, Nc, K, kc, gate);
-    S = int(s6);
-    done = true;
-  } else if (sizeof(TX) == 2 && bf16_mfma_for<TX>() && vec && Nc % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+  // bf16 X: the bf16 MFMA with G split three ways.  fp32 X keeps the f32 MFMA: the
+  // six-product forms measured 385 us (k_gemm_tn_bf16<float>), 489 us (X read straight into
+  // the B fragments) and 479 us (that kernel with its splits between the MFMAs) against
+  // its 374-377 us at the bench workload
+  if (sizeof(TX) == 2 && bf16_mfma_for<TX>() && vec && Nc % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
     hipLaunchKernelGGL(k_gemm_tn_bf16<TX>, dim3(grid_for(Nc, 128), grid_for(Mc, 128), S), dim3(256), 0, stream, G,
                        ldg, X, ldx, part, Mc, Nc, K, kchunk, gate);
     done = true;

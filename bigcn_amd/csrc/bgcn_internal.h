@@ -70,12 +70,9 @@ int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float
                  size_t ws_bytes, hipStream_t stream, int timing_cls, const int32_t* gate);
 size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K);
 // the same GEMMs with the node features X as fp32 or bf16 (xdt: BGCN_DTYPE_*)
-// wimg (optional, w_img_elems(K, Nc) bf16 elements): scratch for the fp32-X kernel's W split
-// once per call (without it every block splits W itself)
 int gemm_xwt_x(const void* X, int xdt, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
                int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
-               hipStream_t stream, const int32_t* gate, uint16_t* wimg = nullptr);
-inline int64_t w_img_elems(int64_t K, int64_t Nc) { return (K + 63) / 64 * 3 * 64 * ((Nc + 127) / 128 * 128); }
+               hipStream_t stream, const int32_t* gate);
 int gemm_tn_x(const float* G, int64_t ldg, const void* X, int xdt, int64_t ldx, float* C0,
               float* C1, int64_t ldc, int64_t split, int64_t Mc, int64_t Nc, int64_t K, void* ws,
               size_t ws_bytes, hipStream_t stream, int timing_cls, const int32_t* gate);
