@@ -134,14 +134,37 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const TX* __restrict__ X, int
 //     (row stride kC2fLd: conflict-free 16-byte LDS stores); the next tile's global loads
 //     are in flight during the current tile's MFMAs.
 constexpr int kC2fBK = 32, kC2fLd = kC2fBK + 8;
-template <class TX>
+// The dense conv2's root block for fp32 X: every node of a tree reads the same root row, so
+// s * relu(x_root) is split three ways once per tree (R[b][p][c], rows zero-padded to ldr,
+// a multiple of the k-tile) and each node only masks the planes by its keep bits - the
+// split was most of the kernel's VALU work (14 VALU instructions per MFMA, r04_dense_pmc).
+__global__ __launch_bounds__(256) void k_root_split(const float* __restrict__ X, int64_t ldx, int64_t F,
+                                                    const int64_t* __restrict__ rootindex, int64_t B, float sc,
+                                                    uint16_t* __restrict__ R, int64_t ldr,
+                                                    const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
+  const int64_t b = blockIdx.y;
+  const int64_t c = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (b >= B || c >= ldr) return;
+  const int64_t root = rootindex[b];
+  const float v = (c < F && root >= 0) ? sc * fmaxf(X[root * ldx + c], 0.f) : 0.f;
+  __bf16 h, m, l;
+  split3_bf16(v, h, m, l);
+  uint16_t* r = R + b * 3 * ldr + c;
+  r[0] = __builtin_bit_cast(uint16_t, h);
+  r[ldr] = __builtin_bit_cast(uint16_t, m);
+  r[2 * ldr] = __builtin_bit_cast(uint16_t, l);
+}
+template <class TX, bool kR = false>
 __global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const TX* __restrict__ X, int64_t ldx, int64_t F,
                                                         const float* __restrict__ H1,
                                                         const int32_t* __restrict__ node_root,
                                                         const float* __restrict__ W2td,
                                                         const float* __restrict__ W2bu,
                                                         float* __restrict__ Z2, int64_t N, KeepSrc keep,
-                                                        const int32_t* __restrict__ gate) {
+                                                        const int32_t* __restrict__ gate,
+                                                        const uint16_t* __restrict__ R = nullptr, int64_t ldr = 0,
+                                                        const int64_t* __restrict__ batch = nullptr) {
   if (gate_closed(gate)) return;
   constexpr int BM = 128, PX = sizeof(TX) == 2 ? 1 : 3;   // A planes: bf16 X exact, fp32 X split
   __shared__ __attribute__((aligned(16))) __bf16 As[PX][BM * kC2fLd];
@@ -199,17 +222,27 @@ __global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const TX* __restrict__ X
   const float* wrow = W2 + int64_t(br) * ldw + H;
   constexpr int kRA = 2 * sizeof(TX) / 2;   // 16-byte X pieces per thread (16 columns)
   constexpr int kPE = 8 / (sizeof(TX) / 2); // X elements per piece
-  u32x4 ra[kRA];
+  u32x4 ra[kR ? 6 : kRA];   // kR: the tree's split planes of s relu(x_root), 3 x 2 pieces
   uint32_t rw = 0;
   float4 rb[2];
+  const uint16_t* rrow = nullptr;
+  if constexpr (kR) rrow = R + (aok ? batch[am_] : 0) * 3 * ldr;
   auto gload = [&](int64_t c0) {   // c0: first X column of the tile
     rw = aok ? keep.get(uint32_t(d), uint32_t(am_), uint32_t((H + c0) >> 5)) : 0u;
+    if constexpr (kR) {   // (R rows are zero-padded to ldr >= the last tile's end)
 #pragma unroll
-    for (int i = 0; i < kRA; ++i) {
-      const int64_t c = c0 + ak + kPE * i;
-      const bool ok = aok && c < F;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(xrow + (ok ? c : 0));
-      ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          ra[2 * p + i] = *reinterpret_cast<const u32x4*>(rrow + p * ldr + c0 + ak + 8 * i);
+    } else {
+#pragma unroll
+      for (int i = 0; i < kRA; ++i) {
+        const int64_t c = c0 + ak + kPE * i;
+        const bool ok = aok && c < F;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(xrow + (ok ? c : 0));
+        ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+      }
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -220,6 +253,23 @@ __global__ __launch_bounds__(256) void k_conv2_fwd_bf16(const TX* __restrict__ X
     }
   };
   auto sstore = [&]() {
+    if constexpr (kR) {   // keep * (the tree's planes): a 16-bit mask per element, no split
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        u32x4 m;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t bits = (rw >> (ak + 8 * i + 2 * q)) & 3u;
+          m[q] = ((bits & 1u) ? 0x0000ffffu : 0u) | ((bits & 2u) ? 0xffff0000u : 0u);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const u32x4 v = ra[2 * p + i];
+          *reinterpret_cast<u32x4*>(&As[p][ar * kC2fLd + ak + 8 * i]) =
+              u32x4{v[0] & m[0], v[1] & m[1], v[2] & m[2], v[3] & m[3]};
+        }
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < 2; ++i) {   // keep * s * relu(x): exact in bf16 for bf16 X (s is 1 or 2)
       bf16x8 v, vm, vl;
@@ -633,6 +683,7 @@ struct FusedWs {
   float* spmm_ws; size_t spmm_bytes;
   float* dw2_part;                        // [2][S2][H][H+F]
   float* tn_ws; size_t tn_bytes;
+  uint16_t* rplanes;                      // dense conv2, fp32 X: the trees' split root rows (k_root_split)
   int S2; int64_t kchunk2;
   int S2d; int64_t kchunk2d;              // the dense feature mode's dW2 node splits (more: shorter loops)
   int Sh; int64_t kchunkh;
@@ -698,6 +749,7 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   t.dw2_part = c.take<float>(dense_part > sparse_part ? dense_part : sparse_part);
   t.tn_bytes = tn_ws_size(2 * H, F, N);
   t.tn_ws = c.take<float>(t.tn_bytes / sizeof(float) + 1);
+  t.rplanes = c.take<uint16_t>(size_t(B) * 3 * size_t((F + kC2fBK - 1) / kC2fBK * kC2fBK));
   if (w) *w = t;
   return c.off;
 }
@@ -966,10 +1018,17 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
       hipLaunchKernelGGL(k_conv2_fwd_bf16<bf16_t>, dim3(grid_for(N, 128), 2), dim3(256), 0, s,
                          static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
                          a->bu_w2, w.z2, N, keep, gate);
-    else if (a->x_dtype == BGCN_DTYPE_F32 && bf16_mfma_ok(a))
-      hipLaunchKernelGGL(k_conv2_fwd_bf16<float>, dim3(grid_for(N, 128), 2), dim3(256), 0, s,
+    else if (a->x_dtype == BGCN_DTYPE_F32 && bf16_mfma_ok(a)) {
+      // the trees' root planes once, then the conv2 that only masks them
+      const int64_t ldr = (F + kC2fBK - 1) / kC2fBK * kC2fBK;
+      hipLaunchKernelGGL(k_root_split, dim3(grid_for(ldr, 256), unsigned(B)), dim3(256), 0, s,
+                         static_cast<const float*>(a->x), a->ldx, F, a->rootindex, B, keep.scale(), w.rplanes,
+                         ldr, gate);
+      BGCN_CHECK_LAUNCH();
+      hipLaunchKernelGGL((k_conv2_fwd_bf16<float, true>), dim3(grid_for(N, 128), 2), dim3(256), 0, s,
                          static_cast<const float*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
-                         a->bu_w2, w.z2, N, keep, gate);
+                         a->bu_w2, w.z2, N, keep, gate, w.rplanes, ldr, a->batch);
+    }
     else if (a->x_dtype == BGCN_DTYPE_BF16)
       hipLaunchKernelGGL(k_conv2_fwd<bf16_t>, dim3(grid_for(N, 64), 2), dim3(256), 0, s,
                          static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
