@@ -95,8 +95,8 @@ SPARSE_CAP = 32
 ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2): "bgcn::k_conv2_sparse",
                  ("auto", 3): "bgcn::k_bwd_mid<float>", ("auto", 5): "bgcn::k_bwd_tail<0, 0>",
                  ("auto", 7): "bgcn::k_prep_b<float>",
-                 ("dense", 0): "bgcn::k_gemm_xwt<true, false, float>", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
-                 ("dense", 2): "bgcn::k_conv2_fwd<float>", ("dense", 3): "bgcn::k_dw2_f32"}
+                 ("dense", 0): "bgcn::k_gemm_xwt_x6p", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
+                 ("dense", 2): "bgcn::k_conv2_fwd_bf16<float, true>", ("dense", 3): "bgcn::k_dw2_f32"}
 
 
 def pmc_file(workload: str) -> str:
