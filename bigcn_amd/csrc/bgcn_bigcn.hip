@@ -1018,7 +1018,7 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
       hipLaunchKernelGGL(k_conv2_fwd_bf16<bf16_t>, dim3(grid_for(N, 128), 2), dim3(256), 0, s,
                          static_cast<const bf16_t*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
                          a->bu_w2, w.z2, N, keep, gate);
-    else if (a->x_dtype == BGCN_DTYPE_F32 && bf16_mfma_ok(a) && N >= 32 * B) {
+    else if (a->x_dtype == BGCN_DTYPE_F32 && bf16_mfma_ok(a) && N >= kX6MinRows && N >= 32 * B) {
       // the trees' root planes once, then the conv2 that only masks them (trees of >= 32
       // nodes on average: PHEME's ~10-node trees share too little to pay the extra launch,
       // 34 -> 56 us at pheme768)
@@ -1030,7 +1030,7 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
       hipLaunchKernelGGL((k_conv2_fwd_bf16<float, true>), dim3(grid_for(N, 128), 2), dim3(256), 0, s,
                          static_cast<const float*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
                          a->bu_w2, w.z2, N, keep, gate, w.rplanes, ldr, a->batch);
-    } else if (a->x_dtype == BGCN_DTYPE_F32 && bf16_mfma_ok(a))
+    } else if (a->x_dtype == BGCN_DTYPE_F32 && bf16_mfma_ok(a) && N >= kX6MinRows)
       hipLaunchKernelGGL(k_conv2_fwd_bf16<float>, dim3(grid_for(N, 128), 2), dim3(256), 0, s,
                          static_cast<const float*>(a->x), a->ldx, F, a->h1, w.node_root, a->td_w2,
                          a->bu_w2, w.z2, N, keep, gate);

@@ -908,7 +908,7 @@ static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1
   bool vec = K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0 && xal && aligned16(W0) &&
              (!W1 || aligned16(W1));
   // fp32 X: the six-product kernel with X straight into the A fragments
-  if (sizeof(TX) == 4 && bf16_mfma_for<TX>() && vec && Nc % 128 == 0 && split % 64 == 0 &&
+  if (sizeof(TX) == 4 && bf16_mfma_for<TX>() && M >= kX6MinRows && vec && Nc % 128 == 0 && split % 64 == 0 &&
       (reinterpret_cast<uintptr_t>(X) & 15) == 0 && M * ldx * 4 < (int64_t(1) << 32) - 16 &&
       64 * ldw * 4 < (int64_t(1) << 32)) {
     static const int pipe = [] { const char* e = std::getenv("BGCN_X6_PIPE"); return e ? atoi(e) : 1; }();

@@ -70,6 +70,11 @@ int gemm_tn_impl(const float* G, int64_t ldg, const float* X, int64_t ldx, float
                  size_t ws_bytes, hipStream_t stream, int timing_cls, const int32_t* gate);
 size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K);
 // the same GEMMs with the node features X as fp32 or bf16 (xdt: BGCN_DTYPE_*)
+// fp32 X takes the six-product bf16-MFMA kernels (128-row tiles, about one block per CU)
+// only from this many rows on: at PHEME's ~1.2k nodes per batch their 10-20 blocks leave the
+// GPU idle, where the f32-MFMA kernels' 64-row tiles run twice the blocks (pheme768 conv2
+// 34 vs 56-59 us)
+constexpr int64_t kX6MinRows = 8192;
 int gemm_xwt_x(const void* X, int xdt, int64_t ldx, const float* W0, const float* W1, int64_t ldw,
                int64_t split, float* Y, int64_t ldy, int64_t M, int64_t Nc, int64_t K,
                hipStream_t stream, const int32_t* gate);
