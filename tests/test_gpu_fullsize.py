@@ -102,7 +102,7 @@ def _oracle_batch(b, drops, drop_seed):
     return ref
 
 
-@pytest.mark.parametrize("workload,mode", [("twitter15", "auto"), ("weibo_bf16", "auto"),
+@pytest.mark.parametrize("workload,mode", [("twitter15", "auto"), ("twitter15", "dense"), ("weibo_bf16", "auto"),
                                            ("weibo_bf16", "dense"), ("synth1024_bf16", "auto"),
                                            ("twitter15_tail", "auto")])
 def test_full_size_step_matches_oracle(workload, mode):
@@ -110,8 +110,9 @@ def test_full_size_step_matches_oracle(workload, mode):
     configs[2] (weibo_bf16: 128 x mean 816, bf16 X, 2-class Net, no DropEdge) and the
     per-GPU shape of configs[4] (synth1024_bf16: 128 x mean 1024, bf16 X, DropEdge), and
     twitter15 with 1 % of the rows holding 40-300 words (the spill pool): loss, log-probs
-    and all ten gradients of the bench's step against the fp64 oracle.  weibo_bf16 also
-    on the dense MFMA path (feat_mode "dense": conv1 / dW1 on the bf16 MFMA)."""
+    and all ten gradients of the bench's step against the fp64 oracle.  twitter15 and
+    weibo_bf16 also on the dense MFMA path (feat_mode "dense": fp32 X through the
+    six-product conv1 / conv2 with the trees' root planes, bf16 X through the bf16 MFMA)."""
     from bigcn_amd import FusedTrainStep
     from bigcn_amd.ops import keep_words, unpack_keep
     wl = bench.WORKLOADS[workload]
@@ -144,7 +145,7 @@ def test_full_size_step_matches_oracle(workload, mode):
     h1, h2 = h1.cpu(), h2.cpu()
     masks = {d: (h1[:, 64 * k:64 * (k + 1)] > 0, h2[:, 64 * k:64 * (k + 1)] > 0)
              for k, d in enumerate(("TDrumorGCN", "BUrumorGCN"))}
-    # weibo_bf16 runs twice (sparse, dense) on the same batch, seeds and parameters: the
+    # twitter15 / weibo_bf16 run twice (sparse, dense) on the same batch, seeds and parameters: the
     # fp64 oracle (the bulk of this test's time) is reused when the relu' decisions agree
     key = (workload, step.last_drop_seed)
     hit = _ORACLE_CACHE.get(key)

@@ -245,7 +245,7 @@ def test_spmm_deterministic():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("M,Nc,K", [(1000, 128, 5000), (77, 64, 5064), (130, 20, 37), (5, 128, 8)])
+@pytest.mark.parametrize("M,Nc,K", [(1000, 128, 5000), (8300, 128, 5000), (77, 64, 5064), (130, 20, 37), (5, 128, 8)])
 def test_gemm_xwt(M, Nc, K):
     from bigcn_amd import _lib
     from bigcn_amd._lib import check, ptr, stream_handle
