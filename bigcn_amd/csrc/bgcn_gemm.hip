@@ -921,8 +921,10 @@ static int gemm_xwt_t(const TX* X, int64_t ldx, const float* W0, const float* W1
     BGCN_CHECK_LAUNCH();
     return BGCN_OK;
   }
-  // the bf16 MFMA with W split three ways (bf16 X exact, fp32 X split too: XPlanes)
-  if (bf16_mfma_for<TX>() && vec && K % 8 == 0 && ldx % 8 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+  // bf16 X: the bf16 MFMA with W split three ways (fp32 X below kX6MinRows keeps the f32
+  // MFMA: the XPlanes form of this kernel measured 466 us against its 377 at full size)
+  if (sizeof(TX) == 2 && bf16_mfma_for<TX>() && vec && K % 8 == 0 && ldx % 8 == 0 &&
+      (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
     hipLaunchKernelGGL(k_gemm_xwt_bf16<TX>, dim3(grid_for(M, 128), grid_for(Nc, 128)), dim3(256), 0, stream,
                        X, ldx, W0, W1, ldw, split, Y, ldy, M, Nc, K, gate);
     BGCN_CHECK_LAUNCH();
