@@ -106,7 +106,7 @@ def pmc_file(workload: str) -> str:
 
 def pmc_traffic(mode: str, cls: int, workload: str = "twitter15", xbf16: bool = False):
     """HBM bytes per launch of a kernel class from the committed PMC passes
-    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, the same workload's bench), or None."""
+    (tools/prof.py traffic: FETCH_SIZE x2 + WRITE_SIZE, the same workload's bench), or None."""
     name = ROCPROF_NAMES.get((mode, cls))
     if name is None:
         return None

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Evidence for profiles/ (round 4): per workload the bench line, rocprofv3 kernel stats of
 # the same command, separate FETCH_SIZE / WRITE_SIZE PMC passes (MI355X_MICROARCH.md recipe;
-# tools/pmc_traffic.py applies the gfx950 corrections) -> pmc_traffic_<workload>.json (what
+# tools/prof.py traffic applies the gfx950 corrections) -> pmc_traffic_<workload>.json (what
 # bench.py's roofline.traffic reads from profiles/r04_pmc_traffic_<workload>.json), the
 # device-side step timelines and the 5000-wide aggregation probe with its PMC traffic.
 #   gpurun -- 'bash tools/profile_round.sh gpurun_out/prof_r04 twitter15 weibo_bf16 synth1024_bf16'
@@ -19,13 +19,13 @@ for w in $WLS; do
     python bench.py --workload $w $LIGHT --steps 5 --warmup 2 > /dev/null 2> "$OUT/fetch_$w.log"
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$w" -- \
     python bench.py --workload $w $LIGHT --steps 5 --warmup 2 > /dev/null 2> "$OUT/write_$w.log"
-  python tools/pmc_traffic.py "$OUT/fetch_$w" "$OUT/write_$w" --out "$OUT/pmc_traffic_$w.json" > "$OUT/pmc_traffic_$w.txt"
+  python tools/prof.py traffic "$OUT/fetch_$w" "$OUT/write_$w" --out "$OUT/pmc_traffic_$w.json" > "$OUT/pmc_traffic_$w.txt"
   echo "$w done"
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/timeline" -o run -- \
   python tools/trace_probe.py --mode both > "$OUT/timeline.log" 2>&1
-python tools/step_timeline.py "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 8 > "$OUT/timeline_step.txt"
-python tools/step_timeline.py "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 20 > "$OUT/timeline_chain_alone.txt"
+python tools/prof.py timeline "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 8 > "$OUT/timeline_step.txt"
+python tools/prof.py timeline "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 20 > "$OUT/timeline_chain_alone.txt"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/agg" -o run -- \
   python tools/agg_probe.py > "$OUT/agg_probe.txt" 2> "$OUT/agg.log"
 for g in td bu; do
@@ -33,7 +33,7 @@ for g in td bu; do
     python tools/agg_probe.py --graphs $g --no-streams --iters 5 > /dev/null 2>> "$OUT/agg.log"
   timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/agg_write_$g" -- \
     python tools/agg_probe.py --graphs $g --no-streams --iters 5 > /dev/null 2>> "$OUT/agg.log"
-  python tools/pmc_traffic.py "$OUT/agg_fetch_$g" "$OUT/agg_write_$g" --out "$OUT/agg_pmc_$g.json" \
+  python tools/prof.py traffic "$OUT/agg_fetch_$g" "$OUT/agg_write_$g" --out "$OUT/agg_pmc_$g.json" \
     > "$OUT/agg_pmc_$g.txt"
 done
 echo done

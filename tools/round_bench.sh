@@ -1,17 +1,22 @@
 #!/bin/bash
-# Round-end evidence beside tools/profile_round.sh: the device-side step / chain timelines,
-# the full default bench line (every comparison leg) and the light bench line of the other
-# workloads.  gpurun -- 'bash tools/round_bench.sh gpurun_out/prof_r04'
+# Round-end evidence beside tools/profile_round.sh: optionally the GPU tests, the device-side
+# step / chain timelines, the full default bench line (every comparison leg) and the light
+# bench line of the other workloads.
+#   gpurun -- 'bash tools/round_bench.sh gpurun_out/prof_r04 [tests]'
 set -eo pipefail
 OUT=${1:-gpurun_out/prof}
 mkdir -p "$OUT"
 ROOT=$(pwd)
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
+if [ "${2:-}" = tests ]; then
+  timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
+  tail -2 "$OUT/gpu_tests.log"
+fi
 LIGHT="--no-cpu-baseline --compare-dense 0 --compare-dropedge 0 --aggregation 0 --dropin 0 --host-fed 0"
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/timeline" -o run -- \
   python tools/trace_probe.py --mode both > "$OUT/timeline.log" 2>&1
-python tools/step_timeline.py "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 8 > "$OUT/timeline_step.txt"
-python tools/step_timeline.py "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 20 > "$OUT/timeline_chain_alone.txt"
+python tools/prof.py timeline "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 8 > "$OUT/timeline_step.txt"
+python tools/prof.py timeline "$OUT"/timeline/run_kernel_trace.csv --after k_alu --step 20 > "$OUT/timeline_chain_alone.txt"
 timeout -k 10 400 python bench.py > "$OUT/bench_full.json" 2> "$OUT/bench_full.log"
 echo "full bench done"
 for w in ${WORKLOADS:-weibo_bf16 synth1024_bf16 pheme768 twitter15_tail}; do

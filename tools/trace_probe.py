@@ -4,7 +4,7 @@ step's stream, so the whole step is queued before its first kernel starts; under
 rocprofv3 --kernel-trace the kernels then run exactly as the device schedules them.
 
     rocprofv3 --kernel-trace --output-format csv -d OUT -o run -- python tools/trace_probe.py
-    python tools/step_timeline.py OUT/.../run_kernel_trace.csv --after k_alu
+    python tools/prof.py timeline OUT/.../run_kernel_trace.csv --after k_alu
 
 --mode full: the normal step (next batch prepared on the side lane); --mode alone: the
 prepared batch reused, nothing on the side lane (the chain alone)."""
