@@ -435,7 +435,9 @@ __global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ 
 // The readout backward needs no hand-off inside this launch (dhead is read by later
 // launches), so item blocks never wait for each other at any batch size.
 constexpr int kRoSlices = 16;
-template <int MC>   // classes of the head held in registers (HeadRegs)
+// kSgn = (sgn != nullptr), a template argument so no run-time test sits between the row
+// loads and their use
+template <int MC, bool kSgn>   // MC: classes of the head held in registers (HeadRegs)
 __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseState S, const float* __restrict__ H1,
                                                        const float* __restrict__ H2,
                                                        const int32_t* __restrict__ tree_ptr,
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
   int item0 = 0, nit = 1;
   if (blk < S.max_items) {
     if (blk >= S.tree_item0[S.B]) {
-      if (sgn && threadIdx.x < 2 * H) cnt[int64_t(blk) * (2 * H) + threadIdx.x] = 0.f;
+      if (kSgn && threadIdx.x < 2 * H) cnt[int64_t(blk) * (2 * H) + threadIdx.x] = 0.f;
       return;
     }
     b = S.item_tree[blk];
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
     for (int u = 0; u < 8; ++u) {
       const bool ok = i + u * kRoSlices < end;
       if (ok) s = f4add(s, f4relu(v[u]));
-      if (sgn) {
+      if constexpr (kSgn) {
         // the row's sign word from four ballots over the wave's 4 row slices x 16 lanes;
         // lane 0 of each slice stores its row's word
         const int sh = 16 * (slice & 3);
@@ -504,9 +506,9 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
     }
   }
   red[d][slice][lane] = s;
-  if (sgn) redc[d][slice][lane] = pc;
+  if (kSgn) redc[d][slice][lane] = pc;
   __syncthreads();
-  if (sgn && blk < S.max_items && slice == 0) {   // the item's counts, slices in order
+  if (kSgn && blk < S.max_items && slice == 0) {   // the item's counts, slices in order
     float4 acc = redc[d][0][lane];
 #pragma unroll
     for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, redc[d][q][lane]);
@@ -1050,13 +1052,19 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
   if (sparse) {
     const HeadArgs hd = head ? *head : no_head;
     uint64_t* sgn = readout_sign(a, sp, w) ? reinterpret_cast<uint64_t*>(w.d2) : nullptr;
-    if (hd.C <= 4)
-      hipLaunchKernelGGL(k_readout_items<4>, dim3(unsigned(sp.max_items + B)), dim3(512), 0, s, sp, a->h1,
-                         a->h2, a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd, w.colpart2, sgn);
+    const dim3 g(unsigned(sp.max_items + B));
+    if (hd.C <= 4 && sgn)
+      hipLaunchKernelGGL((k_readout_items<4, true>), g, dim3(512), 0, s, sp, a->h1, a->h2, a->tree_ptr,
+                         a->rootindex, N, B, a->head_in, w.rpart, hd, w.colpart2, sgn);
+    else if (hd.C <= 4)
+      hipLaunchKernelGGL((k_readout_items<4, false>), g, dim3(512), 0, s, sp, a->h1, a->h2, a->tree_ptr,
+                         a->rootindex, N, B, a->head_in, w.rpart, hd, w.colpart2, sgn);
+    else if (sgn)
+      hipLaunchKernelGGL((k_readout_items<kMaxClasses, true>), g, dim3(512), 0, s, sp, a->h1, a->h2,
+                         a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd, w.colpart2, sgn);
     else
-      hipLaunchKernelGGL(k_readout_items<kMaxClasses>, dim3(unsigned(sp.max_items + B)), dim3(512), 0, s, sp,
-                         a->h1, a->h2, a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd, w.colpart2,
-                         sgn);
+      hipLaunchKernelGGL((k_readout_items<kMaxClasses, false>), g, dim3(512), 0, s, sp, a->h1, a->h2,
+                         a->tree_ptr, a->rootindex, N, B, a->head_in, w.rpart, hd, w.colpart2, sgn);
   }
   else
     hipLaunchKernelGGL(k_readout_fwd, dim3(unsigned(B)), dim3(1024), 0, s, a->h1, a->h2,

@@ -146,124 +146,137 @@ __device__ __forceinline__ float4 tree_scale(const SpmmSign& sg, int64_t b, int 
 #ifndef BGCN_SIGN_XT
 #define BGCN_SIGN_XT 1   // A/B only: 0 drops the cross-tree check (wrong for edges across trees)
 #endif
-template <bool kSign>
-__global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BGCN_ROWS_WPE))) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
-  BT_BEGIN
+// kXt (kSign with an edge across trees: the graph build's BGCN_STATUS_CROSS_TREE, never set
+// by PyG collation): every gathered row is scaled by its own tree, the output row not.  The
+// kernel branches on the status word once per block into separate instantiations: a
+// run-time test inside the gather loop made the compiler wait for each gather before the
+// next (the sign-word aggregation ran 1.3-1.8x the plain one's time)
+template <bool kSign, bool kXt>
+__device__ __forceinline__ void rows_chunk(const SpmmBatch& sb, const SpmmProb& P, int64_t g, int hoff,
+                                           const uint64_t* __restrict__ sgn) {
   constexpr int LANES = 16;
-  const SpmmProb& P = sb.p[blockIdx.y];
-  const int lane = threadIdx.x % LANES, grp = threadIdx.x / LANES;
+  const int lane = threadIdx.x % LANES;
   const int fo = lane * 4;
   const int base_lane = ((threadIdx.x & 63) / LANES) * LANES;
-  const int hoff = blockIdx.y == 0 ? kHeadIn / 2 : 0;   // kSign: TD's r1 block sits after BU's
-  const uint64_t* sgn = sb.sg.sgn + blockIdx.y;      // kSign: this problem's word of row j
-  __shared__ float4 red[kRowsGroups][LANES];
-  if (int64_t(blockIdx.x) < nchunk) {
-    // XCD-contiguous chunk ranges: a tree's rows and the neighbours they gather stay in one
-    // L2 (the launch pads gridDim.x to a multiple of 8)
-    const int64_t g = int64_t(xcd_contig(int(blockIdx.x), int(nchunk))) * kRowsGroups + grp;
-    if (g >= (P.capacity + kPlanGrid - 1) / kPlanGrid) return;
-    const int2 bd = P.plan.bnd[g];
-    const int n = bd.y - bd.x;                       // <= 2 * LANES - 1; <= 0: no rows
-    if (n <= 0) return;
-    const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
-    // entries bd.x + lane and bd.x + 16 + lane (clamped, unconditional; masked by n)
-    const int64_t e0 = min<int64_t>(bd.x + lane, P.capacity - 1);
-    const int64_t e1 = min<int64_t>(bd.x + LANES + lane, P.capacity - 1);
-    const int32_t r0 = P.row[e0], c0 = P.col[e0], r1 = P.row[e1], c1 = P.col[e1];
-    const float w0 = P.w[e0], w1 = P.w[e1];
-    // kSign: the trees of the chunk's first and last rows and their scales
-    int64_t bA = 0, bZ = 0;
-    float4 gA = f4zero(), gZ = f4zero();
-    // kSign with an edge across trees (the graph build's BGCN_STATUS_CROSS_TREE, never set
-    // by PyG collation): every gathered row is scaled by its own tree, the output row not
-    const bool xt = kSign && BGCN_SIGN_XT && (*sb.sg.tree_status[blockIdx.y] & BGCN_STATUS_CROSS_TREE) != 0;
-    // kSign: the tree of each entry's row, loaded with the entries (a row's tree is then at
-    // hand when the row finishes - no dependent load per row)
-    int64_t bb0 = 0, bb1 = 0;
-    if constexpr (kSign) {
-      bb0 = sb.sg.batch[max(r0, 0)];
-      bb1 = sb.sg.batch[max(r1, 0)];
-      bA = __shfl(bb0, base_lane, 64);
-      bZ = __shfl(n > LANES ? bb1 : bb0, base_lane + ((n - 1) & (LANES - 1)), 64);
-      gA = tree_scale(sb.sg, bA, hoff, fo);
-      gZ = tree_scale(sb.sg, bZ, hoff, fo);
+  const int2 bd = P.plan.bnd[g];
+  const int n = bd.y - bd.x;                       // <= 2 * LANES - 1; <= 0: no rows
+  if (n <= 0) return;
+  const float4 bv = P.bias ? ld4(P.bias + fo) : f4zero();
+  // entries bd.x + lane and bd.x + 16 + lane (clamped, unconditional; masked by n)
+  const int64_t e0 = min<int64_t>(bd.x + lane, P.capacity - 1);
+  const int64_t e1 = min<int64_t>(bd.x + LANES + lane, P.capacity - 1);
+  const int32_t r0 = P.row[e0], c0 = P.col[e0], r1 = P.row[e1], c1 = P.col[e1];
+  const float w0 = P.w[e0], w1 = P.w[e1];
+  // kSign: the trees of the chunk's first and last rows and their scales
+  int32_t bA = 0, bZ = 0;   // tree ids (< B)
+  float4 gA = f4zero(), gZ = f4zero();
+  // kSign: the tree of each entry's row, loaded with the entries (a row's tree is then at
+  // hand when the row finishes - no dependent load per row)
+  int32_t bb0 = 0, bb1 = 0;
+  if constexpr (kSign && !kXt) {
+    bb0 = int32_t(sb.sg.batch[max(r0, 0)]);
+    bb1 = int32_t(sb.sg.batch[max(r1, 0)]);
+    bA = __shfl(bb0, base_lane, 64);
+    bZ = __shfl(n > LANES ? bb1 : bb0, base_lane + ((n - 1) & (LANES - 1)), 64);
+    gA = tree_scale(sb.sg, bA, hoff, fo);
+    gZ = tree_scale(sb.sg, bZ, hoff, fo);
+  }
+  auto finish = [&](int32_t r, float4 acc, int32_t b) {
+    if constexpr (kSign && kXt) {
+      st4_chain(P.out, int64_t(r) * P.ld_out + fo, acc);
+    } else if constexpr (kSign) {
+      const float4 gs = b == bA ? gA : (b == bZ ? gZ : tree_scale(sb.sg, b, hoff, fo));
+      st4_chain(P.out, int64_t(r) * P.ld_out + fo,
+          make_float4(acc.x * gs.x, acc.y * gs.y, acc.z * gs.z, acc.w * gs.w));
+    } else {
+      st4_chain(P.out, int64_t(r) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
     }
-    auto finish = [&](int32_t r, float4 acc, int64_t b) {
-      if constexpr (kSign) {
-        if (xt) {
-          st4_chain(P.out, int64_t(r) * P.ld_out + fo, acc);
-          return;
-        }
-        const float4 gs = b == bA ? gA : (b == bZ ? gZ : tree_scale(sb.sg, b, hoff, fo));
-        st4_chain(P.out, int64_t(r) * P.ld_out + fo,
-            make_float4(acc.x * gs.x, acc.y * gs.y, acc.z * gs.z, acc.w * gs.w));
-      } else {
-        st4_chain(P.out, int64_t(r) * P.ld_out + fo, epilogue(acc, bv, sb.epi));
+  };
+  float4 acc = f4zero();
+  int32_t cur = -1;
+  int32_t curb = 0;
+  if constexpr (kXt) {   // rare (no PyG batch has it): one entry at a time, few registers
+    for (int k = 0; k < n; ++k) {
+      const int src = base_lane + (k & (LANES - 1));
+      const bool hi = k >= LANES;
+      const int32_t r = __shfl(hi ? r1 : r0, src, 64);
+      const int32_t ck = __shfl(hi ? c1 : c0, src, 64);
+      const float w = __shfl(hi ? w1 : w0, src, 64);
+      const float4 v = f4mul(sign_bits(sgn[int64_t(ck) * 2], lane), tree_scale(sb.sg, sb.sg.batch[ck], hoff, fo));
+      if (r != cur) {
+        if (cur >= 0) finish(cur, acc, 0);
+        cur = r;
+        acc = f4zero();
       }
-    };
-    float4 acc = f4zero();
-    int32_t cur = -1;
-    int64_t curb = 0;
-    for (int k0 = 0; k0 < n; k0 += 8) {
-      float4 v[8];
-      int32_t rr[8];
-      int64_t bk[8];
-      float ww[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u;                        // < 32
-        const int src = base_lane + (k & (LANES - 1));
-        const bool hi = k >= LANES;                  // uniform
-        const int32_t rk = __shfl(hi ? r1 : r0, src, 64);
-        const int32_t ck = __shfl(hi ? c1 : c0, src, 64);
-        ww[u] = __shfl(hi ? w1 : w0, src, 64);
-        if constexpr (kSign) bk[u] = __shfl(hi ? bb1 : bb0, src, 64);
-        else bk[u] = 0;
-        rr[u] = k < n ? rk : -1;
-        if constexpr (kSign) {
-          v[u] = sign_bits(sgn[int64_t(ck) * 2], lane);    // unconditional (ck is a real row)
-          if (xt) v[u] = f4mul(v[u], tree_scale(sb.sg, sb.sg.batch[ck], hoff, fo));
-        } else
-          v[u] = ld4(P.in + int64_t(ck) * P.ld_in + fo);   // unconditional (ck is a real row)
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int32_t r = rr[u];
-        if (r < 0) break;
-        if (r != cur) {
-          if (cur >= 0) finish(cur, acc, curb);
-          cur = r;
-          curb = bk[u];
-          acc = f4zero();
-        }
-        acc = f4fma(ww[u], v[u], acc);
-      }
+      acc = f4fma(w, v, acc);
     }
-    if (cur >= 0) finish(cur, acc, curb);
-    BT_END(3);
+    if (cur >= 0) finish(cur, acc, 0);
     return;
   }
-  // long rows: one block per row
+  for (int k0 = 0; k0 < n; k0 += 8) {
+    float4 v[8];
+    int32_t rr[8];
+    int32_t bk[8];
+    float ww[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u;                        // < 32
+      const int src = base_lane + (k & (LANES - 1));
+      const bool hi = k >= LANES;                  // uniform
+      const int32_t rk = __shfl(hi ? r1 : r0, src, 64);
+      const int32_t ck = __shfl(hi ? c1 : c0, src, 64);
+      ww[u] = __shfl(hi ? w1 : w0, src, 64);
+      if constexpr (kSign && !kXt) bk[u] = __shfl(hi ? bb1 : bb0, src, 64);
+      else bk[u] = 0;
+      rr[u] = k < n ? rk : -1;
+      if constexpr (kSign)
+        v[u] = sign_bits(sgn[int64_t(ck) * 2], lane);    // unconditional (ck is a real row)
+      else
+        v[u] = ld4(P.in + int64_t(ck) * P.ld_in + fo);   // unconditional (ck is a real row)
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int32_t r = rr[u];
+      if (r < 0) break;
+      if (r != cur) {
+        if (cur >= 0) finish(cur, acc, curb);
+        cur = r;
+        curb = bk[u];
+        acc = f4zero();
+      }
+      acc = f4fma(ww[u], v[u], acc);
+    }
+  }
+  if (cur >= 0) finish(cur, acc, curb);
+}
+
+// long rows: one block per row (the 32 groups of 16 lanes sum entries q, q + 32, ... and
+// combine their partials in LDS in group order)
+template <bool kSign, bool kXt>
+__device__ __forceinline__ void rows_long(const SpmmBatch& sb, const SpmmProb& P, int64_t nchunk, int nlongblk,
+                                          int hoff, const uint64_t* __restrict__ sgn,
+                                          float4 (*red)[16]) {
+  constexpr int LANES = 16;
+  const int lane = threadIdx.x % LANES, grp = threadIdx.x / LANES;
+  const int fo = lane * 4;
   const int nl = *P.plan.nlong;
   for (int j = int(blockIdx.x - nchunk); j < nl; j += nlongblk) {
     const int32_t r = P.plan.longs[j];
     const int64_t rs = P.ptr[r], re = P.ptr[r + 1];
     float4 gs = f4zero();
-    const bool xt = kSign && BGCN_SIGN_XT && (*sb.sg.tree_status[blockIdx.y] & BGCN_STATUS_CROSS_TREE) != 0;
-    if constexpr (kSign) gs = xt ? make_float4(1.f, 1.f, 1.f, 1.f) : tree_scale(sb.sg, sb.sg.batch[r], hoff, fo);
+    if constexpr (kSign) gs = kXt ? make_float4(1.f, 1.f, 1.f, 1.f) : tree_scale(sb.sg, sb.sg.batch[r], hoff, fo);
     float4 acc = f4zero();
     int64_t e = rs + grp;
-    for (; e + 7 * kRowsGroups < re; e += 8 * kRowsGroups) {
+    for (; !kXt && e + 7 * kRowsGroups < re; e += 8 * kRowsGroups) {
       float4 v[8];
       float ww[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int64_t eu = e + u * kRowsGroups;
         ww[u] = P.w[eu];
-        if constexpr (kSign) {
+        if constexpr (kSign)
           v[u] = sign_bits(sgn[int64_t(P.col[eu]) * 2], lane);
-          if (xt) v[u] = f4mul(v[u], tree_scale(sb.sg, sb.sg.batch[P.col[eu]], hoff, fo));
-        } else
+        else
           v[u] = ld4(P.in + int64_t(P.col[eu]) * P.ld_in + fo);
       }
 #pragma unroll
@@ -272,7 +285,7 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
     for (; e < re; e += kRowsGroups) {
       if constexpr (kSign) {
         float4 v = sign_bits(sgn[int64_t(P.col[e]) * 2], lane);
-        if (xt) v = f4mul(v, tree_scale(sb.sg, sb.sg.batch[P.col[e]], hoff, fo));
+        if constexpr (kXt) v = f4mul(v, tree_scale(sb.sg, sb.sg.batch[P.col[e]], hoff, fo));
         acc = f4fma(P.w[e], v, acc);
       } else
         acc = f4fma(P.w[e], ld4(P.in + int64_t(P.col[e]) * P.ld_in + fo), acc);
@@ -292,7 +305,29 @@ __global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BG
     }
     __syncthreads();
   }
-  if (nl > int(blockIdx.x - nchunk)) BT_END(4);
+}
+
+template <bool kSign>
+__global__ __launch_bounds__(kRowsThreads) __attribute__((amdgpu_waves_per_eu(BGCN_ROWS_WPE))) void k_spmm_rows(SpmmBatch sb, int64_t nchunk, int nlongblk) {
+  BT_BEGIN
+  const SpmmProb& P = sb.p[blockIdx.y];
+  const int hoff = blockIdx.y == 0 ? kHeadIn / 2 : 0;   // kSign: TD's r1 block sits after BU's
+  const uint64_t* sgn = sb.sg.sgn + blockIdx.y;      // kSign: this problem's word of row j
+  __shared__ float4 red[kRowsGroups][16];
+  const bool xt = kSign && BGCN_SIGN_XT && (*sb.sg.tree_status[blockIdx.y] & BGCN_STATUS_CROSS_TREE) != 0;
+  if (int64_t(blockIdx.x) < nchunk) {
+    // XCD-contiguous chunk ranges: a tree's rows and the neighbours they gather stay in one
+    // L2 (the launch pads gridDim.x to a multiple of 8)
+    const int64_t g = int64_t(xcd_contig(int(blockIdx.x), int(nchunk))) * kRowsGroups + threadIdx.x / 16;
+    if (g >= (P.capacity + kPlanGrid - 1) / kPlanGrid) return;
+    if (xt) rows_chunk<kSign, true>(sb, P, g, hoff, sgn);
+    else rows_chunk<kSign, false>(sb, P, g, hoff, sgn);
+    BT_END(3);
+    return;
+  }
+  if (xt) rows_long<kSign, true>(sb, P, nchunk, nlongblk, hoff, sgn, red);
+  else rows_long<kSign, false>(sb, P, nchunk, nlongblk, hoff, sgn, red);
+  if (*P.plan.nlong > int(blockIdx.x - nchunk)) BT_END(4);
 }
 
 // Fixup, F <= 128: one block per SG = 256/LANES chunk boundaries, sub-group s checking
