@@ -72,3 +72,20 @@ def test_committed_traffic_files(path):
     k = d["kernels"]
     name = next(n for n in k if n.startswith("bgcn::k_prep_b"))
     assert k[name]["read_bytes"] > 1e8 and k[name]["dispatches"] >= 1
+
+
+def test_ab_variant_env(monkeypatch):
+    """tools/ab.py's variant parsing: base drops BGCN_LIB, a .so path sets it, NAME=VALUE
+    pairs set the overrides."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import ab
+    finally:
+        sys.path.pop(0)
+    monkeypatch.setenv("BGCN_LIB", "/elsewhere/libbgcn.so")
+    assert "BGCN_LIB" not in ab.variant_env("base")
+    assert ab.variant_env("build/variants/libbgcn_x.so")["BGCN_LIB"].endswith("build/variants/libbgcn_x.so")
+    e = ab.variant_env("BGCN_PREP_LANES=1,BGCN_X6_PIPE=0")
+    assert e["BGCN_PREP_LANES"] == "1" and e["BGCN_X6_PIPE"] == "0" and "BGCN_LIB" not in e
+    with pytest.raises(SystemExit):
+        ab.variant_env("nonsense")
