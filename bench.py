@@ -22,6 +22,55 @@ import platform
 import sys
 import time
 
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, dry_run: bool = False) -> int:
+    """`python bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment):
+    start N fresh child processes of this script, one per GPU, with the torchrun
+    environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), relay
+    rank 0's JSON line, and return non-zero if any child failed.  The parent makes no GPU
+    call and imports nothing of bigcn_amd before (or after) spawning: only the children
+    touch the device."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE, text=True))
+    outs, codes = [], []
+    for p in procs:
+        out, _ = p.communicate()
+        outs.append(out or "")
+        codes.append(p.returncode)
+    # rank 0 prints the bench line; a dry run prints one environment line per rank
+    for r, out in enumerate(outs):
+        if r == 0 or dry_run:
+            sys.stdout.write(out)
+    sys.stdout.flush()
+    bad = [(r, c) for r, c in enumerate(codes) if c != 0]
+    for r, c in bad:
+        print(f"rank {r} exited with status {c}", file=sys.stderr, flush=True)
+    return next((c for _, c in bad if c > 0), 1) if bad else 0
+
+
+if __name__ == "__main__":
+    # `--gpus N` without torchrun: this process only launches the N ranks - decided before
+    # torch (or anything that could touch the GPU) is imported
+    _pre = argparse.ArgumentParser(add_help=False)
+    _pre.add_argument("--gpus", type=int, default=1)
+    _pre.add_argument("--launch-dry-run", action="store_true")
+    _a, _ = _pre.parse_known_args()
+    if _a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(_a.gpus, sys.argv[1:], _a.launch_dry_run))
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -180,12 +229,12 @@ def cpu_threads() -> int:
     return max(1, min(n, cap if cap > 0 else n))
 
 
-def cpu_baseline(wl, trees: int, steps: int, warmup: int = 1, repeats: int = 3):
+def cpu_baseline(wl, trees: int, steps: int, warmup: int = 3, repeats: int = 3):
     """The oracle (op-for-op plain-PyTorch restatement of the reference step) on the
     host cores: Python root loops, materialised [N, 5064] concat, aten dropout, autograd,
-    Adam with 3 groups.  BASELINE.md protocol: B = 128 trees, the median of `repeats`
-    timed repeats; the warm-up and the steps per repeat are cut to fit the bench's time
-    budget (the line states both)."""
+    Adam with 3 groups.  BASELINE.md protocol (3 warm-up, >= 10 timed steps, the median of
+    `repeats` repeats) on a bounded sample: batches of `trees` trees of the workload's
+    distribution (32 by default, ~1 s per step; the line states it)."""
     from bigcn_amd.data import synth_batch, synth_tree_sizes
     from oracle import bigcn_oracle as O
     cores = cpu_threads()
@@ -220,9 +269,10 @@ def cpu_baseline(wl, trees: int, steps: int, warmup: int = 1, repeats: int = 3):
             "sample": f"median of {repeats} repeats x {steps} timed steps (+{warmup} warm-up) of one "
                       f"{trees}-tree batch ({int(sizes.sum())} nodes), the workload's tree/feature "
                       f"distribution, fp32; oracle/bigcn_oracle.py train_step, torch {torch.__version__} "
-                      f"on {cpu}, {cores} threads; baseline only.  Deviation from BASELINE.md's "
-                      f"protocol (3 warm-up, >= 10 timed steps per repeat): cut to keep the default "
-                      f"bench run within minutes"}
+                      f"on {cpu}, {cores} threads; baseline only.  BASELINE.md's protocol (3 warm-up, "
+                      f">= 10 timed steps, median of 3 repeats) on batches of {trees} trees instead of 128 "
+                      f"(the per-tree cost is linear in the nodes: dropout over [N, 5064] dominates), so the "
+                      f"default bench run stays within minutes"}
 
 
 def step_roofline(N_avg: float, wl, sec_per_step: float):
@@ -406,13 +456,16 @@ def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="test hook: each rank prints its launcher environment and exits before any device work")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="twitter15", choices=sorted(WORKLOADS))
     ap.add_argument("--pool", type=int, default=4)
-    ap.add_argument("--cpu-trees", type=int, default=128)
-    ap.add_argument("--cpu-steps", type=int, default=2, help="CPU baseline: timed steps per repeat")
-    ap.add_argument("--cpu-warmup", type=int, default=1)
+    ap.add_argument("--cpu-trees", type=int, default=32,
+                    help="CPU baseline: trees per step (a bounded sample of the workload, ~1 s per step)")
+    ap.add_argument("--cpu-steps", type=int, default=10, help="CPU baseline: timed steps per repeat")
+    ap.add_argument("--cpu-warmup", type=int, default=3)
     ap.add_argument("--cpu-repeats", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -443,10 +496,20 @@ def main():
     ap.add_argument("--host-fed-workers", type=int, default=5,
                     help="DataLoader worker processes of the host-fed run (the reference's num_workers=5)")
     ap.add_argument("--host-fed-trees", type=int, default=2048, help="trees in the host-fed run's store")
+    ap.add_argument("--eval-path", type=int, default=1,
+                    help="at N=1 also time the fused evaluation step (the reference's test loop body)")
     ap.add_argument("--dropin", type=int, default=1,
                     help="at N=1 also time the drop-in path (model(data), loss.backward(), the "
                          "optimiser: --path autograd) and report it beside the main line")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun around us (bench imported and main() called): launch the N ranks
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_dry_run))
+    if args.launch_dry_run:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                          "MASTER_PORT", "BGCN_DIST_BACKEND")}), flush=True)
+        return
 
     from bigcn_amd import BiGCN, FusedTrainStep, Net
     from bigcn_amd import ops
@@ -640,6 +703,33 @@ def main():
         ctx["path"] = "autograd"
         dropin_res = run(args.feat_mode, max(5, args.steps // 2), 3)
         ctx["pool"], ctx["path"] = pool, args.path
+    eval_res = None
+    if world == 1 and args.path == "fused" and args.eval_path:
+        # the reference's per-epoch test loop (BiGCN_Twitter.py:207-222) in the fused form:
+        # eval-mode forward + head + NLL mean + argmax / correct count per batch, the next
+        # batch prepared on the side lane, no host sync inside the timed loop
+        n_eval = max(5, args.steps // 2)
+        model.eval()
+        with torch.cuda.stream(stream):
+            for i in range(3):
+                fused.evaluate(pool[i % len(pool)], next_data=pool[(i + 1) % len(pool)])
+            fused.discard_prefetch()
+            torch.cuda.synchronize()
+            fused.run_report(reset=True)
+            t0 = time.perf_counter()
+            for i in range(n_eval):
+                ev_loss, ev_correct = fused.evaluate(pool[i % len(pool)],
+                                                     next_data=pool[(i + 1) % len(pool)] if i + 1 < n_eval else None)
+            torch.cuda.synchronize()
+            dt_eval = time.perf_counter() - t0
+        rep = fused.run_report(reset=True)
+        model.train()
+        eval_res = {"value": round(wl["trees"] * n_eval / dt_eval, 2), "unit": "trees/s",
+                    "ms_per_step": round(dt_eval / n_eval * 1e3, 4), "steps": n_eval, "status": rep["status"],
+                    "last_loss": round(float(ev_loss), 5), "last_correct": int(ev_correct),
+                    "what": "FusedTrainStep.evaluate: the test loop body (BiGCN_Twitter.py:207-222: model.eval(), "
+                            "model(data), nll_loss, argmax, correct count) per pool batch, the next batch "
+                            "prepared beside it; no DropEdge, no dropout"}
     agg = None
     if world == 1 and args.aggregation:
         agg = aggregation_bench(pool[0])
@@ -688,6 +778,8 @@ def main():
             out["dropedge_" + drop_res["where"]] = {
                 "value": round(drop_res["value"], 2), "unit": "trees/s",
                 "ms_per_step": round(drop_res["dt"] / max(3, args.steps // 2) * 1e3, 4)}
+        if eval_res is not None:
+            out["eval_path"] = eval_res
         if dropin_res is not None:
             n = max(5, args.steps // 2)
             out["dropin_path"] = {

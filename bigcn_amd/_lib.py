@@ -32,7 +32,7 @@ BGCN_SPARSE_CAP = 32
 BGCN_SPARSE_SPILL_PER_ROW = 32   # spill pool capacity per row (rows over the ELL cap)
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1
-ABI_VERSION = 7   # BGCN_ABI_VERSION of include/bgcn.h
+ABI_VERSION = 8   # BGCN_ABI_VERSION of include/bgcn.h
 BGCN_STATUS_CROSS_TREE = 16
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
@@ -51,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_keep_words", "bgcn_set_kernel_timing", "bgcn_kernel_timing", "bgcn_kernel_span", "bgcn_adam_step",
     "bgcn_prepare_workspace_size", "bgcn_prepare_batch", "bgcn_csr_to_dense",
     "bgcn_train_step_workspace_size", "bgcn_train_step", "bgcn_train_step_dw1", "bgcn_join_side",
-    "bgcn_weight_images_size", "bgcn_train_step_saved",
+    "bgcn_weight_images_size", "bgcn_train_step_saved", "bgcn_eval_step",
 )
 
 
@@ -183,6 +183,7 @@ _SIGS = {
     "bgcn_train_step_workspace_size": (c_size_t, [c_int64, c_int64, c_int64, c_int64, c_int64, c_int64]),
     "bgcn_train_step": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_train_step_dw1": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "bgcn_eval_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "bgcn_join_side": (c_int, [c_void_p]),
     "bgcn_train_step_saved": (c_int, [c_void_p, c_size_t, c_int64, c_int64, c_int64, c_int64,
                                       POINTER(c_void_p), POINTER(c_void_p)]),

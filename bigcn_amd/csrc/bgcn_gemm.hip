@@ -594,11 +594,12 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_x6(const float* __restrict__ X
   const int64_t n0 = int64_t(blockIdx.y) * 128;
   const int64_t row = int64_t(blockIdx.x) * 128 + wave * 32 + r32;
   const bool rok = row < M;
-  // range-checked buffer loads (rows past M read zeros; one 32-bit offset register per
-  // operand, the tile offset in an SGPR, the piece in the immediate): the host checks that
-  // M * ldx * 4 and the W rows fit 32-bit offsets
+  // range-checked buffer loads: the tile offset rides in the VGPR offset with the row (the
+  // hardware range check covers voffset + the immediate, not the SGPR offset), so the ring's
+  // prefetches past the last k-tile of the last row / W row read zeros; the piece is in the
+  // immediate.  The host checks that M * ldx * 4 and the W rows fit 32-bit offsets
   const __amdgpu_buffer_rsrc_t xr = row_rsrc(X, uint32_t(M * ldx * 4));
-  const uint32_t xo = rok ? uint32_t((row * ldx + 4 * h) * 4) : 0xfffffff0u;
+  const uint32_t xo = rok ? uint32_t((row * ldx + 4 * h) * 4) : 0u;   // (rows past M: row 0, discarded)
   const int wcol = tid & 127, wkh = (tid >> 7) * 32;           // W staging: column, k-half
   const int64_t wn0 = n0 + (wcol & ~63);                        // the wave's 64 columns: one of W0 / W1
   const __amdgpu_buffer_rsrc_t wrs = row_rsrc(wn0 < split ? W0 + wn0 * ldw : W1 + (wn0 - split) * ldw,
@@ -618,11 +619,11 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_x6(const float* __restrict__ X
   // instruction touches a load's registers before its phase)
   auto xload = [&](float4 (&d)[8], int kt) {   // piece i: k = 8i + 4h .. + 3 of the tile
 #pragma unroll
-    for (int i = 0; i < 8; ++i) d[i] = ld(xr, xo + 32 * i, kt * kX6KT * 4);
+    for (int i = 0; i < 8; ++i) d[i] = ld(xr, xo + uint32_t(kt * kX6KT * 4) + 32 * i, 0);
   };
   auto wload = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) wr[i] = ld(wrs, wo + 16 * i, kt * kX6KT * 4);
+    for (int i = 0; i < 8; ++i) wr[i] = ld(wrs, wo + uint32_t(kt * kX6KT * 4) + 16 * i, 0);
   };
   // LDS position of tile k inside its 16-group: 8 ((k >> 2) & 1) + 4 (k >> 3) + (k & 3), so
   // that lane h's b128 at 16 s + 8 h holds k = 16 s + 4 h + (0..3) and 16 s + 8 + 4 h + (0..3),
@@ -732,7 +733,7 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_x6p(const float* __restrict__ 
   const int64_t row = int64_t(blockIdx.x) * 128 + wave * 32 + r32;
   const bool rok = row < M;
   const __amdgpu_buffer_rsrc_t xr = row_rsrc(X, uint32_t(M * ldx * 4));
-  const uint32_t xo = rok ? uint32_t((row * ldx + 4 * h) * 4) : 0xfffffff0u;
+  const uint32_t xo = rok ? uint32_t((row * ldx + 4 * h) * 4) : 0u;   // (rows past M: row 0, discarded)
   const int wcol = tid & 127, wkh = (tid >> 7) * 32;
   const int64_t wn0 = n0 + (wcol & ~63);
   const __amdgpu_buffer_rsrc_t wrs = row_rsrc(wn0 < split ? W0 + wn0 * ldw : W1 + (wn0 - split) * ldw,
@@ -750,11 +751,11 @@ __global__ __launch_bounds__(256) void k_gemm_xwt_x6p(const float* __restrict__ 
   };
   auto xload = [&](float4 (&d)[8], int kt) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) d[i] = ld(xr, xo + 32 * i, kt * kX6KT * 4);
+    for (int i = 0; i < 8; ++i) d[i] = ld(xr, xo + uint32_t(kt * kX6KT * 4) + 32 * i, 0);
   };
   auto wload = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) wr[i] = ld(wrs, wo + 16 * i, kt * kX6KT * 4);
+    for (int i = 0; i < 8; ++i) wr[i] = ld(wrs, wo + uint32_t(kt * kX6KT * 4) + 16 * i, 0);
   };
   // two elements (e, e + 1) of X piece st of tile kt into fragment slot st
   auto xpart = [&](const float4 (&d)[8], int kt, int st, int e) {

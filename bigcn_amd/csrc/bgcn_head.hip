@@ -98,7 +98,63 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ head
 
 bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// The evaluation loop's per-batch reductions (BiGCN_Twitter.py:218-222: val_loss =
+// F.nll_loss(val_out, y); _, val_pred = val_out.max(dim=1); correct = val_pred.eq(y).sum())
+// on the device, one 256-thread block: the mean NLL over the head's per-tree terms summed in
+// the order the training step's loss uses (head_grad_block: strided thread sums, then a
+// halving tree), the argmax per tree (the first maximal class, as torch's max), the count of
+// correct predictions, and the step's status folded into status_seen.
+__global__ __launch_bounds__(256) void k_eval_finish(const float* __restrict__ loss_row,
+                                                     const float* __restrict__ logp,
+                                                     const int64_t* __restrict__ y, int64_t B, int C,
+                                                     float* __restrict__ loss, int32_t* __restrict__ correct,
+                                                     int64_t* __restrict__ pred, const int32_t* status,
+                                                     int32_t* status_seen) {
+  __shared__ float ls[256];
+  __shared__ int32_t cs[256];
+  const int t = threadIdx.x;
+  float a = 0.f;
+  int32_t n = 0;
+  for (int64_t b = t; b < B; b += 256) {
+    a += loss_row[b];
+    int best = 0;
+    float bv = logp[b * C];
+    for (int c = 1; c < C; ++c) {
+      const float v = logp[b * C + c];
+      if (v > bv) { bv = v; best = c; }
+    }
+    if (pred) pred[b] = best;
+    n += (y[b] == int64_t(best)) ? 1 : 0;
+  }
+  ls[t] = a;
+  cs[t] = n;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      ls[t] += ls[t + o];
+      cs[t] += cs[t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    *loss = ls[0] / float(B);
+    if (correct) *correct = cs[0];
+    const int32_t st = status ? *status & 15 : 0;
+    if (status_seen && st) atomicOr(status_seen, st);
+  }
+}
+
 }  // namespace
+
+int eval_finish_impl(const float* loss_row, const float* logp, const int64_t* y, int64_t B, int32_t C, float* loss,
+                     int32_t* correct, int64_t* pred, const int32_t* status, int32_t* status_seen, hipStream_t s) {
+  BGCN_CHECK_ARG(B > 0 && C > 0 && C <= kMaxClasses, "need B > 0 and 0 < C <= 16");
+  BGCN_CHECK_ARG(loss_row && logp && y && loss, "null pointer");
+  hipLaunchKernelGGL(k_eval_finish, dim3(1), dim3(256), 0, s, loss_row, logp, y, B, C, loss, correct, pred, status,
+                     status_seen);
+  BGCN_CHECK_LAUNCH();
+  return BGCN_OK;
+}
 
 int head_fwd_impl(const float* head, const float* W, const float* bias, int64_t B, int32_t C, float* logp,
                   hipStream_t s) {

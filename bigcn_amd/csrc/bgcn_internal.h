@@ -393,5 +393,8 @@ int drop_edges_impl(const int64_t* td, int64_t Etd, int64_t* td_out, int64_t ld_
 // ---- one training step (bgcn_step.hip)
 size_t train_step_ws_size(int64_t N, int64_t B, int64_t F, int64_t C, int64_t Etd, int64_t Ebu);
 int train_step_impl(const bgcn_step_args* a, void* ws, size_t ws_bytes, hipStream_t s);
+// the evaluation loop's reductions after the head (bgcn_head.hip, k_eval_finish)
+int eval_finish_impl(const float* loss_row, const float* logp, const int64_t* y, int64_t B, int32_t C, float* loss,
+                     int32_t* correct, int64_t* pred, const int32_t* status, int32_t* status_seen, hipStream_t s);
 
 }  // namespace bgcn

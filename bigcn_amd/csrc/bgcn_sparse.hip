@@ -419,19 +419,51 @@ __device__ inline void compact_body(const SparseState& S, const TX* __restrict__
 // compacted, in ascending column order, so the ELL list, the spill pool and the long-row
 // list are filled from them with the contents compact_row writes from the dense row (the
 // step computes the same bits either way).  One 32-lane half-wave per row (a BoW row holds
-// ~12 entries), grid-stride; reads nnz x 8 bytes instead of N x F x 4.
+// ~12 entries), grid-stride; reads nnz x 8 bytes instead of N x F x 4.  The lists come
+// from the host, so every row is checked first: a negative start or count, a column
+// outside [0, F) or columns not strictly ascending set the batch status bit 0 (the step
+// is then rejected like a bad edge index) and the row is written empty, so no later
+// kernel indexes by a bad column.
 __device__ inline void csr_ell_body(const SparseState& S, const int32_t* __restrict__ rp,
                                     const int32_t* __restrict__ rc, const float* __restrict__ rv, int bid,
                                     int nblk) {
   if (S.mode == 1) return;
   const int lane = threadIdx.x & 31;
+  const int half = threadIdx.x & 32;
   const int64_t nhalf = int64_t(nblk) * (blockDim.x / 32);
   for (int64_t i = (int64_t(bid) * blockDim.x + threadIdx.x) / 32; i < S.N; i += nhalf) {
     const int32_t b = rp[i], cnt = rp[i + 1] - b;      // half-wave uniform
+    bool bad = b < 0 || cnt < 0;
+    int32_t c0 = 0;
+    float v0 = 0.f;
+    if (!bad) {
+      bool lbad = false;
+      int32_t prev = -1;
+      for (int k0 = 0; k0 < cnt; k0 += 32) {
+        const int k = k0 + lane;
+        const int32_t c = rc[b + min(k, cnt - 1)];
+        if (k0 == 0) {
+          c0 = c;
+          v0 = rv[b + min(k, cnt - 1)];
+        }
+        int32_t pc = __shfl_up(c, 1, 32);
+        if (lane == 0) pc = prev;
+        lbad = lbad || (k < cnt && (c < 0 || c >= S.F || c <= pc));
+        prev = __shfl(c, 31, 32);                      // (a later chunk exists only if this one is full)
+      }
+      bad = ((__ballot(lbad) >> half) & 0xffffffffull) != 0ull;
+    }
+    if (bad) {
+      if (lane == 0) {
+        S.nnz[i] = 0;
+        if (S.bstatus) atomicOr(S.bstatus, 1);
+      }
+      continue;
+    }
     const int ce = cnt < kCap ? cnt : kCap;
     if (lane < ce) {
-      S.cols[i * kCap + lane] = rc[b + lane];
-      S.vals[i * kCap + lane] = rv[b + lane];
+      S.cols[i * kCap + lane] = c0;
+      S.vals[i * kCap + lane] = v0;
     }
     if (lane == 0) S.nnz[i] = cnt;
     if (cnt > kCap) {   // a long row: its tail to the spill pool, as compact_row does

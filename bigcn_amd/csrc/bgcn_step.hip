@@ -25,7 +25,7 @@ constexpr int H = 64;
 
 
 struct StepWs {
-  float *h1, *h2, *head, *dhead, *dz, *loss_row;
+  float *h1, *h2, *head, *dhead, *dz, *loss_row, *logp;
   void* enc; size_t enc_bytes;
 };
 
@@ -48,6 +48,7 @@ size_t carve_step(Carve& c, int64_t N, int64_t B, int64_t F, int64_t C, StepWs* 
   t.dhead = c.take<float>(size_t(B) * kHeadIn);
   t.dz = c.take<float>(size_t(B) * C);
   t.loss_row = c.take<float>(size_t(B));
+  t.logp = c.take<float>(size_t(B) * C);   // the evaluation step's log-probabilities (no caller buffer)
   t.enc_bytes = bigcn_ws_size(N, B, F, H);
   t.enc = c.take<char>(t.enc_bytes);
   if (w) *w = t;
@@ -291,6 +292,84 @@ static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w
   return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr, &hj, img, a->defer_dw1 != 0);
 }
 
+// One evaluation step (the test loop body, BiGCN_Twitter.py:207-222: model.eval();
+// val_out = model(Batch_data); val_loss = F.nll_loss(val_out, y); val_pred = argmax;
+// correct = val_pred.eq(y).sum()) as one call: the prepared batch's forward in eval mode
+// (no dropout; the batch carries no DropEdge), the head fused into the readout, then the
+// loss mean, the predictions and the correct count on the device.  No backward, no host
+// sync; the next batch's preparation rides on the side lane as in the training step.
+int eval_step_impl(const bgcn_step_args* a, int32_t* correct, int64_t* pred, void* ws, size_t ws_bytes,
+                   hipStream_t s) {
+  BGCN_CHECK_ARG(a, "null args");
+  BGCN_TRY(check_batch(&a->cur));
+  const int64_t N = a->cur.num_nodes, B = a->cur.num_graphs, F = a->in_feats, C = a->num_classes;
+  BGCN_CHECK_ARG(F > 0, "bad sizes");
+  BGCN_TRY(check_feat_input(&a->cur, a->feat_mode, F));
+  BGCN_CHECK_ARG(C >= 1 && C <= kMaxClasses, "num_classes must be in [1, 16]");
+  BGCN_CHECK_ARG(a->y && a->loss, "null pointer");
+  BGCN_CHECK_ARG(a->training == 0, "the evaluation step runs in eval mode (training = 0)");
+  BGCN_CHECK_ARG(a->cur.td_droprate == 0.0 && a->cur.bu_droprate == 0.0,
+                 "the evaluation step drops no edges (the test set's BiGraphDataset)");
+  for (int k = 0; k < BGCN_STEP_PARAMS; ++k) BGCN_CHECK_ARG(a->params[k], "null parameter pointer");
+  BGCN_CHECK_ARG(ws && ws_bytes >= train_step_ws_size(N, B, F, C, 0, 0), "workspace too small");
+  BGCN_CHECK_ARG(a->prepared, "a prepared buffer is required (bgcn_prepare_workspace_size)");
+  if (a->next) {
+    BGCN_TRY(check_batch(a->next));
+    BGCN_TRY(check_feat_input(a->next, a->feat_mode, F));
+    BGCN_CHECK_ARG(a->next_prepared && a->next_prepared != a->prepared, "next_prepared must be a separate buffer");
+  }
+  StepWs w;
+  Carve c(ws, ws_bytes);
+  carve_step(c, N, B, F, C, &w);
+  BGCN_CHECK_ARG(c.ok(), "workspace too small");
+  BGCN_CHECK_ARG(a->images || !a->images_current, "images_current without an image buffer");
+  Prepared p;
+  int graph_lane = -1;
+  BGCN_TRY(aux_prep_wait(s));
+  if (!a->prepared_ready) {
+    hipStream_t g = s;
+    if (!a->next) BGCN_TRY(aux_fork(s, kLaneSide, &g));
+    BGCN_TRY(prepare_into(&a->cur, F, a->degree_on, a->feat_mode, a->prepared, a->prepared_bytes, s, &p, g));
+    if (g != s) graph_lane = kLaneSide;
+  } else {
+    BGCN_CHECK_ARG(a->prepared_bytes >= prepared_size(N, B, F, a->cur.td_num_edges, a->cur.bu_num_edges),
+                   "prepared buffer too small");
+    Carve cp(a->prepared, a->prepared_bytes);
+    carve_prepared(cp, N, B, F, a->cur.td_num_edges, a->cur.bu_num_edges, &p);
+  }
+  if (a->next) {
+    hipStream_t x;
+    BGCN_TRY(aux_fork(s, kLaneSide, &x));
+    BGCN_TRY(prepare_into(a->next, F, a->degree_on, a->feat_mode, a->next_prepared, a->next_prepared_bytes, x,
+                          nullptr, x));
+    BGCN_TRY(aux_prep_done(s));
+  }
+  bgcn_bigcn_args e{};
+  e.x = a->cur.x; e.x_dtype = a->cur.x_dtype;
+  e.ldx = a->cur.ldx; e.num_nodes = N; e.num_graphs = B; e.in_feats = F; e.hid = H;
+  e.batch = a->cur.batch; e.rootindex = a->cur.rootindex;
+  e.td = view_of(p.td, p.td_cap);
+  e.bu = view_of(p.bu, p.bu_cap);
+  e.td_w1 = a->params[0]; e.td_b1 = a->params[1]; e.td_w2 = a->params[2]; e.td_b2 = a->params[3];
+  e.bu_w1 = a->params[4]; e.bu_b1 = a->params[5]; e.bu_w2 = a->params[6]; e.bu_b2 = a->params[7];
+  e.training = 0; e.seed = 0; e.keep_words = nullptr;
+  e.feat_mode = a->feat_mode;
+  e.x_flags = p.x_flags; e.x_nnz = p.x_nnz; e.x_cols = p.x_cols; e.x_vals = p.x_vals;
+  e.tree_ptr = p.tree_ptr; e.h1 = w.h1; e.h2 = w.h2; e.head_in = w.head; e.dhead_in = w.dhead;
+  e.save_for_backward = 0;
+  float* logp = a->logp ? a->logp : w.logp;
+  const HeadArgs hd{a->params[8], a->params[9], a->y, int(C), logp, w.dz, w.loss_row, w.dhead,
+                    a->status, p.status, a->feat_mode == BGCN_FEAT_SPARSE ? p.x_flags : nullptr};
+  WeightImages im{};
+  if (a->images) {
+    Carve ci(a->images, bgcn_weight_images_size(F));
+    carve_images(ci, F, &im);
+  }
+  BGCN_TRY(bigcn_forward_impl(&e, w.enc, w.enc_bytes, s, graph_lane, &hd, &p, a->images ? &im : nullptr,
+                              a->images_current != 0));
+  return eval_finish_impl(w.loss_row, logp, a->y, B, int(C), a->loss, correct, pred, a->status, a->status_seen, s);
+}
+
 // the encoder arguments of a step (the dW1 call re-derives them from the same inputs)
 static void step_encoder_args(const bgcn_step_args* a, const Prepared& p, const StepWs& w, bgcn_bigcn_args* e) {
   *e = bgcn_bigcn_args{};
@@ -377,6 +456,11 @@ extern "C" int bgcn_train_step(const bgcn_step_args* args, void* workspace, size
                                bgcn_stream_t stream) {
   return bgcn::train_step_impl(args, workspace, workspace_bytes,
                                reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int bgcn_eval_step(const bgcn_step_args* args, int32_t* correct, int64_t* pred, void* workspace,
+                              size_t workspace_bytes, bgcn_stream_t stream) {
+  return bgcn::eval_step_impl(args, correct, pred, workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int bgcn_train_step_dw1(const bgcn_step_args* args, void* workspace, size_t workspace_bytes,

@@ -122,6 +122,10 @@ class TreeStore:
                 v = np.asarray(v, dtype=np.float32)
                 order = np.argsort(c, kind="stable")
                 c, v = c[order], v[order]
+                if c.size and (c[0] < 0 or c[-1] >= in_feats):
+                    raise ValueError(f"tree {len(eids)}: a feature column outside [0, {in_feats})")
+                if c.size > 1 and not np.all(c[1:] > c[:-1]):
+                    raise ValueError(f"tree {len(eids)}: a feature column repeated within a node's row")
                 keep = v != 0
                 node_nnz.append(int(keep.sum()))
                 cols.append(c[keep].astype(np.int32))
@@ -329,7 +333,10 @@ def pack_batch(store: TreeStore, trees: Sequence[int], tddroprate: float = 0.0, 
     rp = sec("x_row_ptr")
     rp[0] = 0
     np.cumsum(cnt, out=rp[1:])
-    np.concatenate([store.cols[a:b] for a, b in zip(e0, e1)] or [np.zeros(0, np.int32)], out=sec("x_col"))
+    xc = sec("x_col")
+    np.concatenate([store.cols[a:b] for a, b in zip(e0, e1)] or [np.zeros(0, np.int32)], out=xc)
+    if nnz and (int(xc.min()) < 0 or int(xc.max()) >= store.in_feats):
+        raise ValueError(f"a feature column outside [0, {store.in_feats}) in the store")
     xv = sec("x_val")
     np.concatenate([store.vals[a:b] for a, b in zip(e0, e1)] or [np.zeros(0, np.float32)], out=xv)
     if bf16_values:   # the bf16 configuration: values as the bf16 x holds them
@@ -350,6 +357,7 @@ def pack_batch(store: TreeStore, trees: Sequence[int], tddroprate: float = 0.0, 
     sec("ptr")[:] = offs
     spill = int(np.maximum(cnt.astype(np.int64) - SPARSE_CAP, 0).sum()) if N else 0
     meta = {"N": N, "B": B, "nnz": nnz, "Etd": Etd, "Ebu": Ebu, "in_feats": store.in_feats,
+            "bf16_values": bool(bf16_values),
             "nnz_max": int(cnt.max()) if N else 0, "spill": spill, "layout": lay, "bytes": total}
     return HostBatch(buf, meta, np.asarray(store.root_tweetid[t]))
 
@@ -417,6 +425,17 @@ class PinnedSlotRing:
         return {"nslots": self.nslots, "slot_bytes": self.slot_bytes, "buf": self.buf,
                 "events": [None] * self.nslots, "seqs": [-1] * self.nslots, "_registered": None}
 
+    def quiesce(self) -> None:
+        """Wait for every issued copy out of the ring and forget the slots' batches: a new
+        pass of the loader (after a DataLoader reset - a `break` out of the previous pass -
+        whose packed-but-never-copied batches the loader discarded) starts from an empty
+        ring with sequence numbers from 0."""
+        for e in self.events:
+            if e is not None:
+                e.synchronize()
+        self.events = [None] * self.nslots
+        self.seqs = [-1] * self.nslots
+
     def free_for(self, s: int, seq: int) -> None:
         """Block until slot s may take batch ``seq``: the batch ``seq - nslots`` that used it
         has been copied out (its copy issued - else the ring is too small - and complete)."""
@@ -460,6 +479,11 @@ class SlotBatchSampler:
         return len(self.inner) * self.epochs
 
     def __iter__(self):
+        # runs at the first prefetch of a loader pass: with persistent workers that is after
+        # the DataLoader's reset has drained the workers, so no worker still packs into a
+        # slot of the previous pass
+        self.ring.quiesce()
+        self._seq = 0
         for _ in range(self.epochs):
             for idx in self.inner:
                 seq = self._seq
@@ -600,6 +624,8 @@ class PackedBatch:
                                                     N, F, x.data_ptr(), F,
                                                     _lib.BGCN_DTYPE_BF16 if self.x_dtype == torch.bfloat16
                                                     else _lib.BGCN_DTYPE_F32, st.data_ptr(), _lib.stream_handle()))
+            if int(st.item()) & 1:   # (one host read, on the first access only)
+                raise IndexError("a feature column outside [0, in_feats) in the batch's x_col")
             self._x = x
         return self._x
 
@@ -643,6 +669,12 @@ class DeviceFeeder:
         self.batches = 0
 
     def _issue(self, hb: HostBatch, consumer) -> PackedBatch:
+        # the bf16 configuration has two knobs that must agree: the workers round x_val to
+        # bf16 (PackedTreeDataset(bf16_values=True)) exactly when the step's x is bf16 (the
+        # dense bf16 path and bgcn_csr_to_dense round the same values)
+        if hb.meta.get("bf16_values", False) != (self.x_dtype == torch.bfloat16):
+            raise ValueError(f"DeviceFeeder(x_dtype={self.x_dtype}) over batches packed with bf16_values="
+                             f"{hb.meta.get('bf16_values', False)}: set both for the bf16 configuration")
         ring = self.ring
         if hb.slot is not None:
             ring.register()

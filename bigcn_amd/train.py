@@ -158,8 +158,9 @@ class FusedTrainStep:
         """{parameter: gradient view} of the last step (before the DP all-reduce)."""
         return dict(zip(self.step_params, self.step_grads))
 
-    def _desc(self, data):
-        """bgcn_batch of a collated batch (+ the tensors it points into, kept alive)."""
+    def _desc(self, data, drop: bool = True):
+        """bgcn_batch of a collated batch (+ the tensors it points into, kept alive);
+        ``drop=False``: no DropEdge whatever the model's mode (evaluation batches)."""
         if _compacted(data):
             F = _in_feats(data)
             want = [(HID, F), (HID,), (HID, HID + F), (HID,)] * 2
@@ -168,7 +169,8 @@ class FusedTrainStep:
                     raise ValueError(f"parameter of shape {tuple(p.shape)}, expected {shp} for in_feats={F}")
             d = BatchDesc()
             data.fill_desc(d)
-            self._drop_fields(d)
+            if drop:
+                self._drop_fields(d)
             return d, (data,)
         x = features(data.x)                         # fp32, or bf16 kept as is
         check_encoder_shapes(x, data.batch, data.rootindex, self.step_params[:8])
@@ -184,7 +186,8 @@ class FusedTrainStep:
         d.batch, d.rootindex = ptr(batch), ptr(root)
         d.td_edge_index, d.td_num_edges = ptr(td_ei), td_ei.size(1)
         d.bu_edge_index, d.bu_num_edges = ptr(bu_ei), bu_ei.size(1)
-        self._drop_fields(d)
+        if drop:
+            self._drop_fields(d)
         return d, (x, td_ei, bu_ei, batch, root)
 
     def _drop_fields(self, d) -> None:
@@ -283,6 +286,88 @@ class FusedTrainStep:
             raise
         return loss.view(())
 
+    def evaluate(self, data, next_data=None, logp: Optional[torch.Tensor] = None, pred: bool = False):
+        """One evaluation batch of the reference's test loop (``BiGCN_Twitter.py:207-222``:
+        ``model.eval(); val_out = model(Batch_data); val_loss = F.nll_loss(val_out, y);
+        _, val_pred = val_out.max(dim=1); correct = val_pred.eq(y).sum()``) as one call
+        (``bgcn_eval_step``): the forward in eval mode whatever ``model.training`` says (no
+        dropout; no DropEdge, as the test set's ``BiGraphDataset``), the head, and the mean
+        NLL, the argmax predictions and the correct count on the device - no host sync.
+
+        Returns ``(loss, correct)`` (0-dim fp32 / int32 device tensors), plus ``pred`` ([B]
+        int64 device tensor) when ``pred=True``.  ``logp``: an optional [B, C] fp32 output
+        for the log-probabilities.  ``next_data``: the next evaluation batch, prepared on the
+        side lane during this call.  Validity: ``check_status()`` / ``run_report()``."""
+        if self._dw1_pending is not None:
+            raise RuntimeError("a step run with defer_dw1=True is pending: call finish_dw1() first")
+        m = self.model
+        F = _in_feats(data)
+        dev = _device(data)
+        y = _need(data.y, torch.int64, "y")
+        mode = _step_feat_mode(m.feat_mode, data)
+        key = (mode == _lib.BGCN_FEAT_DENSE, False)
+        pend = self._pending
+        if pend is not None and pend[0] is data and pend[2] == key:
+            prep, keep, d = pend[1], pend[3], pend[4]
+            ready = 1
+        else:
+            if pend is not None:
+                self._join_side()
+            d, keep = self._desc(data, drop=False)
+            prep = self._prep_buffer(d, F)
+            ready = 0
+        if logp is not None and (logp.dtype != torch.float32 or not logp.is_contiguous()
+                                 or logp.numel() != d.num_graphs * self.num_classes):
+            raise ValueError("logp must be a contiguous fp32 [B, C] tensor")
+        a = self._args
+        a.cur = d
+        a.in_feats = F
+        a.y = ptr(y)
+        a.training, a.seed = 0, 0
+        a.feat_mode = mode
+        a.prepared_ready = ready
+        a.prepared, a.prepared_bytes = ptr(prep), prep.numel()
+        a.defer_dw1 = 0
+        self._pending = None
+        nxt = None
+        if next_data is not None:
+            nd, nkeep = self._desc(next_data, drop=False)
+            nbuf = self._prep_buffer(nd, F)
+            self._next_desc = nd
+            a.next = ctypes.pointer(self._next_desc)
+            a.next_prepared, a.next_prepared_bytes = ptr(nbuf), nbuf.numel()
+            nxt = (next_data, nbuf, key, nkeep, nd)
+        else:
+            a.next = None
+            a.next_prepared, a.next_prepared_bytes = 0, 0
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        correct = torch.empty(1, dtype=torch.int32, device=dev)
+        pr = torch.empty(d.num_graphs, dtype=torch.int64, device=dev) if pred else None
+        a.loss, a.logp, a.status = ptr(loss), ptr(logp), ptr(self.status)
+        a.status_flag = None
+        a.status_seen = ptr(self.status_seen)
+        img = self._image_buffer(F)
+        a.images = ptr(img)
+        current = self._images_key is not None and self._images_key == self._image_key()
+        a.images_current = int(current)
+        L = _lib.lib()
+        N, B = d.num_nodes, d.num_graphs
+        ws = workspace(L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
+                                                        d.bu_num_edges), dev)
+        self._stream = stream_handle()
+        self._pending = nxt
+        try:
+            check(L.bgcn_eval_step(ctypes.addressof(a), ptr(correct), ptr(pr), ptr(ws), ws.numel(), self._stream))
+        except Exception:
+            if nxt is not None:
+                self._join_side()
+                self._pending = None
+            raise
+        # (stale images were re-derived into the buffer on the sparse path only, so the key
+        # is left as it was: after a training step's Adam they are current anyway)
+        out = (loss.view(()), correct.view(()))
+        return out + (pr,) if pred else out
+
     def finish_dw1(self) -> None:
         """The conv1 weight gradients of a step run with ``defer_dw1`` (bgcn_train_step_dw1:
         same arguments and buffers, on the current stream)."""
@@ -377,7 +462,8 @@ class FusedTrainStep:
         s = int(self.status.item())
         if s & 1:
             raise IndexError("edge_index or batch contains an index out of range "
-                             "([0, num_nodes) / [0, num_graphs))")
+                             "([0, num_nodes) / [0, num_graphs)), or a host-fed feature row a column "
+                             "outside [0, in_feats) or out of ascending order")
         if s & 2:
             raise IndexError("label out of range [0, num_classes)")
         if s & 4:

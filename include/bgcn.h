@@ -48,7 +48,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 7
+#define BGCN_ABI_VERSION 8
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -414,7 +414,9 @@ int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree
  * data-parallel bucket; the all-reduce and bgcn_adam_step follow.  Parameter order:
  * td_w1 td_b1 td_w2 td_b2 bu_w1 bu_b1 bu_w2 bu_b2 fc_w [C, 256] fc_b [C] (the
  * reference state_dict layout).  *status (optional, zeroed by the call): bit 0 = an
- * edge index outside [0, N) or a batch id outside [0, B), bit 1 = a label outside [0, C),
+ * edge index outside [0, N) or a batch id outside [0, B) (or, host-fed features, a row of
+ * x_col with a column outside [0, F) or out of ascending order, or a negative x_row_ptr
+ * start / count: the row is then left empty), bit 1 = a label outside [0, C),
  * bit 2 = a batch whose feature rows overflow the spill pool under BGCN_FEAT_SPARSE,
  * bit 3 = an internal cross-workgroup hand-off timed out (never expected).  ANY set bit
  * makes the step's results invalid: through status_flag the optimiser skips the update.
@@ -477,6 +479,19 @@ int bgcn_train_step(const bgcn_step_args* args, void* workspace, size_t workspac
  * conv1 dW (BiGCN_Twitter.py:187 loss.backward(), the GCNConv lin weight of :22/:73). */
 int bgcn_train_step_dw1(const bgcn_step_args* args, void* workspace, size_t workspace_bytes,
                         bgcn_stream_t stream);
+/* (ABI 8) One evaluation step: the test loop body of BiGCN_Twitter.py:207-222
+ *   model.eval(); val_out = model(Batch_data); val_loss = F.nll_loss(val_out, Batch_data.y)
+ *   _, val_pred = val_out.max(dim=1); correct = val_pred.eq(Batch_data.y).sum()
+ * as one call with no host sync: the forward of the (prepared or not) batch in eval mode,
+ * the head, then on the device *loss = the mean NLL, correct[0] = the number of trees whose
+ * argmax class (the first maximal one, as torch's max) equals y, and pred[b] (optional,
+ * [B] int64) = that argmax (what the reference hands to evaluation4class).  args is the
+ * training step's struct: training must be 0 and cur must carry no DropEdge; grads,
+ * status_flag and defer_dw1 are ignored; logp (optional) receives the log-probabilities;
+ * status / status_seen as in the training step; next / next_prepared prefetch the next
+ * evaluation batch.  Workspace: bgcn_train_step_workspace_size. */
+int bgcn_eval_step(const bgcn_step_args* args, int32_t* correct, int64_t* pred, void* workspace,
+                   size_t workspace_bytes, bgcn_stream_t stream);
 /* The saved pre-activation conv outputs of the last step run in a step workspace (the
  * fused step's form of the per-stage dumps of explain_PHEME.py:91-162): h1 = conv1 output
  * H1 (pre-relu, also the detached x2), h2 = conv2 output H2 (pre-relu), each [N, 128]

@@ -164,7 +164,7 @@ def test_slot_ring_loader_packs_in_place(tmp_path):
     assert ring.nslots == 8 and ring.slot_bytes >= FD.pack_batch(store, range(56, 60)).meta["bytes"]
     for epoch in range(2):   # > nslots batches per epoch: every slot is reused
         for k, hb in enumerate(loader):
-            assert hb.buf is None and hb.slot == hb.seq % ring.nslots and hb.seq == 15 * epoch + k
+            assert hb.buf is None and hb.slot == hb.seq % ring.nslots and hb.seq == k
             ref = FD.pack_batch(store, range(4 * k, 4 * k + 4))
             assert hb.meta == ref.meta
             view = FD.HostBatch(ring.slot(hb.slot)[:hb.meta["bytes"]], hb.meta, hb.root_tweetids)
@@ -176,3 +176,41 @@ def test_slot_ring_loader_packs_in_place(tmp_path):
     with pytest.raises(RuntimeError, match="slot ring too small"):
         for hb in loader:
             pass
+
+
+def test_slot_ring_loader_break_and_reiterate(tmp_path):
+    """A `break` out of a pass (early stopping, islice) and a new pass over the same
+    persistent-worker loader: the batches the DataLoader discarded at its reset never had
+    their copies issued, and the new pass must not wait for them (it starts from an empty
+    ring, sequence numbers from 0)."""
+    store = FD.TreeStore.synthetic(60, 15, seed=9, in_feats=100)
+    loader = FD.host_fed_loader(store, batch_size=4, num_workers=2, shuffle=False, prefetch_factor=2)
+    ring = loader.dataset.ring
+    for k, hb in enumerate(loader):
+        ring.events[hb.slot], ring.seqs[hb.slot] = _DoneEvent(), hb.seq
+        if k == 2:
+            break
+    seen = []
+    for k, hb in enumerate(loader):
+        assert hb.seq == k
+        ref = FD.pack_batch(store, range(4 * k, 4 * k + 4))
+        view = FD.HostBatch(ring.slot(hb.slot)[:hb.meta["bytes"]], hb.meta, hb.root_tweetids)
+        assert np.array_equal(view.section("x_col"), ref.section("x_col"))
+        ring.events[hb.slot], ring.seqs[hb.slot] = _DoneEvent(), hb.seq
+        seen.append(k)
+    assert seen == list(range(15))
+
+
+def test_store_rejects_bad_feature_columns():
+    rows = [(np.array([3, 7]), np.array([1.0, 2.0], np.float32))]
+    tree = {"x_rows": rows, "edges": np.zeros((2, 0), np.int64), "rootindex": 0, "y": 0}
+    FD.TreeStore.from_trees([tree], in_feats=8)
+    with pytest.raises(ValueError, match="outside"):
+        FD.TreeStore.from_trees([tree], in_feats=7)
+    dup = dict(tree, x_rows=[(np.array([3, 3]), np.array([1.0, 2.0], np.float32))])
+    with pytest.raises(ValueError, match="repeated"):
+        FD.TreeStore.from_trees([dup], in_feats=8)
+    store = FD.TreeStore.synthetic(4, 10, seed=2, in_feats=64)
+    store.in_feats = 32          # a store whose columns reach past in_feats
+    with pytest.raises(ValueError, match="outside"):
+        FD.pack_batch(store, [0, 1, 2, 3])

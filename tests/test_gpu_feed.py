@@ -163,3 +163,35 @@ def test_feeder_end_to_end_matches_dense(tmp_path):
     dense = [_dense_batch(store, range(8 * k, 8 * k + 8)) for k in range(6)]
     _assert_same(_run(dense, 5000), _run(got, 5000))
     loader.dataset.ring.close()
+
+
+@pytest.mark.parametrize("bad", ["range", "order", "negative"])
+def test_bad_feature_columns_reject_the_step(bad):
+    """Host-fed lists are checked on the device: a column outside [0, F), columns out of
+    ascending order or a negative row count set status bit 0 (the step is invalid and the
+    fused Adam skips it), never an out-of-bounds access."""
+    from bigcn_amd import FusedTrainStep
+    store = FD.TreeStore.synthetic(16, 40, seed=26, in_feats=1000)
+    pk = _packed(store, range(16))
+    rp = pk.x_row_ptr
+    col = pk.x_col
+    r = 7                                            # a row of >= 2 entries
+    while int(rp[r + 1] - rp[r]) < 2:
+        r += 1
+    a = int(rp[r])
+    if bad == "range":
+        col[a + 1] = 1000 + 17
+    elif bad == "order":
+        col[a + 1] = col[a]
+    else:
+        rp[r + 1] = rp[r] - 1
+    m = _model(1000, 5)
+    before = [p.detach().clone() for p in m.parameters()]
+    st = FusedTrainStep(m, tddroprate=0.2, budroprate=0.2, drop_seed=3)
+    st(pk, seed=1)
+    torch.cuda.synchronize()
+    with pytest.raises(IndexError):
+        st.check_status()
+    assert st.run_report()["invalid_steps"] == 1
+    for p, q in zip(m.parameters(), before):
+        assert torch.equal(p.detach(), q)           # the update was skipped

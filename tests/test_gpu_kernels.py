@@ -260,6 +260,40 @@ def test_gemm_xwt(M, Nc, K):
     close(Y, X @ W.t(), 1e-5, "X W^T")
 
 
+def _segment_tail(rows, cols):
+    """A [rows, cols] fp32 view ending exactly at the end of its own allocation (a fresh
+    2 MiB-multiple block of the caching allocator): any read past its last element leaves
+    the allocation."""
+    n = rows * cols
+    seg = 2 << 20
+    total = (n * 4 + seg - 1) // seg * seg // 4
+    torch.cuda.empty_cache()
+    buf = torch.empty(total, device=DEV)
+    return buf[total - n:].view(rows, cols)
+
+
+def test_gemm_xwt_operands_at_allocation_end():
+    """The six-product conv1 (k_gemm_xwt_x6p, >= 8192 rows) prefetches k-tiles past the last
+    one; with X and W ending exactly at their allocations' ends those loads must read zeros
+    through the buffer range check (the tile offset rides in the VGPR offset), not past the
+    allocation."""
+    from bigcn_amd import _lib
+    from bigcn_amd._lib import check, ptr, stream_handle
+    M, Nc, K = 8200, 128, 5000
+    torch.manual_seed(7)
+    X = torch.randn(M, K, dtype=torch.float64)
+    W = torch.randn(Nc, K, dtype=torch.float64)
+    Xd = _segment_tail(M, K)
+    Xd.copy_(X.float())
+    Wd = _segment_tail(Nc, K)
+    Wd.copy_(W.float())
+    Y = torch.empty(M, Nc, device=DEV)
+    split = Nc // 2
+    check(_lib.lib().bgcn_gemm_xwt(ptr(Xd), K, ptr(Wd), ptr(Wd[split:]), K, split, ptr(Y), Nc, M, Nc, K,
+                                   stream_handle()))
+    close(Y, X @ W.t(), 1e-5, "X W^T at the allocation end")
+
+
 @pytest.mark.parametrize("M,Nc,K", [(500, 5000, 64), (33, 13, 7), (64, 128, 128)])
 def test_gemm_xw(M, Nc, K):
     from bigcn_amd import _lib
