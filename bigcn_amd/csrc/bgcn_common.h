@@ -100,16 +100,31 @@ constexpr int32_t kStatusInternal = 8;
 
 // ---------------------------------------------------------------- device
 // Dropout keep word for (seed, direction, node, word): 32 keep bits covering
-// columns [32*word, 32*word+32) of the [H + F] concat.  splitmix64 finalizer of a
-// unique 41-bit key; every bit is an independent fair coin (F.dropout p = 0.5).
+// columns [32*word, 32*word+32) of the [H + F] concat (F.dropout p = 0.5: every bit a fair
+// coin).  Two rounds of a 32-bit mixer (lowbias32, Wellons: a bijection with full
+// avalanche): a per-node base mix32(node ^ seed_lo), then per (word, direction) mix32(base ^
+// ((2 word + dir) * golden + seed_hi)).  The base is shared by every word of a node, so a
+// kernel that needs many words of one node (conv2's root slots: up to 17 per lane and
+// tile) hoists it (KeepSrc::base / get_b): 32-bit multiplies only, against three 64-bit
+// ones per word of the splitmix64 form this replaced (which dominated conv2's VALU time).
+// The restatement (oracle/bigcn_oracle.py keep_word) is bit-exact (test_gpu_dropedge).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t keep_node_base(uint64_t seed, uint32_t node) {
+  return mix32(node ^ uint32_t(seed));
+}
+__device__ __forceinline__ uint32_t keep_word_at(uint64_t seed, uint32_t base, uint32_t dir, uint32_t word) {
+  return mix32(base ^ (((word << 1) | (dir & 1u)) * 0x9E3779B9u + uint32_t(seed >> 32)));
+}
 __device__ __forceinline__ uint32_t keep_word(uint64_t seed, uint32_t dir, uint32_t node,
                                               uint32_t word) {
-  uint64_t key = (uint64_t(node) << 9) | (uint64_t(word & 255u) << 1) | uint64_t(dir & 1u);
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (key + 1ull);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return uint32_t(z >> 32);
+  return keep_word_at(seed, keep_node_base(seed, node), dir, word);
 }
 
 // Keep word source used by the fused kernels.
@@ -123,6 +138,13 @@ struct KeepSrc {
     if (!training) return 0xffffffffu;
     if (words) return words[(size_t(dir) * size_t(num_nodes) + node) * size_t(nw) + w];
     return keep_word(seed, dir, node, w);
+  }
+  // the node's hash base (generated words only): get_b(dir, node, base(node), w) == get(dir, node, w)
+  __device__ __forceinline__ uint32_t base(uint32_t node) const { return keep_node_base(seed, node); }
+  __device__ __forceinline__ uint32_t get_b(uint32_t dir, uint32_t node, uint32_t b, uint32_t w) const {
+    if (!training) return 0xffffffffu;
+    if (words) return words[(size_t(dir) * size_t(num_nodes) + node) * size_t(nw) + w];
+    return keep_word_at(seed, b, dir, w);
   }
   __host__ __device__ __forceinline__ float scale() const { return training ? 2.0f : 1.0f; }
 };

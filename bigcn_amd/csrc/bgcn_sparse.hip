@@ -731,6 +731,20 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   __shared__ uint32_t rk[kCap];
   const int d = blockIdx.y;
   const int64_t beg = S.item_beg[item], end = S.item_end[item];
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
+  // the wave's first H1 tile is requested before the B fill's dependent chain (root ->
+  // its ELL slots -> W2^T rows) starts, so its latency hides behind the fill; a tile past
+  // the item loads (clamped) rows it then ignores - no load under a branch
+  auto h1load = [&](int t, float4 (&hv)[8]) {   // coalesced: 8 x 1 KiB per wave
+    const int64_t i0 = beg + 32 * t;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = l + 64 * u, rr = e >> 4, q = (e & 15) * 4;
+      hv[u] = ld4(H1 + min<int64_t>(i0 + rr, end - 1) * (2 * H) + d * H + q);
+    }
+  };
+  float4 hv[8];
+  h1load(wv, hv);
   const int64_t r = S.item_root[item];
   const int rn_all = S.nnz[r];
   const int rn = min(rn_all, kCap);   // root slots in the ELL (the rest spilled)
@@ -768,35 +782,30 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   __syncthreads();
   BT_MARK(2, 0);
 
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
   float* hs = &Hs[wv * 32 * kC2Ld];   // this wave's staged 32 x 64 H1 tile
+  auto h1stage = [&](const float4 (&hv)[8]) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = l + 64 * u, rr = e >> 4, q = (e & 15) * 4;
+      float* dst = &hs[rr * kC2Ld + q];
+      dst[0] = hv[u].x; dst[1] = hv[u].y; dst[2] = hv[u].z; dst[3] = hv[u].w;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+  };
   // the main product of tile t (32 nodes of the item): H1 tile staged through LDS, the
   // dropout-masked relu(H1) and the root keep bits generated in registers, six-product
   // bf16 MFMAs; the root keep masks go to S.rbits
+  // (the tile's H1 rows are in the wave's LDS tile already: h1stage)
   auto tile = [&](int t, f32x16& acc0, f32x16& acc1) {
     const int64_t i0 = beg + 32 * t;
     const int64_t i = i0 + r32;
     const bool ok = i < end;
-    {   // coalesced staging: 8 x 1 KiB per wave instead of 32 scattered rows per load
-      float4 hv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = l + 64 * u, rr = e >> 4, q = (e & 15) * 4;
-        hv[u] = ld4(H1 + min<int64_t>(i0 + rr, end - 1) * (2 * H) + d * H + q);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = l + 64 * u, rr = e >> 4, q = (e & 15) * 4;
-        float* dst = &hs[rr * kC2Ld + q];
-        dst[0] = hv[u].x; dst[1] = hv[u].y; dst[2] = hv[u].z; dst[3] = hv[u].w;
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's LDS writes landed
-      __builtin_amdgcn_wave_barrier();
-    }
     if (t == wv) BT_MARK(2, 1);
     const float* hrow = &hs[r32 * kC2Ld + 32 * h];
     const uint32_t ni = uint32_t(ok ? i : beg);
-    const uint32_t wd = keep.get(uint32_t(d), ni, uint32_t(h));
+    const uint32_t kb = keep.base(ni);   // the node's hash base, shared by its words
+    const uint32_t wd = keep.get_b(uint32_t(d), ni, kb, uint32_t(h));
     uint32_t m = 0;
 #pragma unroll
     for (int j = 0; j < kCap / 2; ++j) {
@@ -804,7 +813,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
       if (j < mh) {
         const int sl = 2 * j + h;
         const uint32_t k = rk[sl];
-        bit = sl < rn ? (keep.get(uint32_t(d), ni, k >> 5) >> (k & 31)) & 1u : 0u;
+        bit = sl < rn ? (keep.get_b(uint32_t(d), ni, kb, k >> 5) >> (k & 31)) & 1u : 0u;
       }
       m |= bit << (2 * j + h);
     }
@@ -868,11 +877,19 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   };
   static_assert(kChunk / 32 == 8, "two tiles per wave");
   if (rn_all <= kCap) {
-    for (int t = wv; t < kChunk / 32; t += 4) {
-      if (beg + 32 * t >= end) break;
+    // tile wv (its H1 rows requested at the start), then tile wv + 4, whose rows are
+    // requested as soon as the first tile's are staged: in flight during its products
+    if (beg + 32 * wv < end) {
+      h1stage(hv);
+      h1load(wv + 4, hv);
       f32x16 acc0, acc1;
-      tile(t, acc0, acc1);
-      store(t, acc0, acc1);
+      tile(wv, acc0, acc1);
+      store(wv, acc0, acc1);
+      if (beg + 32 * (wv + 4) < end) {
+        h1stage(hv);
+        tile(wv + 4, acc0, acc1);
+        store(wv + 4, acc0, acc1);
+      }
     }
   } else {
     // The root's spilled non-zeros (a root row of more than kCap words, rare): further
@@ -885,7 +902,11 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
     f32x16 acc[2][2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      if (beg + 32 * (wv + 4 * j) < end) tile(wv + 4 * j, acc[j][0], acc[j][1]);
+      if (beg + 32 * (wv + 4 * j) < end) {
+        if (j == 1) h1load(wv + 4, hv);
+        h1stage(hv);
+        tile(wv + 4 * j, acc[j][0], acc[j][1]);
+      }
     const int64_t off = S.ovf_off[r];
     const int nsp = rn_all - kCap;
     const int sq0 = threadIdx.x >> 4, sq1 = (threadIdx.x + 256) >> 4, qq = (threadIdx.x & 15) * 4;
@@ -927,13 +948,14 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
         if (i0 >= end) continue;
         const int64_t i = i0 + r32;
         const uint32_t ni = uint32_t(i < end ? i : beg);
+        const uint32_t kb = keep.base(ni);
         uint32_t m = 0;
 #pragma unroll
         for (int jj = 0; jj < kCap / 2; ++jj) {
           const int sl = 2 * jj + h;
           if (jj < mc && sl < cn) {
             const uint32_t k = rk[sl];
-            m |= ((keep.get(uint32_t(d), ni, k >> 5) >> (k & 31)) & 1u) << sl;
+            m |= ((keep.get_b(uint32_t(d), ni, kb, k >> 5) >> (k & 31)) & 1u) << sl;
           }
         }
 #pragma unroll

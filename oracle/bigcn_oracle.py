@@ -345,3 +345,36 @@ def drop_edges(edge_index, batch, num_graphs: int, droprate: float, seed: int, d
             out[1, e0 + nk:e1] = seg[1, dr]
         return out
     return ei[:, keep]
+
+
+# ----------------------------------------------------------------------------
+# Dropout keep words (F.dropout p = 0.5 of BiGCN_Twitter.py:54 as drawn in-kernel):
+# restatement of bgcn_common.h keep_word, bit-exact
+# ----------------------------------------------------------------------------
+def _mix32(x):
+    import numpy as np
+    x = np.asarray(x, dtype=np.uint32).copy()
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x7FEB352D)
+        x ^= x >> np.uint32(15)
+        x *= np.uint32(0x846CA68B)
+        x ^= x >> np.uint32(16)
+    return x
+
+
+def keep_words(seed: int, num_nodes: int, num_words: int):
+    """[2, N, nw] uint32 keep words of the in-kernel dropout draw (bgcn_keep_words): word w
+    of node i in direction d holds the keep bits of concat columns [32 w, 32 w + 32);
+    ``mix32(mix32(i ^ seed_lo) ^ ((2 w + d) * 0x9E3779B9 + seed_hi))``."""
+    import numpy as np
+    seed = int(seed) & _M64
+    s0, s1 = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
+    base = _mix32(np.arange(num_nodes, dtype=np.uint32) ^ s0)
+    out = np.empty((2, num_nodes, num_words), dtype=np.uint32)
+    w = np.arange(num_words, dtype=np.uint32)
+    with np.errstate(over="ignore"):
+        for d in range(2):
+            c = ((w << np.uint32(1)) | np.uint32(d)) * np.uint32(0x9E3779B9) + s1
+            out[d] = _mix32(base[:, None] ^ c[None, :])
+    return out

@@ -116,3 +116,15 @@ def test_train_step_device_dropedge_matches_oracle(prefetch):
             close(g[prm], rgrads[k], what=k)
         step.check_status()
     assert seeds == [1000, 1001]
+
+
+@pytest.mark.parametrize("seed", [0, 987654321, 2**63 + 12345])
+def test_keep_words_match_restatement(seed):
+    """The in-kernel dropout draw (bgcn_keep_words = what every fused kernel computes from
+    (seed, direction, node, word)) equals O.keep_words bit for bit."""
+    from bigcn_amd.ops import keep_words
+    N, F = 3001, 5000
+    got = keep_words(seed, N, F, torch.device("cuda:0")).cpu().numpy().view(np.uint32)
+    want = O.keep_words(seed, N, (64 + F + 31) // 32)
+    assert got.shape == want.shape
+    assert np.array_equal(got, want)

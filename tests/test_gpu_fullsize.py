@@ -322,11 +322,23 @@ def test_ragged_trees_step_matches_oracle(mode):
     masks = {d: (h1[:, 64 * k:64 * (k + 1)] > 0, h2[:, 64 * k:64 * (k + 1)] > 0)
              for k, d in enumerate(("TDrumorGCN", "BUrumorGCN"))}
     rlogp, rloss, rgrads, st = _oracle(ref, p, True, mk[0], mk[1], relu_masks=masks)
+    ties, tie_depth = {}, {}
+    table = {k: errors(g, rgrads[k]) for k, g in zip(KEYS, grads)}
+    table["logp"] = errors(logp, rlogp)
+    table["loss"] = errors(loss, rloss)
     for k, d in enumerate(("TDrumorGCN", "BUrumorGCN")):
         for name, mine in (("h1", h1), ("h2", h2)):
             r = st[f"{d}.{name}"]
-            flip = (mine[:, 64 * k:64 * (k + 1)] > 0) != (r > 0)
-            assert bool((r[flip].abs() <= 1e-5 * r.abs().max()).all()), f"{d}.{name}: relu' off a tie"
+            got = mine[:, 64 * k:64 * (k + 1)]
+            table[f"{d}.{name} (saved)"] = errors(got, r)
+            flip = (got > 0) != (r > 0)
+            ties[f"{d}.{name}"] = int(flip.sum())
+            depth = float(r[flip].abs().max() / r.abs().max()) if bool(flip.any()) else 0.0
+            tie_depth[f"{d}.{name}"] = depth
+            # the full-size tests' bar: a differing decision is a tie, and rare
+            assert depth <= TIE_WINDOW, f"{d}.{name}: relu' off a tie ({depth:.2e} of max|h|)"
+            assert ties[f"{d}.{name}"] <= TIE_FLIPS, f"{d}.{name}: {ties[f'{d}.{name}']} relu' decisions differ"
+    _dump_table(f"ragged_{mode}", N, table, ties, tie_depth)
     close_elem(logp, rlogp, what="logp")
     close_elem(loss.reshape(1), rloss.reshape(1), what="loss")
     for k, g in zip(KEYS, grads):

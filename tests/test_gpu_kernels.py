@@ -408,6 +408,27 @@ def test_gcnconv_edge_weight_fwd_bwd(degree_on):
     close(conv.bias.grad, b.grad, what="db")
 
 
+def _dump_errors(name, pairs, floors=None):
+    """Per tensor the max-scaled error and the worst elementwise ratio |a - b| / (|b| +
+    floor max|b|) (the test's own floor: 1e-3 unless `floors` names another) against the fp64
+    reference, under gpurun_out/parity/ (kept per round under profiles/)."""
+    import json
+    import os
+    out = {}
+    for k, (a, b) in pairs.items():
+        a = torch.as_tensor(a).detach().double().cpu()
+        b = torch.as_tensor(b).detach().double().cpu()
+        m = float(b.abs().max())
+        err = (a - b).abs()
+        fl = (floors or {}).get(k, 1e-3)
+        out[k] = {"max_scaled": float(err.max()) / max(m, 1e-300), "floor": fl,
+                  "elementwise": float((err / (b.abs() + fl * m).clamp_min(1e-300)).max())}
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, name + ".json"), "w") as f:
+        json.dump({"tol": 1e-4, "errors": out}, f, indent=1)
+
+
 def close_elem(a, b, what="", rtol=1e-4, floor=1e-3):
     """Elementwise: |a - b| <= rtol * (|b| + floor * max|b|) (fp32 kernels vs fp64 oracle)."""
     a = torch.as_tensor(a).detach().double().cpu()
@@ -454,6 +475,10 @@ def test_gcnconv_learned_edge_weight(degree_on):
     out = conv(xd, ei.to(DEV), ewd)
     out.backward(gout.float().to(DEV))
     close(out, ref, what="out")
+    _dump_errors(f"edge_weight_{degree_on}", {
+        "out": (out, ref), "d edge_weight": (ewd.grad, ew.grad), "dx": (xd.grad, x.grad),
+        "dW": (conv.lin.weight.grad, w.grad), "db": (conv.bias.grad, b.grad),
+        "d fc.weight": (fcd.weight.grad, fc.weight.grad)}, floors={"d edge_weight": 1e-2})
     # dL/dw_e = g_e dis[s] dis[d] + dL/ddeg[key]: the two terms nearly cancel on some edges,
     # so the elementwise floor is 1e-2 of the largest gradient (still 1e-6 of it absolute)
     close_elem(ewd.grad, ew.grad, what="d edge_weight", floor=1e-2)

@@ -224,3 +224,29 @@ def test_drop_edges_oracle_uniform():
     kept[posmap[out[1]]] = True
     freq = kept.reshape(len(sizes), 10).mean(axis=0)
     assert np.all(np.abs(freq - 0.8) < 0.03), freq
+
+
+def test_keep_words_restatement_statistics():
+    """The in-kernel dropout draw (restated bit-exactly by O.keep_words; checked against the
+    device in test_gpu_dropedge) is F.dropout(p = 0.5)'s coin per element: each column's
+    and each node's kept fraction within 4.5 sigma of 1/2, no correlation between adjacent
+    columns, adjacent nodes, the two directions or the seeds."""
+    N, nw = 8000, 160
+    w0 = O.keep_words(12345, N, nw)
+    w1 = O.keep_words(12346, N, nw)
+    bits = np.unpackbits(w0.view(np.uint8), bitorder="little").reshape(2, N, nw * 32).astype(np.float64)
+    other = np.unpackbits(w1.view(np.uint8), bitorder="little").reshape(2, N, nw * 32).astype(np.float64)
+    assert abs(bits.mean() - 0.5) < 4.5 * np.sqrt(0.25 / bits.size)
+    col = bits[0].mean(0)
+    assert np.abs(col - 0.5).max() < 4.5 * np.sqrt(0.25 / N)
+    row = bits[0].mean(1)
+    assert np.abs(row - 0.5).max() < 4.5 * np.sqrt(0.25 / (nw * 32))
+
+    def corr(a, b):
+        a, b = a.ravel() - a.mean(), b.ravel() - b.mean()
+        return float((a * b).mean() / np.sqrt((a * a).mean() * (b * b).mean()))
+    lim = 4.5 / np.sqrt(bits[0].size)
+    assert abs(corr(bits[0][:, :-1], bits[0][:, 1:])) < lim
+    assert abs(corr(bits[0][:-1], bits[0][1:])) < lim
+    assert abs(corr(bits[0], bits[1])) < lim
+    assert abs(corr(bits[0], other[0])) < lim

@@ -27,7 +27,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIGHT = ["--no-cpu-baseline", "--compare-dense", "0", "--compare-dropedge", "0", "--aggregation", "0",
-         "--dropin", "0", "--host-fed", "0"]
+         "--dropin", "0", "--host-fed", "0", "--eval-path", "0"]
 
 
 def variant_env(v: str) -> dict:

@@ -10,7 +10,7 @@ OUT=${1:-gpurun_out/prof}; shift
 WLS=${@:-twitter15}
 mkdir -p "$OUT"
 ROOT=$(pwd)
-LIGHT="--no-cpu-baseline --compare-dense 0 --compare-dropedge 0 --aggregation 0 --dropin 0 --host-fed 0"
+LIGHT="--no-cpu-baseline --compare-dense 0 --compare-dropedge 0 --aggregation 0 --dropin 0 --host-fed 0 --eval-path 0"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
 for w in $WLS; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_$w" -o run -- \
