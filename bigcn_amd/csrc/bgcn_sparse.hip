@@ -715,6 +715,9 @@ __global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __res
 // columns [32h, 32h + 32) (k-step s: columns 32h + 8s + j) and root slots 2j + h (k-step
 // t: slots 2(8t + j) + h), so each lane hashes only its own keep words and the steps past
 // the root's non-zeros are skipped; the keep bits are exact in bf16 (three products).
+#ifndef BGCN_C2_PREFETCH
+#define BGCN_C2_PREFETCH 1   // 0: each H1 tile requested when it is staged (30 VGPRs fewer)
+#endif
 constexpr int kC2Ld = H + 1;             // f32 row stride of the staged H1 tiles
 constexpr int kC2K = H + kCap;           // B rows: 64 H1 columns + 32 root slot positions
 constexpr int kC2Ld16 = kC2K + 8;        // bf16 row stride of the split B (16-byte aligned)
@@ -744,7 +747,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
     }
   };
   float4 hv[8];
-  h1load(wv, hv);
+  if (BGCN_C2_PREFETCH) h1load(wv, hv);
   const int64_t r = S.item_root[item];
   const int rn_all = S.nnz[r];
   const int rn = min(rn_all, kCap);   // root slots in the ELL (the rest spilled)
@@ -880,12 +883,14 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
     // tile wv (its H1 rows requested at the start), then tile wv + 4, whose rows are
     // requested as soon as the first tile's are staged: in flight during its products
     if (beg + 32 * wv < end) {
+      if (!BGCN_C2_PREFETCH) h1load(wv, hv);
       h1stage(hv);
-      h1load(wv + 4, hv);
+      if (BGCN_C2_PREFETCH) h1load(wv + 4, hv);
       f32x16 acc0, acc1;
       tile(wv, acc0, acc1);
       store(wv, acc0, acc1);
       if (beg + 32 * (wv + 4) < end) {
+        if (!BGCN_C2_PREFETCH) h1load(wv + 4, hv);
         h1stage(hv);
         tile(wv + 4, acc0, acc1);
         store(wv + 4, acc0, acc1);
@@ -903,7 +908,7 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       if (beg + 32 * (wv + 4 * j) < end) {
-        if (j == 1) h1load(wv + 4, hv);
+        if (j == 1 || !BGCN_C2_PREFETCH) h1load(wv + 4 * j, hv);
         h1stage(hv);
         tile(wv + 4 * j, acc[j][0], acc[j][1]);
       }
@@ -984,6 +989,181 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
   BT_END(2);
 }
 
+
+// The same conv2 with every wave on ONE 32-node tile: a block takes half a work item
+// (tiles 4 half .. 4 half + 3; the second half of an item of <= 128 nodes exits at once), so
+// no wave runs two tiles in series (the whole kernel was the fill plus two tiles' products
+// on the items of 256 nodes), and each lane loads its H1 A-fragment (row r32, columns
+// [32h, 32h + 32) of direction d: eight 16-byte loads, a 128-byte run) straight into
+// registers at the kernel's start, under the B fill - no LDS staging of H1 (the block's LDS
+// is the B operand only).  BGCN_C2_HALF=0 keeps k_conv2_sparse.
+#ifndef BGCN_C2_HALF
+#define BGCN_C2_HALF 1
+#endif
+__global__ __launch_bounds__(256) void k_conv2_half(SparseState S, const float* __restrict__ H1,
+                                                    float* __restrict__ Z2, KeepSrc keep) {
+  BT_BEGIN
+  if (!use_sparse(S)) return;
+  const int item = int(blockIdx.x >> 1), half = int(blockIdx.x & 1);
+  if (item >= S.tree_item0[S.B]) return;
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3][H * kC2Ld16];   // hi, mid, lo
+  __shared__ uint32_t rk[kCap];
+  const int d = blockIdx.y;
+  const int64_t beg = S.item_beg[item], end = S.item_end[item];
+  if (beg + 128 * half >= end) return;               // block-uniform: no tile in this half
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
+  const int t = 4 * half + wv;
+  const int64_t i0 = beg + 32 * t;
+  const int64_t i = i0 + r32;
+  const bool ok = i < end;
+  const bool live = i0 < end;                        // wave-uniform: the wave has a tile
+  // this lane's A-fragment rows, requested first (clamped: a row past the item reads the
+  // item's last row and is masked by `ok`)
+  float4 hv[8];
+  {
+    const float* src = H1 + min<int64_t>(i, end - 1) * (2 * H) + d * H + 32 * h;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) hv[u] = ld4(src + 4 * u);
+  }
+  const int64_t r = S.item_root[item];
+  const int rn_all = S.nnz[r];
+  const int rn = min(rn_all, kCap);
+  const int mh = (rn + 1) / 2;
+  const float sc = keep.scale();
+  const int64_t K2 = S.F + H;
+  const float* w2t = S.w2t + int64_t(d) * K2 * H;
+  if (threadIdx.x < kCap)
+    rk[threadIdx.x] = threadIdx.x < rn ? uint32_t(H + S.cols[r * kCap + threadIdx.x]) : 0u;
+  {
+    const __bf16* src = S.w2s + int64_t(d) * 3 * H * kW2sLd;
+    for (int e = threadIdx.x; e < 3 * H * 8; e += 256) {
+      const int part = e / (H * 8), o = (e / 8) % H, q = (e % 8) * 8;
+      *reinterpret_cast<uint4*>(&Bs[part][o * kC2Ld16 + q]) =
+          *reinterpret_cast<const uint4*>(src + (int64_t(part) * H + o) * kW2sLd + q);
+    }
+  }
+  for (int e = threadIdx.x; e < kCap * (H / 4); e += 256) {
+    const int s = e >> 4, q = (e & 15) * 4;
+    const int64_t slot = r * kCap + s;
+    const int32_t col = min(max(S.cols[slot], 0), int32_t(S.F - 1));
+    const float val = S.vals[slot];
+    const float4 w = ld4(w2t + int64_t(H + col) * H + q);
+    const float av = s < rn ? sc * fmaxf(val, 0.f) : 0.f;
+    const float vv[4] = {av * w.x, av * w.y, av * w.z, av * w.w};
+    const int k = H + (s & 1) * (kCap / 2) + (s >> 1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int o = (q + u) * kC2Ld16 + k;
+      split3_bf16(vv[u], Bs[0][o], Bs[1][o], Bs[2][o]);
+    }
+  }
+  __syncthreads();
+  BT_MARK(2, 0);
+  // a wave without a tile (the half's last tiles past a short item) computes nothing but
+  // stays for the spill rounds' barriers
+  const uint32_t ni = uint32_t(ok ? i : beg);
+  const uint32_t kb = keep.base(ni);
+  f32x16 acc0 = {}, acc1 = {};
+  if (live) {
+    const uint32_t wd = keep.get_b(uint32_t(d), ni, kb, uint32_t(h));
+    const float hf[32] = {hv[0].x, hv[0].y, hv[0].z, hv[0].w, hv[1].x, hv[1].y, hv[1].z, hv[1].w,
+                          hv[2].x, hv[2].y, hv[2].z, hv[2].w, hv[3].x, hv[3].y, hv[3].z, hv[3].w,
+                          hv[4].x, hv[4].y, hv[4].z, hv[4].w, hv[5].x, hv[5].y, hv[5].z, hv[5].w,
+                          hv[6].x, hv[6].y, hv[6].z, hv[6].w, hv[7].x, hv[7].y, hv[7].z, hv[7].w};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {   // H1 columns 32h + 8s + j
+      bf16x8 ah, am, al;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = 8 * s + j;
+        const float a = ((wd >> kk) & 1u) ? sc * fmaxf(hf[kk], 0.f) : 0.f;
+        __bf16 x, y, z;
+        split3_bf16(a, x, y, z);
+        ah[j] = x; am[j] = y; al[j] = z;
+      }
+      const int k = 32 * h + 8 * s;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int o = (32 * hh + r32) * kC2Ld16 + k;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(&Bs[0][o]);
+        const bf16x8 bm = *reinterpret_cast<const bf16x8*>(&Bs[1][o]);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(&Bs[2][o]);
+        if (hh == 0) acc0 = mfma_x6(ah, am, al, bh, bm, bl, acc0);
+        else acc1 = mfma_x6(ah, am, al, bh, bm, bl, acc1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (t == 4 * half) BT_MARK(2, 2);
+  // the root slots (exact 0/1 keep bits times the staged root rows, three products); a root
+  // row over the ELL cap continues from the spill pool in rounds of kCap entries
+  const int64_t off = rn_all > kCap ? S.ovf_off[r] : 0;
+  const int nsp = rn_all > kCap ? rn_all - kCap : 0;
+  for (int c0 = -kCap; c0 < nsp; c0 += kCap) {
+    const int cn = c0 < 0 ? rn : min(kCap, nsp - c0);
+    if (c0 >= 0) {   // a spill round: the next kCap pool entries into the root slots
+      __syncthreads();   // every wave is done with the previous round's slots (all waves loop alike)
+      const int tk = min(int(threadIdx.x), kCap - 1);
+      const uint2 ek = S.ovf[off + min(c0 + tk, nsp - 1)];
+      if (threadIdx.x < kCap) rk[threadIdx.x] = uint32_t(H + min(max(int32_t(ek.x), 0), int32_t(S.F - 1)));
+      for (int e = threadIdx.x; e < kCap * (H / 4); e += 256) {
+        const int s = e >> 4, q = (e & 15) * 4;
+        const uint2 ent = S.ovf[off + min(c0 + s, nsp - 1)];
+        const float4 w = ld4(w2t + int64_t(H + min(max(int32_t(ent.x), 0), int32_t(S.F - 1))) * H + q);
+        const float av = s < cn ? sc * fmaxf(__uint_as_float(ent.y), 0.f) : 0.f;
+        const float vv[4] = {av * w.x, av * w.y, av * w.z, av * w.w};
+        const int k = H + (s & 1) * (kCap / 2) + (s >> 1);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int o = (q + u) * kC2Ld16 + k;
+          split3_bf16(vv[u], Bs[0][o], Bs[1][o], Bs[2][o]);
+        }
+      }
+      __syncthreads();
+    }
+    const int mc = (cn + 1) / 2;
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < kCap / 2; ++j) {
+      const int sl = 2 * j + h;
+      if (j < mc && sl < cn) {
+        const uint32_t k = rk[sl];
+        m |= ((keep.get_b(uint32_t(d), ni, kb, k >> 5) >> (k & 31)) & 1u) << sl;
+      }
+    }
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      if (live && 8 * tt < mc) {
+        bf16x8 ar;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ar[j] = __bf16(((m >> (2 * (8 * tt + j) + h)) & 1u) ? 1.f : 0.f);
+        const int k = H + (kCap / 2) * h + 8 * tt;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int o = (32 * hh + r32) * kC2Ld16 + k;
+          f32x16 c = hh == 0 ? acc0 : acc1;
+          c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[2][o]), c);
+          c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[1][o]), c);
+          c = mfma_bf16(ar, *reinterpret_cast<const bf16x8*>(&Bs[0][o]), c);
+          if (hh == 0) acc0 = c; else acc1 = c;
+        }
+      }
+    }
+    if (c0 < 0) {   // the ELL slots' keep mask, for the dW2 root columns of the backward
+      m |= __shfl_xor(m, 32);
+      if (h == 0 && ok) S.rbits[int64_t(d) * S.N + i] = m;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t ii = i0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    if (ii < end) {
+      Z2[ii * (2 * H) + d * H + r32] = acc0[q];
+      Z2[ii * (2 * H) + d * H + 32 + r32] = acc1[q];
+    }
+  }
+  BT_END(2);
+}
 
 // ---------------------------------------------------------------- dW2 root columns, part 1
 // Work item = (tree b, chunk of <= kChunk nodes of b), blockIdx.y = direction:
@@ -1861,8 +2041,17 @@ __device__ inline void prep_b_body(const PrepArgs& a) {
 
 // a.span (the kernel-timing hook, class 7): every block min's its start and max's its end
 // into the launch's wall-clock pair - the kernel's own span, as rocprofv3 reports it
+// Register budget of the pass over X: with fp32 X 1.5 blocks per CU (two waves of this
+// launch on half the SIMDs) run beside the training chain, and a chain kernel's wave shares
+// those SIMDs only if 2 x this budget + its own registers fit 512.  At its natural 201
+// (-> 208) the X-window kernels (conv2 116, the aggregations 88-116, the readout 106) fit
+// on only the CUs holding ONE block of the pass: conv2's waves ran on 124 of 256 CUs and
+// started up to 60 us late (profiles/r05_block_trace_instep*.txt).  192 leaves them 128.
+#ifndef BGCN_PREP_B_WAVES
+#define BGCN_PREP_B_WAVES 3
+#endif
 template <class TX>
-__global__ __launch_bounds__(256) void k_prep_b(PrepArgs a) {
+__global__ __launch_bounds__(256, BGCN_PREP_B_WAVES) void k_prep_b(PrepArgs a) {
   if (a.span && threadIdx.x == 0 && blockIdx.x < kSpanStarts)
     a.span[blockIdx.x] = uint64_t(wall_clock64());
   prep_b_body<TX>(a);
@@ -1872,6 +2061,27 @@ __global__ __launch_bounds__(256) void k_prep_b(PrepArgs a) {
       atomicMax(reinterpret_cast<unsigned long long*>(a.span) + kSpanStarts + blockIdx.x % kSpanEnds,
                 static_cast<unsigned long long>(wall_clock64()));
   }
+}
+
+// The graph lane's launches of the two-lane preparation carry only their K1 / DropEdge
+// roles, as kernels of their own: a merged launch is allocated the registers of its
+// heaviest role (k_prep_b: the fp32 pass over X, 201 VGPRs; k_prep_f: the CSC placement,
+// 234), so the DropEdge select's 256 blocks held 201 registers per wave for the ~90 us they
+// run beside the pass - one block per CU that the chain's conv2 (236 registers) then could
+// not share: conv2's waves started up to 60 us late in the X window
+// (profiles/r05_block_trace_instep.txt).
+__global__ __launch_bounds__(256) void k_prep_select(PrepArgs a) {
+  const int b = int(blockIdx.x);
+  if (b >= a.nsel) return;
+  const int d = b / int(a.S.B);
+  drop_select_body(a.dl[d], d, int64_t(b % int(a.S.B)), a.batch, a.S.N, a.S.B, a.seed, a.eptr, 1, nullptr,
+                   a.status);
+}
+
+__global__ __launch_bounds__(256) void k_prep_f_graph(PrepArgs a) {
+  const int per = a.ne + a.nn + a.np;
+  const int b = int(blockIdx.x);
+  if (b < 2 * per) graph_rank_norm_body(a.gb, a.gb.g[b / per], b % per, a.ne, a.nn);
 }
 
 __global__ __launch_bounds__(256) void k_prep_c(PrepArgs a) {
@@ -2204,8 +2414,11 @@ int sparse_items(SparseState& S, const int32_t* tree_ptr, const int64_t* rootind
 
 int sparse_conv2(SparseState& S, const float* H1, const int32_t* tree_ptr, const int64_t* rootindex,
                  float* Z2, KeepSrc keep, hipStream_t s) {
-  hipLaunchKernelGGL(k_conv2_sparse, dim3(unsigned(S.max_items), 2), dim3(256), 0, s, S, H1,
-                     tree_ptr, rootindex, Z2, keep);
+  if (BGCN_C2_HALF)
+    hipLaunchKernelGGL(k_conv2_half, dim3(unsigned(2 * S.max_items), 2), dim3(256), 0, s, S, H1, Z2, keep);
+  else
+    hipLaunchKernelGGL(k_conv2_sparse, dim3(unsigned(S.max_items), 2), dim3(256), 0, s, S, H1,
+                       tree_ptr, rootindex, Z2, keep);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
@@ -2339,15 +2552,14 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
     PrepArgs ax = a;           // X chain: tree items, the pass over X, the CSC of X
     ax.nsel = 0; ax.nce = 0; ax.ntile = 0; ax.ne = 0; ax.nn = 0; ax.np = 0;
     if (ag.nsel > 0) {
-      if (bt->x_dtype == BGCN_DTYPE_BF16) hipLaunchKernelGGL(k_prep_b<bf16_t>, dim3(unsigned(ag.nsel)), blk, 0, g, ag);
-      else hipLaunchKernelGGL(k_prep_b<float>, dim3(unsigned(ag.nsel)), blk, 0, g, ag);
+      hipLaunchKernelGGL(k_prep_select, dim3(unsigned(ag.nsel)), blk, 0, g, ag);
       BGCN_CHECK_LAUNCH();
     }
     if (ag.nce > 0) hipLaunchKernelGGL(k_prep_c, dim3(unsigned(2 * ag.nce)), blk, 0, g, ag);
     if (ag.ntile > 0) hipLaunchKernelGGL(k_prep_d, dim3(unsigned(2 * ag.ntile)), blk, 0, g, ag);
     if (ag.ne + ag.nn > 0) hipLaunchKernelGGL(k_prep_e, dim3(unsigned(2 * (ag.ne + ag.nn))), blk, 0, g, ag);
     if (ag.ne + ag.nn + ag.np > 0)
-      hipLaunchKernelGGL(k_prep_f, dim3(unsigned(2 * (ag.ne + ag.nn + ag.np))), blk, 0, g, ag);
+      hipLaunchKernelGGL(k_prep_f_graph, dim3(unsigned(2 * (ag.ne + ag.nn + ag.np))), blk, 0, g, ag);
     BGCN_CHECK_LAUNCH();
     timing_begin(7, s);
     ax.span = span_slot(7);

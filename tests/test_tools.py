@@ -87,5 +87,7 @@ def test_ab_variant_env(monkeypatch):
     assert ab.variant_env("build/variants/libbgcn_x.so")["BGCN_LIB"].endswith("build/variants/libbgcn_x.so")
     e = ab.variant_env("BGCN_PREP_LANES=1,BGCN_X6_PIPE=0")
     assert e["BGCN_PREP_LANES"] == "1" and e["BGCN_X6_PIPE"] == "0" and "BGCN_LIB" not in e
+    e = ab.variant_env("build/variants/libbgcn_x.so,BGCN_PREP_BLOCKS=256")
+    assert e["BGCN_LIB"].endswith("libbgcn_x.so") and e["BGCN_PREP_BLOCKS"] == "256"
     with pytest.raises(SystemExit):
         ab.variant_env("nonsense")

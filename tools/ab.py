@@ -4,10 +4,10 @@
                        [--steps 200] [--warmup 10] [--bench-args "--feat-mode dense"]
                        [--probe "tools/agg_probe.py --graphs td"] [--out gpurun_out/ab.txt]
 
-A VARIANT is ``base`` (the in-tree library, the default), a library built with other
-compile-time knobs (a path ending in ``.so``, selected per run through BGCN_LIB), or one or
-more comma-separated ``NAME=VALUE`` environment overrides the library reads per call
-(``BGCN_PREP_LANES=1``, ``BGCN_X6_PIPE=0,BGCN_GEMM_X6=1``).  Every (rep, workload, variant)
+A VARIANT is ``base`` (the in-tree library, the default), or comma-separated items: a
+library built with other compile-time knobs (a path ending in ``.so``, selected per run
+through BGCN_LIB) and/or ``NAME=VALUE`` environment overrides the library reads per call
+(``BGCN_PREP_LANES=1``, ``BGCN_X6_PIPE=0,BGCN_GEMM_X6=1``, ``v.so,BGCN_PREP_BLOCKS=256``).  Every (rep, workload, variant)
 runs as its own child process with its own time limit - reps outermost, so box drift shows
 up as spread rather than as a difference - and prints one line: the bench's trees/s,
 ms/step, the roofline kernel's span and fraction, and the standalone pass's paced /
@@ -35,10 +35,10 @@ def variant_env(v: str) -> dict:
     env.pop("BGCN_LIB", None)
     if v == "base":
         return env
-    if v.endswith(".so"):
-        env["BGCN_LIB"] = os.path.abspath(v)
-        return env
     for kv in v.split(","):
+        if kv.endswith(".so"):       # a library variant (may be combined with NAME=VALUE items)
+            env["BGCN_LIB"] = os.path.abspath(kv)
+            continue
         k, _, val = kv.partition("=")
         if not k or not _:
             raise SystemExit(f"bad variant {v!r}: base, a .so path or NAME=VALUE[,NAME=VALUE]")

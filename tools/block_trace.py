@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--mhz", type=float, default=100.0)
     ap.add_argument("--in-step", action="store_true",
                     help="record a step with the next batch's preparation running beside it")
+    ap.add_argument("--spin", type=int, default=0,
+                    help="ALU-spin iterations (tools/libinterfere.so) queued ahead of the recorded step, so the "
+                         "whole step is enqueued before its first kernel starts (as tools/trace_probe.py)")
     args = ap.parse_args()
     import bench
     from bigcn_amd import BiGCN, FusedTrainStep, _lib
@@ -61,6 +64,10 @@ def main():
         for r in readers:
             r(None, 0, 1)           # reset + enable
         fused._pending = pend
+        if args.spin:
+            sink = torch.zeros(4, device=dev)
+            Li = ctypes.CDLL(os.path.join(ROOT, "tools", "libinterfere.so"))
+            Li.ifr_alu(1, args.spin, ctypes.c_void_p(sink.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
         if args.in_step:
             fused(pool[0], next_data=pool[1])
             fused.discard_prefetch()
