@@ -956,7 +956,7 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
       BGCN_TRY(sparse_prologue(sp, a, w.node_root, s, false));
     if (sparse) {
       timing_begin(0, s);
-      BGCN_TRY(sparse_conv1_gather(sp, w.z1, s));
+      BGCN_TRY(sparse_conv1_gather(sp, w.z1, s, a->rootindex, keep.scale()));
       timing_end(0, s);
     }
     if (dense_launched(a, sp))

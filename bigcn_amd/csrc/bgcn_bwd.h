@@ -276,7 +276,7 @@ __device__ inline void dw2_bf16_body(const bf16_t* __restrict__ X, int64_t ldx, 
 // dW2_d[o][c] = sum_s part[d][s][o][c] (fixed order) for c < ldp; the dense config
 // reduces all 64+F columns, the sparse config the relu(H1) block (the root columns come
 // from the root-column body).  A 256-thread group owns 64 consecutive outputs (a tile);
-// its 4 waves take splits s = q (mod 4), four loads in flight each, combined in wave
+// its 4 waves take splits s = q (mod 4), eight loads in flight each, combined in wave
 // order: deterministic.  A 1024-thread block runs 4 groups on 4 consecutive tiles and
 // strides over the tiles in step (every group passes the same barriers); `blocks` of
 // the configuration share the tiles, so a small grid retires cheaply when the gate
@@ -308,10 +308,12 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
     float acc = 0.f;
     int s = q;
     if (valid) {
-      for (; s + 12 < S; s += 16) {
-        const float v0 = p[int64_t(s) * per], v1 = p[int64_t(s + 4) * per];
-        const float v2 = p[int64_t(s + 8) * per], v3 = p[int64_t(s + 12) * per];
-        acc += v0; acc += v1; acc += v2; acc += v3;
+      for (; s + 28 < S; s += 32) {   // eight loads in flight, summed in split order
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[int64_t(s + 4 * u) * per];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
       }
       for (; s < S; s += 4) acc += p[int64_t(s) * per];
     }

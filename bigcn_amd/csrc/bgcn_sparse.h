@@ -53,6 +53,13 @@ struct SparseState {
   int32_t* bstatus = nullptr;     // batch status word (bit 0: a batch id outside [0, B)), or nullptr
   const int32_t* root_map = nullptr;   // node -> its tree's root (the CSC placement flags root rows)
   int conv1_clears = 0;           // conv1's block 0 clears zero_word / rtick (no prologue launch)
+  // per tree and direction, conv2's root-slot B operand (2 relu(x_root,col_s) W2_d^T[64 + col_s],
+  // split three ways) built by extra blocks of conv1's launch (rimg_ready): conv2's fill then
+  // copies it instead of walking root -> ELL slots -> W2^T rows
+  __bf16* rimg = nullptr;         // [B][2][3][64 o][kCap] bf16
+  uint32_t* rcols = nullptr;      // [B][kCap] H + col_s of the root's ELL slots (0 past nnz)
+  int32_t* rinfo = nullptr;       // [B] the root row's non-zero count (ELL + spill)
+  int rimg_ready = 0;
 };
 // The weight images of the sparse path in a caller-owned persistent buffer
 // (bgcn_weight_images_size): kept current by bgcn_adam_step, so a step whose images are
@@ -85,7 +92,9 @@ struct Prepared;
 int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
                    const int64_t* batch, const int64_t* rootindex, const void* X, int xdt, int64_t ldx,
                    hipStream_t s, int part = 3, const bgcn_batch* csr = nullptr);
-int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s);
+// rootindex (optional): also build conv2's per-tree root images (SparseState::rimg) in the launch
+int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s, const int64_t* rootindex = nullptr,
+                        float sc = 1.f);
 int sparse_compact_conv1(SparseState& S, const void* X, int xdt, int64_t ldx, float* Z1,
                          hipStream_t s);
 int sparse_items(SparseState& S, const int32_t* tree_ptr, const int64_t* rootindex, hipStream_t s);

@@ -672,18 +672,64 @@ __device__ __forceinline__ float4 conv1_half_entries(const SparseState& S, int32
   }
   return acc;
 }
-// Blocks [0, kLongRowBlocks): the long rows (conv1_long_rows); then two rows per wave.
+// conv2's root-slot B operand of tree b, direction d (SparseState::rimg): slot s of the
+// root's ELL list holds 2 relu(x_root,col_s) W2_d^T[64 + col_s] at k = (s & 1) 16 + (s >> 1)
+// of the image's 32-wide rows, split hi / mid / lo - the operand conv2's fill built per item
+// from three dependent loads (item root -> its ELL slots -> W2^T rows); one block per (tree,
+// direction) of conv1's launch, where the chain has the loads' latency to spare.
+__device__ inline void root_image_block(const SparseState& S, const int64_t* __restrict__ rootindex, float sc,
+                                        int blk) {
+  const int b = blk >> 1, d = blk & 1;
+  const int64_t r0 = rootindex[b];
+  const int64_t r = r0 >= 0 && r0 < S.N ? r0 : 0;   // (a bad root id is flagged by the batch checks)
+  const int rn_all = S.nnz[r];
+  const int rn = min(rn_all, kCap);
+  const float* w2t = S.w2t + int64_t(d) * (S.F + H) * H;
+  __bf16* img = S.rimg + (int64_t(b) * 2 + d) * 3 * H * kCap;
+  if (d == 0 && threadIdx.x < kCap)
+    S.rcols[int64_t(b) * kCap + threadIdx.x] = threadIdx.x < rn ? uint32_t(H + S.cols[r * kCap + threadIdx.x]) : 0u;
+  if (d == 0 && threadIdx.x == 0) S.rinfo[b] = rn_all;
+  for (int e = threadIdx.x; e < kCap * (H / 4); e += int(blockDim.x)) {
+    const int s = e >> 4, q = (e & 15) * 4;
+    const int64_t slot = r * kCap + s;
+    const int32_t col = min(max(S.cols[slot], 0), int32_t(S.F - 1));
+    const float val = S.vals[slot];
+    const float4 w = ld4(w2t + int64_t(H + col) * H + q);
+    const float av = s < rn ? sc * fmaxf(val, 0.f) : 0.f;
+    const float vv[4] = {av * w.x, av * w.y, av * w.z, av * w.w};
+    const int k = (s & 1) * (kCap / 2) + (s >> 1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      __bf16 x, y, z;
+      split3_bf16(vv[u], x, y, z);
+      const int64_t o = int64_t(q + u) * kCap + k;
+      img[o] = x;
+      img[H * kCap + o] = y;
+      img[2 * H * kCap + o] = z;
+    }
+  }
+}
+
+// Blocks [0, nroot): conv2's root images (root_image_block, 2 per tree when the caller wants
+// them, else none); then [nroot, nroot + kLongRowBlocks): the long rows (conv1_long_rows);
+// then two rows per wave.
 template <int kStep>
-__global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __restrict__ Z1) {
+__global__ __launch_bounds__(256) void k_conv1_rows2(SparseState S, float* __restrict__ Z1,
+                                                     const int64_t* __restrict__ rootindex, float sc, int nroot) {
   BT_BEGIN
   conv1_clears(S);
   if (!use_sparse(S)) return;
-  if (blockIdx.x < kLongRowBlocks) {
-    conv1_long_rows(S, Z1, int(blockIdx.x), kLongRowBlocks);
+  if (int(blockIdx.x) < nroot) {
+    root_image_block(S, rootindex, sc, int(blockIdx.x));
+    return;
+  }
+  const int bx = int(blockIdx.x) - nroot;
+  if (bx < kLongRowBlocks) {
+    conv1_long_rows(S, Z1, bx, kLongRowBlocks);
     return;
   }
   const int lane = threadIdx.x & 63, hl = lane & 31;
-  const int64_t i = (int64_t(blockIdx.x - kLongRowBlocks) * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const int64_t i = (int64_t(bx - kLongRowBlocks) * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   const bool live = i < S.N;
   const int64_t ic = live ? i : S.N - 1;
   const int nall = live ? S.nnz[ic] : 0;
@@ -1000,7 +1046,20 @@ __global__ __launch_bounds__(256) void k_conv2_sparse(SparseState S, const float
 #ifndef BGCN_C2_HALF
 #define BGCN_C2_HALF 1
 #endif
-__global__ __launch_bounds__(256) void k_conv2_half(SparseState S, const float* __restrict__ H1,
+// 1: conv2_half copies per-tree root images that extra blocks of conv1's launch build (one
+// dependent level less in conv2's fill).  Measured (profiles/r05_pass_regs_ab.txt,
+// r05_timeline_*_rimg.txt): conv1 alone 15.6 -> 19.5 us for its 2B extra blocks, conv2
+// unchanged (20.6 -> 20.2), the step not faster - off.
+#ifndef BGCN_C2H_WAVES
+#define BGCN_C2H_WAVES 1   // min waves per SIMD (register budget: 5 -> <= 96, beside two waves of the pass)
+#endif
+#ifndef BGCN_C2H_PREFETCH
+#define BGCN_C2H_PREFETCH 1
+#endif
+#ifndef BGCN_C2_RIMG
+#define BGCN_C2_RIMG 0
+#endif
+__global__ __launch_bounds__(256, BGCN_C2H_WAVES) void k_conv2_half(SparseState S, const float* __restrict__ H1,
                                                     float* __restrict__ Z2, KeepSrc keep) {
   BT_BEGIN
   if (!use_sparse(S)) return;
@@ -1017,23 +1076,20 @@ __global__ __launch_bounds__(256) void k_conv2_half(SparseState S, const float* 
   const int64_t i = i0 + r32;
   const bool ok = i < end;
   const bool live = i0 < end;                        // wave-uniform: the wave has a tile
-  // this lane's A-fragment rows, requested first (clamped: a row past the item reads the
-  // item's last row and is masked by `ok`)
+  // this lane's A-fragment rows (clamped: a row past the item reads the item's last row and
+  // is masked by `ok`), requested before the fill (BGCN_C2H_PREFETCH) or after it - the
+  // latter keeps the 32 registers free during the fill: 114 -> ~84 per wave, so the kernel
+  // fits beside two waves of the pass over X (2 x 208 + 96 <= 512) on every CU
   float4 hv[8];
-  {
-    const float* src = H1 + min<int64_t>(i, end - 1) * (2 * H) + d * H + 32 * h;
+  const float* hsrc = H1 + min<int64_t>(i, end - 1) * (2 * H) + d * H + 32 * h;
+  if (BGCN_C2H_PREFETCH) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) hv[u] = ld4(src + 4 * u);
+    for (int u = 0; u < 8; ++u) hv[u] = ld4(hsrc + 4 * u);
   }
   const int64_t r = S.item_root[item];
-  const int rn_all = S.nnz[r];
-  const int rn = min(rn_all, kCap);
-  const int mh = (rn + 1) / 2;
   const float sc = keep.scale();
   const int64_t K2 = S.F + H;
   const float* w2t = S.w2t + int64_t(d) * K2 * H;
-  if (threadIdx.x < kCap)
-    rk[threadIdx.x] = threadIdx.x < rn ? uint32_t(H + S.cols[r * kCap + threadIdx.x]) : 0u;
   {
     const __bf16* src = S.w2s + int64_t(d) * 3 * H * kW2sLd;
     for (int e = threadIdx.x; e < 3 * H * 8; e += 256) {
@@ -1042,7 +1098,26 @@ __global__ __launch_bounds__(256) void k_conv2_half(SparseState S, const float* 
           *reinterpret_cast<const uint4*>(src + (int64_t(part) * H + o) * kW2sLd + q);
     }
   }
-  for (int e = threadIdx.x; e < kCap * (H / 4); e += 256) {
+  int rn_all;
+  if (S.rimg_ready) {   // the tree's root image from conv1's launch: one dependent level
+    const int b = S.item_tree[item];
+    rn_all = S.rinfo[b];
+    if (threadIdx.x < kCap) rk[threadIdx.x] = S.rcols[int64_t(b) * kCap + threadIdx.x];
+    const __bf16* img = S.rimg + (int64_t(b) * 2 + d) * 3 * H * kCap;
+    for (int e = threadIdx.x; e < 3 * H * (kCap / 8); e += 256) {   // 16-byte pieces: 4 per 32-wide row
+      const int part = e / (H * 4), o = (e / 4) % H, q = (e % 4) * 8;
+      *reinterpret_cast<uint4*>(&Bs[part][o * kC2Ld16 + H + q]) =
+          *reinterpret_cast<const uint4*>(img + (int64_t(part) * H + o) * kCap + q);
+    }
+  } else {
+    rn_all = S.nnz[r];
+  }
+  const int rn = min(rn_all, kCap);
+  const int mh = (rn + 1) / 2;
+  (void)mh;
+  if (!S.rimg_ready && threadIdx.x < kCap)
+    rk[threadIdx.x] = threadIdx.x < rn ? uint32_t(H + S.cols[r * kCap + threadIdx.x]) : 0u;
+  for (int e = threadIdx.x; !S.rimg_ready && e < kCap * (H / 4); e += 256) {
     const int s = e >> 4, q = (e & 15) * 4;
     const int64_t slot = r * kCap + s;
     const int32_t col = min(max(S.cols[slot], 0), int32_t(S.F - 1));
@@ -1059,6 +1134,10 @@ __global__ __launch_bounds__(256) void k_conv2_half(SparseState S, const float* 
   }
   __syncthreads();
   BT_MARK(2, 0);
+  if (!BGCN_C2H_PREFETCH) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) hv[u] = ld4(hsrc + 4 * u);
+  }
   // a wave without a tile (the half's last tiles past a short item) computes nothing but
   // stays for the spill rounds' barriers
   const uint32_t ni = uint32_t(ok ? i : beg);
@@ -1817,6 +1896,10 @@ constexpr int kSliceW = 2 * H / kSlices;          // outputs per slice
 constexpr int kSliceLanes = kSliceW / 4;          // lanes per entry (one float4 each)
 constexpr int kSliceGroups = 64 / kSliceLanes;    // entries per gather instruction
 constexpr int kSliceDepth = BGCN_DW1_DEPTH;
+#ifndef BGCN_DW1_CSC_PF
+#define BGCN_DW1_CSC_PF 1
+#endif
+constexpr bool kDw1CscPf = BGCN_DW1_CSC_PF != 0;
 static_assert(8 % kSlices == 0 && kSliceW <= H && kSliceLanes >= 1, "slices");
 __device__ __forceinline__ float4 shfl4(float4 v, int src) {
   return make_float4(__shfl(v.x, src, 64), __shfl(v.y, src, 64), __shfl(v.z, src, 64), __shfl(v.w, src, 64));
@@ -1845,22 +1928,33 @@ __device__ inline void dw1_sliced_body(const SparseState& S, const float* __rest
                                        const float* __restrict__ dZ2, const KeepSrc& keep) {
   if (!use_sparse(S)) return;
   const int W = int(blockDim.x >> 6);
+  const int64_t F = S.F;
   const int x = bid & 7, sl_ = x % kSlices;
   const int64_t cg = int64_t(bid >> 3) * (8 / kSlices) + x / kSlices;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane / kSliceLanes, q = lane % kSliceLanes;
   const int so = kSliceW * sl_, d = so / H, oo = so % H + 4 * q;   // slice start, direction, my outputs
-  const int64_t F = S.F;
   const int64_t c = cg * W + wave;
   float4 a1 = f4zero(), a2 = f4zero();
   bool spill_root = false;
   if (c < F) {
     const int64_t beg = S.col_start[c], end = S.col_end[c];
-    for (int64_t u0 = beg; u0 < end; u0 += 64) {
-      const int64_t u = min<int64_t>(u0 + lane, end - 1);   // clamped: duplicates, x masked
-      const uint2 ent = S.csc[u];
+    // the next 64 CSC entries are requested before this chunk's gathers (BGCN_DW1_CSC_PF):
+    // loads retire in order, so they cost no wait, and the chunk loop then takes one
+    // dependent round trip less per 64 entries
+    // (32-bit entry indices: the CSC holds fewer than 2^31 entries, kSparseMaxN)
+    const int32_t be = int32_t(beg), en = int32_t(end);
+    uint2 ent_nx = be < en ? S.csc[min(be + lane, en - 1)] : make_uint2(0u, 0u);
+    for (int32_t u0 = be; u0 < en; u0 += 64) {
+      uint2 ent;
+      if constexpr (kDw1CscPf) {
+        ent = ent_nx;
+        if (u0 + 64 < en) ent_nx = S.csc[min(u0 + 64 + lane, en - 1)];
+      } else {
+        ent = S.csc[min(u0 + lane, en - 1)];   // clamped: duplicates, x masked
+      }
       const uint32_t slot = ent.x & kCscSlotMask;
-      const int n = int(min<int64_t>(64, end - u0));
+      const int n = min(64, en - u0);
       const float x_l = lane < n ? __uint_as_float(ent.y) : 0.f;
       const int32_t i_l = int32_t(slot / kCap);
       for (int j0 = 0; j0 < n; j0 += kSliceGroups * kSliceDepth) {
@@ -2041,14 +2135,17 @@ __device__ inline void prep_b_body(const PrepArgs& a) {
 
 // a.span (the kernel-timing hook, class 7): every block min's its start and max's its end
 // into the launch's wall-clock pair - the kernel's own span, as rocprofv3 reports it
-// Register budget of the pass over X: with fp32 X 1.5 blocks per CU (two waves of this
-// launch on half the SIMDs) run beside the training chain, and a chain kernel's wave shares
-// those SIMDs only if 2 x this budget + its own registers fit 512.  At its natural 201
-// (-> 208) the X-window kernels (conv2 116, the aggregations 88-116, the readout 106) fit
-// on only the CUs holding ONE block of the pass: conv2's waves ran on 124 of 256 CUs and
-// started up to 60 us late (profiles/r05_block_trace_instep*.txt).  192 leaves them 128.
+// Register budget of the pass over X (min waves per SIMD of __launch_bounds__): with fp32
+// X 1.5 blocks per CU run beside the training chain, and at the pass's natural 201 (-> 208)
+// VGPRs the X-window kernels (conv2 116, the aggregations 88-116, the readout 106) fit only
+// on the CUs holding ONE block of the pass: conv2's waves ran on 124 of 256 CUs and started
+// up to 60 us late (profiles/r05_block_trace_instep.txt).  Capping the pass (3: 168 VGPRs,
+// 4: 128, no spills) lets them in everywhere, but the step got SLOWER (twitter15 474k ->
+// 453k / 445k, profiles/r05_pass_regs_ab.txt): the pass then ran 158 instead of 121 us
+// beside a chain that was no faster - the X window is bound by the memory system, not by
+// CU room, so the pass keeps its registers.
 #ifndef BGCN_PREP_B_WAVES
-#define BGCN_PREP_B_WAVES 3
+#define BGCN_PREP_B_WAVES 2
 #endif
 template <class TX>
 __global__ __launch_bounds__(256, BGCN_PREP_B_WAVES) void k_prep_b(PrepArgs a) {
@@ -2113,7 +2210,10 @@ __global__ __launch_bounds__(256) void k_prep_e(PrepArgs a) {
   csc_colscan_body(a.S);
 }
 
-__global__ __launch_bounds__(256) void k_prep_f(PrepArgs a) {
+#ifndef BGCN_PREP_F_WAVES
+#define BGCN_PREP_F_WAVES 2   // (3 caps the CSC placement at 168 VGPRs with 85 spilled: not taken)
+#endif
+__global__ __launch_bounds__(256, BGCN_PREP_F_WAVES) void k_prep_f(PrepArgs a) {
   extern __shared__ __attribute__((aligned(16))) int32_t dsm[];
   int b = int(blockIdx.x);
   const int per = a.ne + a.nn + a.np;
@@ -2368,6 +2468,9 @@ size_t carve_sparse(Carve& c, int64_t N, int64_t B, int64_t F, SparseState* S) {
   t.ovf_cap = N * kSpillPerRow;             // batch brings its own)
   t.ovf = c.take<uint2>(size_t(t.ovf_cap));
   t.long_rows = c.take<int32_t>(size_t(N));
+  t.rimg = c.take<__bf16>(size_t(B) * 2 * 3 * H * kCap);
+  t.rcols = c.take<uint32_t>(size_t(B) * kCap);
+  t.rinfo = c.take<int32_t>(size_t(B));
   if (S) {
     t.mode = S->mode;
     t.flags = S->flags;
@@ -2440,12 +2543,8 @@ int sparse_csc(SparseState& S, hipStream_t s) {
 #ifndef BGCN_PREP_LANES_DEFAULT
 #define BGCN_PREP_LANES_DEFAULT 2   // profiles/r03_chain_experiments_late.txt
 #endif
-int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree_on, int mode,
-                  hipStream_t s, bool x_part) {
-  const int64_t N = bt->num_nodes, B = bt->num_graphs;
-  BGCN_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int32_t), s));
-  PrepArgs a{};
-  SparseState& S = a.S;
+// the sparse state of a prepared batch's buffers
+static void prepared_state(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode, SparseState& S) {
   S.mode = mode;
   S.N = N; S.F = F; S.B = B;
   S.max_items = int(N / kChunk + B + 1);
@@ -2457,6 +2556,15 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   S.ovf_off = p.x_ovf_off; S.ovf = p.x_ovf; S.ovf_cap = p.ovf_cap; S.long_rows = p.x_long;
   S.root_map = p.node_root;
   S.bstatus = p.status;
+}
+
+int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree_on, int mode,
+                  hipStream_t s, bool x_part) {
+  const int64_t N = bt->num_nodes, B = bt->num_graphs;
+  BGCN_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int32_t), s));
+  PrepArgs a{};
+  SparseState& S = a.S;
+  prepared_state(p, N, B, F, mode, S);
   a.batch = bt->batch; a.rootindex = bt->rootindex;
   a.node_root = p.node_root; a.tree_ptr = p.tree_ptr; a.status = p.status;
   a.X = bt->x; a.ldx = bt->ldx;
@@ -2632,12 +2740,18 @@ int sparse_prepare(const Prepared& p, int64_t N, int64_t B, int64_t F, int mode,
   return (part & 2) ? sparse_csc(S, s) : BGCN_OK;
 }
 
-int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s) {
+int sparse_conv1_gather(SparseState& S, float* Z1, hipStream_t s, const int64_t* rootindex, float sc) {
+  // conv2's root images ride in this launch (BGCN_C2_HALF, BGCN_C2_RIMG; rootindex given)
+  const int nroot = (BGCN_C2_HALF && BGCN_C2_RIMG && rootindex) ? int(2 * S.B) : 0;
+  S.rimg_ready = nroot > 0 ? 1 : 0;
 #if BGCN_C1_MODE == 1
-  hipLaunchKernelGGL(k_conv1_rows2<8>, dim3(kLongRowBlocks + grid_for(S.N, 8)), dim3(256), 0, s, S, Z1);
+  hipLaunchKernelGGL(k_conv1_rows2<8>, dim3(nroot + kLongRowBlocks + grid_for(S.N, 8)), dim3(256), 0, s, S, Z1,
+                     rootindex, sc, nroot);
 #elif BGCN_C1_MODE == 2
-  hipLaunchKernelGGL(k_conv1_rows2<4>, dim3(kLongRowBlocks + grid_for(S.N, 8)), dim3(256), 0, s, S, Z1);
+  hipLaunchKernelGGL(k_conv1_rows2<4>, dim3(nroot + kLongRowBlocks + grid_for(S.N, 8)), dim3(256), 0, s, S, Z1,
+                     rootindex, sc, nroot);
 #else
+  S.rimg_ready = 0;
   hipLaunchKernelGGL(k_conv1_gather, dim3(grid_for(S.N, (kC1Threads / 64) * kC1Rows)), dim3(kC1Threads), 0, s,
                      S, Z1);
 #endif

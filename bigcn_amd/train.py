@@ -67,6 +67,8 @@ class FusedTrainStep:
     """``step = FusedTrainStep(model)``; ``loss = step(batch)`` per training batch.
 
     ``model``: :class:`bigcn_amd.BiGCN` / :class:`bigcn_amd.Net` (hid = out = 64).
+    The loss a step returns is a 0-dim device tensor that keeps its value for the next
+    4095 steps (a ring of loss slots: no allocation per step).
     ``optimizer``: a :class:`FusedAdam` over the model's parameters (default: the
     reference's three groups, :func:`bigcn_amd.optim.bigcn_adam`).  Gradients live in
     ``self.bucket`` (``grads()`` maps them back to the parameters)."""
@@ -136,6 +138,14 @@ class FusedTrainStep:
         self._images = None
         self._images_F = None
         self._images_key = None
+        # Per-step device buffers are kept and reused (a torch.empty per buffer and step cost
+        # ~9 us of host time each in the host-fed loop, tools/host_profile.py): the step
+        # workspace, two prepared-batch buffers taken in turn (the batch a step trains on and
+        # the next one its side lane prepares) and a ring of loss slots.  A buffer is kept per
+        # stream (a call on another stream allocates afresh).
+        self._bufs = {}
+        self._loss_ring = None
+        self._loss_at = 0
 
     def _image_key(self):
         return (self.opt.step_count, tuple(p._version for p in self._img_params),
@@ -196,10 +206,36 @@ class FusedTrainStep:
             d.drop_seed = (self._drop_seed + self._drop_count) & (2**64 - 1)
             self._drop_count += 1
 
-    def _prep_buffer(self, d, F):
+    def _buffer(self, key, nbytes: int) -> torch.Tensor:
+        dev = self.status.device
+        stream = stream_handle()
+        b = self._bufs.get(key)
+        if b is None or b[0].numel() < nbytes or b[1] != stream:
+            # headroom: batches of one workload vary in size around their mean
+            self._bufs[key] = b = (workspace(int(nbytes * 1.25) + 4096, dev), stream)
+        return b[0]
+
+    def _prep_buffer(self, d, F, avoid=None):
+        """One of the two prepared-batch buffers, not ``avoid`` (the buffer of the batch the
+        call trains on, while the other receives the next batch's preparation)."""
         L = _lib.lib()
         n = L.bgcn_prepare_workspace_size(d.num_nodes, d.num_graphs, F, d.td_num_edges, d.bu_num_edges)
-        return workspace(n, self.status.device)
+        for k in (0, 1):
+            b = self._bufs.get(("prep", k))
+            if avoid is not None and b is not None and b[0] is avoid:
+                continue
+            return self._buffer(("prep", k), n)
+        raise AssertionError("unreachable")
+
+    def _loss_slot(self, dev) -> torch.Tensor:
+        """A 0-dim fp32 device slot for the step's loss, from a ring of 4096: a returned loss
+        tensor holds its value for the next 4095 calls."""
+        if self._loss_ring is None or self._loss_ring.device != dev:
+            self._loss_ring = torch.empty(4096, dtype=torch.float32, device=dev)
+            self._loss_at = 0
+        k = self._loss_at
+        self._loss_at = (k + 1) % 4096
+        return self._loss_ring[k]
 
     def forward_backward(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None,
                          next_data=None, defer_dw1: bool = False):
@@ -248,7 +284,7 @@ class FusedTrainStep:
         nxt = None
         if next_data is not None:
             nd, nkeep = self._desc(next_data)
-            nbuf = self._prep_buffer(nd, F)
+            nbuf = self._prep_buffer(nd, F, avoid=prep)
             self._next_desc = nd                     # the struct must outlive the call
             a.next = ctypes.pointer(self._next_desc)
             a.next_prepared, a.next_prepared_bytes = ptr(nbuf), nbuf.numel()
@@ -257,7 +293,7 @@ class FusedTrainStep:
             a.next = None
             a.next_prepared, a.next_prepared_bytes = 0, 0
         self.last_drop_seed = int(a.cur.drop_seed) if a.cur.td_droprate > 0 or a.cur.bu_droprate > 0 else None
-        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        loss = self._loss_slot(dev)
         a.loss, a.logp, a.status = ptr(loss), ptr(logp), ptr(self.status)
         a.status_flag = ptr(self.bucket.flag)
         a.status_seen = ptr(self.status_seen)
@@ -266,8 +302,8 @@ class FusedTrainStep:
         a.images_current = int(self._images_key is not None and self._images_key == self._image_key())
         L = _lib.lib()
         N, B = d.num_nodes, d.num_graphs
-        ws = workspace(L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
-                                                        d.bu_num_edges), dev)
+        ws = self._buffer("ws", L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
+                                                                 d.bu_num_edges))
         # every branch the step forks joins back into the caller's stream inside the call
         # (the workspace can return to the allocator afterwards), except the next batch's
         # preparation, which outlives the call: its buffer is held in self._pending until
@@ -284,7 +320,7 @@ class FusedTrainStep:
                 self._join_side()        # nothing may still write the buffer once it is freed
                 self._pending = None
             raise
-        return loss.view(())
+        return loss
 
     def evaluate(self, data, next_data=None, logp: Optional[torch.Tensor] = None, pred: bool = False):
         """One evaluation batch of the reference's test loop (``BiGCN_Twitter.py:207-222``:
@@ -332,7 +368,7 @@ class FusedTrainStep:
         nxt = None
         if next_data is not None:
             nd, nkeep = self._desc(next_data, drop=False)
-            nbuf = self._prep_buffer(nd, F)
+            nbuf = self._prep_buffer(nd, F, avoid=prep)
             self._next_desc = nd
             a.next = ctypes.pointer(self._next_desc)
             a.next_prepared, a.next_prepared_bytes = ptr(nbuf), nbuf.numel()
@@ -352,8 +388,8 @@ class FusedTrainStep:
         a.images_current = int(current)
         L = _lib.lib()
         N, B = d.num_nodes, d.num_graphs
-        ws = workspace(L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
-                                                        d.bu_num_edges), dev)
+        ws = self._buffer("ws", L.bgcn_train_step_workspace_size(N, B, F, self.num_classes, d.td_num_edges,
+                                                                 d.bu_num_edges))
         self._stream = stream_handle()
         self._pending = nxt
         try:
@@ -426,7 +462,7 @@ class FusedTrainStep:
     def saved_activations(self):
         """(H1, H2) of the last step: the pre-relu conv1 / conv2 outputs, [N, 128] fp32
         device tensors (TD columns [0, 64), BU [64, 128)), views of the step's workspace
-        (valid until the next step) - the per-stage intermediates the reference's
+        (valid until the next step or evaluation call) - the per-stage intermediates the reference's
         explain_PHEME.py:91-162 dumps."""
         if getattr(self, "_last", None) is None:
             raise RuntimeError("no step has run yet")

@@ -13,6 +13,9 @@ ROOT=$(pwd)
 LIGHT="--no-cpu-baseline --compare-dense 0 --compare-dropedge 0 --aggregation 0 --dropin 0 --host-fed 0 --eval-path 0"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
 for w in $WLS; do
+  # the same command without the profiler first: the profiler slows the step (its span of the
+  # pass then reads the perturbed step's), so both step times are kept side by side
+  timeout -k 10 300 python bench.py --workload $w $LIGHT > "$OUT/bench_unprofiled_$w.json" 2> "$OUT/unprofiled_$w.log"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_$w" -o run -- \
     python bench.py --workload $w $LIGHT > "$OUT/bench_under_rocprof_$w.json" 2> "$OUT/stats_$w.log"
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$w" -- \
