@@ -16,6 +16,7 @@ Infinity Cache).  Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import platform
@@ -368,15 +369,18 @@ def compaction_standalone(fused, b, wl, iters: int = 10):
     return out
 
 
-def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int, trees: int):
+def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int, trees: int,
+                   native: bool = True):
     """SURVEY.md 8(f) row 1 / 8(d) "staging reported separately": the same training step fed
     from the host the way the reference's loop is (BiGCN_Twitter.py:168,174-176:
-    DataLoader(..., shuffle=True, num_workers=5) -> Batch_data.to(device)) - a real
-    torch.utils.data.DataLoader with worker processes over a packed store of synthetic trees
-    of the workload's shape; workers collate each 128-tree batch into a shared page-locked
-    slot with x as the CSR of its non-zeros; one H2D copy per batch on a dedicated stream,
-    issued `depth` batches ahead; the step prepares the next batch from the compacted lists
-    (no pass over a dense x).  Timed: everything (loader, copies, steps, Adam)."""
+    DataLoader(..., shuffle=True, num_workers=5) -> Batch_data.to(device)) over a packed store
+    of synthetic trees of the workload's shape, each 128-tree batch collated with x as the CSR
+    of its non-zeros into a page-locked slot, one H2D copy per batch on a dedicated stream
+    issued `depth` batches ahead, the step preparing the next batch from the compacted lists
+    (no pass over a dense x).  native: libbgcn's loader (C++ collating threads,
+    feed.NativeLoader); else a torch.utils.data.DataLoader with worker processes packing into
+    a shared slot ring (feed.host_fed_loader).  Timed: everything (loader, copies, steps,
+    Adam)."""
     from bigcn_amd import feed as FD
     t0 = time.perf_counter()
     store = FD.TreeStore.synthetic(trees, wl["mean"], seed=20250205 + 9, in_feats=wl["feats"],
@@ -384,9 +388,14 @@ def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int
     t_store = time.perf_counter() - t0
     per_epoch = trees // wl["trees"]
     epochs = (steps + warmup + 4) // per_epoch + 2
-    loader = FD.host_fed_loader(store, batch_size=wl["trees"], num_workers=workers, seed=7, epochs=epochs,
-                                bf16_values=wl.get("xdtype") == "bf16")
-    xdt = torch.bfloat16 if wl.get("xdtype") == "bf16" else torch.float32
+    bf16 = wl.get("xdtype") == "bf16"
+    if native:
+        loader = FD.NativeLoader(store, batch_size=wl["trees"], num_workers=workers, seed=7, epochs=epochs,
+                                 bf16_values=bf16)
+    else:
+        loader = FD.host_fed_loader(store, batch_size=wl["trees"], num_workers=workers, seed=7, epochs=epochs,
+                                    bf16_values=bf16)
+    xdt = torch.bfloat16 if bf16 else torch.float32
     with torch.cuda.stream(stream):
         feeder = FD.DeviceFeeder(loader, dev, depth=3, x_dtype=xdt, timing=True)
         it = iter(feeder)
@@ -413,44 +422,73 @@ def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         fused.discard_prefetch()
-        # the same compacted batches resident on the device (no loader, no copies): the
-        # device-side rate of the compacted-input step
-        pool = [next(it) for _ in range(4)]
-        for k in range(6):
-            fused(pool[k % 4], next_data=pool[(k + 1) % 4])
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for k in range(steps):
-            fused(pool[k % 4], next_data=pool[(k + 1) % 4])
-        torch.cuda.synchronize()
-        dt_res = time.perf_counter() - t1
-        fused.discard_prefetch()
+        res = None
+        if native:
+            # the same compacted batches resident on the device (no loader, no copies): the
+            # device-side rate of the compacted-input step
+            pool = [next(it) for _ in range(4)]
+            for k in range(6):
+                fused(pool[k % 4], next_data=pool[(k + 1) % 4])
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for k in range(steps):
+                fused(pool[k % 4], next_data=pool[(k + 1) % 4])
+            torch.cuda.synchronize()
+            dt_res = time.perf_counter() - t1
+            fused.discard_prefetch()
+            res = {"value": round(wl["trees"] * steps / dt_res, 2), "unit": "trees/s",
+                   "ms_per_step": round(dt_res / steps * 1e3, 4),
+                   "what": "4 compacted batches resident in HBM, cycled (no loader, no H2D): "
+                           "the step without the pass over a dense x"}
+            del pool
     n, mean_bytes, copy_ms = feeder.copy_stats()
     report = fused.run_report()
-    loader.dataset.ring.close()
-    del it, feeder, loader
+    del cur, nxt, it, feeder
+    if native:
+        loader.close()
+    else:
+        loader.dataset.ring.close()
+    del loader
     dense_bytes = nodes / steps * wl["feats"] * (2 if xdt == torch.bfloat16 else 4)
-    return {"host_fed": {"value": round(wl["trees"] * steps / dt, 2), "unit": "trees/s",
-                         "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
-                         "status": report["status"], "invalid_steps": report["invalid_steps"],
-                         "host_ms_per_step_in_loader": round(t_next / steps * 1e3, 4),
-                         "host_ms_per_step_in_step_call": round(t_call / steps * 1e3, 4)},
-            "compacted_resident": {"value": round(wl["trees"] * steps / dt_res, 2), "unit": "trees/s",
-                                   "ms_per_step": round(dt_res / steps * 1e3, 4),
-                                   "what": "4 compacted batches resident in HBM, cycled (no loader, no H2D): "
-                                           "the step without the pass over a dense x"},
-            "h2d_bytes_per_batch": round(mean_bytes), "h2d_ms_per_batch": round(copy_ms, 4),
-            "h2d_gbs": round(mean_bytes / (copy_ms * 1e-3) / 1e9, 2) if copy_ms > 0 else None,
-            "dense_x_bytes_per_batch": round(dense_bytes),
-            "dense_x_h2d_ms_at_measured_rate": (round(dense_bytes / (mean_bytes / copy_ms), 3)
-                                                if mean_bytes > 0 and copy_ms > 0 else None),
-            "loader": {"num_workers": workers, "batch_size": wl["trees"], "store_trees": trees,
-                       "store_build_s": round(t_store, 2), "avg_nodes_per_batch": round(nodes / steps, 1),
-                       "copy_depth": 3},
-            "what": "torch.utils.data.DataLoader (worker processes, shuffle) over a packed tree store -> "
-                    "batch packed by the worker into a shared page-locked slot (x as CSR of its non-zeros) "
-                    "-> one H2D copy per batch on a copy stream, 3 batches ahead -> FusedTrainStep with "
-                    "next-batch prefetch and device DropEdge; whole loop timed (BiGCN_Twitter.py:168,174-176)"}
+    leg = {"value": round(wl["trees"] * steps / dt, 2), "unit": "trees/s",
+           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+           "status": report["status"], "invalid_steps": report["invalid_steps"],
+           "host_ms_per_step_in_loader": round(t_next / steps * 1e3, 4),
+           "host_ms_per_step_in_step_call": round(t_call / steps * 1e3, 4),
+           "loader": ({"kind": "native (feed.NativeLoader: libbgcn bgcn_loader_*, C++ collating threads)",
+                       "threads": workers} if native else
+                      {"kind": "torch.utils.data.DataLoader, worker processes, shared slot ring "
+                               "(feed.host_fed_loader)", "num_workers": workers}),
+           "h2d_bytes_per_batch": round(mean_bytes), "h2d_ms_per_batch": round(copy_ms, 4),
+           "h2d_gbs": round(mean_bytes / (copy_ms * 1e-3) / 1e9, 2) if copy_ms > 0 else None}
+    out = {"leg": leg, "store_build_s": round(t_store, 2), "avg_nodes_per_batch": round(nodes / steps, 1),
+           "dense_x_bytes_per_batch": round(dense_bytes),
+           "dense_x_h2d_ms_at_measured_rate": (round(dense_bytes / (mean_bytes / copy_ms), 3)
+                                               if mean_bytes > 0 and copy_ms > 0 else None)}
+    if res is not None:
+        out["compacted_resident"] = res
+    return out
+
+
+def staging_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int, trees: int):
+    """The host-fed legs: libbgcn's native loader (the "host_fed" figure) and the torch
+    DataLoader with worker processes beside it (the reference's loader form)."""
+    nat = host_fed_bench(fused, wl, dev, stream, steps, warmup, workers, trees, native=True)
+    dl = host_fed_bench(fused, wl, dev, stream, steps, warmup, workers, trees, native=False)
+    out = {"host_fed": nat["leg"], "host_fed_dataloader": dl["leg"],
+           "compacted_resident": nat["compacted_resident"],
+           "h2d_bytes_per_batch": nat["leg"]["h2d_bytes_per_batch"],
+           "h2d_ms_per_batch": nat["leg"]["h2d_ms_per_batch"], "h2d_gbs": nat["leg"]["h2d_gbs"],
+           "dense_x_bytes_per_batch": nat["dense_x_bytes_per_batch"],
+           "dense_x_h2d_ms_at_measured_rate": nat["dense_x_h2d_ms_at_measured_rate"],
+           "store": {"trees": trees, "build_s": nat["store_build_s"],
+                     "avg_nodes_per_batch": nat["avg_nodes_per_batch"], "batch_size": wl["trees"],
+                     "copy_depth": 3},
+           "what": "a packed tree store -> each batch collated (x as CSR of its non-zeros) into a page-locked "
+                   "slot by loader threads / worker processes -> one H2D copy per batch on a copy stream, "
+                   "3 batches ahead -> FusedTrainStep with next-batch prefetch and device DropEdge; whole "
+                   "loop timed (BiGCN_Twitter.py:168,174-176)"}
+    return out
 
 
 def main():
@@ -565,13 +603,16 @@ def main():
             opt.step()
         return loss
 
-    def run(mode: str, steps: int, warmup: int):
+    def run(mode: str, steps: int, warmup: int, timing: bool = True):
         with torch.cuda.stream(stream):
-            return run_on_stream(mode, steps, warmup)
+            return run_on_stream(mode, steps, warmup, timing)
 
-    def run_on_stream(mode: str, steps: int, warmup: int):
+    def run_on_stream(mode: str, steps: int, warmup: int, timing: bool = True):
         model.feat_mode = mode
-        timing = not args.no_kernel_timing
+        # the kernel-timing hook records HIP events around the timed class: on the per-op
+        # path those land on the caller's stream, each a queue-draining barrier (~6 us), so
+        # the drop-in leg runs without it (it reports no roofline)
+        timing = timing and not args.no_kernel_timing
         # warm-up: every kernel class timed (after the first step, which pays one-time
         # code-object loading), to find the dominant one; the timed loop then records
         # events only around that class (2 events per step)
@@ -682,11 +723,21 @@ def main():
                 "loss": float(loss.item()), "status": int(v[0]), "invalid_steps": int(v[1])}
 
     main_res = run(args.feat_mode, args.steps, args.warmup)
+
+    def fresh_allocator():
+        # each comparison leg starts from the caching allocator state a fresh process would
+        # have: the blocks earlier legs cached (and their pending stream uses) made the
+        # per-op leg's ~40 allocations per step slower (host enqueue 0.47 vs 0.28 ms per step)
+        torch.cuda.synchronize()
+        gc.collect()
+        torch.cuda.empty_cache()
     dense_res = None
     if world == 1 and args.feat_mode != "dense" and args.compare_dense:
+        fresh_allocator()
         dense_res = run("dense", max(3, args.steps // 2), 2)
     drop_res = None
     if world == 1 and args.path == "fused" and args.compare_dropedge:
+        fresh_allocator()
         other = not device_drop                         # the other DropEdge placement
         ctx["pool"] = make_pool(wl, rank, args.pool, dev, (0.0, 0.0) if other else None)
         d2 = wl["drop"] if other else (0.0, 0.0)
@@ -699,9 +750,10 @@ def main():
         # the north_star drop-in form: the reference's loop body verbatim on the per-op
         # modules (gcn_norm/CSR rebuilt every step as GCNConv does), DropEdge applied by the
         # host DataLoader as in the reference (once per pool batch here, untimed)
+        fresh_allocator()
         ctx["pool"] = make_pool(wl, rank, args.pool, dev, None)
         ctx["path"] = "autograd"
-        dropin_res = run(args.feat_mode, max(5, args.steps // 2), 3)
+        dropin_res = run(args.feat_mode, max(5, args.steps // 2), 3, timing=False)
         ctx["pool"], ctx["path"] = pool, args.path
     eval_res = None
     if world == 1 and args.path == "fused" and args.eval_path:
@@ -740,8 +792,8 @@ def main():
     staging = None
     if world == 1 and args.path == "fused" and args.host_fed and args.feat_mode == "auto":
         # same model / optimiser / DropEdge as the headline step (its state continues)
-        staging = host_fed_bench(fused, wl, dev, stream, max(20, args.steps), min(args.warmup, 10),
-                                 args.host_fed_workers, args.host_fed_trees)
+        staging = staging_bench(fused, wl, dev, stream, max(20, args.steps), min(args.warmup, 10),
+                                args.host_fed_workers, args.host_fed_trees)
     if rank == 0:
         value, dt, N_avg = main_res["value"], main_res["dt"], main_res["N_avg"]
         roof, kernels, final_loss = main_res["roof"], main_res["kernels"], main_res["loss"]

@@ -32,7 +32,7 @@ BGCN_SPARSE_CAP = 32
 BGCN_SPARSE_SPILL_PER_ROW = 32   # spill pool capacity per row (rows over the ELL cap)
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1
-ABI_VERSION = 8   # BGCN_ABI_VERSION of include/bgcn.h
+ABI_VERSION = 9   # BGCN_ABI_VERSION of include/bgcn.h
 BGCN_STATUS_CROSS_TREE = 16
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_prepare_workspace_size", "bgcn_prepare_batch", "bgcn_csr_to_dense",
     "bgcn_train_step_workspace_size", "bgcn_train_step", "bgcn_train_step_dw1", "bgcn_join_side",
     "bgcn_weight_images_size", "bgcn_train_step_saved", "bgcn_eval_step",
+    "bgcn_loader_create", "bgcn_loader_slot_bytes", "bgcn_loader_len", "bgcn_loader_next", "bgcn_loader_destroy",
 )
 
 
@@ -187,6 +188,13 @@ _SIGS = {
     "bgcn_join_side": (c_int, [c_void_p]),
     "bgcn_train_step_saved": (c_int, [c_void_p, c_size_t, c_int64, c_int64, c_int64, c_int64,
                                       POINTER(c_void_p), POINTER(c_void_p)]),
+    "bgcn_loader_create": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int, c_int, c_uint64, c_int64,
+                                   c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "bgcn_loader_slot_bytes": (c_int64, [c_void_p]),
+    "bgcn_loader_len": (c_int64, [c_void_p]),
+    "bgcn_loader_next": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_int64,
+                                 POINTER(c_void_p)]),
+    "bgcn_loader_destroy": (None, [c_void_p]),
     "bgcn_set_kernel_timing": (c_int, [c_int]),
     "bgcn_kernel_timing": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),
     "bgcn_kernel_span": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),

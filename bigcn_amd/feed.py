@@ -33,6 +33,7 @@ of the same trees (``tests/test_gpu_feed.py``).
 """
 from __future__ import annotations
 
+import ctypes
 import json
 import os
 import weakref
@@ -729,9 +730,57 @@ class DeviceFeeder:
         weakref.finalize(pb, self._release, pool).atexit = False
         return pb
 
+    def _issue_native(self):
+        """The next batch of a :class:`NativeLoader`: one library call (the loader's threads
+        packed it) that issues the copy on the copy stream."""
+        L = self.loader
+        pool, free_ev = self._take(L.slot_bytes)
+        cs = self.copy_stream
+        if free_ev is not None:
+            cs.wait_event(free_ev)
+        t0 = None
+        if self.timing:
+            t0 = torch.cuda.Event(enable_timing=True)
+            t0.record(cs)
+        got = L.next_into(pool, cs.cuda_stream)
+        if got is None:
+            self._free.append((pool, free_ev))
+            return None
+        meta, rt = got
+        ev = torch.cuda.Event(enable_timing=self.timing)
+        ev.record(cs)
+        if self.timing:
+            self._events.append((t0, ev))
+        self.bytes_copied += meta["bytes"]
+        self.batches += 1
+        pb = PackedBatch(pool[:meta["bytes"]], meta, rt, ev, self.x_dtype)
+        weakref.finalize(pb, self._release, pool).atexit = False
+        return pb
+
+    def _iter_native(self, consumer):
+        q = deque()
+        while len(q) < self.depth:
+            pb = self._issue_native()
+            if pb is None:
+                break
+            q.append(pb)
+        while q:
+            pb = q.popleft()
+            nxt = self._issue_native()   # keep `depth` copies in flight
+            if nxt is not None:
+                q.append(nxt)
+            consumer.wait_event(pb.event)
+            yield pb
+
     def __iter__(self):
         consumer = torch.cuda.current_stream(self.device)
         self._consumer = consumer
+        if isinstance(self.loader, NativeLoader):
+            if self.loader.bf16_values != (self.x_dtype == torch.bfloat16):
+                raise ValueError(f"DeviceFeeder(x_dtype={self.x_dtype}) over a NativeLoader with bf16_values="
+                                 f"{self.loader.bf16_values}: set both for the bf16 configuration")
+            yield from self._iter_native(consumer)
+            return
         it = iter(self.loader)
         q = deque()
         for hb in it:
@@ -757,6 +806,127 @@ class DeviceFeeder:
         if reset:
             self._events.clear()
         return out
+
+
+class _TreeStoreArgs(ctypes.Structure):
+    """bgcn_tree_store (include/bgcn.h)."""
+    _fields_ = [("num_trees", ctypes.c_int64), ("in_feats", ctypes.c_int64), ("tree_node", ctypes.c_void_p),
+                ("node_nnz", ctypes.c_void_p), ("entry_off", ctypes.c_void_p), ("cols", ctypes.c_void_p),
+                ("vals", ctypes.c_void_p), ("tree_edge", ctypes.c_void_p), ("edges", ctypes.c_void_p),
+                ("edges_ld", ctypes.c_int64), ("rootindex", ctypes.c_void_p), ("y", ctypes.c_void_p)]
+
+
+class _LoaderBatch(ctypes.Structure):
+    """bgcn_loader_batch (include/bgcn.h)."""
+    _fields_ = [("num_nodes", ctypes.c_int64), ("num_graphs", ctypes.c_int64), ("nnz", ctypes.c_int64),
+                ("td_num_edges", ctypes.c_int64), ("bu_num_edges", ctypes.c_int64), ("nnz_max", ctypes.c_int64),
+                ("spill", ctypes.c_int64), ("bytes", ctypes.c_int64), ("off", ctypes.c_int64 * 9),
+                ("seq", ctypes.c_int64)]
+
+
+_SECTION_NAMES = tuple(name for name, _ in _SECTIONS)
+
+
+class NativeLoader:
+    """The host-fed loader in libbgcn (``bgcn_loader_*``): ``num_workers`` C++ threads collate
+    each batch of a :class:`TreeStore` into a page-locked slot exactly as :func:`pack_batch`
+    does (byte for byte, ``tests/test_feed.py``), and :class:`DeviceFeeder` copies it to the
+    device with one call per batch - the role of the reference's ``DataLoader(traindata_list,
+    batch_size=128, shuffle=True, num_workers=5)`` (``BiGCN_Twitter.py:168``) without a
+    Python worker protocol: :func:`host_fed_loader`'s torch DataLoader spent ~170 us of the
+    main process per batch on its index queue, result unpickling, sampler and copy
+    bookkeeping.  Batches come in a Fisher-Yates order per epoch from ``seed`` (or in order
+    with ``shuffle=False``); DropEdge is drawn on the device (``FusedTrainStep``).
+    ``pinned=False``: plain host slots and no copy (``next_host``, tests)."""
+
+    def __init__(self, store, batch_size: int = 128, num_workers: int = 5, shuffle: bool = True,
+                 drop_last: bool = True, seed: Optional[int] = None, epochs: int = 1, bf16_values: bool = False,
+                 indices: Optional[Sequence[int]] = None, nslots: Optional[int] = None, pinned: bool = True):
+        from . import _lib
+        st = TreeStore.load(store, mmap=True) if isinstance(store, str) else store
+        self.store = st
+        self.bf16_values = bool(bf16_values)
+        self.batch_size = int(batch_size)
+
+        def arr(a, dt):
+            return np.ascontiguousarray(np.asarray(a), dtype=dt)
+        # the arrays the threads read, kept alive (and in the dtypes bgcn_tree_store names)
+        self._arrays = {
+            "tree_node": arr(st.tree_node, np.int64), "node_nnz": arr(st.node_nnz, np.int32),
+            "entry_off": arr(st.entry_off, np.int64), "cols": arr(st.cols, np.int32),
+            "vals": arr(st.vals, np.float32), "tree_edge": arr(st.tree_edge, np.int64),
+            "edges": arr(st.edges, np.int32).reshape(2, -1), "rootindex": arr(st.rootindex, np.int32),
+            "y": arr(st.y, np.int64)}
+        a = self._arrays
+        s = _TreeStoreArgs()
+        s.num_trees, s.in_feats = len(st), int(st.in_feats)
+        for k in ("tree_node", "node_nnz", "entry_off", "cols", "vals", "tree_edge", "edges", "rootindex", "y"):
+            setattr(s, k, a[k].ctypes.data)
+        s.edges_ld = a["edges"].shape[1]
+        self._store_args = s
+        self._indices = None if indices is None else arr(indices, np.int64)
+        n = 0 if self._indices is None else self._indices.size
+        # the host-only form needs no device (its threads only pack)
+        self._L = _lib.lib() if pinned else _lib.load_library()
+        h = ctypes.c_void_p()
+        seed = int(torch.initial_seed() if seed is None else seed) & (2**64 - 1)
+        nslots = int(nslots) if nslots is not None else max(2 * num_workers, 4) + 4
+        _lib.check(self._L.bgcn_loader_create(ctypes.addressof(s), None if self._indices is None
+                                                 else self._indices.ctypes.data, n, self.batch_size,
+                                                 int(drop_last), int(shuffle), seed, int(epochs),
+                                                 max(1, int(num_workers)), nslots, int(bf16_values),
+                                                 int(pinned), ctypes.byref(h)))
+        self._h = h
+        self._lib = _lib
+        self.slot_bytes = int(self._L.bgcn_loader_slot_bytes(h))
+        self._out = _LoaderBatch()
+        self._trees = np.empty(self.batch_size, np.int64)
+
+    def __len__(self) -> int:
+        return int(self._L.bgcn_loader_len(self._h))
+
+    def _meta(self, o) -> dict:
+        N, B, nnz, E = o.num_nodes, o.num_graphs, o.nnz, o.td_num_edges
+        counts = (N + 1, nnz, nnz, 2 * E, 2 * E, N, B, B, B + 1)
+        return {"N": N, "B": B, "nnz": nnz, "Etd": E, "Ebu": o.bu_num_edges, "in_feats": self.store.in_feats,
+                "bf16_values": self.bf16_values, "nnz_max": o.nnz_max, "spill": o.spill,
+                "layout": dict(zip(_SECTION_NAMES, zip(o.off, counts))), "bytes": o.bytes}
+
+    def next_into(self, dst: torch.Tensor, stream_handle):
+        """The next batch copied into device memory ``dst`` on ``stream_handle``: (meta, root
+        tweet ids), or None after the last batch."""
+        o = self._out
+        rc = self._L.bgcn_loader_next(self._h, dst.data_ptr(), dst.numel(), stream_handle,
+                                              ctypes.addressof(o), self._trees.ctypes.data, self._trees.size, None)
+        if rc == 1:
+            return None
+        self._lib.check(rc)
+        B = o.num_graphs
+        return self._meta(o), self.store.root_tweetid[self._trees[:B]]
+
+    def next_host(self) -> Optional[HostBatch]:
+        """(``pinned=False``) the next batch as a :class:`HostBatch` over a copy of its bytes."""
+        o = self._out
+        p = ctypes.c_void_p()
+        rc = self._L.bgcn_loader_next(self._h, None, 0, None, ctypes.addressof(o), self._trees.ctypes.data,
+                                              self._trees.size, ctypes.byref(p))
+        if rc == 1:
+            return None
+        self._lib.check(rc)
+        raw = np.ctypeslib.as_array((ctypes.c_uint8 * o.bytes).from_address(p.value)).copy()
+        self.last_trees = self._trees[:o.num_graphs].copy()
+        return HostBatch(torch.from_numpy(raw), self._meta(o), self.store.root_tweetid[self.last_trees])
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.bgcn_loader_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # interpreter shutdown
+            pass
 
 
 def host_fed_loader(store, batch_size: int = 128, num_workers: int = 5, shuffle: bool = True,

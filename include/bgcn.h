@@ -48,7 +48,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 8
+#define BGCN_ABI_VERSION 9
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -571,6 +571,47 @@ int bgcn_kernel_timing(int kernel_class, float* total_ms, int64_t* launches);
  * (hipDeviceAttributeWallClockRate), i.e. the kernel's own duration as rocprofv3 reports
  * it, without the dispatch delay an event bracket on a busy lane includes.  Synchronises. */
 int bgcn_kernel_span(int kernel_class, float* total_ms, int64_t* launches);
+
+/* ---- Native host-fed loader (ABI 9; replaces, for the fused step, the reference's
+ * DataLoader(traindata_list, batch_size, shuffle=True, num_workers=5) + Batch_data.to(device),
+ * model/Twitter/BiGCN_Twitter.py:168,174-176, and feed.py's worker-process DataLoader).
+ * A tree store (feed.TreeStore's arrays, caller-owned for the loader's lifetime): */
+typedef struct bgcn_tree_store {
+  int64_t num_trees, in_feats;
+  const int64_t* tree_node;   /* [T+1] node offsets */
+  const int32_t* node_nnz;    /* [Nall] non-zeros per node */
+  const int64_t* entry_off;   /* [T+1] non-zero offsets */
+  const int32_t* cols;        /* [nnz] ascending per node */
+  const float* vals;          /* [nnz] */
+  const int64_t* tree_edge;   /* [T+1] edge offsets */
+  const int32_t* edges;       /* [2, edges_ld]: (parent, child) in local ids */
+  int64_t edges_ld;
+  const int32_t* rootindex;   /* [T] local */
+  const int64_t* y;           /* [T] */
+} bgcn_tree_store;
+/* One packed batch: feed.pack_batch's layout (sections x_row_ptr int32 [N+1], x_col int32,
+ * x_val fp32, edge_index int64 [2,E], BU_edge_index int64 [2,E], batch int64 [N], rootindex
+ * int64 [B], y int64 [B], ptr int64 [B+1], each at a 256-byte aligned byte offset off[k]). */
+typedef struct bgcn_loader_batch {
+  int64_t num_nodes, num_graphs, nnz, td_num_edges, bu_num_edges, nnz_max, spill, bytes;
+  int64_t off[9];
+  int64_t seq;
+} bgcn_loader_batch;
+/* indices (optional): the trees of the dataset (else all); batches of batch_size in a
+ * Fisher-Yates order per epoch from `seed` (shuffle) or in order; num_threads collating
+ * threads over nslots page-locked slots (pinned = 0: plain memory, host-only use). */
+int bgcn_loader_create(const bgcn_tree_store* store, const int64_t* indices, int64_t num_indices,
+                       int64_t batch_size, int drop_last, int shuffle, uint64_t seed, int64_t epochs,
+                       int num_threads, int nslots, int bf16_values, int pinned, void** handle);
+int64_t bgcn_loader_slot_bytes(void* handle);   /* an upper bound of any batch's bytes */
+int64_t bgcn_loader_len(void* handle);          /* batches over all epochs */
+/* The next batch in order: its layout in *out, its trees (store ids) in trees[0..B) when
+ * given; with dst, one host-to-device copy of its bytes into dst on `stream` (the slot is
+ * reused once that copy completed); without dst (host-only loader), *host_bytes points at
+ * the packed bytes until the next call.  Returns 1 after the last batch. */
+int bgcn_loader_next(void* handle, void* dst, size_t dst_bytes, bgcn_stream_t stream, bgcn_loader_batch* out,
+                     int64_t* trees, int64_t trees_cap, const void** host_bytes);
+void bgcn_loader_destroy(void* handle);
 
 #ifdef __cplusplus
 }

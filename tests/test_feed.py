@@ -214,3 +214,60 @@ def test_store_rejects_bad_feature_columns():
     store.in_feats = 32          # a store whose columns reach past in_feats
     with pytest.raises(ValueError, match="outside"):
         FD.pack_batch(store, [0, 1, 2, 3])
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_native_loader_bytes_equal_pack_batch(tmp_path, bf16):
+    """The native loader (libbgcn's bgcn_loader_*: C++ threads collating into slots) packs
+    every batch byte for byte as pack_batch does (sections, offsets, sizes, bf16 rounding),
+    hands them out in order, and each epoch visits every tree once in a fresh order - on a
+    saved, memory-mapped store with rows over the ELL cap."""
+    eids = _npz_trees(tmp_path, count=9)
+    st = FD.TreeStore.from_npz_dir(str(tmp_path), eids, in_feats=64)
+    st = FD.TreeStore.load(st.save(str(tmp_path / "store")), mmap=True)
+    big = FD.TreeStore.synthetic(200, 40, seed=5, in_feats=5000, num_classes=4)
+    for store, bs in ((st, 4), (big, 16)):
+        L = FD.NativeLoader(store, batch_size=bs, num_workers=3, seed=11, epochs=3, pinned=False,
+                            bf16_values=bf16, drop_last=True)
+        per = len(store) // bs
+        assert len(L) == 3 * per
+        got = []
+        while True:
+            hb = L.next_host()
+            if hb is None:
+                break
+            ref = FD.pack_batch(store, L.last_trees, bf16_values=bf16)
+            assert hb.meta["layout"] == ref.meta["layout"]
+            for k in ("N", "B", "nnz", "Etd", "Ebu", "nnz_max", "spill", "bytes"):
+                assert hb.meta[k] == ref.meta[k], k
+            for name, _ in FD._SECTIONS:
+                assert np.array_equal(hb.section(name), ref.section(name)), name
+            assert np.array_equal(hb.root_tweetids, np.asarray(store.root_tweetid)[L.last_trees])
+            got.append(L.last_trees)
+        assert len(got) == 3 * per
+        for e in range(3):   # every tree at most once per epoch, all of the kept batches distinct
+            ep = np.concatenate(got[e * per:(e + 1) * per])
+            assert len(np.unique(ep)) == ep.size == per * bs
+        assert not all(np.array_equal(a, b) for a, b in zip(got[:per], got[per:2 * per]))
+        L.close()
+
+
+def test_native_loader_order_and_indices():
+    """shuffle=False keeps the given tree order; indices restrict the dataset; a bad index
+    is refused; the same seed gives the same batches."""
+    st = FD.TreeStore.synthetic(40, 20, seed=2, in_feats=64, num_classes=4)
+    idx = np.arange(5, 35)
+    L = FD.NativeLoader(st, batch_size=7, num_workers=2, shuffle=False, drop_last=False, indices=idx, pinned=False)
+    out = []
+    while (hb := L.next_host()) is not None:
+        out.append(L.last_trees)
+    assert np.array_equal(np.concatenate(out), idx) and [len(o) for o in out] == [7, 7, 7, 7, 2]
+    L.close()
+    with pytest.raises(Exception):
+        FD.NativeLoader(st, batch_size=4, indices=[0, 40], pinned=False)
+    runs = []
+    for _ in range(2):
+        L = FD.NativeLoader(st, batch_size=8, num_workers=4, seed=99, pinned=False)
+        runs.append([L.next_host() and L.last_trees for _ in range(len(L))])
+        L.close()
+    assert all(np.array_equal(a, b) for a, b in zip(*runs))

@@ -165,6 +165,39 @@ def test_feeder_end_to_end_matches_dense(tmp_path):
     loader.dataset.ring.close()
 
 
+def test_native_loader_feeder_end_to_end_matches_dense(tmp_path):
+    """libbgcn's native loader (C++ collating threads -> page-locked slots -> one H2D copy per
+    batch on the copy stream, feed.NativeLoader) through DeviceFeeder, in order: the device
+    bytes equal pack_batch's, the steps the same bits as the dense batches of the same trees
+    in the same order, the root tweet ids travel with each batch; recycled device buffers are
+    never overwritten while a batch (or a view of one) is alive."""
+    store = FD.TreeStore.synthetic(48, 100, seed=25, in_feats=5000)
+    path = store.save(str(tmp_path / "store"))
+    loader = FD.NativeLoader(path, batch_size=8, num_workers=3, shuffle=False, epochs=2, nslots=4)
+    feeder = FD.DeviceFeeder(loader, DEV, depth=2, timing=True)
+    got = []
+    views = []
+    for k, b in enumerate(feeder):
+        if k < 6:
+            got.append(b)
+        else:
+            views.append(b.y)          # a view kept past its batch's life
+    assert [int(b.num_graphs) for b in got] == [8] * 6
+    for k, b in enumerate(got):
+        assert np.array_equal(b.root_tweetids, store.root_tweetid[8 * k:8 * k + 8])
+        ref = FD.pack_batch(store, list(range(8 * k, 8 * k + 8)))
+        for name, _ in FD._SECTIONS:
+            assert np.array_equal(getattr(b, name).cpu().numpy().reshape(-1), ref.section(name)), name
+    torch.cuda.synchronize()
+    for k, v in enumerate(views):
+        assert torch.equal(v.cpu(), torch.as_tensor(store.y[8 * k:8 * k + 8]))
+    n, mean_bytes, ms = feeder.copy_stats()
+    assert n == 12 and mean_bytes > 0 and ms > 0
+    dense = [_dense_batch(store, range(8 * k, 8 * k + 8)) for k in range(6)]
+    _assert_same(_run(dense, 5000), _run(got, 5000))
+    loader.close()
+
+
 @pytest.mark.parametrize("bad", ["range", "order", "negative"])
 def test_bad_feature_columns_reject_the_step(bad):
     """Host-fed lists are checked on the device: a column outside [0, F), columns out of

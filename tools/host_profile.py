@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--mode", default="resident", choices=["resident", "host_fed", "dropin"])
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--loader", default="native", choices=["native", "dataloader"])
     args = ap.parse_args()
     import bench
     import torch.nn.functional as F
@@ -82,9 +83,13 @@ def main():
             from bigcn_amd import feed as FD
             store = FD.TreeStore.synthetic(2048, wl["mean"], seed=11, in_feats=wl["feats"],
                                            num_classes=wl["classes"])
-            loader = FD.host_fed_loader(store, batch_size=wl["trees"], num_workers=5, seed=7,
-                                        epochs=(2 * args.steps + args.warmup) * wl["trees"] // 2048 + 3,
-                                        bf16_values=wl.get("xdtype") == "bf16")
+            ep = (2 * args.steps + args.warmup) * wl["trees"] // 2048 + 3
+            if args.loader == "native":
+                loader = FD.NativeLoader(store, batch_size=wl["trees"], num_workers=5, seed=7, epochs=ep,
+                                         bf16_values=wl.get("xdtype") == "bf16")
+            else:
+                loader = FD.host_fed_loader(store, batch_size=wl["trees"], num_workers=5, seed=7, epochs=ep,
+                                            bf16_values=wl.get("xdtype") == "bf16")
             xdt = torch.bfloat16 if wl.get("xdtype") == "bf16" else torch.float32
             with torch.cuda.stream(stream):
                 feeder = FD.DeviceFeeder(loader, dev, depth=3, x_dtype=xdt)
