@@ -753,7 +753,8 @@ def main():
         fresh_allocator()
         ctx["pool"] = make_pool(wl, rank, args.pool, dev, None)
         ctx["path"] = "autograd"
-        dropin_res = run(args.feat_mode, max(5, args.steps // 2), 3, timing=False)
+        dropin_res = run(args.feat_mode, max(5, args.steps // 2), int(os.environ.get("BGCN_BENCH_DROPIN_WARMUP", "3")),
+                         timing=False)
         ctx["pool"], ctx["path"] = pool, args.path
     eval_res = None
     if world == 1 and args.path == "fused" and args.eval_path:

@@ -32,7 +32,7 @@ BGCN_SPARSE_CAP = 32
 BGCN_SPARSE_SPILL_PER_ROW = 32   # spill pool capacity per row (rows over the ELL cap)
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1
-ABI_VERSION = 9   # BGCN_ABI_VERSION of include/bgcn.h
+ABI_VERSION = 10   # BGCN_ABI_VERSION of include/bgcn.h
 BGCN_STATUS_CROSS_TREE = 16
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
@@ -123,6 +123,7 @@ class StepArgs(Structure):
         ("images", c_void_p), ("images_current", c_int32),
         ("status_seen", c_void_p),
         ("defer_dw1", c_int32),
+        ("adam", c_void_p),
     ]
 
 

@@ -435,6 +435,91 @@ __global__ __launch_bounds__(1024) void k_readout_fwd(const float* __restrict__ 
 // The readout backward needs no hand-off inside this launch (dhead is read by later
 // launches), so item blocks never wait for each other at any batch size.
 constexpr int kRoSlices = 16;
+// The end of an item block of the readout (k_readout_items): the per-slice
+// sums (and sign-mode positive counts) reduced in slice order, the item's counts stored, and
+// - when the item completes its tree - the tree's mean row, root half and head.  An item of
+// a multi-item tree stores its partial; the tree's last arrival (rtick) adds the partials
+// in item order (deterministic whichever block arrives last).
+template <int MC, bool kSgn>
+__device__ __forceinline__ void readout_item_finish(const SparseState& S, int blk, int64_t b, int item0, int nit,
+                                                    float4 s, float4 pc, const int32_t* __restrict__ tree_ptr,
+                                                    int64_t N, int64_t B, float* __restrict__ head,
+                                                    float* __restrict__ rpart, const HeadArgs& hd,
+                                                    float* __restrict__ cnt, const HeadRegs<MC>& hreg,
+                                                    float4 hroot, int64_t root, float4 (*red)[kRoSlices][16],
+                                                    float4 (*redc)[kRoSlices][16], float4* hrow) {
+  const int d = threadIdx.x >> 8, t = threadIdx.x & 255;
+  const int lane = t & 15, slice = t >> 4;
+  const int dd = (threadIdx.x >> 4) & 1, ll = threadIdx.x & 15;   // wave 0: (dir, lane)
+  red[d][slice][lane] = s;
+  if (kSgn) redc[d][slice][lane] = pc;
+  __syncthreads();
+  if (kSgn && blk < S.max_items && slice == 0) {   // the item's counts, slices in order
+    float4 acc = redc[d][0][lane];
+#pragma unroll
+    for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, redc[d][q][lane]);
+    st4(cnt + int64_t(blk) * (2 * H) + d * H + lane * 4, acc);
+  }
+  if (threadIdx.x >= 64) return;   // wave 0 finishes the item (and the tree)
+  bool last = true;
+  float4 acc = f4zero();
+  if (threadIdx.x < 32) {
+    acc = red[dd][0][ll];
+#pragma unroll
+    for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, red[dd][q][ll]);
+  }
+  if (nit > 1) {
+    // partials go out as agent-scope atomic stores (write-through past the XCD's L2) and
+    // are read back by the last arrival with agent-scope atomic loads: no L2 write-back /
+    // invalidate (a __threadfence per block cost the launch 13.7 -> 48 us)
+    float* p = rpart + int64_t(blk) * (2 * H) + dd * H + ll * 4;
+    if (threadIdx.x < 32) {
+      __hip_atomic_store(p + 0, acc.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 1, acc.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 2, acc.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 3, acc.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);   // the stores are acknowledged before the ticket
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    int tk = 0;
+    if (threadIdx.x == 0)
+      tk = __hip_atomic_fetch_add(&S.rtick[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tk = __shfl(tk, 0, 64);
+    last = tk == nit - 1;
+    if (last && threadIdx.x < 32) {
+      const float* q0 = rpart + int64_t(item0) * (2 * H) + dd * H + ll * 4;
+      for (int q = 0; q < nit; ++q) {
+        const float* pq = q0 + int64_t(q) * (2 * H);
+        const float4 v = make_float4(__hip_atomic_load(pq + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(pq + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                     __hip_atomic_load(pq + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        acc = q == 0 ? v : f4add(acc, v);
+      }
+    }
+  }
+  if (last) {
+    const int64_t t0 = tree_ptr[b], t1 = tree_ptr[b + 1];
+    const int base = (dd == 1 ? 0 : 2 * H) + ll * 4;   // BU first (:128)
+    if (threadIdx.x < 32) {
+      const float n = float(t1 - t0 > 0 ? t1 - t0 : 1);
+      acc = make_float4(acc.x / n, acc.y / n, acc.z / n, acc.w / n);
+      st4(head + b * (4 * H) + base, acc);
+      hrow[base / 4] = acc;
+    } else {
+      const float4 hr = (t1 > t0 && root >= 0 && root < N) ? hroot : f4zero();
+      st4(head + b * (4 * H) + base + H, hr);
+      hrow[(base + H) / 4] = hr;
+    }
+    if (hd.W != nullptr) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): wave 0's hrow writes have landed
+      __builtin_amdgcn_wave_barrier();
+      head_row(hd, b, B, hrow[threadIdx.x], hreg);
+    }
+  }
+}
+
 // kSgn = (sgn != nullptr), a template argument so no run-time test sits between the row
 // loads and their use
 template <int MC, bool kSgn>   // MC: classes of the head held in registers (HeadRegs)
@@ -505,73 +590,8 @@ __global__ __launch_bounds__(512, MC <= 4 ? 4 : 2) void k_readout_items(SparseSt
       }
     }
   }
-  red[d][slice][lane] = s;
-  if (kSgn) redc[d][slice][lane] = pc;
-  __syncthreads();
-  if (kSgn && blk < S.max_items && slice == 0) {   // the item's counts, slices in order
-    float4 acc = redc[d][0][lane];
-#pragma unroll
-    for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, redc[d][q][lane]);
-    st4(cnt + int64_t(blk) * (2 * H) + d * H + lane * 4, acc);
-  }
-  if (threadIdx.x >= 64) return;   // wave 0 finishes the item (and the tree)
-  bool last = true;
-  float4 acc = f4zero();
-  if (threadIdx.x < 32) {
-    acc = red[dd][0][ll];
-#pragma unroll
-    for (int q = 1; q < kRoSlices; ++q) acc = f4add(acc, red[dd][q][ll]);
-  }
-  if (nit > 1) {
-    // partials go out as agent-scope atomic stores (write-through past the XCD's L2) and
-    // are read back by the last arrival with agent-scope atomic loads: no L2 write-back /
-    // invalidate (a __threadfence per block cost the launch 13.7 -> 48 us)
-    float* p = rpart + int64_t(blk) * (2 * H) + dd * H + ll * 4;
-    if (threadIdx.x < 32) {
-      __hip_atomic_store(p + 0, acc.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p + 1, acc.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p + 2, acc.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p + 3, acc.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);   // the stores are acknowledged before the ticket
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    int tk = 0;
-    if (threadIdx.x == 0)
-      tk = __hip_atomic_fetch_add(&S.rtick[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    tk = __shfl(tk, 0, 64);
-    last = tk == nit - 1;
-    if (last && threadIdx.x < 32) {
-      const float* q0 = rpart + int64_t(item0) * (2 * H) + dd * H + ll * 4;
-      for (int q = 0; q < nit; ++q) {
-        const float* pq = q0 + int64_t(q) * (2 * H);
-        const float4 v = make_float4(__hip_atomic_load(pq + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                     __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                     __hip_atomic_load(pq + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                     __hip_atomic_load(pq + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        acc = q == 0 ? v : f4add(acc, v);
-      }
-    }
-  }
-  if (last) {
-    const int64_t t0 = tree_ptr[b], t1 = tree_ptr[b + 1];
-    const int base = (dd == 1 ? 0 : 2 * H) + ll * 4;   // BU first (:128)
-    if (threadIdx.x < 32) {
-      const float n = float(t1 - t0 > 0 ? t1 - t0 : 1);
-      acc = make_float4(acc.x / n, acc.y / n, acc.z / n, acc.w / n);
-      st4(head + b * (4 * H) + base, acc);
-      hrow[base / 4] = acc;
-    } else {
-      const float4 hr = (t1 > t0 && root >= 0 && root < N) ? hroot : f4zero();
-      st4(head + b * (4 * H) + base + H, hr);
-      hrow[(base + H) / 4] = hr;
-    }
-    if (hd.W != nullptr) {
-      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): wave 0's hrow writes have landed
-      __builtin_amdgcn_wave_barrier();
-      head_row(hd, b, B, hrow[threadIdx.x], hreg);
-    }
-  }
+  readout_item_finish<MC, kSgn>(S, blk, b, item0, nit, s, pc, tree_ptr, N, B, head, rpart, hd, cnt, hreg, hroot,
+                                root, red, redc, hrow);
   BT_END(5);
 }
 
@@ -1079,7 +1099,8 @@ static int forward_tail(const bgcn_bigcn_args* a, FusedWs& w, SparseState& sp, K
 // block, root partials, root columns), db1 and the gated dense dW1; joined at the end.
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
                         const Prepared* prep, bool side_busy, const HeadGradJob* head,
-                        const WeightImages* img, bool defer_dw1) {
+                        const WeightImages* img, bool defer_dw1, const TailAdam* adam, bool* adam_done) {
+  if (adam_done) *adam_done = false;
   BGCN_TRY(check_args(a, prep != nullptr));
   BGCN_CHECK_ARG(a->dhead_in && a->td_dw1 && a->bu_dw1 && a->td_dw2 && a->bu_dw2 && a->td_db1 &&
                      a->bu_db1 && a->td_db2 && a->bu_db2,
@@ -1205,7 +1226,12 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   timing_begin(5, s);
   // deferred dW1 (bgcn_train_step with defer_dw1): every gradient but dW1 is final when
   // this launch ends; bigcn_backward_dw1 runs the dW1 waves later
+  // the step's optimiser step in the same launch (bgcn_step_args.adam): on the sparse path
+  // with no dense kernel launched (the gated dense dW1 would arrive after the tail's blocks)
+  if (adam && adam->on && sparse && !dense_launched(a, sp) && !defer_dw1) t.adam = *adam;
   BGCN_TRY(bwd_tail_launch(t, s, defer_dw1 ? 1 : 0));
+  // (the launcher clears adam.on for a tail form that cannot carry it: BGCN_DW1_SPLIT != 0)
+  if (adam_done) *adam_done = t.adam.on != 0;
   timing_end(5, s);
   (void)side_busy;
   timing_end(9, s);   // the main stream's own chain (span class, bgcn_train_step)

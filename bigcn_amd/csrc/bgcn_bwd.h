@@ -283,10 +283,13 @@ __device__ inline void dw2_bf16_body(const bf16_t* __restrict__ X, int64_t ldx, 
 // skips it.
 
 constexpr int kRedSmem = 4 * 4 * 64;
+// ad (the step's fused optimiser step, sparse config only): each finished W2_d[o][c < 64]
+// gradient updates its parameter and writes the weight images (W2^T and the bf16 splits of
+// W2[:, :64]) as bgcn_optim.hip's image tiles do.
 __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K2,
                                        float* __restrict__ dw_td, float* __restrict__ dw_bu,
                                        const int32_t* __restrict__ gate, const RedCfg& c0,
-                                       const RedCfg& c1, int bid, float* smem) {
+                                       const RedCfg& c1, int bid, float* smem, const TailAdam* ad = nullptr) {
   const bool second = bid >= c0.blocks;
   const RedCfg& cfg = second ? c1 : c0;
   const int bl = second ? bid - c0.blocks : bid;
@@ -305,6 +308,16 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
     const int d = valid ? int(idx / per) : 0;
     const int64_t e = valid ? idx % per : 0;
     const float* p = part + int64_t(d) * S * per + e;
+    const int64_t o = e / ldp, cw = e % ldp;   // the gradient's W2_d[o][cw] (sparse config: cw < 64)
+    const bool fa = ad && ad->on && !cfg.want_dense && q == 0 && valid && cw < H && !ad->skip();
+    const int ka = d == 0 ? 2 : 6;
+    const int64_t ia = o * K2 + cw;
+    float ap = 0.f, am = 0.f, av = 0.f;
+    if (fa) {   // requested before the split sums
+      ap = ad->p[ka][ia];
+      am = ad->m[ka][ia];
+      av = ad->v[ka][ia];
+    }
     float acc = 0.f;
     int s = q;
     if (valid) {
@@ -319,8 +332,29 @@ __device__ inline void reduce_dw2_body(const float* __restrict__ part, int64_t K
     }
     red[q][t] = acc;
     __syncthreads();
-    if (q == 0 && valid)
-      (d == 0 ? dw_td : dw_bu)[(e / ldp) * K2 + e % ldp] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    if (q == 0 && valid) {
+      const float gsum = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+      (d == 0 ? dw_td : dw_bu)[(e / ldp) * K2 + e % ldp] = gsum;
+      if (fa) {
+        adam_elem(ap, gsum, am, av, ad->c(ka));
+        ad->p[ka][ia] = ap;
+        ad->m[ka][ia] = am;
+        ad->v[ka][ia] = av;
+        if (ad->w2t) {
+          ad->w2t[(int64_t(d) * K2 + cw) * H + o] = ap;
+          __bf16 x, y, z;
+          split3_bf16(ap, x, y, z);
+          __bf16* cs = ad->w2s + int64_t(d) * 3 * H * kW2sLd + o * kW2sLd + cw;   // conv2's [o][k]
+          cs[0] = x;
+          cs[H * kW2sLd] = y;
+          cs[2 * H * kW2sLd] = z;
+          __bf16* ds = ad->w2d + int64_t(d) * 3 * H * kW2dLd + cw * kW2dLd + o;   // the middle launch's [c][o]
+          ds[0] = x;
+          ds[H * kW2dLd] = y;
+          ds[2 * H * kW2dLd] = z;
+        }
+      }
+    }
     __syncthreads();
   }
 }

@@ -193,6 +193,46 @@ __device__ inline void head_row(const HeadArgs& hd, int64_t b, int64_t B, float4
 // per column stride the partials (p = g, g + 16, ...), the 16 group sums are then added
 // in group order - a fixed order (deterministic).  Job block jb of kColsumGroups *
 // blockDim.x / 16 ... : each block holds blockDim.x / 16 whole columns.
+// One Adam element (torch semantics, amsgrad off, L2 weight decay in the gradient):
+// bgcn_optim.hip's launch and the step's fused form (TailAdam) share it, so their bits agree.
+struct AdamConst {
+  float b1, b2, wd, eps, step, inv_bc2, gs;
+};
+// Every product and sum is spelled out (fmaf / __fmul_rn / __fadd_rn): with contraction
+// left to the compiler, the inlined copies fused a * b + c * d differently per call site and
+// the fused step's moments drifted an ulp from the separate launch's.
+__device__ __forceinline__ void adam_elem(float& p, float gr, float& m, float& v, const AdamConst& c) {
+  const float g = fmaf(c.wd, p, __fmul_rn(gr, c.gs));
+  m = fmaf(1.0f - c.b1, __fsub_rn(g, m), m);                 // exp_avg.lerp_(grad, 1 - beta1)
+  v = fmaf(1.0f - c.b2, __fmul_rn(g, g), __fmul_rn(v, c.b2));   // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+  const float denom = fmaf(sqrtf(v), c.inv_bc2, c.eps);
+  p = fmaf(-c.step, __fdiv_rn(m, denom), p);
+}
+
+// The optimiser step fused into the backward's tail launch (bgcn_step_args.adam): per step
+// parameter k (bgcn_step_args order: td_w1 td_b1 td_w2 td_b2 bu_w1 bu_b1 bu_w2 bu_b2 fc_w
+// fc_b) its Adam state and step size; the images are the step's weight images.
+constexpr int kStepParams = 10;
+struct TailAdam {
+  int on = 0;
+  const float* skip_flag = nullptr;
+  int32_t* skip_count = nullptr;
+  float b1 = 0, b2 = 0, wd = 0, eps = 0, bc1 = 1, bc2s = 1, gs = 0;
+  float* p[kStepParams] = {};
+  float* m[kStepParams] = {};
+  float* v[kStepParams] = {};
+  const float* g[kStepParams] = {};
+  float lr[kStepParams] = {};
+  int64_t n[kStepParams] = {};
+  float* w1t = nullptr;      // [F][128]
+  float* w2t = nullptr;      // [2][64+F][64]
+  __bf16* w2s = nullptr;     // [2][3][64 o][kW2sLd]
+  __bf16* w2d = nullptr;     // [2][3][64 c][kW2dLd]
+  // (the same expressions as k_adam's constants: the same bits)
+  __device__ AdamConst c(int k) const { return AdamConst{b1, b2, wd, eps, lr[k] / bc1, 1.0f / bc2s, gs}; }
+  __device__ bool skip() const { return skip_flag && *skip_flag != 0.0f; }
+};
+
 struct ColsumJob {
   const float* part;   // [P][128] or nullptr (no job)
   int P;
@@ -206,11 +246,20 @@ __host__ __device__ constexpr int colsum_job_blocks(int threads) {
 // sm: kColsumSmem floats of the caller's shared memory (a merged launch passes its role
 // buffer, so the job adds no LDS of its own to the launch)
 constexpr int kColsumSmem = kColsumGroups * 64;
-__device__ inline void colsum_job_block(const ColsumJob& j, int jb, float* sm) {
+__device__ inline void colsum_job_block(const ColsumJob& j, int jb, float* sm, const TailAdam* ad = nullptr) {
   float* red = sm;
   const int cpb = int(blockDim.x) / kColsumGroups;    // columns per block (<= 64)
   const int cl = threadIdx.x % cpb, g = threadIdx.x / cpb;
   const int c = jb * cpb + cl;
+  // the fused optimiser step (b1): the parameter's state requested before the sums
+  const bool fa = ad && ad->on && g == 0 && !ad->skip();
+  const int ka = c < 64 ? 1 : 5, ia = c & 63;
+  float ap = 0.f, am = 0.f, av = 0.f;
+  if (fa) {
+    ap = ad->p[ka][ia];
+    am = ad->m[ka][ia];
+    av = ad->v[ka][ia];
+  }
   float acc = 0.f;
   int p = g;
   for (; p + 3 * kColsumGroups < j.P; p += 4 * kColsumGroups) {   // 4 loads in flight
@@ -226,6 +275,12 @@ __device__ inline void colsum_job_block(const ColsumJob& j, int jb, float* sm) {
     float s = red[cl];
     for (int q = 1; q < kColsumGroups; ++q) s += red[q * cpb + cl];
     if (c < 64) j.out_td[c] = s; else j.out_bu[c - 64] = s;
+    if (fa) {
+      adam_elem(ap, s, am, av, ad->c(ka));
+      ad->p[ka][ia] = ap;
+      ad->m[ka][ia] = am;
+      ad->v[ka][ia] = av;
+    }
   }
 }
 
@@ -350,7 +405,7 @@ int bigcn_forward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipS
 int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s,
                         const Prepared* prep = nullptr, bool side_busy = false,
                         const HeadGradJob* head = nullptr, const WeightImages* img = nullptr,
-                        bool defer_dw1 = false);
+                        bool defer_dw1 = false, const TailAdam* adam = nullptr, bool* adam_done = nullptr);
 // the dW1 of a backward run with defer_dw1 (same arguments and buffers)
 int bigcn_backward_dw1(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s, const Prepared* prep,
                        const WeightImages* img);

@@ -18,19 +18,6 @@ namespace {
 constexpr int kChunkElems = 256 * 4;  // elements per block (256 threads x one float4)
 constexpr int H = 64;                  // rows of the conv weights with images
 
-struct AdamConst {
-  float b1, b2, wd, eps, step, inv_bc2, gs;
-};
-
-__device__ __forceinline__ void adam_elem(float& p, float gr, float& m, float& v,
-                                          const AdamConst& c) {
-  const float g = gr * c.gs + c.wd * p;
-  m = fmaf(1.0f - c.b1, g - m, m);            // exp_avg.lerp_(grad, 1 - beta1)
-  v = fmaf(1.0f - c.b2, g * g, v * c.b2);     // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-  const float denom = sqrtf(v) * c.inv_bc2 + c.eps;
-  p = p - c.step * (m / denom);
-}
-
 // four consecutive elements from e (vector when the tensor's arrays are 16-byte aligned)
 __device__ __forceinline__ void adam_quad(const bgcn_adam_tensor& T, int64_t e, int n, bool vec,
                                           const AdamConst& c, float out[4]) {

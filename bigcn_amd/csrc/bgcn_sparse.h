@@ -151,6 +151,7 @@ struct BwdTailArgs {
   const int32_t* gate;
   RedCfg red_dense, red_sparse;
   ColsumJob db1;
+  TailAdam adam;                 // the step's fused optimiser step (adam.on), part 0 only
 };
 int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s);
 int dw2_bf16_launch(BwdMidArgs& a, hipStream_t s);   // dense mode, bf16 X: dW2 root columns

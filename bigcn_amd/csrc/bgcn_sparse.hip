@@ -1925,7 +1925,8 @@ __device__ inline void dw1_sliced_body(const SparseState& S, const float* __rest
                                        float* __restrict__ dw1_td, float* __restrict__ dw1_bu,
                                        const int64_t* __restrict__ batch, float* __restrict__ dw2_td,
                                        float* __restrict__ dw2_bu, float scale, int bid, float* smem,
-                                       const float* __restrict__ dZ2, const KeepSrc& keep) {
+                                       const float* __restrict__ dZ2, const KeepSrc& keep,
+                                       const TailAdam* ad = nullptr) {
   if (!use_sparse(S)) return;
   const int W = int(blockDim.x >> 6);
   const int64_t F = S.F;
@@ -1935,6 +1936,19 @@ __device__ inline void dw1_sliced_body(const SparseState& S, const float* __rest
   const int g = lane / kSliceLanes, q = lane % kSliceLanes;
   const int so = kSliceW * sl_, d = so / H, oo = so % H + 4 * q;   // slice start, direction, my outputs
   const int64_t c = cg * W + wave;
+  // the fused optimiser step (TailAdam, kPart 0): this block's kSliceW outputs x W columns of
+  // W1_d and of W2_d's root columns - their parameters and moments requested here, beside
+  // the gathers, and updated with the finished gradients at the end
+  const bool fa = kPart == 0 && ad && ad->on && int(threadIdx.x) < kSliceW * W && !ad->skip();
+  const int ka1 = d == 0 ? 0 : 4, ka2 = d == 0 ? 2 : 6;
+  const int a_ol = int(threadIdx.x) / W, a_tx = int(threadIdx.x) % W;
+  const int64_t a_cc = min<int64_t>(cg * W + a_tx, F - 1);
+  const int64_t ia1 = int64_t(so % H + a_ol) * F + a_cc, ia2 = int64_t(so % H + a_ol) * (F + H) + H + a_cc;
+  float ap1 = 0.f, am1 = 0.f, av1 = 0.f, ap2 = 0.f, am2 = 0.f, av2 = 0.f;
+  if (fa) {
+    ap1 = ad->p[ka1][ia1]; am1 = ad->m[ka1][ia1]; av1 = ad->v[ka1][ia1];
+    ap2 = ad->p[ka2][ia2]; am2 = ad->m[ka2][ia2]; av2 = ad->v[ka2][ia2];
+  }
   float4 a1 = f4zero(), a2 = f4zero();
   bool spill_root = false;
   if (c < F) {
@@ -2058,8 +2072,42 @@ __device__ inline void dw1_sliced_body(const SparseState& S, const float* __rest
     const int64_t cc = cg * W + tx;
     if (cc >= F) continue;
     const int o = so % H + ol;
-    w1[int64_t(o) * F + cc] = t1[ol * (W + 1) + tx];
-    if (kPart != 2) w2[int64_t(o) * K2 + H + cc] = t2[ol * (W + 1) + tx];
+    const float g1 = t1[ol * (W + 1) + tx], g2 = t2[ol * (W + 1) + tx];
+    w1[int64_t(o) * F + cc] = g1;
+    if (kPart != 2) w2[int64_t(o) * K2 + H + cc] = g2;
+    if (fa && e == int(threadIdx.x)) {   // (this thread's prefetched pair: a_ol == ol, a_cc == cc)
+      adam_elem(ap1, g1, am1, av1, ad->c(ka1));
+      ad->p[ka1][ia1] = ap1; ad->m[ka1][ia1] = am1; ad->v[ka1][ia1] = av1;
+      adam_elem(ap2, g2, am2, av2, ad->c(ka2));
+      ad->p[ka2][ia2] = ap2; ad->m[ka2][ia2] = am2; ad->v[ka2][ia2] = av2;
+      if (ad->w1t) {
+        ad->w1t[cc * (2 * H) + d * H + o] = ap1;                 // W1^T[c][d*64 + o]
+        ad->w2t[(int64_t(d) * K2 + H + cc) * H + o] = ap2;       // W2^T_d[64 + c][o]
+      }
+    }
+  }
+}
+
+// The fused optimiser step's parameters without a tail role of their own (b2: the middle
+// launch's db2; the head's fc weight and bias), one extra block of the tail launch; it also
+// counts a skipped update as k_adam does.
+__device__ inline void tail_adam_block(const TailAdam& ad) {
+  if (ad.skip()) {
+    if (threadIdx.x == 0 && ad.skip_count) atomicAdd(ad.skip_count, 1);
+    return;
+  }
+  const int ks[4] = {3, 7, 8, 9};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = ks[q];
+    const AdamConst c = ad.c(k);
+    for (int64_t e = threadIdx.x; e < ad.n[k]; e += blockDim.x) {
+      float p = ad.p[k][e], m = ad.m[k][e], v = ad.v[k][e];
+      adam_elem(p, ad.g[k][e], m, v, c);
+      ad.p[k][e] = p;
+      ad.m[k][e] = m;
+      ad.v[k][e] = v;
+    }
   }
 }
 
@@ -2321,7 +2369,7 @@ __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
                      a.dZ2, a.keep);
     else if constexpr (kDw1Split == 0)
       dw1_sliced_body<kPart>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b,
-                             smem, a.dZ2, a.keep);
+                             smem, a.dZ2, a.keep, &a.adam);
     else
       dw1_body<kDw1Split, kPart>(a.S, a.dZ1, a.dw1_td, a.dw1_bu, a.batch, a.dw2_td, a.dw2_bu, a.keep_scale, b,
                                  smem, a.dZ2, a.keep);
@@ -2331,12 +2379,18 @@ __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
   if (kPart == 2) return;
   b -= a.n_dw1;
   if (b < a.red_dense.blocks + a.red_sparse.blocks) {
-    reduce_dw2_body(a.dw2_part, a.S.F + H, a.dw2_td, a.dw2_bu, a.gate, a.red_dense, a.red_sparse, b, smem);
+    reduce_dw2_body(a.dw2_part, a.S.F + H, a.dw2_td, a.dw2_bu, a.gate, a.red_dense, a.red_sparse, b, smem,
+                    &a.adam);
     BT_END(82);
     return;
   }
-  colsum_job_block(a.db1, b - a.red_dense.blocks - a.red_sparse.blocks, smem);
-  BT_END(83);
+  b -= a.red_dense.blocks + a.red_sparse.blocks;
+  if (b < colsum_job_blocks(kTailThreads)) {
+    colsum_job_block(a.db1, b, smem, &a.adam);
+    BT_END(83);
+    return;
+  }
+  if (a.adam.on) tail_adam_block(a.adam);   // the launch's last block
 }
 
 }  // namespace
@@ -2401,8 +2455,10 @@ int bwd_tail_launch(BwdTailArgs& a, hipStream_t s, int part) {
   // the reduction configurations are sized in 1024-thread blocks (4 groups of 256)
   a.red_dense.blocks *= 1024 / kTailThreads;
   a.red_sparse.blocks *= 1024 / kTailThreads;
+  if (part != 0 || split != 0) a.adam.on = 0;   // (bigcn_backward_impl only fuses into part 0's sliced form)
   const int n = part == 2 ? a.n_dw1
-                          : a.n_dw1 + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(kTailThreads);
+                          : a.n_dw1 + a.red_dense.blocks + a.red_sparse.blocks + colsum_job_blocks(kTailThreads) +
+                                (a.adam.on ? 1 : 0);
   if (n == 0) return BGCN_OK;
   if (part == 1) {
     hipLaunchKernelGGL((k_bwd_tail<1, 1>), dim3(unsigned(n)), dim3(kTailThreads), 0, s, a);

@@ -184,6 +184,39 @@ static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_
 static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w, hipStream_t s,
                            int graph_lane);
 
+// bgcn_step_args.adam as the tail's fused form: its tensors must be exactly the ten step
+// parameters (gradient pointers = the step's grads, torch's sizes), its images the step's
+static bool tail_adam_args(const bgcn_step_args* a, const WeightImages* img, TailAdam& t) {
+  const bgcn_adam_args* A = a->adam;
+  const int64_t F = a->in_feats, C = a->num_classes;
+  if (!A || A->count != kStepParams) return false;
+  const int64_t want[kStepParams] = {H * F, H, H * (H + F), H, H * F, H, H * (H + F), H, C * 4 * H, C};
+  for (int k = 0; k < kStepParams; ++k) {
+    int j = 0;
+    while (j < A->count && A->t[j].param != a->params[k]) ++j;
+    if (j == A->count || A->t[j].grad != a->grads[k] || A->t[j].numel != want[k]) return false;
+    t.p[k] = A->t[j].param;
+    t.m[k] = A->t[j].exp_avg;
+    t.v[k] = A->t[j].exp_avg_sq;
+    t.g[k] = A->t[j].grad;
+    t.lr[k] = A->t[j].lr;
+    t.n[k] = want[k];
+  }
+  if (A->images) {
+    if (A->images != a->images || A->images_in_feats != F || !img) return false;
+    t.w1t = img->w1t;
+    t.w2t = img->w2t;
+    t.w2s = img->w2s;
+    t.w2d = img->w2d;
+  }
+  t.b1 = A->beta1; t.b2 = A->beta2; t.wd = A->weight_decay; t.eps = A->eps;
+  t.bc1 = A->bias_correction1; t.bc2s = A->bias_correction2_sqrt; t.gs = A->grad_scale;
+  t.skip_flag = A->skip_flag;
+  t.skip_count = A->skip_count;
+  t.on = 1;
+  return true;
+}
+
 size_t train_step_ws_size(int64_t N, int64_t B, int64_t F, int64_t C, int64_t Etd, int64_t Ebu) {
   (void)Etd; (void)Ebu;
   Carve c(nullptr, 0);
@@ -289,7 +322,19 @@ static int train_step_body(const bgcn_step_args* a, const Prepared& p, StepWs& w
   // the side lane the dW2 chain stays on this stream, which balances the two)
   const HeadGradJob hj{w.head, w.dz, B, int(C), w.loss_row, a->grads[8], a->grads[9], a->loss,
                        a->status, a->status_flag, a->status_seen};
-  return bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr, &hj, img, a->defer_dw1 != 0);
+  TailAdam ta;
+  const bool fuse = a->adam && !a->defer_dw1 && tail_adam_args(a, img, ta);
+  bool done = false;
+  BGCN_TRY(bigcn_backward_impl(&e, w.enc, w.enc_bytes, s, &p, a->next != nullptr, &hj, img, a->defer_dw1 != 0,
+                               fuse ? &ta : nullptr, &done));
+  // the optimiser step the tail did not take: its own launch (same bits)
+  if (a->adam && !done) {
+    BGCN_CHECK_ARG(!a->defer_dw1, "adam with defer_dw1: the update needs dW1 (run bgcn_adam_step after "
+                                  "bgcn_train_step_dw1)");
+    const int rc = bgcn_adam_step(a->adam, reinterpret_cast<bgcn_stream_t>(s));
+    if (rc != BGCN_OK) return rc;
+  }
+  return BGCN_OK;
 }
 
 // One evaluation step (the test loop body, BiGCN_Twitter.py:207-222: model.eval();

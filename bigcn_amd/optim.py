@@ -72,7 +72,20 @@ class FusedAdam:
     def step(self, grads: Optional[Sequence[torch.Tensor]] = None, grad_scale: float = 1.0,
              skip_flag: Optional[torch.Tensor] = None, images=None,
              skip_count: Optional[torch.Tensor] = None) -> None:
-        """``grads`` overrides ``p.grad`` (e.g. views of a reduced flat DP bucket).
+        a = self.prepare(grads, grad_scale, skip_flag, images, skip_count)
+        self.step_count += 1
+        if a is not None:
+            check(_lib.lib().bgcn_adam_step(ctypes.addressof(a), stream_handle()))
+
+    def prepare(self, grads: Optional[Sequence[torch.Tensor]] = None, grad_scale: float = 1.0,
+                skip_flag: Optional[torch.Tensor] = None, images=None,
+                skip_count: Optional[torch.Tensor] = None):
+        """The ``bgcn_adam_args`` of the next :meth:`step` (step count + 1) without launching it
+        - for a caller that hands them to the training step (``bgcn_step_args.adam``, which
+        performs the update inside the step) and then advances ``step_count`` itself; None when
+        no parameter has a gradient.
+
+        ``grads`` overrides ``p.grad`` (e.g. views of a reduced flat DP bucket).
         ``skip_flag``: a one-element fp32 device tensor; when it holds a non-zero value at
         execution time the launch updates nothing (an invalid training step, decided on
         the device without a host sync; the step counter still advances).
@@ -84,8 +97,7 @@ class FusedAdam:
 
         Learning rates are read from ``param_groups`` on every call, so schedulers that
         edit ``group['lr']`` (as with torch.optim.Adam) take effect."""
-        self.step_count += 1
-        t = self.step_count
+        t = self.step_count + 1
         b1, b2 = self.betas
         ps = self.params()
         gs = list(grads) if grads is not None else [p.grad for p in ps]
@@ -126,7 +138,7 @@ class FusedAdam:
         keep = []   # non-contiguous gradients: contiguous copies, alive through the launch
         a, ents, groups = cached[1], cached[2], cached[3]
         if a.count == 0:
-            return
+            return None
         for e, gi, gj in zip(ents, cached[4], groups):
             gr = gs[gi]
             if not gr.is_contiguous():
@@ -151,7 +163,8 @@ class FusedAdam:
                 a.image_role[k] = roles.get(id(ps[gi]), 0)
         else:
             a.images, a.images_in_feats = None, 0
-        check(_lib.lib().bgcn_adam_step(ctypes.addressof(a), stream_handle()))
+        self._keep = keep
+        return a
 
     def _entries(self, cached):
         """params() index of each table entry (gradients that are None have no entry)."""

@@ -75,7 +75,7 @@ class FusedTrainStep:
 
     def __init__(self, model: BiGCN, optimizer: Optional[FusedAdam] = None, degree_on: Optional[str] = None,
                  group=None, tddroprate: float = 0.0, budroprate: float = 0.0,
-                 drop_seed: Optional[int] = None):
+                 drop_seed: Optional[int] = None, fuse_optimizer: Optional[bool] = None):
         self.model = model
         # DropEdge on the device (dataset.py:68-90): batches are then passed UNDROPPED
         # (BiGraphDataset(tddroprate=0, budroprate=0)) and each preparation draws its own
@@ -88,6 +88,14 @@ class FusedTrainStep:
         self.last_drop_seed = None
         self.opt = optimizer if optimizer is not None else bigcn_adam(model)
         self.group = group
+        # fuse_optimizer (single process): the optimiser step inside the training step's last
+        # launch (bgcn_step_args.adam; bit-identical to the separate bgcn_adam_step, which the
+        # library falls back to when the step cannot take it).  Off by default: its ~36 MB of
+        # parameter / moment traffic lengthens the tail by as much as the separate launch
+        # costs.  BGCN_FUSED_OPTIMIZER=1 turns it on when not given.
+        if fuse_optimizer is None:
+            fuse_optimizer = os.environ.get("BGCN_FUSED_OPTIMIZER", "0") == "1"
+        self.fuse_optimizer = bool(fuse_optimizer)
         # the conv1 weight gradients (the step's last, bgcn_train_step_dw1) at the bucket's
         # end: with world > 1 the rest of the bucket is all-reduced while they compute
         enc = list(model.encoder_params())
@@ -159,7 +167,9 @@ class FusedTrainStep:
     def _image_buffer(self, F: int):
         if self._images is None or self._images_F != F:
             n = _lib.lib().bgcn_weight_images_size(F)
-            self._images = workspace(n, self.status.device)
+            # zeroed once: the rows' padding words are never written, so two steps' buffers
+            # compare equal word for word when their images do
+            self._images = workspace(n, self.status.device).zero_()
             self._images_F = F
             self._images_key = None
         return self._images
@@ -238,7 +248,7 @@ class FusedTrainStep:
         return self._loss_ring[k]
 
     def forward_backward(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None,
-                         next_data=None, defer_dw1: bool = False):
+                         next_data=None, defer_dw1: bool = False, adam=None):
         """bgcn_train_step only (no all-reduce, no optimiser step); returns the loss.
 
         ``next_data``: the batch the next call will train on.  Its weight-independent
@@ -280,6 +290,7 @@ class FusedTrainStep:
         a.prepared_ready = ready
         a.prepared, a.prepared_bytes = ptr(prep), prep.numel()
         a.defer_dw1 = 1 if defer_dw1 else 0
+        a.adam = ctypes.addressof(adam) if adam is not None else None   # (the optimiser's own struct)
         self._pending = None
         nxt = None
         if next_data is not None:
@@ -428,6 +439,15 @@ class FusedTrainStep:
             for w in (work_a, work_b):
                 if w is not None:
                     w.wait()
+        elif world == 1 and self.fuse_optimizer:
+            # the update inside the step (an invalid step skips it there, as below)
+            F = _in_feats(data)
+            adam = self.opt.prepare(grads=self.bucket.views(), grad_scale=1.0, skip_flag=self.bucket.flag,
+                                    images=(self._image_buffer(F), F, self._img_roles), skip_count=self.skipped)
+            loss = self.forward_backward(data, seed, logp, next_data, adam=adam)
+            self.opt.step_count += 1
+            self._images_key = self._image_key()
+            return loss
         else:
             loss = self.forward_backward(data, seed, logp, next_data)
             self.bucket.allreduce_sum_(self.group)

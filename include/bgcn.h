@@ -48,7 +48,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 9
+#define BGCN_ABI_VERSION 10
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -432,6 +432,7 @@ int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int32_t degree
  *   rank's step was invalid.
  * -------------------------------------------------------------------------- */
 #define BGCN_STEP_PARAMS 10
+struct bgcn_adam_args;
 typedef struct bgcn_step_args {
   bgcn_batch cur;                /* the batch trained on                     */
   int64_t in_feats;              /* F                                        */
@@ -462,6 +463,13 @@ typedef struct bgcn_step_args {
    * data-parallel caller can all-reduce the rest of the bucket while dW1 computes
    * (overlap the conv1 dW with communication). */
   int32_t defer_dw1;
+  /* adam (optional, ABI 10): the optimiser step of this training step (bgcn_adam_step's
+   * arguments, its tensors the ten step parameters with grad = grads[k]), performed by the
+   * call: fused into the backward's last launch (each dW1 / dW2 / db1 block updates the
+   * parameters whose gradients it has just finished, one extra block the head's and db2's)
+   * where the step runs the sparse path in one call, else as the separate launch.  The
+   * result is bit-identical to calling bgcn_adam_step after the step.  NULL: no update. */
+  const struct bgcn_adam_args* adam;
 } bgcn_step_args;
 
 /* Bytes of a weight-image buffer for in_feats = F (W1^T [F][128], W2^T [2][F+64][64]

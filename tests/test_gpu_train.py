@@ -648,3 +648,47 @@ def test_deferred_dw1_matches_one_call(split, monkeypatch):
     assert torch.equal(res[0][0], res[1][0])
     for k, a, c in zip(KEYS, res[0][1], res[1][1]):
         assert torch.equal(a, c), k
+
+
+@pytest.mark.parametrize("mode,classes,split", [("auto", 4, "0"), ("sparse", 2, "0"), ("dense", 4, "0"),
+                                                ("auto", 4, "1")])
+def test_optimizer_inside_step_matches_separate_launch(mode, classes, split, monkeypatch):
+    """The single-process step with the Adam update inside its last launch
+    (bgcn_step_args.adam) leaves bitwise the parameters, moments, weight images and losses
+    of the step followed by its own bgcn_adam_step, over six steps with the next batch
+    prepared beside each; an invalid step (bad label, step 3) is skipped and counted in
+    both.  dense / BGCN_DW1_SPLIT=1: the library falls back to the separate launch."""
+    from bigcn_amd import FusedTrainStep
+    monkeypatch.setenv("BGCN_DW1_SPLIT", split)
+    batches = [_synth(70 + k, 24, 150) for k in range(3)]
+    for b in batches:
+        b.y = b.y % classes
+    bad = _synth(73, 24, 150)
+    bad.y = bad.y.clone() % classes
+    bad.y[2] = 9
+    p = O.make_params(5000, 64, 64, classes, seed=43)
+    runs = []
+    for fuse in (True, False):
+        m = _model(p, mode, classes)
+        m.train()
+        step = FusedTrainStep(m, tddroprate=0.2, budroprate=0.2, drop_seed=11, fuse_optimizer=fuse)
+        seq = [batches[0], batches[1], bad, batches[2], batches[0], batches[1]]
+        losses = []
+        for it, b in enumerate(seq):
+            nxt = seq[it + 1] if it + 1 < len(seq) else None
+            losses.append(step(b, seed=300 + it, next_data=nxt).clone())
+        torch.cuda.synchronize()
+        runs.append((losses, [v.clone() for v in m.state_dict().values()],
+                     [t.clone() for mv in step.opt.state.values() for t in mv],
+                     step._images.clone(), int(step.skipped), step.opt.step_count))
+    a, b = runs
+    for x, y in zip(a[0], b[0]):
+        assert torch.equal(x, y)
+    for k, (x, y) in enumerate(zip(a[1], b[1])):
+        assert torch.equal(x, y), k
+    for x, y in zip(a[2], b[2]):
+        assert torch.equal(x, y)
+    assert torch.equal(a[3], b[3])
+    assert a[4] == b[4] == 1
+    assert a[5] == b[5] == 6
+

@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--mode", default="resident", choices=["resident", "host_fed", "dropin"])
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--loader", default="native", choices=["native", "dataloader"])
+    ap.add_argument("--pre-timing", action="store_true", help="the kernel-timing hook on during the pre-fused steps")
+    ap.add_argument("--pre-fused", type=int, default=0,
+                    help="dropin: first run this many fused steps on the same model / optimiser (as the bench does)")
     args = ap.parse_args()
     import bench
     import torch.nn.functional as F
@@ -60,6 +63,24 @@ def main():
     stream = torch.cuda.Stream(dev)
     wrap_native()
     if args.mode == "dropin":
+        if args.pre_fused:
+            fpool = bench.make_pool(wl, 0, 4, dev, (0.0, 0.0))
+            fs = FusedTrainStep(model, opt, tddroprate=wl["drop"][0], budroprate=wl["drop"][1], drop_seed=7)
+            from bigcn_amd import ops
+            with torch.cuda.stream(stream):
+                for i in range(args.pre_fused):
+                    if args.pre_timing and i == 10:
+                        torch.cuda.synchronize()
+                        ops.set_kernel_timing(True, [7])
+                    fs(fpool[i % 4], next_data=fpool[(i + 1) % 4])
+                if args.pre_timing:
+                    torch.cuda.synchronize()
+                    ops.set_kernel_timing(False)
+                    ops.kernel_timing(7)
+                    ops.kernel_span(7)
+                fs.discard_prefetch()
+                torch.cuda.synchronize()
+            del fs, fpool
         pool = bench.make_pool(wl, 0, 4, dev, None)
 
         def step(i):

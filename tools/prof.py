@@ -123,8 +123,15 @@ def cmd_timeline(a):
     i0 = marks[a.step]
     if a.after == "k_adam":
         i1 = marks[a.step + 1]
-    else:   # through the step's Adam
-        i1 = next(i for i in range(i0 + 1, len(rows)) if "k_adam" in rows[i]["Kernel_Name"])
+    else:   # through the step's Adam (its own launch, or - fused - the main stream's last kernel
+        # before the next mark)
+        nxt = marks[a.step + 1] if a.step + 1 < len(marks) else len(rows)
+        ia = [i for i in range(i0 + 1, nxt) if "k_adam" in rows[i]["Kernel_Name"]]
+        if ia:
+            i1 = ia[0]
+        else:
+            s0 = rows[i0 + 1]["Stream_Id"]
+            i1 = max(i for i in range(i0 + 1, nxt) if rows[i]["Stream_Id"] == s0)
     t0 = int(rows[i0]["End_Timestamp"])
     busy = collections.defaultdict(float)
     for r in rows[i0 + 1:i1 + 1]:
