@@ -753,8 +753,12 @@ def main():
         fresh_allocator()
         ctx["pool"] = make_pool(wl, rank, args.pool, dev, None)
         ctx["path"] = "autograd"
-        dropin_res = run(args.feat_mode, max(5, args.steps // 2), int(os.environ.get("BGCN_BENCH_DROPIN_WARMUP", "3")),
-                         timing=False)
+        # (a sixty-step window after ten warm-up steps: the per-op loop's host enqueue jitters
+        # by tens of us per step, so a ten-step window after three read 8-25 % low,
+        # DESIGN.md 7)
+        dropin_steps = max(60, args.steps)
+        dropin_res = run(args.feat_mode, dropin_steps,
+                         int(os.environ.get("BGCN_BENCH_DROPIN_WARMUP", "10")), timing=False)
         ctx["pool"], ctx["path"] = pool, args.path
     eval_res = None
     if world == 1 and args.path == "fused" and args.eval_path:
@@ -834,7 +838,7 @@ def main():
         if eval_res is not None:
             out["eval_path"] = eval_res
         if dropin_res is not None:
-            n = max(5, args.steps // 2)
+            n = dropin_steps
             out["dropin_path"] = {
                 "value": round(dropin_res["value"], 2), "unit": "trees/s",
                 "ms_per_step": round(dropin_res["dt"] / n * 1e3, 4), "steps": n,

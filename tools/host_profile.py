@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--loader", default="native", choices=["native", "dataloader"])
     ap.add_argument("--pre-timing", action="store_true", help="the kernel-timing hook on during the pre-fused steps")
+    ap.add_argument("--reset", default="none", choices=["none", "alloc", "timing", "gc", "sync", "empty"],
+                    help="dropin after --pre-fused: what runs between the two loops (the bench's "
+                         "fresh_allocator = alloc; a kernel-timing enable/disable = timing)")
     ap.add_argument("--pre-fused", type=int, default=0,
                     help="dropin: first run this many fused steps on the same model / optimiser (as the bench does)")
     args = ap.parse_args()
@@ -81,6 +84,17 @@ def main():
                 fs.discard_prefetch()
                 torch.cuda.synchronize()
             del fs, fpool
+            import gc
+            if args.reset == "alloc":
+                torch.cuda.synchronize(); gc.collect(); torch.cuda.empty_cache()
+            elif args.reset == "empty":
+                torch.cuda.synchronize(); torch.cuda.empty_cache()
+            elif args.reset == "gc":
+                gc.collect()
+            elif args.reset == "sync":
+                torch.cuda.synchronize()
+            elif args.reset == "timing":
+                ops.set_kernel_timing(True, [7]); ops.set_kernel_timing(False)
         pool = bench.make_pool(wl, 0, 4, dev, None)
 
         def step(i):

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Evidence for profiles/ (round 4): per workload the bench line, rocprofv3 kernel stats of
+# Evidence for profiles/ (round 5): per workload the bench line, rocprofv3 kernel stats of
 # the same command, separate FETCH_SIZE / WRITE_SIZE PMC passes (MI355X_MICROARCH.md recipe;
 # tools/prof.py traffic applies the gfx950 corrections) -> pmc_traffic_<workload>.json (what
 # bench.py's roofline.traffic reads from profiles/r04_pmc_traffic_<workload>.json), the
 # device-side step timelines and the 5000-wide aggregation probe with its PMC traffic.
-#   gpurun -- 'bash tools/profile_round.sh gpurun_out/prof_r04 twitter15 weibo_bf16 synth1024_bf16'
+#   gpurun -- 'bash tools/profile_round.sh gpurun_out/prof_r05 twitter15 weibo_bf16 synth1024_bf16'
 set -eo pipefail
 OUT=${1:-gpurun_out/prof}; shift
 WLS=${@:-twitter15}
