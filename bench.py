@@ -151,7 +151,7 @@ ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2):
 
 def pmc_file(workload: str) -> str:
     """The committed PMC passes of a workload's bench command (tools/profile_round.sh)."""
-    return os.path.join(ROOT, "profiles", f"r04_pmc_traffic_{workload}.json")
+    return os.path.join(ROOT, "profiles", f"r05_pmc_traffic_{workload}.json")
 
 
 def pmc_traffic(mode: str, cls: int, workload: str = "twitter15", xbf16: bool = False):
