@@ -588,7 +588,7 @@ def main():
 
     def step(i):
         pool, fused = ctx["pool"], ctx["fused"]
-        b = pool[i % len(pool)]
+        b = next(ctx["ahead"]) if ctx.get("ahead") is not None else pool[i % len(pool)]
         if ctx["path"] == "fused":                      # K1 + fwd + head + loss + bwd in one call;
             nxt = pool[(i + 1) % len(pool)] if args.prefetch else None   # the next batch's
             return fused(b, next_data=nxt)              # preparation overlaps this step
@@ -757,8 +757,18 @@ def main():
         # by tens of us per step, so a ten-step window after three read 8-25 % low,
         # DESIGN.md 7)
         dropin_steps = max(60, args.steps)
-        dropin_res = run(args.feat_mode, dropin_steps,
-                         int(os.environ.get("BGCN_BENCH_DROPIN_WARMUP", "10")), timing=False)
+        dropin_warm = int(os.environ.get("BGCN_BENCH_DROPIN_WARMUP", "10"))
+        dropin_res = run(args.feat_mode, dropin_steps, dropin_warm, timing=False)
+        # the same loop body over the batches as feed.prepare_ahead hands them out (each
+        # batch's K1 and pass over X queued on a side stream one step ahead, beside the
+        # previous step - the data pipeline's stage, the loop body untouched)
+        from bigcn_amd.feed import prepare_ahead
+        fresh_allocator()
+        dp = ctx["pool"]
+        ctx["ahead"] = iter(prepare_ahead((dp[i % len(dp)] for i in range(dropin_steps + dropin_warm + 1)),
+                                          model))
+        dropin_ahead_res = run(args.feat_mode, dropin_steps, dropin_warm, timing=False)
+        ctx["ahead"] = None
         ctx["pool"], ctx["path"] = pool, args.path
     eval_res = None
     if world == 1 and args.path == "fused" and args.eval_path:
@@ -845,7 +855,13 @@ def main():
                 "host_enqueue_ms_per_step": round(dropin_res["t_host"] / n * 1e3, 4),
                 "what": "--path autograd: model(data) -> F.nll_loss -> loss.backward() -> optimiser "
                         "step per batch (BiGCN_Twitter.py:183-189 verbatim on the drop-in GCNConv / "
-                        "scatter_mean modules), host DropEdge once per pool batch (untimed)"}
+                        "scatter_mean modules), host DropEdge once per pool batch (untimed)",
+                "prepared_ahead": {
+                    "value": round(dropin_ahead_res["value"], 2), "unit": "trees/s",
+                    "ms_per_step": round(dropin_ahead_res["dt"] / n * 1e3, 4),
+                    "host_enqueue_ms_per_step": round(dropin_ahead_res["t_host"] / n * 1e3, 4),
+                    "what": "the same loop over feed.prepare_ahead(batches, model): each batch's K1 and "
+                            "pass over X queued on a side stream one step ahead"}}
         if dense_res is not None:
             out["dense_path"] = {"value": round(dense_res["value"], 2), "unit": "trees/s",
                                  "ms_per_step": round(dense_res["dt"] / max(3, args.steps // 2) * 1e3, 4),

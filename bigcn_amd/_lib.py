@@ -32,7 +32,7 @@ BGCN_SPARSE_CAP = 32
 BGCN_SPARSE_SPILL_PER_ROW = 32   # spill pool capacity per row (rows over the ELL cap)
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1
-ABI_VERSION = 10   # BGCN_ABI_VERSION of include/bgcn.h
+ABI_VERSION = 11   # BGCN_ABI_VERSION of include/bgcn.h
 BGCN_STATUS_CROSS_TREE = 16
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
@@ -91,6 +91,8 @@ class BiGCNArgs(Structure):
         ("td_dw1", c_void_p), ("td_db1", c_void_p), ("td_dw2", c_void_p), ("td_db2", c_void_p),
         ("bu_dw1", c_void_p), ("bu_db1", c_void_p), ("bu_dw2", c_void_p), ("bu_db2", c_void_p),
         ("save_for_backward", c_int32), ("x_dtype", c_int32),
+        ("prepared", c_void_p), ("prepared_bytes", c_size_t),
+        ("td_num_edges", c_int64), ("bu_num_edges", c_int64),
     ]
 
 

@@ -18,7 +18,8 @@ import torch
 import torch.nn.functional as F
 
 from .conv import GCNConv
-from .ops import Graph, bigcn_encoder, bigcn_net, build_graph_pair, degree_code, feat_path, head_fits, scatter_mean
+from .ops import (Graph, _feat_code, bigcn_encoder, bigcn_net, build_graph_pair, degree_code, feat_path,
+                  head_fits, scatter_mean)
 
 
 def _graphs(data, degree_on: str = "col"):
@@ -144,23 +145,34 @@ class BiGCN(torch.nn.Module):
         return (t.conv1.lin.weight, t.conv1.bias, t.conv2.lin.weight, t.conv2.bias,
                 b.conv1.lin.weight, b.conv1.bias, b.conv2.lin.weight, b.conv2.bias)
 
-    def encode(self, data, seed=None):
+    def _inputs(self, data):
+        """(td, bu, prep, feat code): the batch's preparation when a data pipeline attached
+        one that is still of this batch (``feed.prepare_ahead``: no K1 and no pass over X in
+        the forward), else its graphs (built once per batch object)."""
+        feat = self._feat(data)
+        prep = getattr(data, "_bgcn_prep", None)
+        if prep is not None and prep.matches(data, self.degree_on, _feat_code(feat)):
+            return None, None, prep, feat
         td, bu = _graphs(data, self.degree_on)
+        return td, bu, None, feat
+
+    def encode(self, data, seed=None):
+        td, bu, prep, feat = self._inputs(data)
         if seed is None:
             seed = _draw_seed() if self.training else 0
         return bigcn_encoder(data.x, data.batch, data.rootindex, td, bu, _num_graphs(data),
                              self.encoder_params(), training=self.training, seed=seed,
-                             keep_words=self.keep_words, feat_mode=self._feat(data))
+                             keep_words=self.keep_words, feat_mode=feat, prep=prep)
 
     def forward(self, data, seed=None):
         if self.fused_head and head_fits(self.fc):
             # :126-130 as one autograd node (encoder + the K9 fc / log_softmax kernels)
-            td, bu = _graphs(data, self.degree_on)
+            td, bu, prep, feat = self._inputs(data)
             if seed is None:
                 seed = _draw_seed() if self.training else 0
             return bigcn_net(data.x, data.batch, data.rootindex, td, bu, _num_graphs(data),
                              self.encoder_params(), self.fc.weight, self.fc.bias, training=self.training,
-                             seed=seed, keep_words=self.keep_words, feat_mode=self._feat(data))
+                             seed=seed, keep_words=self.keep_words, feat_mode=feat, prep=prep)
         x = self.encode(data, seed)            # cat(BU_x, TD_x)  (:126-128)
         x = self.fc(x)                         # :129
         return F.log_softmax(x, dim=1)         # :130

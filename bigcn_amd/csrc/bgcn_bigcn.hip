@@ -1280,11 +1280,17 @@ extern "C" size_t bgcn_bigcn_workspace_size(int64_t num_nodes, int64_t num_graph
 }
 extern "C" int bgcn_bigcn_forward(const bgcn_bigcn_args* args, void* workspace,
                                   size_t workspace_bytes, bgcn_stream_t stream) {
+  if (args && args->prepared)
+    return bgcn::bigcn_prepared_call(args, workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream),
+                                     false);
   return bgcn::bigcn_forward_impl(args, workspace, workspace_bytes,
                                   reinterpret_cast<hipStream_t>(stream), -1, nullptr, nullptr);
 }
 extern "C" int bgcn_bigcn_backward(const bgcn_bigcn_args* args, void* workspace,
                                    size_t workspace_bytes, bgcn_stream_t stream) {
+  if (args && args->prepared)
+    return bgcn::bigcn_prepared_call(args, workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream),
+                                     true);
   return bgcn::bigcn_backward_impl(args, workspace, workspace_bytes,
                                    reinterpret_cast<hipStream_t>(stream), nullptr, false);
 }

@@ -437,6 +437,8 @@ struct Prepared {
 };
 size_t carve_prepared(Carve& c, int64_t N, int64_t B, int64_t F, int64_t Etd, int64_t Ebu,
                       Prepared* p);
+// bgcn_bigcn_forward / _backward on a caller's prepared batch (bgcn_bigcn_args.prepared)
+int bigcn_prepared_call(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s, bool backward);
 
 // ---- DropEdge (bgcn_drop.hip)
 size_t drop_ws_size(int64_t B);

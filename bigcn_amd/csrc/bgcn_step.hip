@@ -133,6 +133,28 @@ static size_t prepared_size(int64_t N, int64_t B, int64_t F, int64_t Etd, int64_
   return carve_prepared(c, N, B, F, Etd, Ebu, nullptr) + 256;
 }
 
+// The per-op encoder on a batch a data pipeline prepared ahead (bgcn_bigcn_args.prepared):
+// the args with the prepared buffer's graphs, ELL of X and tree pointers in place of the
+// caller's, then the same forward / backward bodies bgcn_train_step runs on its prepared
+// batches (no K1, no pass over X, no CSC build in the call).
+int bigcn_prepared_call(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hipStream_t s, bool backward) {
+  BGCN_CHECK_ARG(a && a->prepared, "null args / prepared buffer");
+  const int64_t N = a->num_nodes, B = a->num_graphs, F = a->in_feats;
+  BGCN_CHECK_ARG(N > 0 && B > 0 && F > 0 && a->td_num_edges >= 0 && a->bu_num_edges >= 0, "bad sizes");
+  BGCN_CHECK_ARG(a->prepared_bytes >= prepared_size(N, B, F, a->td_num_edges, a->bu_num_edges),
+                 "prepared buffer too small for these sizes");
+  Prepared p;
+  Carve cp(const_cast<void*>(a->prepared), a->prepared_bytes);
+  carve_prepared(cp, N, B, F, a->td_num_edges, a->bu_num_edges, &p);
+  bgcn_bigcn_args e = *a;
+  e.td = view_of(p.td, p.td_cap);
+  e.bu = view_of(p.bu, p.bu_cap);
+  e.x_flags = p.x_flags; e.x_nnz = p.x_nnz; e.x_cols = p.x_cols; e.x_vals = p.x_vals;
+  e.tree_ptr = p.tree_ptr;
+  if (backward) return bigcn_backward_impl(&e, ws, ws_bytes, s, &p, false);
+  return bigcn_forward_impl(&e, ws, ws_bytes, s, -1, nullptr, &p);
+}
+
 // gs: stream of the graph build (K1); the caller joins it before the graphs are used
 static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_mode, void* buf,
                         size_t bytes, hipStream_t s, Prepared* out, hipStream_t gs) {

@@ -929,6 +929,65 @@ class NativeLoader:
             pass
 
 
+class prepare_ahead:
+    """The drop-in loop's data pipeline stage that prepares each batch one step ahead:
+
+        for Batch_data in prepare_ahead(batches, model):      # batches: the reference's
+            out_labels = model(Batch_data)                     # DataLoader + .to(device)
+            loss = F.nll_loss(out_labels, Batch_data.y)        # (BiGCN_Twitter.py:174-189,
+            optimizer.zero_grad(); loss.backward(); optimizer.step()   # the body untouched)
+
+    When batch k is handed out, batch k+1's weight-independent preparation
+    (``ops.prepare_batch``: DropEdge-free K1 of both directions, tree items, the ELL / CSC
+    of X - the HBM-bound pass over X) is queued on a side stream behind everything the
+    caller has queued so far, so it runs beside step k on the device; the model's forward
+    finds it on ``Batch_data._bgcn_prep`` and skips K1 and the pass over X.  The loop body
+    is the reference's; the batches are dense-x device batches (collated ``Batch``).
+    ``slots`` prepared buffers are reused in turn: a preparation into a slot waits for the
+    caller's stream, so the step that read the slot's previous batch has finished."""
+
+    def __init__(self, batches, model, slots: int = 2):
+        if slots < 2:
+            raise ValueError("prepare_ahead needs at least two buffers")
+        self.batches, self.model, self.slots = batches, model, slots
+        self._bufs = [None] * slots
+        self._stream = None
+
+    def _launch(self, data, slot: int):
+        from .ops import prepare_batch
+        main = torch.cuda.current_stream(data.x.device)
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(data.x.device)
+        self._stream.wait_stream(main)          # the batch's tensors and the slot's last reader
+        m = self.model
+        feat = m._feat(data) if hasattr(m, "_feat") else "auto"
+        with torch.cuda.stream(self._stream):
+            prep = prepare_batch(data, m.degree_on, feat, buf=self._bufs[slot], stream=self._stream)
+        self._bufs[slot] = prep.buf
+        data._bgcn_prep = prep
+
+    def __iter__(self):
+        it = iter(self.batches)
+        try:
+            cur = next(it)
+        except StopIteration:
+            return
+        self._launch(cur, 0)
+        k = 0
+        while True:
+            try:
+                nxt = next(it)
+            except StopIteration:
+                nxt = None
+            if nxt is not None:
+                self._launch(nxt, (k + 1) % self.slots)
+            yield cur
+            if nxt is None:
+                return
+            cur = nxt
+            k += 1
+
+
 def host_fed_loader(store, batch_size: int = 128, num_workers: int = 5, shuffle: bool = True,
                     drop_last: bool = True, prefetch_factor: int = 2, seed: Optional[int] = None,
                     epochs: int = 1, **ds_kw):

@@ -507,13 +507,18 @@ def _fill_args(a: BiGCNArgs, x, batch, rootindex, td, bu, B, training, seed, kee
 
 
 def _encoder_forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training, seed, keep_words,
-                     feat_mode, params, stream):
+                     feat_mode, params, stream, prep=None):
     """The encoder's native forward; returns (head [B, 256], tensors for backward) and
-    keeps the rest of the forward -> backward state on ``ctx`` (``_encoder_backward``)."""
+    keeps the rest of the forward -> backward state on ``ctx`` (``_encoder_backward``).
+    ``prep`` (a ``PreparedBatch`` of this batch, ``td`` / ``bu`` then None): the graphs,
+    tree pointers, items and ELL / CSC of X come from it (bgcn_bigcn_args.prepared)."""
     x = features(x)
     N, F = x.shape
     dev = x.device
     L = _lib.lib()
+    if prep is not None:
+        return _encoder_forward_prepared(ctx, x, batch, rootindex, B, training, seed, keep_words, feat_mode,
+                                         params, stream, prep)
     xs = None
     if feat_mode != _lib.BGCN_FEAT_DENSE:
         cap = _lib.BGCN_SPARSE_CAP
@@ -545,6 +550,121 @@ def _encoder_forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training
 _ENC_SAVED = 11   # tensors of _encoder_forward's `saved` before the parameters
 
 
+def _encoder_forward_prepared(ctx, x, batch, rootindex, B, training, seed, keep_words, feat_mode, params,
+                              stream, prep):
+    N, F = x.shape
+    dev = x.device
+    prep.check_matches(x, batch, rootindex, B, feat_mode)
+    L = _lib.lib()
+    a = BiGCNArgs()
+    a.x, a.ldx, a.num_nodes, a.num_graphs, a.in_feats, a.hid = x.data_ptr(), x.stride(0), N, B, F, HID
+    a.x_dtype = x_dtype_code(x)
+    a.batch, a.rootindex = batch.data_ptr(), rootindex.data_ptr()
+    a.td_w1, a.td_b1, a.td_w2, a.td_b2, a.bu_w1, a.bu_b1, a.bu_w2, a.bu_b2 = (p.data_ptr() for p in params)
+    a.training, a.seed = int(bool(training)), int(seed) & (2**64 - 1)
+    a.keep_words = ptr(keep_words)
+    a.feat_mode = feat_mode
+    a.prepared, a.prepared_bytes = prep.buf.data_ptr(), prep.buf.numel()
+    a.td_num_edges, a.bu_num_edges = prep.td_num_edges, prep.bu_num_edges
+    h1 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
+    h2 = torch.empty(N, 2 * HID, dtype=torch.float32, device=dev)
+    head = torch.empty(B, 4 * HID, dtype=torch.float32, device=dev)
+    a.h1, a.h2, a.head_in = h1.data_ptr(), h2.data_ptr(), head.data_ptr()
+    a.save_for_backward = 1 if any(ctx.needs_input_grad) else 0
+    prep.wait()                                    # its preparation ordered before this forward
+    ws = workspace(L.bgcn_bigcn_workspace_size(N, B, F, HID), dev)
+    check(L.bgcn_bigcn_forward(ctypes.byref(a), ws.data_ptr(), ws.numel(), stream))
+    ctx.ws = ws if a.save_for_backward else None
+    ctx.args = a
+    ctx.graphs = (prep,)                           # the prepared buffer lives until the backward
+    ctx.meta = (B, N, params[0].device)
+    ctx.has_keep = keep_words is not None
+    empty = x.new_empty(0)
+    saved = (x, batch, rootindex, keep_words if keep_words is not None else empty, empty, h1, h2,
+             empty, empty, empty, empty, *params)
+    return head, saved
+
+
+class PreparedBatch:
+    """A batch's weight-independent state built ahead of its forward (``prepare_batch``:
+    K1 gcn_norm + CSR of both directions with their aggregation plans, tree pointers and
+    work items, the ELL / spill pool / CSC of X - bgcn_prepare_batch) in a caller-side
+    buffer, plus the event that ends its preparation.  The drop-in model's forward takes it
+    from ``data._bgcn_prep`` (``prepare_ahead`` attaches it) and then runs no K1 and no pass
+    over X of its own (bgcn_bigcn_args.prepared)."""
+
+    def __init__(self, buf, N, B, F, td_edges, bu_edges, degree_on, dense, key, keep, event):
+        self.buf, self.num_nodes, self.num_graphs, self.in_feats = buf, N, B, F
+        self.td_num_edges, self.bu_num_edges = td_edges, bu_edges
+        self.degree_on, self.dense, self.key, self._keep, self.event = degree_on, dense, key, keep, event
+        self._waited = False
+
+    def matches(self, data, degree_on: str, feat_mode: int) -> bool:
+        """Whether this preparation is of ``data`` as it is now (same tensors, unmodified)
+        for that degree convention and feature path."""
+        return (self.degree_on == degree_on and self.dense == (feat_mode == _lib.BGCN_FEAT_DENSE)
+                and self.key == _prep_key(data))
+
+    def check_matches(self, x, batch, rootindex, B, feat_mode) -> None:
+        if (x.size(0), B, x.size(1)) != (self.num_nodes, self.num_graphs, self.in_feats) or \
+                self.dense != (feat_mode == _lib.BGCN_FEAT_DENSE):
+            raise ValueError("prepared batch does not match the forward's inputs")
+
+    def wait(self) -> None:
+        """The current stream waits for the preparation (once) and is recorded as a user of
+        the buffer (it may have been allocated on the preparing stream)."""
+        if not self._waited:
+            s = torch.cuda.current_stream(self.buf.device)
+            if self.event is not None:
+                s.wait_event(self.event)
+            self.buf.record_stream(s)
+        self._waited = True
+
+
+def _prep_key(data):
+    x = data.x
+    return (x.data_ptr(), x._version, tuple(x.shape), data.edge_index.data_ptr(), data.edge_index._version,
+            int(data.edge_index.size(1)), data.BU_edge_index.data_ptr(), data.BU_edge_index._version,
+            int(data.BU_edge_index.size(1)), data.batch.data_ptr(), data.batch._version,
+            data.rootindex.data_ptr(), data.rootindex._version)
+
+
+def prepare_batch(data, degree_on: str = "col", feat_mode: str = "auto", buf: Optional[torch.Tensor] = None,
+                  stream: Optional[torch.cuda.Stream] = None) -> PreparedBatch:
+    """bgcn_prepare_batch of a collated device batch (its edge lists as they are: the
+    reference's DropEdge happened in the dataset) on ``stream`` (default: the current
+    one), into ``buf`` when it is large enough.  The returned object's event marks the end
+    of the preparation; the batch's tensors must be ready on ``stream`` when it runs."""
+    from ._lib import BatchDesc
+    x = features(data.x)
+    td_ei, bu_ei = _check_ei(data.edge_index), _check_ei(data.BU_edge_index)
+    batch = data.batch if data.batch.dtype == torch.int64 and data.batch.is_contiguous() else \
+        data.batch.to(torch.int64).contiguous()
+    root = data.rootindex if data.rootindex.dtype == torch.int64 and data.rootindex.is_contiguous() else \
+        data.rootindex.to(torch.int64).contiguous()
+    _dev_check(x, td_ei, bu_ei, batch, root)
+    N, F = x.shape
+    B = int(root.numel())
+    code = _feat_code(feat_path(feat_mode, data) if isinstance(feat_mode, str) else feat_mode)
+    d = BatchDesc()
+    d.x, d.ldx, d.num_nodes, d.num_graphs = ptr(x), x.stride(0), N, B
+    d.x_dtype = x_dtype_code(x)
+    d.batch, d.rootindex = ptr(batch), ptr(root)
+    d.td_edge_index, d.td_num_edges = ptr(td_ei), td_ei.size(1)
+    d.bu_edge_index, d.bu_num_edges = ptr(bu_ei), bu_ei.size(1)
+    L = _lib.lib()
+    n = L.bgcn_prepare_workspace_size(N, B, F, d.td_num_edges, d.bu_num_edges)
+    if buf is None or buf.numel() < n:
+        buf = workspace(n, x.device)
+    s = stream if stream is not None else torch.cuda.current_stream(x.device)
+    check(L.bgcn_prepare_batch(ctypes.byref(d), F, degree_code(degree_on), code, buf.data_ptr(), buf.numel(),
+                               s.cuda_stream))
+    ev = torch.cuda.Event()
+    ev.record(s)
+    return PreparedBatch(buf, N, B, F, int(d.td_num_edges), int(d.bu_num_edges), degree_on,
+                         code == _lib.BGCN_FEAT_DENSE, _prep_key(data), (x, td_ei, bu_ei, batch, root), ev)
+
+
 def _encoder_backward(ctx, saved, dhead, stream):
     """Gradients of the 8 encoder parameters (reference order) from dhead [B, 256]."""
     params = saved[_ENC_SAVED:_ENC_SAVED + 8]
@@ -565,9 +685,9 @@ def _encoder_backward(ctx, saved, dhead, stream):
 class _BiGCNEncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training, seed, keep_words,
-                feat_mode, *params):
+                feat_mode, prep, *params):
         head, saved = _encoder_forward(ctx, x, batch, rootindex, td, bu, B, training, seed, keep_words,
-                                       feat_mode, params, stream_handle())
+                                       feat_mode, params, stream_handle(), prep)
         ctx.save_for_backward(*saved)
         return head
 
@@ -575,7 +695,7 @@ class _BiGCNEncoderFn(torch.autograd.Function):
     def backward(ctx, dhead):
         saved = ctx.saved_tensors
         dhead = dhead.contiguous().float()
-        return (None,) * 10 + tuple(_encoder_backward(ctx, saved, dhead, stream_handle()))
+        return (None,) * 11 + tuple(_encoder_backward(ctx, saved, dhead, stream_handle()))
 
 
 class _BiGCNNetFn(torch.autograd.Function):
@@ -586,10 +706,10 @@ class _BiGCNNetFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, batch, rootindex, td: Graph, bu: Graph, B, training, seed, keep_words,
-                feat_mode, fc_w, fc_b, *params):
+                feat_mode, prep, fc_w, fc_b, *params):
         s = stream_handle()
         head, saved = _encoder_forward(ctx, x, batch, rootindex, td, bu, B, training, seed, keep_words,
-                                       feat_mode, params, s)
+                                       feat_mode, params, s, prep)
         C = fc_w.size(0)
         logp = torch.empty(B, C, dtype=torch.float32, device=head.device)
         check(_lib.lib().bgcn_head_forward(head.data_ptr(), fc_w.data_ptr(), fc_b.data_ptr(), B, C,
@@ -609,7 +729,7 @@ class _BiGCNNetFn(torch.autograd.Function):
         check(_lib.lib().bgcn_head_backward(head.data_ptr(), logp.data_ptr(), dlogp.data_ptr(), fc_w.data_ptr(),
                                             B, C, dhead.data_ptr(), dfc_w.data_ptr(), dfc_b.data_ptr(), s))
         grads = _encoder_backward(ctx, saved, dhead, s)
-        return (None,) * 10 + (dfc_w, dfc_b) + tuple(grads)
+        return (None,) * 11 + (dfc_w, dfc_b) + tuple(grads)
 
 
 def _encoder_inputs(x, batch, rootindex, params, keep_words):
@@ -627,7 +747,8 @@ def _encoder_inputs(x, batch, rootindex, params, keep_words):
 
 def bigcn_encoder(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, td: Graph, bu: Graph,
                   num_graphs: int, params, training: bool = False, seed: int = 0,
-                  keep_words: Optional[torch.Tensor] = None, feat_mode: str = "auto") -> torch.Tensor:
+                  keep_words: Optional[torch.Tensor] = None, feat_mode: str = "auto",
+                  prep: Optional["PreparedBatch"] = None) -> torch.Tensor:
     """cat(BU_x, TD_x) [B, 256] of ``BiGCN.forward`` (``BiGCN_Twitter.py:126-128``).
 
     ``params`` = (td_w1, td_b1, td_w2, td_b2, bu_w1, bu_b1, bu_w2, bu_b2) in the
@@ -638,7 +759,7 @@ def bigcn_encoder(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor,
     BGCN_FEAT_SPARSE when the batch's hints say its rows fit)."""
     batch, rootindex, keep_words = _encoder_inputs(x, batch, rootindex, params, keep_words)
     return _BiGCNEncoderFn.apply(x, batch, rootindex, td, bu, int(num_graphs), bool(training), int(seed),
-                                 keep_words, _feat_code(feat_mode), *params)
+                                 keep_words, _feat_code(feat_mode), prep, *params)
 
 
 def head_fits(fc: torch.nn.Module) -> bool:
@@ -659,7 +780,8 @@ def head_fits(fc: torch.nn.Module) -> bool:
 
 def bigcn_net(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, td: Graph, bu: Graph,
               num_graphs: int, params, fc_w: torch.Tensor, fc_b: torch.Tensor, training: bool = False,
-              seed: int = 0, keep_words: Optional[torch.Tensor] = None, feat_mode: str = "auto") -> torch.Tensor:
+              seed: int = 0, keep_words: Optional[torch.Tensor] = None, feat_mode: str = "auto",
+              prep: Optional["PreparedBatch"] = None) -> torch.Tensor:
     """``log_softmax(fc(bigcn_encoder(...)), dim=1)`` [B, C] (``BiGCN_Twitter.py:126-130``)
     as one autograd node: the encoder plus the K9 head kernels.  ``fc_w`` [C, 256] and
     ``fc_b`` [C] are the ``fc`` Linear's parameters (C <= 16)."""
@@ -670,7 +792,7 @@ def bigcn_net(x: torch.Tensor, batch: torch.Tensor, rootindex: torch.Tensor, td:
             or not fc_w.is_contiguous() or not fc_b.is_contiguous()):
         raise ValueError("fc must be a contiguous fp32 Linear(256, C <= 16) with a bias")
     return _BiGCNNetFn.apply(x, batch, rootindex, td, bu, int(num_graphs), bool(training), int(seed), keep_words,
-                             _feat_code(feat_mode), fc_w, fc_b, *params)
+                             _feat_code(feat_mode), prep, fc_w, fc_b, *params)
 
 
 def keep_words(seed: int, num_nodes: int, in_feats: int, device) -> torch.Tensor:

@@ -48,7 +48,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 10
+#define BGCN_ABI_VERSION 11
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -338,6 +338,15 @@ typedef struct bgcn_bigcn_args {
    * of X for dW1) on the library's auxiliary stream, overlapped with the forward */
   int32_t save_for_backward;
   int32_t x_dtype;               /* BGCN_DTYPE_F32 (0) / BGCN_DTYPE_BF16    */
+  /* optional (ABI 11): the batch already prepared by bgcn_prepare_batch (same x, batch,
+   * rootindex and edge lists, no DropEdge rates, the same degree_on and feat_mode), e.g.
+   * by a data pipeline on another stream while the previous batch trained.  The forward
+   * then takes the graphs, tree pointers, tree items and the ELL / CSC of X from it instead
+   * of building them: td, bu, x_flags .. x_vals and tree_ptr are ignored (may be zero).
+   * The work that produced it must be ordered before the forward on `stream`, and the
+   * buffer kept unmodified until the backward has run.  NULL: the forward builds them. */
+  const void* prepared; size_t prepared_bytes;
+  int64_t td_num_edges, bu_num_edges;   /* the prepared batch's edge counts (its layout) */
 } bgcn_bigcn_args;
 
 /* The workspace carries state from the forward to the backward (node -> root map,

@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = _lib.load_library()
     for name in _declared_functions():
         assert hasattr(lib, name), name
-    assert lib.bgcn_abi_version() == 10
+    assert lib.bgcn_abi_version() == 11
 
 
 def test_workspace_queries_without_gpu():

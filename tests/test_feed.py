@@ -271,3 +271,25 @@ def test_native_loader_order_and_indices():
         runs.append([L.next_host() and L.last_trees for _ in range(len(L))])
         L.close()
     assert all(np.array_equal(a, b) for a, b in zip(*runs))
+
+
+def test_prepare_ahead_order_and_slots(monkeypatch):
+    """prepare_ahead hands out every batch in order, queues batch k+1's preparation before it
+    hands out batch k (so it runs beside step k), and takes the buffers in turn (a slot is
+    reused two batches later, after the caller has queued the step that read it)."""
+    from bigcn_amd.feed import prepare_ahead
+    log = []
+    monkeypatch.setattr(prepare_ahead, "_launch", lambda self, data, slot: log.append(("prep", data, slot)))
+    pa = prepare_ahead(range(5), model=None)
+    for b in pa:
+        log.append(("use", b))
+    assert log == [("prep", 0, 0), ("prep", 1, 1), ("use", 0), ("prep", 2, 0), ("use", 1), ("prep", 3, 1),
+                   ("use", 2), ("prep", 4, 0), ("use", 3), ("use", 4)]
+    log.clear()
+    assert list(prepare_ahead([], model=None)) == [] and log == []
+    assert list(prepare_ahead([7], model=None)) == [7] and log == [("prep", 7, 0)]
+    log.clear()
+    assert list(prepare_ahead(range(4), model=None, slots=3)) == [0, 1, 2, 3]
+    assert [s for _, _, s in [e for e in log if e[0] == "prep"]] == [0, 1, 2, 0]
+    with pytest.raises(ValueError):
+        prepare_ahead([], model=None, slots=1)

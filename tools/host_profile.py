@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--mode", default="resident", choices=["resident", "host_fed", "dropin"])
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--ahead", action="store_true", help="dropin: batches through feed.prepare_ahead")
     ap.add_argument("--loader", default="native", choices=["native", "dataloader"])
     ap.add_argument("--pre-timing", action="store_true", help="the kernel-timing hook on during the pre-fused steps")
     ap.add_argument("--reset", default="none", choices=["none", "alloc", "timing", "gc", "sync", "empty"],
@@ -96,9 +97,13 @@ def main():
             elif args.reset == "timing":
                 ops.set_kernel_timing(True, [7]); ops.set_kernel_timing(False)
         pool = bench.make_pool(wl, 0, 4, dev, None)
+        ahead = None
+        if args.ahead:
+            from bigcn_amd.feed import prepare_ahead
+            ahead = iter(prepare_ahead((pool[i % 4] for i in range(args.warmup + 2 * args.steps + 1)), model))
 
         def step(i):
-            b = pool[i % len(pool)]
+            b = next(ahead) if ahead is not None else pool[i % len(pool)]
             b.__dict__.pop("_bgcn_graphs", None)
             logp = model(b)
             loss = F.nll_loss(logp, b.y)
