@@ -536,6 +536,9 @@ def main():
     ap.add_argument("--host-fed-trees", type=int, default=2048, help="trees in the host-fed run's store")
     ap.add_argument("--eval-path", type=int, default=1,
                     help="at N=1 also time the fused evaluation step (the reference's test loop body)")
+    ap.add_argument("--dropin-ahead", type=int, default=0,
+                    help="1: also time the drop-in loop over feed.prepare_ahead (batches prepared one "
+                         "step ahead on a side stream)")
     ap.add_argument("--dropin", type=int, default=1,
                     help="at N=1 also time the drop-in path (model(data), loss.backward(), the "
                          "optimiser: --path autograd) and report it beside the main line")
@@ -762,13 +765,15 @@ def main():
         # the same loop body over the batches as feed.prepare_ahead hands them out (each
         # batch's K1 and pass over X queued on a side stream one step ahead, beside the
         # previous step - the data pipeline's stage, the loop body untouched)
-        from bigcn_amd.feed import prepare_ahead
-        fresh_allocator()
-        dp = ctx["pool"]
-        ctx["ahead"] = iter(prepare_ahead((dp[i % len(dp)] for i in range(dropin_steps + dropin_warm + 1)),
-                                          model))
-        dropin_ahead_res = run(args.feat_mode, dropin_steps, dropin_warm, timing=False)
-        ctx["ahead"] = None
+        dropin_ahead_res = None
+        if args.dropin_ahead:
+            from bigcn_amd.feed import prepare_ahead
+            fresh_allocator()
+            dp = ctx["pool"]
+            ctx["ahead"] = iter(prepare_ahead((dp[i % len(dp)] for i in range(dropin_steps + dropin_warm + 1)),
+                                              model))
+            dropin_ahead_res = run(args.feat_mode, dropin_steps, dropin_warm, timing=False)
+            ctx["ahead"] = None
         ctx["pool"], ctx["path"] = pool, args.path
     eval_res = None
     if world == 1 and args.path == "fused" and args.eval_path:
@@ -856,7 +861,7 @@ def main():
                 "what": "--path autograd: model(data) -> F.nll_loss -> loss.backward() -> optimiser "
                         "step per batch (BiGCN_Twitter.py:183-189 verbatim on the drop-in GCNConv / "
                         "scatter_mean modules), host DropEdge once per pool batch (untimed)",
-                "prepared_ahead": {
+                "prepared_ahead": None if dropin_ahead_res is None else {
                     "value": round(dropin_ahead_res["value"], 2), "unit": "trees/s",
                     "ms_per_step": round(dropin_ahead_res["dt"] / n * 1e3, 4),
                     "host_enqueue_ms_per_step": round(dropin_ahead_res["t_host"] / n * 1e3, 4),
