@@ -407,6 +407,8 @@ def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int
         torch.cuda.synchronize()
         feeder.copy_stats(reset=True)
         fused.run_report(reset=True)
+        if native:
+            loader.stats(reset=True)
         nodes = 0
         t_next = t_call = 0.0
         t0 = time.perf_counter()
@@ -421,6 +423,7 @@ def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int
             cur = nxt
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        lstats = loader.stats() if native else None
         fused.discard_prefetch()
         res = None
         if native:
@@ -461,6 +464,8 @@ def host_fed_bench(fused, wl, dev, stream, steps: int, warmup: int, workers: int
                                "(feed.host_fed_loader)", "num_workers": workers}),
            "h2d_bytes_per_batch": round(mean_bytes), "h2d_ms_per_batch": round(copy_ms, 4),
            "h2d_gbs": round(mean_bytes / (copy_ms * 1e-3) / 1e9, 2) if copy_ms > 0 else None}
+    if lstats is not None:
+        leg["loader_stats"] = lstats
     out = {"leg": leg, "store_build_s": round(t_store, 2), "avg_nodes_per_batch": round(nodes / steps, 1),
            "dense_x_bytes_per_batch": round(dense_bytes),
            "dense_x_h2d_ms_at_measured_rate": (round(dense_bytes / (mean_bytes / copy_ms), 3)
@@ -536,7 +541,7 @@ def main():
     ap.add_argument("--host-fed-trees", type=int, default=2048, help="trees in the host-fed run's store")
     ap.add_argument("--eval-path", type=int, default=1,
                     help="at N=1 also time the fused evaluation step (the reference's test loop body)")
-    ap.add_argument("--dropin-ahead", type=int, default=0,
+    ap.add_argument("--dropin-ahead", type=int, default=1,
                     help="1: also time the drop-in loop over feed.prepare_ahead (batches prepared one "
                          "step ahead on a side stream)")
     ap.add_argument("--dropin", type=int, default=1,

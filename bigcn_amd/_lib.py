@@ -32,7 +32,7 @@ BGCN_SPARSE_CAP = 32
 BGCN_SPARSE_SPILL_PER_ROW = 32   # spill pool capacity per row (rows over the ELL cap)
 BGCN_DTYPE_F32 = 0
 BGCN_DTYPE_BF16 = 1
-ABI_VERSION = 11   # BGCN_ABI_VERSION of include/bgcn.h
+ABI_VERSION = 12   # BGCN_ABI_VERSION of include/bgcn.h
 BGCN_STATUS_CROSS_TREE = 16
 
 # every symbol include/bgcn.h declares (checked by tests/test_capi.py)
@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     "bgcn_train_step_workspace_size", "bgcn_train_step", "bgcn_train_step_dw1", "bgcn_join_side",
     "bgcn_weight_images_size", "bgcn_train_step_saved", "bgcn_eval_step",
     "bgcn_loader_create", "bgcn_loader_slot_bytes", "bgcn_loader_len", "bgcn_loader_next", "bgcn_loader_destroy",
+    "bgcn_loader_wait", "bgcn_loader_get_stats",
 )
 
 
@@ -198,6 +199,8 @@ _SIGS = {
     "bgcn_loader_next": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_int64,
                                  POINTER(c_void_p)]),
     "bgcn_loader_destroy": (None, [c_void_p]),
+    "bgcn_loader_wait": (c_int, [c_void_p]),
+    "bgcn_loader_get_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "bgcn_set_kernel_timing": (c_int, [c_int]),
     "bgcn_kernel_timing": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),
     "bgcn_kernel_span": (c_int, [c_int, POINTER(c_float), POINTER(c_int64)]),

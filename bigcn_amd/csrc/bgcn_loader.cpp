@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <atomic>
 #include <condition_variable>
@@ -91,7 +92,14 @@ struct Loader {
   std::string error;
   std::vector<std::thread> workers;
   int device = 0;
+  // time accounting (bgcn_loader_stats), under mu
+  int64_t packs = 0;
+  double pack_ms = 0, slot_wait_ms = 0, caller_wait_ms = 0;
 };
+
+inline double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
 
 const std::vector<int64_t>& epoch_perm(Loader& L, int64_t e) {   // under L.mu
   while (int64_t(L.perm.size()) <= e) {
@@ -206,6 +214,7 @@ void worker(Loader* L) {
       std::unique_lock<std::mutex> lk(L->mu);
       if (L->stop || L->next_pack >= L->total) return;
       seq = L->next_pack++;
+      const auto tw = std::chrono::steady_clock::now();
       sl = &L->slots[size_t(seq % int64_t(L->slots.size()))];
       // the slot's turn: its previous batch (seq - nslots) handed out - copy issued
       L->cv.wait(lk, [&] { return L->stop || (sl->next == seq && (sl->state == 0 || sl->state == 3)); });
@@ -221,13 +230,19 @@ void worker(Loader* L) {
         hipEvent_t ev = sl->copied;
         lk.unlock();
         (void)hipEventSynchronize(ev);
+        lk.lock();
       }
+      L->slot_wait_ms += ms_since(tw);
     }
     bgcn_loader_batch m{};
     std::string err;
+    const auto tp = std::chrono::steady_clock::now();
     const bool ok = pack(*L, trees, sl->host, L->slot_bytes, m, err);
+    const double tpack = ms_since(tp);
     {
       std::lock_guard<std::mutex> lk(L->mu);
+      L->pack_ms += tpack;
+      ++L->packs;
       m.seq = seq;
       sl->meta = m;
       sl->trees = trees;
@@ -345,7 +360,9 @@ int bgcn_loader_next(void* handle, void* dst, size_t dst_bytes, bgcn_stream_t st
   if (L->next_out >= L->total) return 1;   // the end of the data
   const int64_t seq = L->next_out;
   Slot& s = L->slots[size_t(seq % int64_t(L->slots.size()))];
+  const auto tw = std::chrono::steady_clock::now();
   L->cv.wait(lk, [&] { return s.state == 2 && s.seq == seq; });
+  L->caller_wait_ms += ms_since(tw);
   if (!L->error.empty()) return fail(BGCN_EINVAL, L->error.c_str());
   *out = s.meta;
   if (trees) {
@@ -369,6 +386,36 @@ int bgcn_loader_next(void* handle, void* dst, size_t dst_bytes, bgcn_stream_t st
   ++L->next_out;
   lk.unlock();
   L->cv.notify_all();
+  return BGCN_OK;
+}
+
+int bgcn_loader_wait(void* handle) {
+  Loader* L = static_cast<Loader*>(handle);
+  BGCN_CHECK_ARG(L, "null loader");
+  std::unique_lock<std::mutex> lk(L->mu);
+  if (L->next_out >= L->total) return 1;
+  const int64_t seq = L->next_out;
+  Slot& s = L->slots[size_t(seq % int64_t(L->slots.size()))];
+  const auto tw = std::chrono::steady_clock::now();
+  L->cv.wait(lk, [&] { return s.state == 2 && s.seq == seq; });
+  L->caller_wait_ms += ms_since(tw);
+  if (!L->error.empty()) return fail(BGCN_EINVAL, L->error.c_str());
+  return BGCN_OK;
+}
+
+int bgcn_loader_get_stats(void* handle, bgcn_loader_stats* out, int reset) {
+  Loader* L = static_cast<Loader*>(handle);
+  BGCN_CHECK_ARG(L && out, "null loader / output");
+  std::lock_guard<std::mutex> lk(L->mu);
+  out->packs = L->packs;
+  out->pack_ms = L->pack_ms;
+  out->slot_wait_ms = L->slot_wait_ms;
+  out->caller_wait_ms = L->caller_wait_ms;
+  out->threads = int64_t(L->workers.size());
+  if (reset) {
+    L->packs = 0;
+    L->pack_ms = L->slot_wait_ms = L->caller_wait_ms = 0;
+  }
   return BGCN_OK;
 }
 

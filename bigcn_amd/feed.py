@@ -653,10 +653,11 @@ class DeviceFeeder:
     Each batch is copied host -> device on ``copy_stream`` as soon as it is fetched, ``depth``
     batches ahead of the one being yielded; the yielding thread's current stream waits on
     the copy's event (a device-side wait, no host sync).  Device buffers are recycled: when
-    a yielded batch is released (its last reference dropped), an event is recorded on the
-    consumer stream and the buffer returns to the feeder's pool; a later copy into it waits
-    for that event on the copy stream (no allocation, no ``record_stream`` per batch: those
-    cost ~20 us of host time per batch).  ``timing=True`` records start/end events around
+    a yielded batch is released (its last reference dropped) the buffer returns to the
+    feeder's pool; once no view of it is left either, a later copy into it waits for an
+    event recorded on the consumer stream at that point (no allocation, no ``record_stream``
+    per batch: those cost ~20 us of host time per batch).  A :class:`NativeLoader` makes one
+    pass (``epochs`` of them inside it): iterating a feeder over an exhausted one raises.  ``timing=True`` records start/end events around
     every copy (:meth:`copy_stats`)."""
 
     def __init__(self, loader, device=None, depth: int = 3, x_dtype=torch.float32, timing: bool = False,
@@ -674,17 +675,30 @@ class DeviceFeeder:
         self._free = []          # (device buffer, release event) ready for reuse
         self._consumer = None
 
+    @staticmethod
+    def _views_alive(buf: torch.Tensor) -> bool:
+        """Whether a tensor other than the pool's own references views ``buf`` (a kept
+        ``batch.y``).  Unknown (no use-count query in this torch) counts as alive."""
+        try:
+            return torch._C._storage_Use_Count(buf.untyped_storage()._cdata) > 2
+        except (AttributeError, RuntimeError):
+            return True
+
     def _release(self, buf: torch.Tensor) -> None:
-        # the released batch's work is enqueued on the consumer stream: reuse after it
-        ev = torch.cuda.Event()
-        ev.record(self._consumer)
-        self._free.append((buf, ev))
+        # the buffer returns to the pool when its batch dies; a view of it may outlive the
+        # batch (a kept `batch.y`) and be read by kernels queued later, so the event its
+        # reuse waits for is recorded when it is TAKEN: by then no view is left (checked),
+        # so every kernel that read it is already enqueued on the consumer stream
+        self._free.append((buf, None))
 
     def _take(self, nbytes: int):
         for k, (buf, ev) in enumerate(self._free):
-            # reused only once no tensor of the caller still views it (a kept `batch.y`)
-            if buf.numel() >= nbytes and torch._C._storage_Use_Count(buf.untyped_storage()._cdata) <= 2:
+            # reused only once no tensor of the caller still views it
+            if buf.numel() >= nbytes and not self._views_alive(buf):
                 del self._free[k]
+                if ev is None:
+                    ev = torch.cuda.Event()
+                    ev.record(self._consumer)
                 return buf, ev
         # a new buffer (with headroom: batches vary in size), allocated on the consumer stream
         # and marked used by the copy stream once, so that when the pool drops it the caching
@@ -740,6 +754,9 @@ class DeviceFeeder:
             cs.wait_event(free_ev)
         t0 = None
         if self.timing:
+            # the bracket holds the copy only: the host first waits for the batch's packing
+            # (an event recorded before that wait timed the packing too)
+            L.wait()
             t0 = torch.cuda.Event(enable_timing=True)
             t0.record(cs)
         got = L.next_into(pool, cs.cuda_stream)
@@ -779,6 +796,9 @@ class DeviceFeeder:
             if self.loader.bf16_values != (self.x_dtype == torch.bfloat16):
                 raise ValueError(f"DeviceFeeder(x_dtype={self.x_dtype}) over a NativeLoader with bf16_values="
                                  f"{self.loader.bf16_values}: set both for the bf16 configuration")
+            if self.loader.exhausted:
+                raise RuntimeError("this NativeLoader has handed out all its batches (one pass per loader: "
+                                   "ask for several epochs with NativeLoader(..., epochs=E), or make a new one)")
             yield from self._iter_native(consumer)
             return
         it = iter(self.loader)
@@ -822,6 +842,12 @@ class _LoaderBatch(ctypes.Structure):
                 ("td_num_edges", ctypes.c_int64), ("bu_num_edges", ctypes.c_int64), ("nnz_max", ctypes.c_int64),
                 ("spill", ctypes.c_int64), ("bytes", ctypes.c_int64), ("off", ctypes.c_int64 * 9),
                 ("seq", ctypes.c_int64)]
+
+
+class _LoaderStats(ctypes.Structure):
+    """bgcn_loader_stats (include/bgcn.h)."""
+    _fields_ = [("packs", ctypes.c_int64), ("pack_ms", ctypes.c_double), ("slot_wait_ms", ctypes.c_double),
+                ("caller_wait_ms", ctypes.c_double), ("threads", ctypes.c_int64)]
 
 
 _SECTION_NAMES = tuple(name for name, _ in _SECTIONS)
@@ -881,6 +907,7 @@ class NativeLoader:
         self.slot_bytes = int(self._L.bgcn_loader_slot_bytes(h))
         self._out = _LoaderBatch()
         self._trees = np.empty(self.batch_size, np.int64)
+        self.exhausted = False      # every batch handed out (the loader makes one pass)
 
     def __len__(self) -> int:
         return int(self._L.bgcn_loader_len(self._h))
@@ -899,10 +926,30 @@ class NativeLoader:
         rc = self._L.bgcn_loader_next(self._h, dst.data_ptr(), dst.numel(), stream_handle,
                                               ctypes.addressof(o), self._trees.ctypes.data, self._trees.size, None)
         if rc == 1:
+            self.exhausted = True
             return None
         self._lib.check(rc)
         B = o.num_graphs
         return self._meta(o), self.store.root_tweetid[self._trees[:B]]
+
+    def wait(self) -> bool:
+        """Block until the next batch is packed (without taking it); False after the last."""
+        rc = self._L.bgcn_loader_wait(self._h)
+        if rc == 1:
+            return False
+        self._lib.check(rc)
+        return True
+
+    def stats(self, reset: bool = False) -> dict:
+        """Where the loader's time went (bgcn_loader_get_stats): batches packed, mean ms per pack
+        (one thread), thread-ms waiting for a slot's turn, caller ms waiting for packed
+        batches, threads."""
+        o = _LoaderStats()
+        self._lib.check(self._L.bgcn_loader_get_stats(self._h, ctypes.addressof(o), int(reset)))
+        n = max(int(o.packs), 1)
+        return {"packs": int(o.packs), "pack_ms_per_batch": round(o.pack_ms / n, 4),
+                "slot_wait_ms_per_batch": round(o.slot_wait_ms / n, 4),
+                "caller_wait_ms_total": round(o.caller_wait_ms, 3), "threads": int(o.threads)}
 
     def next_host(self) -> Optional[HostBatch]:
         """(``pinned=False``) the next batch as a :class:`HostBatch` over a copy of its bytes."""
@@ -911,6 +958,7 @@ class NativeLoader:
         rc = self._L.bgcn_loader_next(self._h, None, 0, None, ctypes.addressof(o), self._trees.ctypes.data,
                                               self._trees.size, ctypes.byref(p))
         if rc == 1:
+            self.exhausted = True
             return None
         self._lib.check(rc)
         raw = np.ctypeslib.as_array((ctypes.c_uint8 * o.bytes).from_address(p.value)).copy()
@@ -944,13 +992,19 @@ class prepare_ahead:
     finds it on ``Batch_data._bgcn_prep`` and skips K1 and the pass over X.  The loop body
     is the reference's; the batches are dense-x device batches (collated ``Batch``).
     ``slots`` prepared buffers are reused in turn: a preparation into a slot waits for the
-    caller's stream, so the step that read the slot's previous batch has finished."""
+    caller's stream, so the step that read the slot's previous batch has finished, and it
+    retires the slot's previous preparation (a batch run again after its slot was reused
+    is prepared inline by its forward: ``PreparedBatch.matches``).  The batch's tensors are
+    marked as used by the side stream (``record_stream``), so a batch dropped before its
+    preparation ends keeps its memory until then; when the iteration ends the caller's
+    stream is ordered behind the side stream."""
 
     def __init__(self, batches, model, slots: int = 2):
         if slots < 2:
             raise ValueError("prepare_ahead needs at least two buffers")
         self.batches, self.model, self.slots = batches, model, slots
         self._bufs = [None] * slots
+        self._gens = [[0] for _ in range(slots)]   # per slot: generation of its current batch
         self._stream = None
 
     def _launch(self, data, slot: int):
@@ -961,8 +1015,13 @@ class prepare_ahead:
         self._stream.wait_stream(main)          # the batch's tensors and the slot's last reader
         m = self.model
         feat = m._feat(data) if hasattr(m, "_feat") else "auto"
+        gen = self._gens[slot]
+        gen[0] += 1                             # the slot's previous preparation is stale now
         with torch.cuda.stream(self._stream):
             prep = prepare_batch(data, m.degree_on, feat, buf=self._bufs[slot], stream=self._stream)
+        for t in prep._keep:                    # read by the side stream: freed only after it
+            t.record_stream(self._stream)
+        prep._slot = (gen, gen[0])
         self._bufs[slot] = prep.buf
         data._bgcn_prep = prep
 
@@ -972,20 +1031,26 @@ class prepare_ahead:
             cur = next(it)
         except StopIteration:
             return
-        self._launch(cur, 0)
-        k = 0
-        while True:
-            try:
-                nxt = next(it)
-            except StopIteration:
-                nxt = None
-            if nxt is not None:
-                self._launch(nxt, (k + 1) % self.slots)
-            yield cur
-            if nxt is None:
-                return
-            cur = nxt
-            k += 1
+        try:
+            self._launch(cur, 0)
+            k = 0
+            while True:
+                try:
+                    nxt = next(it)
+                except StopIteration:
+                    nxt = None
+                if nxt is not None:
+                    self._launch(nxt, (k + 1) % self.slots)
+                yield cur
+                if nxt is None:
+                    return
+                cur = nxt
+                k += 1
+        finally:
+            # a preparation no forward consumed (the loop broke early, or its batch no
+            # longer matched) is joined: nothing still writes a buffer the caller drops
+            if self._stream is not None:
+                torch.cuda.current_stream(self._stream.device).wait_stream(self._stream)
 
 
 def host_fed_loader(store, batch_size: int = 128, num_workers: int = 5, shuffle: bool = True,

@@ -598,12 +598,21 @@ class PreparedBatch:
         self.td_num_edges, self.bu_num_edges = td_edges, bu_edges
         self.degree_on, self.dense, self.key, self._keep, self.event = degree_on, dense, key, keep, event
         self._waited = False
+        # (slot, generation) when the buffer is one of a pipeline's reused slots
+        # (prepare_ahead): the slot's counter moves on when a later batch is prepared into
+        # it, and this preparation then no longer matches
+        self._slot = None
+
+    def current(self) -> bool:
+        """Whether the buffer still holds this preparation (a reused slot may have taken a
+        later batch since)."""
+        return self._slot is None or self._slot[0][0] == self._slot[1]
 
     def matches(self, data, degree_on: str, feat_mode: int) -> bool:
-        """Whether this preparation is of ``data`` as it is now (same tensors, unmodified)
-        for that degree convention and feature path."""
-        return (self.degree_on == degree_on and self.dense == (feat_mode == _lib.BGCN_FEAT_DENSE)
-                and self.key == _prep_key(data))
+        """Whether this preparation is of ``data`` as it is now (same tensors, unmodified,
+        its buffer not reused) for that degree convention and feature path."""
+        return (self.current() and self.degree_on == degree_on
+                and self.dense == (feat_mode == _lib.BGCN_FEAT_DENSE) and self.key == _prep_key(data))
 
     def check_matches(self, x, batch, rootindex, B, feat_mode) -> None:
         if (x.size(0), B, x.size(1)) != (self.num_nodes, self.num_graphs, self.in_feats) or \
@@ -678,6 +687,10 @@ def _encoder_backward(ctx, saved, dhead, stream):
     ctx.ws = None
     if ws is None:
         raise RuntimeError("bigcn_encoder: backward called twice or without a saved forward")
+    for g in ctx.graphs:
+        if isinstance(g, PreparedBatch) and not g.current():
+            raise RuntimeError("bigcn_encoder: the forward's prepared batch buffer was reused by a later "
+                               "batch (prepare_ahead) before this backward")
     check(L.bgcn_bigcn_backward(ctypes.byref(a), ws.data_ptr(), ws.numel(), stream))
     return grads
 

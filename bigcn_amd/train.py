@@ -154,6 +154,10 @@ class FusedTrainStep:
         self._bufs = {}
         self._loss_ring = None
         self._loss_at = 0
+        # test hook: take the world > 1 branch of __call__ (defer_dw1 + the two async
+        # all-reduces) on a one-rank process group, so the code an 8-GPU run executes is
+        # exercised over RCCL on a one-GPU box (tests/nccl_gpu_worker.py)
+        self._force_dp_overlap = False
 
     def _image_key(self):
         return (self.opt.step_count, tuple(p._version for p in self._img_params),
@@ -427,15 +431,22 @@ class FusedTrainStep:
 
     def __call__(self, data, seed: Optional[int] = None, logp: Optional[torch.Tensor] = None,
                  next_data=None):
+        """One training step (the step, the all-reduce at world > 1, the optimiser update).
+
+        Returns the loss as a 0-dim fp32 device tensor that is a VIEW into a ring of 4096
+        loss slots: it keeps its value for the next 4095 calls and is then overwritten
+        (no allocation per step).  Keep ``loss.item()`` or ``loss.clone()`` to hold a loss
+        longer.  ``next_data``: see :meth:`forward_backward`."""
         world = self.bucket.world(self.group)
-        overlap = world > 1 and os.environ.get("BGCN_DP_OVERLAP", "1") != "0"
+        overlap = (world > 1 or self._force_dp_overlap) and os.environ.get("BGCN_DP_OVERLAP", "1") != "0"
         if overlap:
             # the bucket in two all-reduces: everything but the conv1 weight gradients (and
             # the status slot) while the tail computes dW1, then dW1 (SURVEY.md 8(e))
             loss = self.forward_backward(data, seed, logp, next_data, defer_dw1=True)
-            work_a = self.bucket.allreduce_part_async("a", self.group)
+            force = self._force_dp_overlap
+            work_a = self.bucket.allreduce_part_async("a", self.group, force=force)
             self.finish_dw1()
-            work_b = self.bucket.allreduce_part_async("b", self.group)
+            work_b = self.bucket.allreduce_part_async("b", self.group, force=force)
             for w in (work_a, work_b):
                 if w is not None:
                     w.wait()

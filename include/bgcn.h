@@ -48,7 +48,7 @@ typedef struct ihipStream_t* bgcn_stream_t; /* == hipStream_t */
 #define BGCN_EINVAL (-1)
 #define BGCN_EHIP (-2)
 
-#define BGCN_ABI_VERSION 11
+#define BGCN_ABI_VERSION 12
 
 /* Degree convention of gcn_norm: PyG >= 1.6 normalises by TARGET (col) degree,
  * PyG 1.3.2 (the version readme.md:28 pins) by SOURCE (row) degree. */
@@ -628,6 +628,19 @@ int64_t bgcn_loader_len(void* handle);          /* batches over all epochs */
  * the packed bytes until the next call.  Returns 1 after the last batch. */
 int bgcn_loader_next(void* handle, void* dst, size_t dst_bytes, bgcn_stream_t stream, bgcn_loader_batch* out,
                      int64_t* trees, int64_t trees_cap, const void** host_bytes);
+/* (ABI 12) Block until the next batch is packed, without taking it (a copy timed after this
+ * call holds only the copy); returns 1 after the last batch. */
+int bgcn_loader_wait(void* handle);
+/* (ABI 12) Where the loader's time goes, since creation or the last reset: batches packed,
+ * thread-milliseconds inside the packing, thread-milliseconds waiting for a slot's turn (its
+ * previous batch's copy issued and completed), caller milliseconds waiting in
+ * bgcn_loader_next / bgcn_loader_wait for a packed batch, and the collating threads. */
+typedef struct bgcn_loader_stats {
+  int64_t packs;
+  double pack_ms, slot_wait_ms, caller_wait_ms;
+  int64_t threads;
+} bgcn_loader_stats;
+int bgcn_loader_get_stats(void* handle, bgcn_loader_stats* out, int reset);
 void bgcn_loader_destroy(void* handle);
 
 #ifdef __cplusplus

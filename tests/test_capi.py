@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = _lib.load_library()
     for name in _declared_functions():
         assert hasattr(lib, name), name
-    assert lib.bgcn_abi_version() == 11
+    assert lib.bgcn_abi_version() == 12
 
 
 def test_workspace_queries_without_gpu():
@@ -67,6 +67,9 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
         "bgcn_bigcn_args": _lib.BiGCNArgs, "bgcn_step_args": _lib.StepArgs,
         "bgcn_adam_args": AdamArgs, "bgcn_batch": _lib.BatchDesc, "bgcn_spmm_plan": _lib.SpmmPlan,
     }
+    from bigcn_amd import feed
+    structs.update({"bgcn_tree_store": feed._TreeStoreArgs, "bgcn_loader_batch": feed._LoaderBatch,
+                    "bgcn_loader_stats": feed._LoaderStats})
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')

@@ -262,6 +262,7 @@ def test_native_loader_order_and_indices():
     while (hb := L.next_host()) is not None:
         out.append(L.last_trees)
     assert np.array_equal(np.concatenate(out), idx) and [len(o) for o in out] == [7, 7, 7, 7, 2]
+    assert L.exhausted and L.next_host() is None      # one pass per loader
     L.close()
     with pytest.raises(Exception):
         FD.NativeLoader(st, batch_size=4, indices=[0, 40], pinned=False)

@@ -105,8 +105,10 @@ def test_two_ranks_on_the_hip_step(tmp_path):
 
 
 def test_rccl_deferred_dw1_one_rank():
-    """The RCCL (`nccl` backend) path of the overlapped two-part all-reduce, on a one-rank
-    group in a fresh process (the box has one GPU; RCCL refuses two ranks on one device)."""
+    """The RCCL (`nccl` backend) path of the overlapped two-part all-reduce through
+    FusedTrainStep.__call__ itself (its world > 1 branch forced on a one-rank group), in a
+    fresh process (the box has one GPU; RCCL refuses two ranks on one device): three steps
+    train to the bits of the world-1 step."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
                LOCAL_RANK="0", WORLD_SIZE="1")
     env.pop("BGCN_DIST_BACKEND", None)

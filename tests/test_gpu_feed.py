@@ -195,6 +195,11 @@ def test_native_loader_feeder_end_to_end_matches_dense(tmp_path):
     assert n == 12 and mean_bytes > 0 and ms > 0
     dense = [_dense_batch(store, range(8 * k, 8 * k + 8)) for k in range(6)]
     _assert_same(_run(dense, 5000), _run(got, 5000))
+    # one pass per loader: a second pass over the exhausted loader raises (it used to
+    # yield nothing, silently)
+    assert loader.exhausted
+    with pytest.raises(RuntimeError):
+        next(iter(FD.DeviceFeeder(loader, DEV)))
     loader.close()
 
 

@@ -64,3 +64,28 @@ def test_prepare_ahead_matches_inline_preparation():
     m = _model(p)
     m(bb, seed=1)
     assert "_bgcn_graphs" in bb.__dict__
+
+
+def test_prepare_ahead_reused_slot_is_not_taken():
+    """A batch run again after its prepared buffer was reused by a later batch (two slots,
+    three batches: batch 0's slot takes batch 2) is prepared inline, and its output is the
+    inline output (advisor finding: the stale buffer held another batch's graphs)."""
+    from oracle import bigcn_oracle as O
+    from test_gpu_bigcn import _synth, close
+    from test_gpu_train import _model
+    from bigcn_amd.feed import prepare_ahead
+    batches = [_synth(120 + k, 16 + 8 * k, 150) for k in range(3)]
+    p = O.make_params(5000, 64, 64, 4, seed=48)
+    m = _model(p)
+    m.eval()
+    for b in batches:
+        b.__dict__.pop("_bgcn_graphs", None)
+        b.__dict__.pop("_bgcn_prep", None)
+    seen = [m(b) for b in prepare_ahead(batches, m)]
+    b0 = batches[0]
+    assert not b0._bgcn_prep.current() and batches[2]._bgcn_prep.current()
+    assert "_bgcn_graphs" not in b0.__dict__
+    again = m(b0)                              # slot 0 now holds batch 2's preparation
+    assert "_bgcn_graphs" in b0.__dict__       # ... so batch 0 was prepared inline
+    torch.cuda.synchronize()
+    close(again, seen[0], tol=1e-6, what="logp of a batch run again")
