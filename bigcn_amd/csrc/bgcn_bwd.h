@@ -98,6 +98,12 @@ __device__ inline void dw2_body(const TX* __restrict__ X, int64_t ldx, int64_t F
     }
   };
 
+  // Blocked accumulation: each 32-node k-tile sums into a fresh accumulator (16 MFMA
+  // steps), which is then added to the running sum - one fp32 accumulator took ~1000
+  // sequential MFMA adds per 2048-node split, and where the node terms cancel (a small
+  // entry of a large sum) that left TD conv2's weight gradient 2.3e-5 off the fp64 oracle
+  // elementwise (4.4x under the 1e-4 bar); the tile sums cut the
+  // sequential depth to 16 + kchunk / 32.
   f32x16 acc = {0};
   const int h = lane >> 5, r32 = lane & 31;
   const int nk = int((ke - kb + BK - 1) / BK);
@@ -111,8 +117,16 @@ __device__ inline void dw2_body(const TX* __restrict__ X, int64_t ldx, int64_t F
     if (kt + 1 < nk) gload(kb + int64_t(kt + 1) * BK);
     const float* A = &As[buf][h * H + wr * 32 + r32];
     const float* B = &Bs[buf][h * BN + wc * 32 + r32];
+#ifdef BGCN_DW2_ONE_ACC   // A/B build: the single running accumulator of round 5
 #pragma unroll
     for (int s = 0; s < BK / 2; ++s) acc = mfma32x32x2(A[2 * s * H], B[2 * s * BN], acc);
+#else
+    f32x16 tile = {0};
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) tile = mfma32x32x2(A[2 * s * H], B[2 * s * BN], tile);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += tile[r];
+#endif
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
   }

@@ -10,8 +10,8 @@
 // ~170 us per batch, more than half the host-fed step.
 //
 // Slot life cycle: FREE -> packed by a worker -> READY -> copy issued by bgcn_loader_next
-// (an event recorded after it on the copy stream) -> FREE again once that event completed
-// (the worker packing batch seq + nslots into it waits for it).  Batches come out in
+// (an event recorded after it on the copy stream) -> FREE again once the caller's thread
+// sees that event completed (the worker packing batch seq + nslots into it waits for it).  Batches come out in
 // sequence order; the permutation of each epoch is a Fisher-Yates shuffle from a
 // counter-based generator of (seed, epoch), so a run is reproducible for a given seed.
 #include <hip/hip_runtime.h>
@@ -204,8 +204,37 @@ bool pack(const Loader& L, const std::vector<int64_t>& t, uint8_t* out, int64_t 
   return true;
 }
 
+// The caller's thread retires copied slots: a slot whose copy was issued (state 3) goes back
+// to the workers (state 0) once its copy event has completed - polled with hipEventQuery,
+// never waited for by a worker.  (Round 6: workers blocking in hipEventSynchronize on their
+// slot's copy stalled the caller's next hipMemcpyAsync by ~6.5 ms every few batches when
+// the copies ran back to back - tools/loader_probe.py, profiles/r06_loader_probe.json.)
+// Under L->mu; true when a slot was retired.
+bool retire_copied(Loader* L) {
+  bool any = false;
+  for (Slot& s : L->slots) {
+    if (s.state == 3 && hipEventQuery(s.copied) == hipSuccess) {
+      s.state = 0;
+      any = true;
+    }
+  }
+  return any;
+}
+
+// The caller waits (under lk) until batch `seq` is packed, retiring completed copies
+// meanwhile so that workers waiting for those slots can go on.
+void wait_packed(Loader* L, std::unique_lock<std::mutex>& lk, Slot& s, int64_t seq) {
+  const auto tw = std::chrono::steady_clock::now();
+  if (retire_copied(L)) L->cv.notify_all();
+  while (!(s.state == 2 && s.seq == seq) && L->error.empty()) {
+    L->cv.wait_for(lk, std::chrono::microseconds(50));
+    if (retire_copied(L)) L->cv.notify_all();
+  }
+  L->caller_wait_ms += ms_since(tw);
+}
+
 void worker(Loader* L) {
-  if (L->pinned) (void)hipSetDevice(L->device);
+  // (the workers make no HIP call: the caller's thread issues the copies and retires them)
   std::vector<int64_t> trees;
   for (;;) {
     int64_t seq;
@@ -216,22 +245,15 @@ void worker(Loader* L) {
       seq = L->next_pack++;
       const auto tw = std::chrono::steady_clock::now();
       sl = &L->slots[size_t(seq % int64_t(L->slots.size()))];
-      // the slot's turn: its previous batch (seq - nslots) handed out - copy issued
-      L->cv.wait(lk, [&] { return L->stop || (sl->next == seq && (sl->state == 0 || sl->state == 3)); });
+      // the slot's turn: its previous batch (seq - nslots) handed out and its copy retired
+      L->cv.wait(lk, [&] { return L->stop || (sl->next == seq && sl->state == 0); });
       if (L->stop) return;
       const std::vector<int64_t>& p = epoch_perm(*L, seq / L->per_epoch);
       const int64_t b0 = (seq % L->per_epoch) * L->batch_size;
       const int64_t b1 = std::min<int64_t>(b0 + L->batch_size, int64_t(p.size()));
       trees.assign(p.begin() + b0, p.begin() + b1);
-      const bool copying = sl->state == 3;
       sl->state = 1;
       sl->seq = seq;
-      if (copying) {   // ... and complete
-        hipEvent_t ev = sl->copied;
-        lk.unlock();
-        (void)hipEventSynchronize(ev);
-        lk.lock();
-      }
       L->slot_wait_ms += ms_since(tw);
     }
     bgcn_loader_batch m{};
@@ -360,9 +382,7 @@ int bgcn_loader_next(void* handle, void* dst, size_t dst_bytes, bgcn_stream_t st
   if (L->next_out >= L->total) return 1;   // the end of the data
   const int64_t seq = L->next_out;
   Slot& s = L->slots[size_t(seq % int64_t(L->slots.size()))];
-  const auto tw = std::chrono::steady_clock::now();
-  L->cv.wait(lk, [&] { return s.state == 2 && s.seq == seq; });
-  L->caller_wait_ms += ms_since(tw);
+  wait_packed(L, lk, s, seq);
   if (!L->error.empty()) return fail(BGCN_EINVAL, L->error.c_str());
   *out = s.meta;
   if (trees) {
@@ -396,9 +416,7 @@ int bgcn_loader_wait(void* handle) {
   if (L->next_out >= L->total) return 1;
   const int64_t seq = L->next_out;
   Slot& s = L->slots[size_t(seq % int64_t(L->slots.size()))];
-  const auto tw = std::chrono::steady_clock::now();
-  L->cv.wait(lk, [&] { return s.state == 2 && s.seq == seq; });
-  L->caller_wait_ms += ms_since(tw);
+  wait_packed(L, lk, s, seq);
   if (!L->error.empty()) return fail(BGCN_EINVAL, L->error.c_str());
   return BGCN_OK;
 }

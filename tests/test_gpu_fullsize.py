@@ -41,6 +41,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 TIE_WINDOW = 1e-6    # |h| / max|h| of an entry whose relu' decision may differ from fp64's
 TIE_FLIPS = 16       # differing relu' decisions allowed per [N, 64] tensor
+DW2_DENSE_TOL = 2e-5  # the fp32 dense path's conv2 weight gradients (k_dw2_f32), both errors
 
 
 def _dump_table(name, N, table, ties, depth):
@@ -67,6 +68,16 @@ def errors(a, b):
     err = (a - b).abs()
     rms = float(b.pow(2).mean().sqrt())
     return float(err.max()) / max(float(b.abs().max()), 1e-300), float((err / (b.abs() + rms).clamp_min(1e-300)).max())
+
+
+def block_errors(a, b, cols):
+    """errors() of the columns ``cols`` of a matrix, scaled by the WHOLE matrix's max and rms."""
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    rms = float(b.pow(2).mean().sqrt())
+    err = (a[:, cols] - b[:, cols]).abs()
+    return (float(err.max()) / max(float(b.abs().max()), 1e-300),
+            float((err / (b[:, cols].abs() + rms).clamp_min(1e-300)).max()))
 
 
 def close_elem(a, b, tol=TOL, what=""):
@@ -157,6 +168,13 @@ def test_full_size_step_matches_oracle(workload, mode):
         _ORACLE_CACHE[key] = (masks, (rlogp, rloss, rgrads, st))
     del mk
     table = {k: errors(g, rgrads[k]) for k, g in zip(KEYS, grads)}
+    # the conv2 weight gradients by column block - the relu(H1) columns [:, :64] and the root
+    # extension [:, 64:] come from different kernels / roles - against the whole tensor's
+    # max and rms (the bar the whole tensor is held to)
+    for k, g in zip(KEYS, grads):
+        if "conv2.lin.weight" in k:
+            for name, cols in (("[:, :64] relu(H1) cols", slice(0, 64)), ("[:, 64:] root cols", slice(64, None))):
+                table[f"{k} {name}"] = block_errors(g, rgrads[k], cols)
     table["logp"] = errors(logp, rlogp)
     table["loss"] = errors(loss, rloss)
     ties, tie_depth = {}, {}
@@ -179,6 +197,12 @@ def test_full_size_step_matches_oracle(workload, mode):
     _dump_table(f"{workload}_{mode}", N, table, ties, tie_depth)
     bad = {k: v for k, v in table.items() if v[0] > TOL or v[1] > TOL}
     assert not bad, f"{workload}: beyond {TOL:g}: {bad}"
+    if mode == "dense" and workload == "twitter15":
+        # fp32 X on the dense path: the conv2 weight gradients come from k_dw2_f32's f32 MFMA
+        # sums over up to 2048 nodes per split; held to 2e-5 (5x under the bar), the margin
+        # its blocked accumulation is meant to keep (round 5: 2.3e-5 with one accumulator)
+        for k in ("TDrumorGCN.conv2.lin.weight", "BUrumorGCN.conv2.lin.weight"):
+            assert max(table[k]) <= DW2_DENSE_TOL, f"{k}: {table[k]} beyond {DW2_DENSE_TOL:g}"
 
 
 def test_steps_under_prefetch_load_stay_valid():
