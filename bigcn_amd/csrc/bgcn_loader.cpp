@@ -64,7 +64,8 @@ inline float round_bf16(float v) {
 }
 
 struct Slot {
-  uint8_t* host = nullptr;       // page-locked (hipHostMalloc), or plain memory (host-only loader)
+  uint8_t* host = nullptr;       // page-locked (registered), or plain memory (host-only loader)
+  const uint8_t* dev = nullptr;  // the same pages in the device's address space (pinned loader)
   int64_t next = 0;              // the batch it takes next (its index, then + nslots per use)
   int64_t seq = -1;              // the batch it holds / is being packed with
   int state = 0;                 // 0 free, 1 packing, 2 ready, 3 copy issued, 4 held (host-only)
@@ -95,6 +96,10 @@ struct Loader {
   // time accounting (bgcn_loader_stats), under mu
   int64_t packs = 0;
   double pack_ms = 0, slot_wait_ms = 0, caller_wait_ms = 0;
+  double copy_call_ms = 0, copy_call_ms_max = 0, record_call_ms_max = 0;   // host time in the copy calls
+  // the H2D copy: k_slot_copy reading the mapped slot (default), or hipMemcpyAsync on the
+  // DMA engine (BGCN_LOADER_COPY=sdma, A/B only: see k_slot_copy)
+  bool sdma = false;
 };
 
 inline double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -202,6 +207,26 @@ bool pack(const Loader& L, const std::vector<int64_t>& t, uint8_t* out, int64_t 
   m.spill = spill;
   m.bytes = off;
   return true;
+}
+
+// The H2D copy of a packed slot: a kernel reading the slot's page-locked pages through their
+// device mapping (PCIe reads, 16 B per lane, four in flight), on the caller's copy stream.
+// (Round 6: hipMemcpyAsync on the DMA engine stalled the issuing call by ~6.5 ms every few
+// batches when copies came back to back - HSA_ENABLE_SDMA=0 removed the stalls - so the
+// library issues its own copy; tools/loader_probe.py, profiles/r06_loader_probe*.json.)
+constexpr int kCopyBlocks = 64;
+typedef unsigned int copy4_t __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_slot_copy(const copy4_t* __restrict__ src, copy4_t* __restrict__ dst,
+                                                  int64_t n16) {
+  const int64_t stride = int64_t(gridDim.x) * 1024;
+  for (int64_t i = int64_t(blockIdx.x) * 1024 + threadIdx.x; i < n16; i += stride) {
+    copy4_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + min<int64_t>(i + 256 * u, n16 - 1));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + 256 * u < n16) __builtin_nontemporal_store(v[u], dst + i + 256 * u);
+  }
 }
 
 // The caller's thread retires copied slots: a slot whose copy was issued (state 3) goes back
@@ -331,18 +356,24 @@ int bgcn_loader_create(const bgcn_tree_store* st, const int64_t* indices, int64_
   L->slots.resize(size_t(nslots));
   for (int i = 0; i < nslots; ++i) L->slots[size_t(i)].next = i;
   if (L->pinned && hipGetDevice(&L->device) != hipSuccess) L->pinned = false;
-  for (Slot& s : L->slots) {
+  if (const char* e = std::getenv("BGCN_LOADER_COPY")) L->sdma = std::strcmp(e, "sdma") == 0;
+  for (size_t k = 0; k < L->slots.size(); ++k) {
+    Slot& s = L->slots[k];
     void* p = nullptr;
     bool ok;
     if (L->pinned) {
       // cached host pages, page-locked for the DMA (the packing threads write ~4.5 MB per
-      // Twitter-sized batch; hipHostMalloc's default mapping made those writes slower)
+      // Twitter-sized batch; hipHostMalloc's default mapping made those writes slower), and
+      // mapped into the device's address space for k_slot_copy
       p = std::aligned_alloc(4096, size_t(L->slot_bytes));
-      ok = p != nullptr && hipHostRegister(p, size_t(L->slot_bytes), hipHostRegisterDefault) == hipSuccess;
+      ok = p != nullptr && hipHostRegister(p, size_t(L->slot_bytes), hipHostRegisterMapped) == hipSuccess;
       if (!ok && p) {
         std::free(p);
         p = nullptr;
       }
+      void* dp = nullptr;
+      ok = ok && hipHostGetDevicePointer(&dp, p, 0) == hipSuccess && dp != nullptr;
+      s.dev = static_cast<const uint8_t*>(dp);
       ok = ok && hipEventCreateWithFlags(&s.copied, hipEventDisableTiming) == hipSuccess;
     } else {
       p = ::operator new(size_t(L->slot_bytes), std::nothrow);
@@ -393,8 +424,23 @@ int bgcn_loader_next(void* handle, void* dst, size_t dst_bytes, bgcn_stream_t st
     BGCN_CHECK_ARG(L->pinned, "a host-only loader copies nothing");
     BGCN_CHECK_ARG(dst_bytes >= size_t(s.meta.bytes), "device buffer too small for the batch");
     auto st = reinterpret_cast<hipStream_t>(stream);
-    BGCN_CHECK_HIP(hipMemcpyAsync(dst, s.host, size_t(s.meta.bytes), hipMemcpyHostToDevice, st));
+    const auto tc = std::chrono::steady_clock::now();
+    if (L->sdma) {
+      BGCN_CHECK_HIP(hipMemcpyAsync(dst, s.host, size_t(s.meta.bytes), hipMemcpyHostToDevice, st));
+    } else {
+      BGCN_CHECK_ARG((reinterpret_cast<uintptr_t>(dst) & 15) == 0, "device buffer must be 16-byte aligned");
+      const int64_t n16 = s.meta.bytes / 16;   // sections are 256-byte padded
+      hipLaunchKernelGGL(k_slot_copy, dim3(unsigned(std::min<int64_t>(kCopyBlocks, (n16 + 1023) / 1024))),
+                         dim3(256), 0, st, reinterpret_cast<const copy4_t*>(s.dev), static_cast<copy4_t*>(dst), n16);
+      BGCN_CHECK_HIP(hipGetLastError());
+    }
+    const double tcall = ms_since(tc);
+    const auto tr = std::chrono::steady_clock::now();
     BGCN_CHECK_HIP(hipEventRecord(s.copied, st));
+    const double trec = ms_since(tr);
+    L->copy_call_ms += tcall + trec;
+    L->copy_call_ms_max = std::max(L->copy_call_ms_max, tcall);
+    L->record_call_ms_max = std::max(L->record_call_ms_max, trec);
     s.state = 3;
     s.next = seq + int64_t(L->slots.size());
   } else {
@@ -430,9 +476,12 @@ int bgcn_loader_get_stats(void* handle, bgcn_loader_stats* out, int reset) {
   out->slot_wait_ms = L->slot_wait_ms;
   out->caller_wait_ms = L->caller_wait_ms;
   out->threads = int64_t(L->workers.size());
+  out->copy_call_ms = L->copy_call_ms;
+  out->copy_call_ms_max = L->copy_call_ms_max;
+  out->record_call_ms_max = L->record_call_ms_max;
   if (reset) {
     L->packs = 0;
-    L->pack_ms = L->slot_wait_ms = L->caller_wait_ms = 0;
+    L->pack_ms = L->slot_wait_ms = L->caller_wait_ms = L->copy_call_ms = L->copy_call_ms_max = L->record_call_ms_max = 0;
   }
   return BGCN_OK;
 }

@@ -847,7 +847,9 @@ class _LoaderBatch(ctypes.Structure):
 class _LoaderStats(ctypes.Structure):
     """bgcn_loader_stats (include/bgcn.h)."""
     _fields_ = [("packs", ctypes.c_int64), ("pack_ms", ctypes.c_double), ("slot_wait_ms", ctypes.c_double),
-                ("caller_wait_ms", ctypes.c_double), ("threads", ctypes.c_int64)]
+                ("caller_wait_ms", ctypes.c_double), ("threads", ctypes.c_int64),
+                ("copy_call_ms", ctypes.c_double), ("copy_call_ms_max", ctypes.c_double),
+                ("record_call_ms_max", ctypes.c_double)]
 
 
 _SECTION_NAMES = tuple(name for name, _ in _SECTIONS)
@@ -949,7 +951,10 @@ class NativeLoader:
         n = max(int(o.packs), 1)
         return {"packs": int(o.packs), "pack_ms_per_batch": round(o.pack_ms / n, 4),
                 "slot_wait_ms_per_batch": round(o.slot_wait_ms / n, 4),
-                "caller_wait_ms_total": round(o.caller_wait_ms, 3), "threads": int(o.threads)}
+                "caller_wait_ms_total": round(o.caller_wait_ms, 3), "threads": int(o.threads),
+                "copy_call_ms_per_batch": round(o.copy_call_ms / n, 4),
+                "memcpy_call_ms_max": round(o.copy_call_ms_max, 3),
+                "record_call_ms_max": round(o.record_call_ms_max, 3)}
 
     def next_host(self) -> Optional[HostBatch]:
         """(``pinned=False``) the next batch as a :class:`HostBatch` over a copy of its bytes."""

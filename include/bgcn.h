@@ -634,11 +634,14 @@ int bgcn_loader_wait(void* handle);
 /* (ABI 12) Where the loader's time goes, since creation or the last reset: batches packed,
  * thread-milliseconds inside the packing, thread-milliseconds waiting for a slot's turn (its
  * previous batch's copy issued and completed), caller milliseconds waiting in
- * bgcn_loader_next / bgcn_loader_wait for a packed batch, and the collating threads. */
+ * bgcn_loader_next / bgcn_loader_wait for a packed batch, the collating threads, and the
+ * caller's host milliseconds inside the copy-issuing HIP calls (total; the largest
+ * hipMemcpyAsync and hipEventRecord call). */
 typedef struct bgcn_loader_stats {
   int64_t packs;
   double pack_ms, slot_wait_ms, caller_wait_ms;
   int64_t threads;
+  double copy_call_ms, copy_call_ms_max, record_call_ms_max;
 } bgcn_loader_stats;
 int bgcn_loader_get_stats(void* handle, bgcn_loader_stats* out, int reset);
 void bgcn_loader_destroy(void* handle);

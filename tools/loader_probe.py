@@ -1,7 +1,8 @@
 """Where the host-fed leg's time goes (round 6): per batch, the host
 time of the feeder's next() and the device time of its H2D copy, for the native loader
-(feed.NativeLoader) and the torch DataLoader form, with and without the training step;
-plus raw H2D copies of one batch's bytes from differently page-locked host buffers.
+(feed.NativeLoader, its copy kernel and the DMA-engine hipMemcpyAsync) and the torch
+DataLoader form, with and without the training step; plus raw H2D copies of one batch's bytes
+from differently page-locked host buffers.
 
     python tools/loader_probe.py [--steps 40]
 """
@@ -130,14 +131,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--copies", default="kernel,sdma", help="the native loader's H2D copy forms (BGCN_LOADER_COPY)")
     args = ap.parse_args()
     from bigcn_amd import feed as FD
     store = FD.TreeStore.synthetic(2048, 256, seed=20250205 + 9, in_feats=5000, num_classes=4)
     res = {"raw": raw_copies(4_500_000)}
-    for native in (True, False):
+    for copy in args.copies.split(","):
+        os.environ["BGCN_LOADER_COPY"] = copy            # read by bgcn_loader_create
         for train in (False, True):
-            res[f"{'native' if native else 'dataloader'}_{'train' if train else 'copyonly'}"] = \
-                feeder_run(store, native, args.steps, args.warmup, train)
+            r = feeder_run(store, True, args.steps, args.warmup, train)
+            r["copy"] = copy
+            res[f"native_{copy}_{'train' if train else 'copyonly'}"] = r
+    os.environ.pop("BGCN_LOADER_COPY", None)
+    for train in (False, True):
+        res[f"dataloader_{'train' if train else 'copyonly'}"] = feeder_run(store, False, args.steps, args.warmup, train)
     res["raw_after"] = raw_copies(4_500_000)
     print(json.dumps(res))
 
