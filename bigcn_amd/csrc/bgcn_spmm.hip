@@ -412,7 +412,10 @@ __global__ __launch_bounds__(256) void k_spmm_fixup_narrow(SpmmBatch sb) {
 // written once.  Chunks of NPGW entries (merge path as above) are row-aligned for rows of
 // <= NPGW entries (the nominal boundary g * NPGW moves back to the start of the row it
 // falls in), so only long rows (BU star roots) leave partial rows for the fixup pass.
-constexpr int NPGW = 16;
+#ifndef BGCN_NPGW
+#define BGCN_NPGW 16
+#endif
+constexpr int NPGW = BGCN_NPGW;
 constexpr int kWideSlice = 1024;   // fixup slice (floats)
 constexpr int kWaveBlock = 256;    // 4 waves per block
 
