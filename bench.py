@@ -149,9 +149,15 @@ ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2):
                  ("dense", 2): "bgcn::k_conv2_fwd_bf16<float, true>", ("dense", 3): "bgcn::k_dw2_f32"}
 
 
-def pmc_file(workload: str) -> str:
-    """The committed PMC passes of a workload's bench command (tools/profile_round.sh)."""
-    return os.path.join(ROOT, "profiles", f"r05_pmc_traffic_{workload}.json")
+def pmc_file(workload: str, mode: str = "auto") -> str:
+    """The committed PMC passes of a workload's bench command (tools/profile_round.sh): the
+    newest round's file for the workload (and the dense feature path's own passes)."""
+    name = workload + ("_dense" if mode == "dense" else "")
+    for r in ("r06", "r05"):
+        f = os.path.join(ROOT, "profiles", f"{r}_pmc_traffic_{name}.json")
+        if os.path.exists(f):
+            return f
+    return os.path.join(ROOT, "profiles", f"r06_pmc_traffic_{name}.json")
 
 
 def pmc_traffic(mode: str, cls: int, workload: str = "twitter15", xbf16: bool = False):
@@ -163,7 +169,7 @@ def pmc_traffic(mode: str, cls: int, workload: str = "twitter15", xbf16: bool = 
     if xbf16:   # the bf16-X instantiation of the templated kernels
         name = name.replace("<float>", "<unsigned short>")
     try:
-        with open(pmc_file(workload)) as f:
+        with open(pmc_file(workload, mode)) as f:
             k = json.load(f)["kernels"].get(name)
     except (OSError, ValueError):
         return None
