@@ -63,6 +63,8 @@ inline float round_bf16(float v) {
   return r;
 }
 
+X
+
 struct Slot {
   uint8_t* host = nullptr;       // page-locked (registered), or plain memory (host-only loader)
   const uint8_t* dev = nullptr;  // the same pages in the device's address space (pinned loader)
@@ -100,6 +102,7 @@ struct Loader {
   // the H2D copy: k_slot_copy reading the mapped slot (default), or hipMemcpyAsync on the
   // DMA engine (BGCN_LOADER_COPY=sdma, A/B only: see k_slot_copy)
   bool sdma = false;
+  int copy_blocks = kCopyBlocks;   // k_slot_copy's grid (BGCN_LOADER_COPY_BLOCKS, A/B)
 };
 
 inline double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -214,7 +217,6 @@ bool pack(const Loader& L, const std::vector<int64_t>& t, uint8_t* out, int64_t 
 // (Round 6: hipMemcpyAsync on the DMA engine stalled the issuing call by ~6.5 ms every few
 // batches when copies came back to back - HSA_ENABLE_SDMA=0 removed the stalls - so the
 // library issues its own copy; tools/loader_probe.py, profiles/r06_loader_probe*.json.)
-constexpr int kCopyBlocks = 64;
 typedef unsigned int copy4_t __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_slot_copy(const copy4_t* __restrict__ src, copy4_t* __restrict__ dst,
                                                   int64_t n16) {
@@ -357,6 +359,7 @@ int bgcn_loader_create(const bgcn_tree_store* st, const int64_t* indices, int64_
   for (int i = 0; i < nslots; ++i) L->slots[size_t(i)].next = i;
   if (L->pinned && hipGetDevice(&L->device) != hipSuccess) L->pinned = false;
   if (const char* e = std::getenv("BGCN_LOADER_COPY")) L->sdma = std::strcmp(e, "sdma") == 0;
+  if (const char* e = std::getenv("BGCN_LOADER_COPY_BLOCKS")) L->copy_blocks = std::max(1, std::atoi(e));
   for (size_t k = 0; k < L->slots.size(); ++k) {
     Slot& s = L->slots[k];
     void* p = nullptr;
@@ -430,7 +433,7 @@ int bgcn_loader_next(void* handle, void* dst, size_t dst_bytes, bgcn_stream_t st
     } else {
       BGCN_CHECK_ARG((reinterpret_cast<uintptr_t>(dst) & 15) == 0, "device buffer must be 16-byte aligned");
       const int64_t n16 = s.meta.bytes / 16;   // sections are 256-byte padded
-      hipLaunchKernelGGL(k_slot_copy, dim3(unsigned(std::min<int64_t>(kCopyBlocks, (n16 + 1023) / 1024))),
+      hipLaunchKernelGGL(k_slot_copy, dim3(unsigned(std::min<int64_t>(L->copy_blocks, (n16 + 1023) / 1024))),
                          dim3(256), 0, st, reinterpret_cast<const copy4_t*>(s.dev), static_cast<copy4_t*>(dst), n16);
       BGCN_CHECK_HIP(hipGetLastError());
     }
