@@ -63,7 +63,10 @@ inline float round_bf16(float v) {
   return r;
 }
 
-X
+// k_slot_copy's default grid: 16 blocks keep ~256 KB of PCIe reads in flight (the copy runs at
+// the 64-block rate, ~0.11 ms per 4.5 MB batch) and leave the step's kernels the other CUs -
+// host-fed 476-488k vs 434-448k trees/s with 64 blocks (profiles/r06_slot_copy_blocks_ab.txt)
+constexpr int kCopyBlocks = 16;
 
 struct Slot {
   uint8_t* host = nullptr;       // page-locked (registered), or plain memory (host-only loader)
@@ -213,7 +216,8 @@ bool pack(const Loader& L, const std::vector<int64_t>& t, uint8_t* out, int64_t 
 }
 
 // The H2D copy of a packed slot: a kernel reading the slot's page-locked pages through their
-// device mapping (PCIe reads, 16 B per lane, four in flight), on the caller's copy stream.
+// device mapping (PCIe reads, 16 B per lane, four in flight; kCopyBlocks blocks), on the
+// caller's copy stream.
 // (Round 6: hipMemcpyAsync on the DMA engine stalled the issuing call by ~6.5 ms every few
 // batches when copies came back to back - HSA_ENABLE_SDMA=0 removed the stalls - so the
 // library issues its own copy; tools/loader_probe.py, profiles/r06_loader_probe*.json.)
