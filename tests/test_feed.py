@@ -263,6 +263,16 @@ def test_native_loader_order_and_indices():
         out.append(L.last_trees)
     assert np.array_equal(np.concatenate(out), idx) and [len(o) for o in out] == [7, 7, 7, 7, 2]
     assert L.exhausted and L.next_host() is None      # one pass per loader
+    ls = L.stats()                                    # bgcn_loader_get_stats (ABI 12)
+    assert ls["packs"] == 5 and ls["threads"] == 2 and ls["pack_ms_per_batch"] >= 0.0
+    assert ls["copy_call_ms_per_batch"] == 0.0       # host-only: no copies issued
+    assert L.stats(reset=True)["packs"] == 5 and L.stats()["packs"] == 0
+    assert not L.wait()                               # bgcn_loader_wait: past the last batch
+    L.close()
+    L = FD.NativeLoader(FD.TreeStore.synthetic(16, 10, seed=3, in_feats=64, num_classes=4),
+                        batch_size=4, num_workers=2, shuffle=False, pinned=False)
+    assert L.wait() and L.wait()                      # waits for batch 0 without taking it
+    assert L.next_host() is not None and L.last_trees.tolist() == [0, 1, 2, 3]
     L.close()
     with pytest.raises(Exception):
         FD.NativeLoader(st, batch_size=4, indices=[0, 40], pinned=False)
