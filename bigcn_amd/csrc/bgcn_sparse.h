@@ -157,9 +157,10 @@ int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s);
 int dw2_bf16_launch(BwdMidArgs& a, hipStream_t s);   // dense mode, bf16 X: dW2 root columns
 int dw2_f32_launch(BwdMidArgs& a, hipStream_t s);    // dense mode, fp32 X: dW2 (k_dw2_f32)
 // the whole weight-independent preparation of one batch on one stream (six launches;
-// mode 1 = dense: no ELL / CSC of X)
+// mode 1 = dense: no ELL / CSC of X); nlanes: 1 = every launch on `s`, 2 = DropEdge + K1
+// forked onto the graph lane beside the pass over X, 0 = the default (BGCN_PREP_LANES)
 int prep_pipeline(const Prepared& p, const bgcn_batch* b, int64_t F, int degree_on, int mode,
-                  hipStream_t s, bool x_part = true);
+                  hipStream_t s, bool x_part = true, int nlanes = 0);
 // part: 0 = the whole tail; 1 = all but dW1; 2 = dW1 only (the deferred-dW1 step)
 int bwd_tail_launch(BwdTailArgs& a, hipStream_t s, int part = 0);
 

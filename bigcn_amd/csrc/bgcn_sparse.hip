@@ -2615,7 +2615,7 @@ static void prepared_state(const Prepared& p, int64_t N, int64_t B, int64_t F, i
 }
 
 int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree_on, int mode,
-                  hipStream_t s, bool x_part) {
+                  hipStream_t s, bool x_part, int nlanes) {
   const int64_t N = bt->num_nodes, B = bt->num_graphs;
   BGCN_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int32_t), s));
   PrepArgs a{};
@@ -2704,10 +2704,11 @@ int prep_pipeline(const Prepared& p, const bgcn_batch* bt, int64_t F, int degree
   // launches then overlap the X window, where the chain is stalled anyway, instead of the
   // chain's second half: twitter15 0.2691-0.2724 vs 0.2732-0.2749 ms per step over five
   // interleaved rounds, synth1024_bf16 -0.7 %, weibo_bf16 within its noise (+0.5 %)
-  static const int lanes = [] {
+  static const int default_lanes = [] {
     const char* e = std::getenv("BGCN_PREP_LANES");
     return e ? atoi(e) : BGCN_PREP_LANES_DEFAULT;
   }();
+  const int lanes = nlanes > 0 ? nlanes : default_lanes;
   if (lanes == 2 && xp) {
     hipStream_t g = s;
     BGCN_TRY(aux_fork(s, kLaneGraph, &g));

@@ -157,7 +157,7 @@ int bigcn_prepared_call(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
 
 // gs: stream of the graph build (K1); the caller joins it before the graphs are used
 static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_mode, void* buf,
-                        size_t bytes, hipStream_t s, Prepared* out, hipStream_t gs) {
+                        size_t bytes, hipStream_t s, Prepared* out, hipStream_t gs, int lanes = 0) {
   BGCN_TRY(check_batch(b));
   BGCN_CHECK_ARG(F > 0 && F % 4 == 0 && b->ldx >= F && b->ldx % 4 == 0, "bad in_feats / ldx");
   const int64_t N = b->num_nodes, B = b->num_graphs;
@@ -175,7 +175,7 @@ static int prepare_into(const bgcn_batch* b, int64_t F, int degree_on, int feat_
   // backward: 0.322 vs 0.329 ms per step), then DropEdge and K1, then the CSC.
   const char* me = std::getenv("BGCN_PREP_MERGED");
   if (s == gs && !(me && atoi(me) == 0)) {
-    BGCN_TRY(prep_pipeline(p, b, F, degree_on, mode, s));
+    BGCN_TRY(prep_pipeline(p, b, F, degree_on, mode, s, true, lanes));
     if (out) *out = p;
     return BGCN_OK;
   }
@@ -493,7 +493,11 @@ extern "C" int bgcn_prepare_batch(const bgcn_batch* batch, int64_t in_feats, int
                                   int32_t feat_mode, void* prepared, size_t prepared_bytes,
                                   bgcn_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  return bgcn::prepare_into(batch, in_feats, degree_on, feat_mode, prepared, prepared_bytes, s, nullptr, s);
+  // one lane: a caller of this entry point already runs it off its critical path (e.g.
+  // feed.prepare_ahead's side stream beside a host-bound per-op loop); forking the graph
+  // build onto a second lane cost that caller's thread ~40 us of host time per batch
+  // (two event records and waits) for no gain it could see (profiles/r06_prep_lanes_dropin.txt)
+  return bgcn::prepare_into(batch, in_feats, degree_on, feat_mode, prepared, prepared_bytes, s, nullptr, s, 1);
 }
 
 extern "C" size_t bgcn_train_step_workspace_size(int64_t num_nodes, int64_t num_graphs,
