@@ -1011,10 +1011,12 @@ class prepare_ahead:
         self._bufs = [None] * slots
         self._gens = [[0] for _ in range(slots)]   # per slot: generation of its current batch
         self._stream = None
+        self._main = None                           # the caller's stream (joined at the end)
 
     def _launch(self, data, slot: int):
         from .ops import prepare_batch
         main = torch.cuda.current_stream(data.x.device)
+        self._main = main
         if self._stream is None:
             self._stream = torch.cuda.Stream(data.x.device)
         self._stream.wait_stream(main)          # the batch's tensors and the slot's last reader
@@ -1055,7 +1057,7 @@ class prepare_ahead:
             # a preparation no forward consumed (the loop broke early, or its batch no
             # longer matched) is joined: nothing still writes a buffer the caller drops
             if self._stream is not None:
-                torch.cuda.current_stream(self._stream.device).wait_stream(self._stream)
+                self._main.wait_stream(self._stream)
 
 
 def host_fed_loader(store, batch_size: int = 128, num_workers: int = 5, shuffle: bool = True,
