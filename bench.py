@@ -82,6 +82,13 @@ sys.path.insert(0, ROOT)
 
 METRIC = "propagation-trees/sec fwd+bwd, batch=128, 5000-dim feats @ 1/2/4/8 MI355X"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (dense)
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 matrix peak (dense)
+# the dense classes whose fp32-grade products run on the bf16 MFMA: products per fp32 product
+# (conv1 / conv2: six-product splits; dW2: the keep bits exact, dZ2 split three ways - its
+# 64 H1 columns of 5064 stay on the f32 MFMA)
+# (bf16 X: X is exact in bf16, so conv1 and conv2's root block take three)
+BF16_PRODUCTS = {("dense", 0, False): 6, ("dense", 2, False): 6, ("dense", 3, False): 3,
+                 ("dense", 0, True): 3, ("dense", 2, True): 3, ("dense", 3, True): 3}
 PEAK_HBM_GBS = 8000.0
 
 WORKLOADS = {
@@ -133,7 +140,9 @@ WORKLOADS = {
 # kernel classes timed by libbgcn's HIP-event hook (bgcn_set_kernel_timing)
 KERNEL_CLASSES = {
     "dense": {0: "conv1 X.W1^T MFMA (TD+BU fused)", 1: "dW1 = dZ1^T X MFMA (TD+BU fused)",
-              2: "conv2 A2.W2^T MFMA (generated A2)", 3: "dW2 = dZ2^T A2 MFMA (generated A2)"},
+              2: "conv2 A2.W2^T MFMA (generated A2)",
+              3: "dW2 = dZ2^T A2 MFMA (root columns: k-tiles of one tree, keep bits x dZ2 on the bf16 MFMA, "
+                 "the root factor per tile in fp32)"},
     "auto": {0: "conv1: k_compact_conv1 (X read + compaction + gather) or gather from prepared ELL",
              2: "conv2 (sparse root gather)", 3: "k_bwd_mid: dW2 partials + root partials + dH1",
              5: "k_bwd_tail: dW1 over CSC(X) + dW2 root columns + reductions",
@@ -146,7 +155,7 @@ ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2):
                  ("auto", 3): "bgcn::k_bwd_mid<float>", ("auto", 5): "bgcn::k_bwd_tail<0, 0>",
                  ("auto", 7): "bgcn::k_prep_b<float>",
                  ("dense", 0): "bgcn::k_gemm_xwt_x6p", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
-                 ("dense", 2): "bgcn::k_conv2_fwd_bf16<float, true>", ("dense", 3): "bgcn::k_dw2_f32"}
+                 ("dense", 2): "bgcn::k_conv2_fwd_bf16<float, true>", ("dense", 3): "bgcn::k_dw2_root<float>"}
 
 
 def pmc_file(workload: str, mode: str = "auto") -> str:
@@ -707,6 +716,11 @@ def main():
                         "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
                         "traffic": pmc_traffic(mode, c, args.workload, wl.get("xdtype") == "bf16"), "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
+                k3 = BF16_PRODUCTS.get((mode, c, wl.get("xdtype") == "bf16"))
+                if k3:   # the hardware the class runs on: fp32-grade products as k bf16 products
+                    roof["bf16_products"] = k3
+                    roof["peak_bf16_emulated"] = round(PEAK_BF16_MFMA_TFLOPS / k3, 1)
+                    roof["frac_of_bf16_emulated_peak"] = round(ach * k3 / PEAK_BF16_MFMA_TFLOPS, 4)
             else:
                 event_ms = avg_ms
                 timer = "HIP events on the launch stream"

@@ -751,7 +751,8 @@ size_t carve_fused(Carve& c, int64_t N, int64_t B, int64_t F, FusedWs* w) {
   // dense feature mode: node splits of >= 2048 nodes, at most 32 (its dW2 blocks loop over
   // a split's nodes: 8 splits left 400+ serial k-tiles per block at Weibo size)
   {
-    int64_t kd = std::max<int64_t>(2048, (N + 31) / 32);
+    static const int64_t kd_env = [] { const char* e = std::getenv("BGCN_DW2D_NODES"); return e ? int64_t(atol(e)) : 0; }();
+    int64_t kd = kd_env > 0 ? kd_env : std::max<int64_t>(2048, (N + 31) / 32);   // (env: A/B runs)
     kd = (kd + 63) / 64 * 64;
     t.kchunk2d = kd;
     t.S2d = int(std::max<int64_t>(1, (N + kd - 1) / kd));
@@ -1159,11 +1160,18 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   m.dw2_sparse = Dw2Cfg{w.kchunkh, w.Sh, 1, 0, int64_t(H), w.dw2_part};
   m.n_dw2_dense = dense_launched(a, sp) ? gxd * S2 * 2 : 0;
   // (fp32 X: the six-product form of k_dw2_bf16 measured 394 + 126 us against the f32
-  // MFMA launch's 469 at the bench workload, so fp32 keeps k_dw2_f32)
-  const bool dw2b = m.n_dw2_dense && sp.mode == 1 && a->x_dtype == BGCN_DTYPE_BF16 && bf16_mfma_ok(a);
+  // MFMA launch's 469 at the bench workload; k_dw2_root<float> takes the root factor out of
+  // the MFMA operand instead, three products as for bf16 X.  BGCN_DW2_ROOT=0: k_dw2_f32)
+  static const bool root_f32 = [] { const char* e = std::getenv("BGCN_DW2_ROOT"); return !(e && atoi(e) == 0); }();
+  const bool dw2b = m.n_dw2_dense && sp.mode == 1 && bf16_mfma_ok(a) &&
+                    (a->x_dtype == BGCN_DTYPE_BF16 || (a->x_dtype == BGCN_DTYPE_F32 && root_f32));
   if (dw2b) {
-    // dense mode, bf16 X: the root columns on the bf16 MFMA (k_dw2_bf16, a launch of its
-    // own), dw2_body keeps column tile 0 (the H1 columns)
+    // dense mode: the root columns on the bf16 MFMA (k_dw2_bf16 / k_dw2_root, a launch
+    // of its own), dw2_body keeps column tile 0 (the H1 columns)
+    // bf16 X takes the same form (weibo_bf16 dense 44.0k -> 48.1k trees/s against k_dw2_bf16,
+    // whose operand carries keep x X; BGCN_DW2_ROOT_BF16=0: k_dw2_bf16)
+    static const bool root_bf16 = [] { const char* e = std::getenv("BGCN_DW2_ROOT_BF16"); return !(e && atoi(e) == 0); }();
+    m.dw2b_f32 = a->x_dtype == BGCN_DTYPE_F32 ? 1 : (root_bf16 ? 2 : 0);
     m.gxb = int(grid_for(F, 128));
     m.n_dw2b = m.gxb * S2 * 2;
     m.dw2_dense.gx = 1;
@@ -1176,6 +1184,13 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
     m.n_dw2f = m.n_dw2_dense;
   }
   m.n_dw2 = dw2_own ? 0 : m.n_dw2_dense;   // the sparse relu(H1) block is formed by the dH1 blocks
+  // the H1 columns in the root columns' launch (its first blocks), not the middle launch's
+  // (there their k-tiles in sequence made it 17 -> 124 us at twitter15 fp32).  BGCN_DW2_H_MID=1: the middle launch
+  static const bool h_mid = [] { const char* e = std::getenv("BGCN_DW2_H_MID"); return e && atoi(e) == 1; }();
+  if (dw2b && !h_mid) {
+    m.n_dw2h = m.n_dw2_dense;
+    m.n_dw2 = 0;
+  }
   m.W2td = a->td_w2; m.W2bu = a->bu_w2; m.dH1 = w.dh1; m.colpart = w.colpart; m.nblk_h = int(nblk_h);
   m.rows_h = w.kchunkh;
   m.db2 = ColsumJob{w.colpart2, sign ? sp.max_items : int(nblk_r), a->td_db2, a->bu_db2};

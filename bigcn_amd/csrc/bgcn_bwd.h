@@ -287,6 +287,211 @@ __device__ inline void dw2_bf16_body(const bf16_t* __restrict__ X, int64_t ldx, 
   }
 }
 
+// The dense config's root columns (fp32 and bf16 X; dw2_bf16_body above is the bf16
+// form it replaced, kept behind BGCN_DW2_ROOT_BF16=0).  A node's root-column operand is
+// keep(d, i, 64 + x) * s * relu(X[root(i)][x]); its second factor is the same for every node
+// of one tree, so over k-tiles that are runs of one root's nodes (<= 64, trees are
+// contiguous) the tile's product factors:
+//   part[d][s][o][64 + x] = sum over tiles T of  s*relu(X[root_T][x]) * sum_{i in T} dZ2_d[i][o] keep(d, i, 64 + x)
+// The inner sum runs on the bf16 MFMA with the keep bits as the exact 0/2 operand and dZ2
+// split three ways (fp32-grade products, as dw2_bf16_body), into a fresh tile accumulator;
+// the root factor is one fp32 FMA per output and tile (the lane's column is fixed, so one
+// factor per lane and 32-column half).  Each tile's run is found by a ballot over its 64
+// node_root entries (every wave computes the same run), so the next tile's start is known
+// when its loads are issued.  Layout, block ids and smem as dw2_bf16_body.
+#ifndef BGCN_DW2R_DEEP
+#define BGCN_DW2R_DEEP 1   // tiles whose loads are in flight (2: +20 VGPRs, two waves per SIMD: 4 % slower)
+#endif
+__device__ __forceinline__ float x_elem(const float* p) { return *p; }
+__device__ __forceinline__ float x_elem(const bf16_t* p) { return bf2f(*p); }
+template <class TX>
+__device__ inline void dw2_root_body(const TX* __restrict__ X, int64_t ldx, int64_t F,
+                                         const float* __restrict__ dZ2, const int32_t* __restrict__ node_root,
+                                         int64_t N, KeepSrc keep, const int32_t* __restrict__ gate,
+                                         const Dw2Cfg& cfg, int gxb, int bid, float* smem) {
+  if (!dense_active(gate)) return;
+  __bf16* As = reinterpret_cast<__bf16*>(smem);                 // [3][64 o][kDw2bLd]
+  __bf16* Bs = As + 3 * H * kDw2bLd;                            // [128 x][kDw2bLd]
+  uint32_t* kwl = reinterpret_cast<uint32_t*>(Bs + 128 * kDw2bLd);   // [64 nodes][4 words]
+  const int S = cfg.S;
+  const int bx = bid % gxb, split = (bid / gxb) % S, d = bid / (gxb * S);
+  const int64_t n0 = int64_t(bx) * 128;                         // first X column of the tile
+  const int64_t kb = int64_t(split) * cfg.kchunk, ke = min<int64_t>(kb + cfg.kchunk, N);
+  const float sc = keep.scale();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1, h = lane >> 5, r32 = lane & 31;
+  constexpr int kGN = kDw2bBK / 4, kBN = kDw2bBK / 2;           // nodes per thread: dZ2 / keep bits
+  const int go = tid & 63, gn = (tid >> 6) * kGN;               // dZ2: column o, kGN nodes
+  const int bc = tid & 127, bn = (tid >> 7) * kBN;              // keep bits: column x, kBN nodes
+  const uint32_t w0 = uint32_t((H + n0) >> 5);                  // the tile's first keep word
+  const uint32_t voff_g = uint32_t(gn * (2 * H) + go) * 4u;     // this thread's first dZ2 element in a tile
+  const float hsc = 0.5f * sc;                                  // exact: sc is 1 or 2
+  // one tile's loads in registers; two of them, so a tile's loads are issued two tiles
+  // before its LDS staging (one tile of MFMA work does not cover a load's latency)
+  struct Stage {
+    float rg[kGN];
+    uint32_t rk;
+    float vn[2];   // the tile's root factors for this lane's two output columns
+    int run;       // the tile's nodes (>= 1)
+  };
+  auto gload = [&](Stage& st, int64_t t0) {
+    const int32_t rl = node_root[min<int64_t>(t0 + lane, ke - 1)];
+    const int32_t r0 = __builtin_amdgcn_readfirstlane(rl);
+    const unsigned long long diff = __ballot(rl != r0 || t0 + lane >= ke);
+    const int run = diff ? int(__builtin_ctzll(diff)) : kDw2bBK;
+    st.run = run;
+    // the run's dZ2 rows through a descriptor of run rows: rows past it read as zero
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(dZ2 + t0 * (2 * H) + d * H, uint32_t(run) * (2 * H) * 4u);
+#pragma unroll
+    for (int u = 0; u < kGN; ++u)
+      st.rg[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff_g + uint32_t(u) * (2 * H) * 4u, 0, 0));
+    {
+      const int k = tid >> 2;
+      const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(t0 + k, ke - 1)), w0 + uint32_t(tid & 3));
+      st.rk = k < run ? wd : 0u;
+    }
+    const TX* xr = X + int64_t(r0) * ldx;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int64_t c = n0 + wc * 64 + ni * 32 + r32;
+      const float x = x_elem(xr + (c < F ? c : F - 1));
+      st.vn[ni] = c < F ? hsc * fmaxf(x, 0.f) : 0.f;   // (the keep operand is 2 per kept bit)
+    }
+  };
+  // dZ2 split exactly by truncation (x = hi + mid + lo, each a bf16: hi keeps x's top 8
+  // significant bits, mid the next 8 of the remainder, lo the rest), two values per packed
+  // word; the keep bits expanded to bf16 0 / 2 two nodes per word, from word-major kwl
+  auto sstore = [&](const Stage& st) {
+    kwl[(tid & 3) * kDw2bBK + (tid >> 2)] = st.rk;
+#pragma unroll
+    for (int j = 0; j < kGN / 8; ++j) {
+      uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        uint32_t xb[2], rb[2], lb[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float x = st.rg[8 * j + 2 * p + e];
+          xb[e] = __float_as_uint(x);
+          const float r = x - __uint_as_float(xb[e] & 0xffff0000u);
+          rb[e] = __float_as_uint(r);
+          lb[e] = __float_as_uint(r - __uint_as_float(rb[e] & 0xffff0000u));
+        }
+        hw[p] = __builtin_amdgcn_perm(xb[1], xb[0], 0x07060302u);   // upper halves: value 0 low
+        mw[p] = __builtin_amdgcn_perm(rb[1], rb[0], 0x07060302u);
+        lw[p] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+      }
+      const int oa = go * kDw2bLd + gn + 8 * j;
+      *reinterpret_cast<uint4*>(&As[oa]) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+      *reinterpret_cast<uint4*>(&As[H * kDw2bLd + oa]) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+      *reinterpret_cast<uint4*>(&As[2 * H * kDw2bLd + oa]) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+    }
+    __syncthreads();   // kwl
+    const int wsel = bc >> 5, bit = bc & 31;
+#pragma unroll
+    for (int j = 0; j < kBN / 8; ++j) {
+      const uint4 k0 = *reinterpret_cast<const uint4*>(&kwl[wsel * kDw2bBK + bn + 8 * j]);
+      const uint4 k1 = *reinterpret_cast<const uint4*>(&kwl[wsel * kDw2bBK + bn + 8 * j + 4]);
+      const uint32_t kw[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+      uint32_t bw[4];   // bf16 2.0 = 0x4000: the bit moved to bit 14 of each half
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        bw[p] = ((__builtin_amdgcn_ubfe(kw[2 * p + 1], bit, 1) << 16) | __builtin_amdgcn_ubfe(kw[2 * p], bit, 1)) << 14;
+      *reinterpret_cast<uint4*>(&Bs[bc * kDw2bLd + bn + 8 * j]) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+    }
+  };
+  f32x16 acc[2] = {};
+  int run = 0;
+  float v0 = 0.f, v1 = 0.f;
+  int64_t tn = ke;   // the start of the tile after the staged one
+  // the staged tile times its root factors into acc: one 32-column half at a time (one
+  // fresh tile accumulator live), the A operands re-read from LDS for the second half
+  auto mul_tile = [&]() {
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      f32x16 tile = {};
+      // (every k-step runs: the rows past the run are zero in A; skipping the empty steps
+      // made the compiler predicate the MFMAs and select the accumulators)
+#pragma unroll
+      for (int s = 0; s < kDw2bBK / 16; ++s) {
+        const int ko = 16 * s + 8 * h;
+        const int oa = (wr * 32 + r32) * kDw2bLd + ko;
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&As[oa]);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&As[H * kDw2bLd + oa]);
+        const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(&As[2 * H * kDw2bLd + oa]);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Bs[(wc * 64 + ni * 32 + r32) * kDw2bLd + ko]);
+        tile = mfma_bf16(a2, b, tile);
+        tile = mfma_bf16(a1, b, tile);
+        tile = mfma_bf16(a0, b, tile);
+      }
+      const float vv = ni ? v1 : v0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[ni][q] = fmaf(vv, tile[q], acc[ni][q]);
+    }
+  };
+#if BGCN_DW2R_DEEP == 2
+  // two tiles' loads in flight: the staged tile is multiplied while `nxt` holds the next
+  // tile's loads (start tn) and the one after is loaded into `fre`
+  auto step = [&](Stage& nxt, Stage& fre) -> bool {
+    const int64_t tnn = tn < ke ? tn + nxt.run : ke;
+    if (tnn < ke) gload(fre, tnn);
+    mul_tile();
+    __syncthreads();
+    if (tn >= ke) return false;   // block-uniform
+    sstore(nxt);
+    __syncthreads();
+    run = nxt.run;
+    v0 = nxt.vn[0]; v1 = nxt.vn[1];
+    tn = tnn;
+    return true;
+  };
+  Stage sa, sb;
+  if (kb < ke) {
+    gload(sa, kb);
+    sstore(sa);
+    run = sa.run;
+    v0 = sa.vn[0]; v1 = sa.vn[1];
+    tn = kb + run;
+    if (tn < ke) gload(sb, tn);
+    __syncthreads();
+    while (step(sb, sa) && step(sa, sb)) {
+    }
+  }
+#else
+  // one tile's loads in flight (the occupancy hides the rest)
+  Stage st;
+  if (kb < ke) {
+    gload(st, kb);
+    sstore(st);
+    run = st.run;
+    v0 = st.vn[0]; v1 = st.vn[1];
+    tn = kb + run;
+    __syncthreads();
+    while (true) {   // block-uniform
+      if (tn < ke) gload(st, tn);
+      mul_tile();
+      __syncthreads();
+      if (tn >= ke) break;
+      sstore(st);
+      __syncthreads();
+      run = st.run;
+      v0 = st.vn[0]; v1 = st.vn[1];
+      tn += run;
+    }
+  }
+#endif
+  float* out = cfg.part + (int64_t(d) * S + split) * (H * cfg.ldp) + H + n0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int o = wr * 32 + acc_row(q, lane);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int c = wc * 64 + ni * 32 + r32;
+      if (n0 + c < F) out[int64_t(o) * cfg.ldp + c] = acc[ni][q];
+    }
+  }
+}
+
 // dW2_d[o][c] = sum_s part[d][s][o][c] (fixed order) for c < ldp; the dense config
 // reduces all 64+F columns, the sparse config the relu(H1) block (the root columns come
 // from the root-column body).  A 256-thread group owns 64 consecutive outputs (a tile);

@@ -124,6 +124,8 @@ struct BwdMidArgs {
   Dw2Cfg dw2_dense, dw2_sparse;  // dW2 partials: dense config blocks first
   int n_dw2_dense, n_dw2;
   int n_dw2b = 0, gxb = 0;        // dense mode, bf16 X: the root columns' blocks (k_dw2_bf16)
+  int dw2b_f32 = 0;               // 1: k_dw2_root<float> (tree-run tiles, root factor per tile); 2: <bf16_t>
+  int n_dw2h = 0;                 // the H1 columns' dw2_body blocks run first in that launch (not the middle one)
   int n_dw2f = 0;                 // dense mode, fp32 X: dw2_body's blocks as k_dw2_f32
   int n_root;                    // (set by launcher)
   const float *W2td, *W2bu;      // dH1
@@ -154,7 +156,7 @@ struct BwdTailArgs {
   TailAdam adam;                 // the step's fused optimiser step (adam.on), part 0 only
 };
 int bwd_mid_launch(BwdMidArgs& a, int x_dtype, hipStream_t s);
-int dw2_bf16_launch(BwdMidArgs& a, hipStream_t s);   // dense mode, bf16 X: dW2 root columns
+int dw2_bf16_launch(BwdMidArgs& a, hipStream_t s);   // dense mode: dW2 root columns (bf16 MFMA)
 int dw2_f32_launch(BwdMidArgs& a, hipStream_t s);    // dense mode, fp32 X: dW2 (k_dw2_f32)
 // the whole weight-independent preparation of one batch on one stream (six launches;
 // mode 1 = dense: no ELL / CSC of X); nlanes: 1 = every launch on `s`, 2 = DropEdge + K1

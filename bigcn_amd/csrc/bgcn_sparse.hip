@@ -2398,15 +2398,52 @@ __global__ __launch_bounds__(kTailThreads) void k_bwd_tail(BwdTailArgs a) {
 // The dense feature mode's dW2 root columns for bf16 X (dw2_bf16_body) as a launch of its
 // own: ~45 KB of LDS, three blocks per CU (inside the middle launch they ran at its two
 // per CU).
+// The H1 columns' blocks (dw2_body's column tile 0: f32 MFMA, a split's k-tiles in
+// sequence, the launch's longest-lived blocks) go first, so they run beside the root
+// columns instead of lengthening the middle launch.
+constexpr int kDw2RootSmem = cmax(kDw2bSmem, kDw2Smem);
 __global__ __launch_bounds__(256) void k_dw2_bf16(BwdMidArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[kDw2bSmem];
+  __shared__ __attribute__((aligned(16))) float smem[kDw2RootSmem];
+  int b = int(blockIdx.x);
+  if (b < a.n_dw2h) {
+    dw2_body<bf16_t>(static_cast<const bf16_t*>(a.X), a.ldx, a.S.F, a.H1, a.dZ2, a.node_root, a.S.N, a.keep,
+                     a.gate, a.dw2_dense, a.dw2_sparse, a.n_dw2_dense, b, smem);
+    return;
+  }
+  b -= a.n_dw2h;
   dw2_bf16_body(static_cast<const bf16_t*>(a.X), a.ldx, a.S.F, a.dZ2, a.node_root, a.S.N, a.keep, a.gate,
-                a.dw2_dense, a.gxb, int(blockIdx.x), smem);
+                a.dw2_dense, a.gxb, b, smem);
+}
+
+// ... and for fp32 X (dw2_root_body: k-tiles of one root's nodes, the root factor
+// applied per tile in fp32), same LDS and block ids; TX = bf16_t: the same form for bf16 X
+// (the default; BGCN_DW2_ROOT_BF16=0 keeps k_dw2_bf16).
+#ifndef BGCN_DW2R_WPE
+#define BGCN_DW2R_WPE 3   // three waves per SIMD (162 VGPRs at BGCN_DW2R_DEEP 1)
+#endif
+template <class TX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BGCN_DW2R_WPE))) void k_dw2_root(BwdMidArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[kDw2RootSmem];
+  int b = int(blockIdx.x);
+  if (b < a.n_dw2h) {
+    dw2_body<TX>(static_cast<const TX*>(a.X), a.ldx, a.S.F, a.H1, a.dZ2, a.node_root, a.S.N, a.keep,
+                 a.gate, a.dw2_dense, a.dw2_sparse, a.n_dw2_dense, b, smem);
+    return;
+  }
+  b -= a.n_dw2h;
+  dw2_root_body<TX>(static_cast<const TX*>(a.X), a.ldx, a.S.F, a.dZ2, a.node_root, a.S.N, a.keep, a.gate,
+                    a.dw2_dense, a.gxb, b, smem);
 }
 
 int dw2_bf16_launch(BwdMidArgs& a, hipStream_t s) {
   if (a.n_dw2b <= 0) return BGCN_OK;
-  hipLaunchKernelGGL(k_dw2_bf16, dim3(unsigned(a.n_dw2b)), dim3(256), 0, s, a);
+  const unsigned n = unsigned(a.n_dw2b + a.n_dw2h);
+  if (a.dw2b_f32 == 1)
+    hipLaunchKernelGGL(k_dw2_root<float>, dim3(n), dim3(256), 0, s, a);
+  else if (a.dw2b_f32 == 2)
+    hipLaunchKernelGGL(k_dw2_root<bf16_t>, dim3(n), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_dw2_bf16, dim3(n), dim3(256), 0, s, a);
   BGCN_CHECK_LAUNCH();
   return BGCN_OK;
 }
