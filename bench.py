@@ -86,9 +86,10 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 matrix peak (dense)
 # the dense classes whose fp32-grade products run on the bf16 MFMA: products per fp32 product
 # (conv1 / conv2: six-product splits; dW2: the keep bits exact, dZ2 split three ways - its
 # 64 H1 columns of 5064 stay on the f32 MFMA)
-# (bf16 X: X is exact in bf16, so conv1 and conv2's root block take three)
+# (bf16 X: X is exact in bf16, so conv1, dW1 and conv2's root block take three; fp32 X's
+# dW1 stays on the f32 MFMA)
 BF16_PRODUCTS = {("dense", 0, False): 6, ("dense", 2, False): 6, ("dense", 3, False): 3,
-                 ("dense", 0, True): 3, ("dense", 2, True): 3, ("dense", 3, True): 3}
+                 ("dense", 0, True): 3, ("dense", 1, True): 3, ("dense", 2, True): 3, ("dense", 3, True): 3}
 PEAK_HBM_GBS = 8000.0
 
 WORKLOADS = {

@@ -69,7 +69,7 @@ __device__ inline void dw2_body(const TX* __restrict__ X, int64_t ldx, int64_t F
     const bool ok = node < ke;
     const int64_t nc = min<int64_t>(node, ke - 1);
     const int64_t c = c0 + bc;
-    gw = keep.get(uint32_t(d), uint32_t(nc), uint32_t(c / 32));
+    gw = keep.get(uint32_t(d), uint32_t(nc), uint32_t(min<int64_t>(c / 32, keep.nw - 1)));   // (clamped: the last tile runs past K2)
     gw = ok ? gw : 0u;
     const int32_t root = node_root[nc];
     const TX* xr = X + int64_t(root < 0 ? 0 : root) * ldx;
@@ -209,7 +209,7 @@ __device__ inline void dw2_bf16_body(const bf16_t* __restrict__ X, int64_t ldx, 
     }
     {
       const int64_t k = k0 + (tid >> 2);
-      const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(k, ke - 1)), w0 + uint32_t(tid & 3));
+      const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(k, ke - 1)), min(w0 + uint32_t(tid & 3), uint32_t(keep.nw - 1)));
       rk = k < ke ? wd : 0u;
     }
   };
@@ -324,6 +324,10 @@ __device__ inline void dw2_root_body(const TX* __restrict__ X, int64_t ldx, int6
   const int go = tid & 63, gn = (tid >> 6) * kGN;               // dZ2: column o, kGN nodes
   const int bc = tid & 127, bn = (tid >> 7) * kBN;              // keep bits: column x, kBN nodes
   const uint32_t w0 = uint32_t((H + n0) >> 5);                  // the tile's first keep word
+  // this thread's keep word, clamped to the node's last (the last column tile's words past
+  // F only feed output columns that are not stored; injected words must not be read past
+  // the array's end)
+  const uint32_t wk = min(w0 + uint32_t(tid & 3), uint32_t(keep.nw - 1));
   const uint32_t voff_g = uint32_t(gn * (2 * H) + go) * 4u;     // this thread's first dZ2 element in a tile
   const float hsc = 0.5f * sc;                                  // exact: sc is 1 or 2
   // one tile's loads in registers; two of them, so a tile's loads are issued two tiles
@@ -347,7 +351,7 @@ __device__ inline void dw2_root_body(const TX* __restrict__ X, int64_t ldx, int6
       st.rg[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff_g + uint32_t(u) * (2 * H) * 4u, 0, 0));
     {
       const int k = tid >> 2;
-      const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(t0 + k, ke - 1)), w0 + uint32_t(tid & 3));
+      const uint32_t wd = keep.get(uint32_t(d), uint32_t(min<int64_t>(t0 + k, ke - 1)), wk);
       st.rk = k < run ? wd : 0u;
     }
     const TX* xr = X + int64_t(r0) * ldx;
