@@ -262,6 +262,87 @@ __global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ G, in
   }
 }
 
+// The same partials with a 64 x 64 wave tile (block 128 x 128, four accumulators per
+// wave): one LDS operand read per f32 MFMA instead of 1.5, and a third less global
+// traffic per flop; 64 KB of LDS, two blocks per CU.  Vector-aligned operands only.
+#ifndef BGCN_TN_WIDE_BK
+#define BGCN_TN_WIDE_BK 16   // k-tile depth (nodes; kchunk stays a multiple of BK = 32): 32 KB of LDS,
+                             // four blocks per CU (32: 0.345 ms, 16: 0.322, 8: 0.327 at twitter15)
+#endif
+__global__ __launch_bounds__(256) void k_gemm_tn_w(const float* __restrict__ G, int64_t ldg,
+                                                   const float* __restrict__ X, int64_t ldx,
+                                                   float* __restrict__ part, int64_t Mc, int64_t Nc,
+                                                   int64_t K, int64_t kchunk,
+                                                   const int32_t* __restrict__ gate) {
+  if (gate_closed(gate)) return;
+  constexpr int BM = 128, BN = 128, TK = BGCN_TN_WIDE_BK;
+  __shared__ float Gs[2][TK * BM];
+  __shared__ float Xs[2][TK * BN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t n0 = int64_t(blockIdx.x) * BN, m0 = int64_t(blockIdx.y) * BM;
+  const int64_t kb = int64_t(blockIdx.z) * kchunk;
+  const int64_t ke = min<int64_t>(kb + kchunk, K);
+  float* out = part + int64_t(blockIdx.z) * Mc * Nc;
+  // staging maps: both tiles TK nodes x 128 -> TK / 8 float4 per thread each
+  const int s_node = tid >> 5, s_q = (tid & 31) * 4;
+  float4 rg[TK / 8], rx[TK / 8];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < TK / 8; ++i) {
+      const int64_t k = k0 + s_node + 8 * i;
+      const int64_t m = m0 + s_q, n = n0 + s_q;
+      rg[i] = (k < ke && m < Mc) ? ld4(G + k * ldg + m) : f4zero();
+      rx[i] = (k < ke && n < Nc) ? ld4(X + k * ldx + n) : f4zero();
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < TK / 8; ++i) {
+      st4(&Gs[buf][(s_node + 8 * i) * BM + s_q], rg[i]);
+      st4(&Xs[buf][(s_node + 8 * i) * BN + s_q], rx[i]);
+    }
+  };
+  f32x16 acc[2][2] = {};
+  const int h = lane >> 5, r32 = lane & 31;
+  const int nk = int((ke - kb + TK - 1) / TK);
+  if (nk > 0) {
+    gload(kb);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kb + int64_t(kt + 1) * TK);
+    const float* A0 = &Gs[buf][h * BM + wr * 64 + r32];
+    const float* B0 = &Xs[buf][h * BN + wc * 64 + r32];
+#pragma unroll
+    for (int s = 0; s < TK / 2; ++s) {
+      const float a0 = A0[2 * s * BM], a1 = A0[2 * s * BM + 32];
+      const float b0 = B0[2 * s * BN], b1 = B0[2 * s * BN + 32];
+      acc[0][0] = mfma32x32x2(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32x32x2(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32x32x2(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32x32x2(a1, b1, acc[1][1]);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t n = n0 + wc * 64 + j * 32 + r32;
+      if (n >= Nc) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int64_t m = m0 + wr * 64 + i * 32 + acc_row(r, lane);
+        if (m < Mc) out[m * Nc + n] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // ============================================================================
 // bf16 X on the bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the k-depth of the f32 MFMA per
 // instruction).  Bag-of-words X is exact in bf16; the fp32 operand (W, or dZ1) is split
@@ -877,8 +958,20 @@ int tn_splits(int64_t Mc, int64_t Nc, int64_t K) {
   return int(s < 1 ? 1 : (s > 64 ? 64 : s));
 }
 
+// k_gemm_tn_w (128 x 128 tiles): node splits for about BGCN_TN_WIDE_BLOCKS blocks (A/B
+// knob, read once; default 1024)
+int tn_splits_w(int64_t Mc, int64_t Nc, int64_t K) {
+  static const int64_t target = [] { const char* e = std::getenv("BGCN_TN_WIDE_BLOCKS"); return e ? std::max<int64_t>(1, atol(e)) : int64_t(1024); }();
+  const int64_t tiles = ((Nc + 127) / 128) * ((Mc + 127) / 128);
+  const int64_t want = std::max<int64_t>(1, target / tiles);
+  const int64_t maxs = (K + BK - 1) / BK;
+  const int64_t s = want < maxs ? want : maxs;
+  return int(s < 1 ? 1 : (s > 64 ? 64 : s));
+}
+
 size_t tn_ws_size(int64_t Mc, int64_t Nc, int64_t K) {
-  return size_t(tn_splits(Mc, Nc, K)) * size_t(Mc) * size_t(Nc) * sizeof(float) + 256;
+  const int S = std::max(tn_splits(Mc, Nc, K), tn_splits_w(Mc, Nc, K));
+  return size_t(S) * size_t(Mc) * size_t(Nc) * sizeof(float) + 256;
 }
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -1034,17 +1127,27 @@ static int gemm_tn_t(const float* G, int64_t ldg, const TX* X, int64_t ldx, floa
   BGCN_CHECK_ARG(ldg >= Mc && ldx >= Nc && ldc >= Nc, "bad leading dimension");
   BGCN_CHECK_ARG(split >= Mc || C1, "C1 required when split < Mc");
   BGCN_CHECK_ARG(ws && ws_bytes >= tn_ws_size(Mc, Nc, K), "workspace too small");
-  int S = tn_splits(Mc, Nc, K);
+  const bool xal = (reinterpret_cast<uintptr_t>(X) & (4 * sizeof(TX) - 1)) == 0;
+  bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) && xal;
+  // fp32 X: the 64 x 64 wave-tile kernel (BGCN_TN_WIDE=0 keeps k_gemm_tn)
+  static const bool wide_on = [] { const char* e = std::getenv("BGCN_TN_WIDE"); return !(e && atoi(e) == 0); }();
+  const bool wide = sizeof(TX) == 4 && vec && wide_on;
+  int S = wide ? tn_splits_w(Mc, Nc, K) : tn_splits(Mc, Nc, K);
   int64_t kchunk = (K + S - 1) / S;
   kchunk = (kchunk + BK - 1) / BK * BK;
   if (kchunk == 0) kchunk = BK;
   S = int((K + kchunk - 1) / kchunk);
   if (S < 1) S = 1;
   float* part = static_cast<float*>(ws);
-  const bool xal = (reinterpret_cast<uintptr_t>(X) & (4 * sizeof(TX) - 1)) == 0;
-  bool vec = Mc % 4 == 0 && Nc % 4 == 0 && ldg % 4 == 0 && ldx % 4 == 0 && aligned16(G) && xal;
   timing_begin(timing_cls, stream);
   bool done = false;
+  if constexpr (sizeof(TX) == 4) {
+    if (wide) {
+      hipLaunchKernelGGL(k_gemm_tn_w, dim3(grid_for(Nc, 128), grid_for(Mc, 128), S), dim3(256), 0, stream, G, ldg,
+                         reinterpret_cast<const float*>(X), ldx, part, Mc, Nc, K, kchunk, gate);
+      done = true;
+    }
+  }
   // bf16 X: the bf16 MFMA with G split three ways.  fp32 X keeps the f32 MFMA: the
   // six-product forms measured 385 us (k_gemm_tn_bf16<float>), 489 us (X read straight into
   // the B fragments) and 479 us (that kernel with its splits between the MFMAs) against
