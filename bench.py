@@ -155,7 +155,7 @@ SPARSE_CAP = 32
 ROCPROF_NAMES = {("auto", 0): "bgcn::k_compact_conv1<true, float>", ("auto", 2): "bgcn::k_conv2_sparse",
                  ("auto", 3): "bgcn::k_bwd_mid<float>", ("auto", 5): "bgcn::k_bwd_tail<0, 0>",
                  ("auto", 7): "bgcn::k_prep_b<float>",
-                 ("dense", 0): "bgcn::k_gemm_xwt_x6p", ("dense", 1): "bgcn::k_gemm_tn<true, float>",
+                 ("dense", 0): "bgcn::k_gemm_xwt_x6p", ("dense", 1): "bgcn::k_gemm_tn_w",
                  ("dense", 2): "bgcn::k_conv2_fwd_bf16<float, true>", ("dense", 3): "bgcn::k_dw2_root<float>"}
 
 
@@ -708,16 +708,23 @@ def main():
                 ent["gbs"] = round(work / (avg_ms * 1e-3) / 1e9, 1)
             kernels[KERNEL_CLASSES[mode][c]] = ent
             if bound is not None and where == "timed loop":
-                best = (c, avg_ms, bound, work)
+                best = (c, avg_ms, bound, work, n_nodes)
         if best is not None:
-            c, avg_ms, bound, work = best
+            c, avg_ms, bound, work, n_nodes = best
             if bound == "mfma":
                 ach = work / (avg_ms * 1e-3) / 1e12
                 roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
                         "traffic": pmc_traffic(mode, c, args.workload, wl.get("xdtype") == "bf16"), "kernel": KERNEL_CLASSES[mode][c], "flops_per_launch": work,
                         "avg_ms": round(avg_ms, 4)}
-                k3 = BF16_PRODUCTS.get((mode, c, wl.get("xdtype") == "bf16"))
+                xb = wl.get("xdtype") == "bf16"
+                k3 = BF16_PRODUCTS.get((mode, c, xb))
+                # the library's own size rules (bgcn_internal.h kX6MinRows = 8192 rows for the
+                # fp32 six-product kernels; dW2's tree-run tiles need >= 32 nodes per tree)
+                if k3 and not xb and c in (0, 2) and n_nodes < 8192:
+                    k3 = None
+                if k3 and c == 3 and n_nodes < 32 * wl["trees"]:
+                    k3 = None if not xb else k3
                 if k3:   # the hardware the class runs on: fp32-grade products as k bf16 products
                     roof["bf16_products"] = k3
                     roof["peak_bf16_emulated"] = round(PEAK_BF16_MFMA_TFLOPS / k3, 1)

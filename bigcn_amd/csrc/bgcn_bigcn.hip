@@ -1163,15 +1163,18 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   // MFMA launch's 469 at the bench workload; k_dw2_root<float> takes the root factor out of
   // the MFMA operand instead, three products as for bf16 X.  BGCN_DW2_ROOT=0: k_dw2_f32)
   static const bool root_f32 = [] { const char* e = std::getenv("BGCN_DW2_ROOT"); return !(e && atoi(e) == 0); }();
+  // (the tree-run tiles need trees of >= 32 nodes on average, as conv2's root planes do:
+  // PHEME's ~10-node trees left 64-node tiles mostly empty, 15.6 -> 43.2 us)
+  const bool big_trees = N >= 32 * B;
   const bool dw2b = m.n_dw2_dense && sp.mode == 1 && bf16_mfma_ok(a) &&
-                    (a->x_dtype == BGCN_DTYPE_BF16 || (a->x_dtype == BGCN_DTYPE_F32 && root_f32));
+                    (a->x_dtype == BGCN_DTYPE_BF16 || (a->x_dtype == BGCN_DTYPE_F32 && root_f32 && big_trees));
   if (dw2b) {
     // dense mode: the root columns on the bf16 MFMA (k_dw2_bf16 / k_dw2_root, a launch
     // of its own), dw2_body keeps column tile 0 (the H1 columns)
     // bf16 X takes the same form (weibo_bf16 dense 44.0k -> 48.1k trees/s against k_dw2_bf16,
     // whose operand carries keep x X; BGCN_DW2_ROOT_BF16=0: k_dw2_bf16)
     static const bool root_bf16 = [] { const char* e = std::getenv("BGCN_DW2_ROOT_BF16"); return !(e && atoi(e) == 0); }();
-    m.dw2b_f32 = a->x_dtype == BGCN_DTYPE_F32 ? 1 : (root_bf16 ? 2 : 0);
+    m.dw2b_f32 = a->x_dtype == BGCN_DTYPE_F32 ? 1 : (root_bf16 && big_trees ? 2 : 0);
     m.gxb = int(grid_for(F, 128));
     m.n_dw2b = m.gxb * S2 * 2;
     m.dw2_dense.gx = 1;
