@@ -1161,19 +1161,22 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   m.n_dw2_dense = dense_launched(a, sp) ? gxd * S2 * 2 : 0;
   // (fp32 X: the six-product form of k_dw2_bf16 measured 394 + 126 us against the f32
   // MFMA launch's 469 at the bench workload; k_dw2_root<float> takes the root factor out of
-  // the MFMA operand instead, three products as for bf16 X.  BGCN_DW2_ROOT=0: k_dw2_f32)
-  static const bool root_f32 = [] { const char* e = std::getenv("BGCN_DW2_ROOT"); return !(e && atoi(e) == 0); }();
+  // the MFMA operand instead, three products as for bf16 X.  BGCN_DW2_ROOT (read per call,
+  // A/B runs and tests): 0 = k_dw2_f32 / k_dw2_bf16, 2 = the root form for any tree size)
+  const char* root_env = std::getenv("BGCN_DW2_ROOT");
+  const int root_mode = root_env ? atoi(root_env) : 1;
+  const bool root_f32 = root_mode != 0;
   // (the tree-run tiles need trees of >= 32 nodes on average, as conv2's root planes do:
   // PHEME's ~10-node trees left 64-node tiles mostly empty, 15.6 -> 43.2 us)
-  const bool big_trees = N >= 32 * B;
+  const bool big_trees = root_mode == 2 || N >= 32 * B;
   const bool dw2b = m.n_dw2_dense && sp.mode == 1 && bf16_mfma_ok(a) &&
                     (a->x_dtype == BGCN_DTYPE_BF16 || (a->x_dtype == BGCN_DTYPE_F32 && root_f32 && big_trees));
   if (dw2b) {
     // dense mode: the root columns on the bf16 MFMA (k_dw2_bf16 / k_dw2_root, a launch
     // of its own), dw2_body keeps column tile 0 (the H1 columns)
     // bf16 X takes the same form (weibo_bf16 dense 44.0k -> 48.1k trees/s against k_dw2_bf16,
-    // whose operand carries keep x X; BGCN_DW2_ROOT_BF16=0: k_dw2_bf16)
-    static const bool root_bf16 = [] { const char* e = std::getenv("BGCN_DW2_ROOT_BF16"); return !(e && atoi(e) == 0); }();
+    // whose operand carries keep x X; BGCN_DW2_ROOT=0: k_dw2_bf16)
+    const bool root_bf16 = root_f32;
     m.dw2b_f32 = a->x_dtype == BGCN_DTYPE_F32 ? 1 : (root_bf16 && big_trees ? 2 : 0);
     m.gxb = int(grid_for(F, 128));
     m.n_dw2b = m.gxb * S2 * 2;
@@ -1189,7 +1192,8 @@ int bigcn_backward_impl(const bgcn_bigcn_args* a, void* ws, size_t ws_bytes, hip
   m.n_dw2 = dw2_own ? 0 : m.n_dw2_dense;   // the sparse relu(H1) block is formed by the dH1 blocks
   // the H1 columns in the root columns' launch (its first blocks), not the middle launch's
   // (there their k-tiles in sequence made it 17 -> 124 us at twitter15 fp32).  BGCN_DW2_H_MID=1: the middle launch
-  static const bool h_mid = [] { const char* e = std::getenv("BGCN_DW2_H_MID"); return e && atoi(e) == 1; }();
+  const char* h_env = std::getenv("BGCN_DW2_H_MID");
+  const bool h_mid = h_env && atoi(h_env) == 1;
   if (dw2b && !h_mid) {
     m.n_dw2h = m.n_dw2_dense;
     m.n_dw2 = 0;

@@ -288,7 +288,7 @@ __device__ inline void dw2_bf16_body(const bf16_t* __restrict__ X, int64_t ldx, 
 }
 
 // The dense config's root columns (fp32 and bf16 X; dw2_bf16_body above is the bf16
-// form it replaced, kept behind BGCN_DW2_ROOT_BF16=0).  A node's root-column operand is
+// form it replaced, kept behind BGCN_DW2_ROOT=0).  A node's root-column operand is
 // keep(d, i, 64 + x) * s * relu(X[root(i)][x]); its second factor is the same for every node
 // of one tree, so over k-tiles that are runs of one root's nodes (<= 64, trees are
 // contiguous) the tile's product factors:

@@ -2417,7 +2417,7 @@ __global__ __launch_bounds__(256) void k_dw2_bf16(BwdMidArgs a) {
 
 // ... and for fp32 X (dw2_root_body: k-tiles of one root's nodes, the root factor
 // applied per tile in fp32), same LDS and block ids; TX = bf16_t: the same form for bf16 X
-// (the default; BGCN_DW2_ROOT_BF16=0 keeps k_dw2_bf16).
+// (the default; BGCN_DW2_ROOT=0 keeps k_dw2_bf16).
 #ifndef BGCN_DW2R_WPE
 #define BGCN_DW2R_WPE 3   // three waves per SIMD (162 VGPRs at BGCN_DW2R_DEEP 1)
 #endif

@@ -69,6 +69,17 @@ def test_fused_matches_golden(name, mode):
         close(grads[k], g["grad:" + k], what=k)
 
 
+@pytest.mark.parametrize("name", GOLDEN)
+def test_dense_dw2_root_tiles_on_small_trees(name, monkeypatch):
+    """The dense path's dW2 root columns as tree-run k-tiles (``k_dw2_root``) forced onto
+    the golden batches (``BGCN_DW2_ROOT=2``; the library keeps ``k_dw2_f32`` below 32 nodes
+    per tree): runs of one node (single-node trees), stars, a root in mid-batch, injected
+    keep words whose last column tile reaches past the node's words (F = 96: the clamped
+    word), against the fixture at the same tolerance."""
+    monkeypatch.setenv("BGCN_DW2_ROOT", "2")
+    test_fused_matches_golden(name, "dense")
+
+
 def _synth(seed, B, mean, F=5000, droprates=(0.2, 0.2), root_random=False):
     from bigcn_amd.data import synth_batch, synth_tree_sizes
     rng = np.random.default_rng(seed)
