@@ -306,13 +306,13 @@ __device__ __forceinline__ float x_elem(const float* p) { return *p; }
 __device__ __forceinline__ float x_elem(const bf16_t* p) { return bf2f(*p); }
 template <class TX>
 __device__ inline void dw2_root_body(const TX* __restrict__ X, int64_t ldx, int64_t F,
-                                         const float* __restrict__ dZ2, const int32_t* __restrict__ node_root,
-                                         int64_t N, KeepSrc keep, const int32_t* __restrict__ gate,
-                                         const Dw2Cfg& cfg, int gxb, int bid, float* smem) {
+                                     const float* __restrict__ dZ2, const int32_t* __restrict__ node_root,
+                                     int64_t N, KeepSrc keep, const int32_t* __restrict__ gate,
+                                     const Dw2Cfg& cfg, int gxb, int bid, float* smem) {
   if (!dense_active(gate)) return;
   __bf16* As = reinterpret_cast<__bf16*>(smem);                 // [3][64 o][kDw2bLd]
   __bf16* Bs = As + 3 * H * kDw2bLd;                            // [128 x][kDw2bLd]
-  uint32_t* kwl = reinterpret_cast<uint32_t*>(Bs + 128 * kDw2bLd);   // [64 nodes][4 words]
+  uint32_t* kwl = reinterpret_cast<uint32_t*>(Bs + 128 * kDw2bLd);   // [4 words][64 nodes]
   const int S = cfg.S;
   const int bx = bid % gxb, split = (bid / gxb) % S, d = bid / (gxb * S);
   const int64_t n0 = int64_t(bx) * 128;                         // first X column of the tile
@@ -330,8 +330,8 @@ __device__ inline void dw2_root_body(const TX* __restrict__ X, int64_t ldx, int6
   const uint32_t wk = min(w0 + uint32_t(tid & 3), uint32_t(keep.nw - 1));
   const uint32_t voff_g = uint32_t(gn * (2 * H) + go) * 4u;     // this thread's first dZ2 element in a tile
   const float hsc = 0.5f * sc;                                  // exact: sc is 1 or 2
-  // one tile's loads in registers; two of them, so a tile's loads are issued two tiles
-  // before its LDS staging (one tile of MFMA work does not cover a load's latency)
+  // one tile's loads in registers (BGCN_DW2R_DEEP 2 keeps two, issued two tiles before
+  // their LDS staging; the default relies on three waves per SIMD instead)
   struct Stage {
     float rg[kGN];
     uint32_t rk;
