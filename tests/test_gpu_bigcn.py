@@ -173,6 +173,25 @@ def test_sparse_and_dense_paths_agree_full_size():
         close(rs[2][k], rd[2][k], what=k)
 
 
+@pytest.mark.parametrize("mean,root", [(8, "1"), (8, "2"), (200, "1"), (200, "0")])
+def test_dense_bf16_dw2_forms_agree_with_sparse_path(mean, root, monkeypatch):
+    """bf16 X on the dense path against the sparse path on the same bf16 batch: small trees
+    (mean 8: ``k_dw2_bf16`` with the H1 columns' blocks in its launch by default, the
+    tree-run tiles of ``k_dw2_root<bf16>`` forced by BGCN_DW2_ROOT=2) and Twitter-sized ones
+    (``k_dw2_root`` by default, ``k_dw2_bf16`` with BGCN_DW2_ROOT=0)."""
+    from bigcn_amd.data import synth_batch, synth_tree_sizes
+    monkeypatch.setenv("BGCN_DW2_ROOT", root)
+    rng = np.random.default_rng(31 + mean)
+    sizes = synth_tree_sizes(rng, 64 if mean == 200 else 400, mean)
+    b = synth_batch(rng, sizes, 5000, 4, 0.2, 0.2, device=DEV, dtype=torch.bfloat16)
+    p = O.make_params(5000, 64, 64, 4, seed=9)
+    rs = gpu_step(b, p, True, None, seed=7, mode="auto")
+    rd = gpu_step(b, p, True, None, seed=7, mode="dense")
+    close(rs[3], rd[3], what="head")
+    for k in rs[2]:
+        close(rs[2][k], rd[2][k], what=k)
+
+
 @pytest.mark.parametrize("dense_rows", [1, 200])
 def test_sparse_overflow_falls_back_to_dense(dense_rows):
     """Dense rows (512 non-zeros): one fits the spill pool (the sparse path adds its spilled
